@@ -1,0 +1,282 @@
+/*
+ * swifthip.h — C ABI of libswifthip: an MI355X (gfx950, CDNA4) HIP
+ * implementation of SWIFT's SPH neighbour loops (density, gradient, force,
+ * ghost h-iteration) and leaf-leaf P2P gravity.
+ *
+ * Plain C: pointers, sizes and POD structs only; no SWIFT, HIP or torch types
+ * in any signature. The SWIFT-signature entry points (runner_doself1_branch_
+ * density(struct runner*, struct cell*) ...) live in the thin C adapter
+ * (swifthip_swift.h) that marshals SWIFT cells into the views below.
+ *
+ * Two families of entry points:
+ *
+ *  (1) Per-task (drop-in, synchronous): one call = one SWIFT task on host
+ *      struct part / struct gpart arrays, results written back in place
+ *      before return. Replaces the bodies of
+ *        DOSELF1_BRANCH / DOPAIR1_BRANCH  src/runner_doiact_functions_hydro.h:2271,1331
+ *        DOSELF2_BRANCH / DOPAIR2_BRANCH  src/runner_doiact_functions_hydro.h:2486,1972
+ *        DOSELF_SUBSET_BRANCH / DOPAIR_SUBSET_BRANCH  :1048, :884
+ *        runner_doself_grav_pp / runner_dopair_grav_pp  src/runner_doiact_grav.c:1788,1202
+ *
+ *  (2) Batch (performance): a device-resident particle set (swh_space) on
+ *      which whole loops run as one launch each, replacing every density /
+ *      gradient / force task of a step plus the ghost and extra ghost
+ *      (src/runner_ghost.c:1085, :992) and runner_do_end_hydro_force
+ *      (src/runner_others.c:618). The interaction set is exactly that of the
+ *      task graph: every active i meets every j with r < H_i (density,
+ *      gradient) or r < max(H_i, H_j) (force), nearest periodic image.
+ *
+ * Errors: every function returns swh_status; nothing aborts. The SWIFT
+ * adapter maps non-zero codes to SWIFT's error() exactly where the reference
+ * calls error() ("Interacting unsorted cells.", ...).
+ *
+ * Precision: interactions and per-particle updates evaluated in fp64 (the
+ * default) or fp32 (SWH_PRECISION_F32, the reference's own precision);
+ * storage stays at struct part precision (float fields, double positions).
+ */
+#ifndef SWIFTHIP_H
+#define SWIFTHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SWH_ABI_VERSION 1
+
+#if defined(__GNUC__)
+#define SWH_API __attribute__((visibility("default")))
+#else
+#define SWH_API
+#endif
+
+typedef enum swh_status {
+  SWH_OK = 0,
+  SWH_ERR_ARG = 1,           /* invalid argument / shape */
+  SWH_ERR_HIP = 2,           /* HIP runtime error (see swh_last_error) */
+  SWH_ERR_UNSORTED = 3,      /* "Interacting unsorted cells." */
+  SWH_ERR_CELL_SMALL = 4,    /* "Cell smaller than smoothing length" */
+  SWH_ERR_NOT_CONVERGED = 5, /* "Smoothing length failed to converge" */
+  SWH_ERR_NO_DEVICE = 6,     /* no usable gfx950 device */
+  SWH_ERR_OOM = 7,           /* device allocation failed */
+  SWH_ERR_STATE = 8          /* call out of order (e.g. loop before rebuild) */
+} swh_status;
+
+typedef enum swh_precision { SWH_PRECISION_F64 = 0, SWH_PRECISION_F32 = 1 } swh_precision;
+
+/* ------------------------------------------------------------------ */
+/* Particle layout descriptors: byte offsets inside the caller's AoS   */
+/* record, so the library never hard-codes struct part (its layout is  */
+/* configure-dependent in SWIFT). -1 = field absent.                   */
+/* ------------------------------------------------------------------ */
+typedef struct swh_part_layout {
+  int32_t stride; /* sizeof(struct part) */
+  int32_t off_id;                                   /* long long */
+  int32_t off_x;                                    /* double[3] */
+  int32_t off_v, off_a_hydro;                       /* float[3]  */
+  int32_t off_mass, off_h, off_u, off_u_dt, off_rho;
+  int32_t off_div_v, off_div_v_dt, off_div_v_previous_step, off_visc_alpha, off_v_sig;
+  int32_t off_laplace_u, off_diff_alpha;
+  /* density union member */
+  int32_t off_wcount, off_wcount_dh, off_rho_dh, off_rot_v; /* rot_v float[3] */
+  /* force union member */
+  int32_t off_f, off_pressure, off_soundspeed, off_h_dt, off_balsara, off_alpha_visc_max_ngb;
+  int32_t off_time_bin;         /* int8 */
+  int32_t off_min_ngb_time_bin; /* int8 */
+} swh_part_layout;
+
+typedef struct swh_gpart_layout {
+  int32_t stride; /* sizeof(struct gpart) */
+  int32_t off_x;          /* double[3] */
+  int32_t off_a_grav;     /* float[3]  */
+  int32_t off_potential;  /* float     */
+  int32_t off_mass;       /* float     */
+  int32_t off_epsilon;    /* float     */
+  int32_t off_time_bin;   /* int8      */
+} swh_gpart_layout;
+
+/* Layouts of SWIFT's default configure (SPHENIX part: 160 B; multi-softening
+ * gpart: 96 B). See include/swift_compat.h for the field map. */
+SWH_API void swh_part_layout_sphenix(swh_part_layout *out);
+SWH_API void swh_gpart_layout_multisoftening(swh_gpart_layout *out);
+
+/* ------------------------------------------------------------------ */
+/* Engine scalars the hydro path reads (struct engine / cosmology /    */
+/* hydro_props fields, SURVEY.md 8b "Preconditions").                  */
+/* ------------------------------------------------------------------ */
+typedef struct swh_hydro_params {
+  double a, H, a2_inv, a_factor_sound_speed, a_factor_Balsara_eps; /* cosmology */
+  double time_base;                                                /* engine    */
+  float eta_neighbours, h_tolerance, h_max, h_min;                 /* hydro_props */
+  int32_t max_smoothing_iterations;
+  int32_t use_mass_weighted_num_ngb;
+  float visc_alpha, visc_alpha_max, visc_alpha_min, visc_length;
+  float diff_alpha, diff_beta, diff_alpha_max, diff_alpha_min;
+  int32_t max_active_bin; /* e->max_active_bin */
+  int32_t periodic;       /* e->s->periodic    */
+  double dim[3];          /* e->s->dim         */
+} swh_hydro_params;
+
+typedef struct swh_grav_params {
+  int32_t periodic;  /* e->mesh->periodic  */
+  float dim[3];      /* e->mesh->dim       */
+  float r_s_inv;     /* e->mesh->r_s_inv   */
+  double r_cut_min;  /* e->mesh->r_cut_min */
+  int32_t max_active_bin;
+} swh_grav_params;
+
+/* ------------------------------------------------------------------ */
+/* Context: one per (process, device). Thread-safe: per-task calls     */
+/* from different host threads use different internal streams.        */
+/* ------------------------------------------------------------------ */
+typedef struct swh_context swh_context;
+
+SWH_API swh_status swh_init(swh_context **ctx, int device);
+SWH_API swh_status swh_finalize(swh_context *ctx);
+SWH_API swh_status swh_set_precision(swh_context *ctx, swh_precision p);
+SWH_API const char *swh_status_string(swh_status s);
+/* Last error text of the calling thread (empty string if none). */
+SWH_API const char *swh_last_error(void);
+SWH_API int swh_abi_version(void);
+
+/* ================================================================== */
+/* (1) Per-task entry points                                          */
+/* ================================================================== */
+typedef struct swh_cell_view {
+  void *parts;     /* host pointer to `count` AoS records (struct part) */
+  int32_t count;
+  int32_t active;  /* cell_is_active_hydro(c, e) */
+  double loc[3];
+  double width[3];
+} swh_cell_view;
+
+/* Density / gradient loops (r < H_i): DOSELF1 / DOPAIR1 semantics. In a pair,
+ * active particles of BOTH cells are updated. `shift` is SWIFT's periodic
+ * shift: particle i of ci interacts as x_i - shift (space_getsid.h:46-82). */
+SWH_API swh_status swh_doself_density(swh_context *ctx, const swh_cell_view *c,
+                              const swh_part_layout *L, const swh_hydro_params *P);
+SWH_API swh_status swh_dopair_density(swh_context *ctx, const swh_cell_view *ci,
+                              const swh_cell_view *cj, const double shift[3],
+                              const swh_part_layout *L, const swh_hydro_params *P);
+SWH_API swh_status swh_doself_gradient(swh_context *ctx, const swh_cell_view *c,
+                               const swh_part_layout *L, const swh_hydro_params *P);
+SWH_API swh_status swh_dopair_gradient(swh_context *ctx, const swh_cell_view *ci,
+                               const swh_cell_view *cj, const double shift[3],
+                               const swh_part_layout *L, const swh_hydro_params *P);
+/* Force loop (r < max(H_i, H_j), + time-bin limiter): DOSELF2 / DOPAIR2. */
+SWH_API swh_status swh_doself_force(swh_context *ctx, const swh_cell_view *c,
+                            const swh_part_layout *L, const swh_hydro_params *P);
+SWH_API swh_status swh_dopair_force(swh_context *ctx, const swh_cell_view *ci,
+                            const swh_cell_view *cj, const double shift[3],
+                            const swh_part_layout *L, const swh_hydro_params *P);
+/* Subset density (ghost reruns): only parts_i[ind[0..count)] of ci are
+ * updated, against all of ci (self) or cj (pair). DOSELF_SUBSET /
+ * DOPAIR_SUBSET semantics. `parts_i` may differ from ci->parts (SWIFT passes
+ * the ghost's leaf array). */
+SWH_API swh_status swh_doself_subset_density(swh_context *ctx, const swh_cell_view *ci,
+                                     void *parts_i, const int32_t *ind, int32_t count,
+                                     const swh_part_layout *L, const swh_hydro_params *P);
+SWH_API swh_status swh_dopair_subset_density(swh_context *ctx, const swh_cell_view *ci,
+                                     void *parts_i, const int32_t *ind, int32_t count,
+                                     const swh_cell_view *cj, const double shift[3],
+                                     const swh_part_layout *L, const swh_hydro_params *P);
+
+/* P2P gravity on host gpart arrays. */
+typedef struct swh_gcell_view {
+  void *gparts;
+  int32_t count;
+  int32_t active;
+  double loc[3];
+  double width[3];
+  double CoM[3];   /* multipole->CoM   */
+  double r_max;    /* multipole->r_max */
+} swh_gcell_view;
+
+SWH_API swh_status swh_grav_self_pp(swh_context *ctx, const swh_gcell_view *c,
+                            const swh_gpart_layout *L, const swh_grav_params *G);
+SWH_API swh_status swh_grav_pair_pp(swh_context *ctx, const swh_gcell_view *ci,
+                            const swh_gcell_view *cj, int symmetric,
+                            const swh_gpart_layout *L, const swh_grav_params *G);
+
+/* ================================================================== */
+/* (2) Batch, device-resident                                         */
+/* ================================================================== */
+typedef struct swh_space swh_space;
+
+SWH_API swh_status swh_space_create(swh_context *ctx, swh_space **s);
+SWH_API swh_status swh_space_destroy(swh_space *s);
+/* Bind a HIP stream (hipStream_t passed as void*; NULL = the space's own). */
+SWH_API swh_status swh_space_set_stream(swh_space *s, void *stream);
+/* Upload from a host AoS array (struct part records) or from a DEVICE AoS
+ * array (`parts` already in HBM, e.g. a torch uint8 tensor). */
+SWH_API swh_status swh_space_upload_parts(swh_space *s, const void *parts, int64_t count,
+                                  const swh_part_layout *L, int on_device);
+/* Fields written back: SWH_FIELDS_DENSITY after density+ghost, SWH_FIELDS_FORCE
+ * after force (the union member of struct part that is live), or ALL. */
+#define SWH_FIELDS_DENSITY 1
+#define SWH_FIELDS_GRADIENT 2
+#define SWH_FIELDS_FORCE 4
+#define SWH_FIELDS_ALL 7
+SWH_API swh_status swh_space_download_parts(swh_space *s, void *parts, const swh_part_layout *L,
+                                    int fields, int on_device);
+SWH_API int64_t swh_space_count(const swh_space *s);
+
+/* Bin the particles into the device neighbour grid (cell width >=
+ * `min_cell_width`, or derived from max H when <= 0). Equivalent of
+ * space_rebuild + runner_do_hydro_sort for this path. */
+SWH_API swh_status swh_space_rebuild(swh_space *s, const swh_hydro_params *P,
+                             double min_cell_width);
+
+/* Loops over all active particles. n_interactions (optional) receives the
+ * number of directed interactions evaluated (r < H_i, resp. max(H_i,H_j)). */
+SWH_API swh_status swh_space_init_parts(swh_space *s, const swh_hydro_params *P);
+SWH_API swh_status swh_density_loop(swh_space *s, const swh_hydro_params *P, int64_t *n_interactions);
+SWH_API swh_status swh_ghost(swh_space *s, const swh_hydro_params *P, int32_t *iterations,
+                     int64_t *n_unconverged);
+SWH_API swh_status swh_gradient_loop(swh_space *s, const swh_hydro_params *P, int64_t *n_interactions);
+SWH_API swh_status swh_extra_ghost(swh_space *s, const swh_hydro_params *P);
+SWH_API swh_status swh_force_loop(swh_space *s, const swh_hydro_params *P, int64_t *n_interactions);
+SWH_API swh_status swh_end_force(swh_space *s, const swh_hydro_params *P);
+/* Wait for all queued work on the space's stream. */
+SWH_API swh_status swh_space_sync(swh_space *s);
+
+/* Kernel-tuning knobs of the batch loops (bench/diagnostics). */
+typedef struct swh_tuning {
+  int32_t cell_factor;  /* neighbour-grid cells per H_max (1..4) */
+  int32_t loop_variant; /* 0 = default */
+} swh_tuning;
+SWH_API swh_status swh_space_set_tuning(swh_space *s, const swh_tuning *t);
+
+/* Batch P2P gravity over leaf cells of a device-resident gpart set. Leaves
+ * are contiguous [start, start+count) ranges; for each i-leaf, the CSR list
+ * pairs[pair_offset[i] .. pair_offset[i+1]) names the source leaves
+ * (including i itself for the self term) with a per-pair truncation flag
+ * (runner_doself/dopair_grav_pp's full-vs-truncated choice). */
+typedef struct swh_gspace swh_gspace;
+typedef struct swh_leaf {
+  int32_t start;
+  int32_t count;
+} swh_leaf;
+typedef struct swh_leaf_pair {
+  int32_t j;         /* source leaf index */
+  int32_t truncated; /* 1: long-range truncated kernel */
+} swh_leaf_pair;
+SWH_API swh_status swh_gspace_create(swh_context *ctx, swh_gspace **g);
+SWH_API swh_status swh_gspace_destroy(swh_gspace *g);
+SWH_API swh_status swh_gspace_upload(swh_gspace *g, const void *gparts, int64_t count,
+                             const swh_gpart_layout *L, int on_device);
+SWH_API swh_status swh_gspace_set_leaves(swh_gspace *g, const swh_leaf *leaves, int32_t nleaves,
+                                 const int32_t *pair_offset, const swh_leaf_pair *pairs,
+                                 int32_t npairs);
+SWH_API swh_status swh_grav_pp_batch(swh_gspace *g, const swh_grav_params *G, int64_t *n_interactions);
+SWH_API swh_status swh_gspace_download(swh_gspace *g, void *gparts, const swh_gpart_layout *L,
+                               int on_device);
+SWH_API swh_status swh_gspace_sync(swh_gspace *g);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SWIFTHIP_H */

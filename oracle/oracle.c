@@ -1,0 +1,2188 @@
+/*
+ * oracle/oracle.c — TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C restatement of SWIFT's SPH density/gradient/force neighbour loops
+ * and leaf-leaf P2P gravity (reference: /root/reference @ SWIFT 0.9.0), used
+ * as the parity CHECKER for the HIP path and as the CPU baseline timer
+ * (bench.py cpu_baseline, kind "port"). Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load this library; the product
+ * (swift_subtask_dev_amd) never links or calls it.
+ *
+ * Compiled twice (oracle/Makefile):
+ *   ORACLE_F32 -> liboracle_f32.so, symbols orf_*: float arithmetic with the
+ *      reference's exact operation order, operating in place on the 160-byte
+ *      struct part (include/swift_compat.h). This is the faithful restatement.
+ *   ORACLE_F64 -> liboracle_f64.so, symbols ord_*: the same formulas with every
+ *      float temporary and accumulator promoted to double (constants keep the
+ *      reference's float values). This is the fp64 reference the GPU's fp64
+ *      path is compared with at ~float-ulp tolerance.
+ *
+ * Pinning (see DESIGN.md "Oracle"): the reference C build needs a generated
+ * config.h and an hdf5.h stand-in, so per the task rules it is treated as
+ * unbuildable here. The restatement is pinned by the reference's own tests:
+ *   - test27cells/test125cells/testActivePair/testPeriodicBC structure: sorted
+ *     DOSELF/DOPAIR loops vs brute force under tests/tolerance_*.dat;
+ *   - testPotentialSelf/testPotentialPair analytic KATs (rel 1e-6 / 2e-6);
+ *   - testSymmetry identity (symmetric iact == two non-symmetric iacts);
+ *   - test125cells analytic fields (get_solution: rho, div_v, a_hydro);
+ *   - reference-run values recorded in SURVEY.md (kernel_root 0.418429,
+ *     kernel_norm 25.492, sizeof(struct part)=160, 47.82 directed density
+ *     interactions per particle on the perturbed-lattice recipe).
+ */
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "swift_compat.h"
+
+#if defined(ORACLE_F64)
+typedef double real;
+#define PFX(name) ord_##name
+#define SQRT sqrt
+#define FABS fabs
+#define EXP exp
+#else
+#define ORACLE_F32 1
+typedef float real;
+#define PFX(name) orf_##name
+#define SQRT sqrtf
+#define FABS fabsf
+#define EXP expf
+#endif
+
+#define API __attribute__((visibility("default")))
+
+static inline real rmax(real a, real b) { return a > b ? a : b; }
+static inline real rmin(real a, real b) { return a < b ? a : b; }
+
+/* ======================================================================== */
+/* Constants — restated from src/kernel_hydro.h:45-64,195-241 (cubic spline,
+ * 3D), src/dimension.h:40-43, src/adiabatic_index.h:43-44,
+ * src/hydro/SPHENIX/hydro_parameters.h:53. Same C expressions, so the float
+ * values are bit-identical to the reference macros.                         */
+/* ======================================================================== */
+#define kernel_degree 3
+#define kernel_ivals 2
+#define kernel_gamma ((float)(1.825742))
+#define kernel_constant ((float)(16. * M_1_PI))
+#define kernel_gamma_inv ((float)(1. / kernel_gamma))
+#define kernel_gamma2 ((float)(kernel_gamma * kernel_gamma))
+#define kernel_gamma_dim ((float)(kernel_gamma * kernel_gamma * kernel_gamma))
+#define kernel_gamma_inv_dim \
+  ((float)(1. / (kernel_gamma * kernel_gamma * kernel_gamma)))
+#define kernel_gamma_inv_dim_plus_one \
+  ((float)(1. / (kernel_gamma * kernel_gamma * kernel_gamma * kernel_gamma)))
+#define kernel_ivals_f ((float)(kernel_ivals))
+static const float kernel_coeffs[(kernel_degree + 1) * (kernel_ivals + 1)] = {
+    3.f, -3.f, 0.f, 0.5f, -1.f, 3.f, -3.f, 1.f, 0.f, 0.f, 0.f, 0.f};
+#define kernel_root \
+  ((float)(kernel_coeffs[kernel_degree]) * kernel_constant * kernel_gamma_inv_dim)
+#define hydro_dimension 3.f
+#define hydro_dimension_inv 0.3333333333f
+#define hydro_dimension_unit_sphere ((float)(4. * M_PI / 3.))
+#define kernel_norm ((float)(hydro_dimension_unit_sphere * kernel_gamma_dim))
+#define hydro_gamma 1.66666666666666667f
+#define hydro_gamma_minus_one 0.66666666666666667f
+#define const_viscosity_beta 3.0f
+
+API float PFX(kernel_root)(void) { return kernel_root; }
+API float PFX(kernel_norm)(void) { return kernel_norm; }
+API float PFX(kernel_gamma)(void) { return kernel_gamma; }
+
+static inline real pow_dimension(real x) { return x * x * x; }
+static inline real pow_dimension_plus_one(real x) {
+  const real x2 = x * x;
+  return x2 * x2;
+}
+static inline real pow_dimension_minus_one(real x) { return x * x; }
+
+/* src/kernel_hydro.h:257-284 */
+static inline void kernel_deval(real u, real *W, real *dW_dx) {
+  const real x = u * (real)kernel_gamma_inv;
+  const int temp = (int)(x * (real)kernel_ivals_f);
+  const int ind = temp > kernel_ivals ? kernel_ivals : temp;
+  const float *const coeffs = &kernel_coeffs[ind * (kernel_degree + 1)];
+  real w = (real)coeffs[0] * x + (real)coeffs[1];
+  real dw_dx = (real)coeffs[0];
+  for (int k = 2; k <= kernel_degree; k++) {
+    dw_dx = dw_dx * x + w;
+    w = x * w + (real)coeffs[k];
+  }
+  w = rmax(w, (real)0);
+  dw_dx = rmin(dw_dx, (real)0);
+  *W = w * (real)kernel_constant * (real)kernel_gamma_inv_dim;
+  *dW_dx = dw_dx * (real)kernel_constant * (real)kernel_gamma_inv_dim_plus_one;
+}
+
+API void PFX(kernel_deval)(real u, real *W, real *dW) { kernel_deval(u, W, dW); }
+
+/* ======================================================================== */
+/* Oracle particle record. In the f32 build it IS the ABI struct part; in   */
+/* the f64 build every float field is promoted to double (x is double in    */
+/* both, as in the reference).                                              */
+/* ======================================================================== */
+#ifdef ORACLE_F32
+typedef struct part opart;
+#else
+typedef struct opart {
+  long long id;
+  double x[3];
+  real v[3];
+  real a_hydro[3];
+  real mass, h, u, u_dt, rho;
+  struct {
+    real div_v, div_v_dt, div_v_previous_step, alpha, v_sig;
+  } viscosity;
+  struct {
+    real laplace_u, alpha;
+  } diffusion;
+  union {
+    struct {
+      real wcount, wcount_dh, rho_dh, rot_v[3];
+    } density;
+    struct {
+      real f, pressure, soundspeed, h_dt, balsara, alpha_visc_max_ngb;
+    } force;
+  };
+  timebin_t time_bin;
+  struct {
+    timebin_t min_ngb_time_bin;
+  } limiter_data;
+} opart;
+#endif
+
+/* Which union member is live when converting f64 records <-> ABI parts. */
+enum { PHASE_DENSITY = 0, PHASE_FORCE = 1 };
+
+static void part_to_opart(const struct part *p, opart *o, int phase) {
+#ifdef ORACLE_F32
+  (void)phase;
+  *o = *p;
+#else
+  o->id = p->id;
+  for (int k = 0; k < 3; k++) {
+    o->x[k] = p->x[k];
+    o->v[k] = p->v[k];
+    o->a_hydro[k] = p->a_hydro[k];
+  }
+  o->mass = p->mass; o->h = p->h; o->u = p->u; o->u_dt = p->u_dt; o->rho = p->rho;
+  o->viscosity.div_v = p->viscosity.div_v;
+  o->viscosity.div_v_dt = p->viscosity.div_v_dt;
+  o->viscosity.div_v_previous_step = p->viscosity.div_v_previous_step;
+  o->viscosity.alpha = p->viscosity.alpha;
+  o->viscosity.v_sig = p->viscosity.v_sig;
+  o->diffusion.laplace_u = p->diffusion.laplace_u;
+  o->diffusion.alpha = p->diffusion.alpha;
+  if (phase == PHASE_DENSITY) {
+    o->density.wcount = p->density.wcount;
+    o->density.wcount_dh = p->density.wcount_dh;
+    o->density.rho_dh = p->density.rho_dh;
+    for (int k = 0; k < 3; k++) o->density.rot_v[k] = p->density.rot_v[k];
+  } else {
+    o->force.f = p->force.f;
+    o->force.pressure = p->force.pressure;
+    o->force.soundspeed = p->force.soundspeed;
+    o->force.h_dt = p->force.h_dt;
+    o->force.balsara = p->force.balsara;
+    o->force.alpha_visc_max_ngb = p->force.alpha_visc_max_ngb;
+  }
+  o->time_bin = p->time_bin;
+  o->limiter_data.min_ngb_time_bin = p->limiter_data.min_ngb_time_bin;
+#endif
+}
+
+static void opart_to_part(const opart *o, struct part *p, int phase) {
+#ifdef ORACLE_F32
+  (void)phase;
+  *p = *o;
+#else
+  for (int k = 0; k < 3; k++) {
+    p->v[k] = (float)o->v[k];
+    p->a_hydro[k] = (float)o->a_hydro[k];
+  }
+  p->h = (float)o->h; p->u = (float)o->u; p->u_dt = (float)o->u_dt;
+  p->rho = (float)o->rho;
+  p->viscosity.div_v = (float)o->viscosity.div_v;
+  p->viscosity.div_v_dt = (float)o->viscosity.div_v_dt;
+  p->viscosity.div_v_previous_step = (float)o->viscosity.div_v_previous_step;
+  p->viscosity.alpha = (float)o->viscosity.alpha;
+  p->viscosity.v_sig = (float)o->viscosity.v_sig;
+  p->diffusion.laplace_u = (float)o->diffusion.laplace_u;
+  p->diffusion.alpha = (float)o->diffusion.alpha;
+  if (phase == PHASE_DENSITY) {
+    p->density.wcount = (float)o->density.wcount;
+    p->density.wcount_dh = (float)o->density.wcount_dh;
+    p->density.rho_dh = (float)o->density.rho_dh;
+    for (int k = 0; k < 3; k++) p->density.rot_v[k] = (float)o->density.rot_v[k];
+  } else {
+    p->force.f = (float)o->force.f;
+    p->force.pressure = (float)o->force.pressure;
+    p->force.soundspeed = (float)o->force.soundspeed;
+    p->force.h_dt = (float)o->force.h_dt;
+    p->force.balsara = (float)o->force.balsara;
+    p->force.alpha_visc_max_ngb = (float)o->force.alpha_visc_max_ngb;
+  }
+  p->limiter_data.min_ngb_time_bin = o->limiter_data.min_ngb_time_bin;
+#endif
+}
+
+static inline int part_is_active(const opart *p, timebin_t max_active_bin) {
+  return p->time_bin <= max_active_bin; /* src/active.h:357-373 */
+}
+static inline int part_is_inhibited(const opart *p) {
+  return p->time_bin == time_bin_inhibited; /* src/active.h */
+}
+
+/* ======================================================================== */
+/* SPHENIX interaction functions — src/hydro/SPHENIX/hydro_iact.h.          */
+/* a=1,H=0-independent except where the reference uses them.                */
+/* ======================================================================== */
+
+/* hydro_iact.h:46-116 */
+static inline void iact_density(real r2, const real dx[3], real hi, real hj,
+                                opart *pi, opart *pj, real a, real H) {
+  (void)a; (void)H;
+  real wi, wj, wi_dx, wj_dx, dv[3], curlvr[3];
+  const real r = SQRT(r2);
+  const real mi = pi->mass, mj = pj->mass;
+  const real hi_inv = (real)1 / hi;
+  const real ui = r * hi_inv;
+  kernel_deval(ui, &wi, &wi_dx);
+  pi->rho += mj * wi;
+  pi->density.rho_dh -= mj * ((real)hydro_dimension * wi + ui * wi_dx);
+  pi->density.wcount += wi;
+  pi->density.wcount_dh -= ((real)hydro_dimension * wi + ui * wi_dx);
+  const real hj_inv = (real)1 / hj;
+  const real uj = r * hj_inv;
+  kernel_deval(uj, &wj, &wj_dx);
+  pj->rho += mi * wj;
+  pj->density.rho_dh -= mi * ((real)hydro_dimension * wj + uj * wj_dx);
+  pj->density.wcount += wj;
+  pj->density.wcount_dh -= ((real)hydro_dimension * wj + uj * wj_dx);
+  const real r_inv = r ? (real)1 / r : (real)0;
+  const real faci = mj * wi_dx * r_inv;
+  const real facj = mi * wj_dx * r_inv;
+  dv[0] = pi->v[0] - pj->v[0];
+  dv[1] = pi->v[1] - pj->v[1];
+  dv[2] = pi->v[2] - pj->v[2];
+  const real dvdr = dv[0] * dx[0] + dv[1] * dx[1] + dv[2] * dx[2];
+  pi->viscosity.div_v -= faci * dvdr;
+  pj->viscosity.div_v -= facj * dvdr;
+  curlvr[0] = dv[1] * dx[2] - dv[2] * dx[1];
+  curlvr[1] = dv[2] * dx[0] - dv[0] * dx[2];
+  curlvr[2] = dv[0] * dx[1] - dv[1] * dx[0];
+  pi->density.rot_v[0] += faci * curlvr[0];
+  pi->density.rot_v[1] += faci * curlvr[1];
+  pi->density.rot_v[2] += faci * curlvr[2];
+  pj->density.rot_v[0] += facj * curlvr[0];
+  pj->density.rot_v[1] += facj * curlvr[1];
+  pj->density.rot_v[2] += facj * curlvr[2];
+}
+
+/* hydro_iact.h:130-178 */
+static inline void iact_nonsym_density(real r2, const real dx[3], real hi,
+                                       real hj, opart *pi, const opart *pj,
+                                       real a, real H) {
+  (void)hj; (void)a; (void)H;
+  real wi, wi_dx, dv[3], curlvr[3];
+  const real mj = pj->mass;
+  const real r = SQRT(r2);
+  const real h_inv = (real)1 / hi;
+  const real ui = r * h_inv;
+  kernel_deval(ui, &wi, &wi_dx);
+  pi->rho += mj * wi;
+  pi->density.rho_dh -= mj * ((real)hydro_dimension * wi + ui * wi_dx);
+  pi->density.wcount += wi;
+  pi->density.wcount_dh -= ((real)hydro_dimension * wi + ui * wi_dx);
+  const real r_inv = r ? (real)1 / r : (real)0;
+  const real faci = mj * wi_dx * r_inv;
+  dv[0] = pi->v[0] - pj->v[0];
+  dv[1] = pi->v[1] - pj->v[1];
+  dv[2] = pi->v[2] - pj->v[2];
+  const real dvdr = dv[0] * dx[0] + dv[1] * dx[1] + dv[2] * dx[2];
+  pi->viscosity.div_v -= faci * dvdr;
+  curlvr[0] = dv[1] * dx[2] - dv[2] * dx[1];
+  curlvr[1] = dv[2] * dx[0] - dv[0] * dx[2];
+  curlvr[2] = dv[0] * dx[1] - dv[1] * dx[0];
+  pi->density.rot_v[0] += faci * curlvr[0];
+  pi->density.rot_v[1] += faci * curlvr[1];
+  pi->density.rot_v[2] += faci * curlvr[2];
+}
+
+/* src/hydro/SPHENIX/hydro.h:490-498 (via src/signal_velocity.h) */
+static inline real signal_velocity(const opart *pi, const opart *pj, real mu_ij,
+                                   real beta) {
+  return pi->force.soundspeed + pj->force.soundspeed - beta * mu_ij;
+}
+
+/* hydro_iact.h:196-257 */
+static inline void iact_gradient(real r2, const real dx[3], real hi, real hj,
+                                 opart *pi, opart *pj, real a, real H) {
+  const real r = SQRT(r2);
+  const real r_inv = r ? (real)1 / r : (real)0;
+  const real fac_mu = (real)1; /* pow_three_gamma_minus_five_over_two, gamma=5/3 */
+  const real a2_Hubble = a * a * H;
+  const real dvdr = (pi->v[0] - pj->v[0]) * dx[0] + (pi->v[1] - pj->v[1]) * dx[1] +
+                    (pi->v[2] - pj->v[2]) * dx[2];
+  const real dvdr_Hubble = dvdr + a2_Hubble * r2;
+  const real omega_ij = rmin(dvdr_Hubble, (real)0);
+  const real mu_ij = fac_mu * r_inv * omega_ij;
+  const real new_v_sig = signal_velocity(pi, pj, mu_ij, (real)const_viscosity_beta);
+  pi->viscosity.v_sig = rmax(pi->viscosity.v_sig, new_v_sig);
+  pj->viscosity.v_sig = rmax(pj->viscosity.v_sig, new_v_sig);
+  real wi, wi_dx, wj, wj_dx;
+  const real ui = r / hi;
+  const real uj = r / hj;
+  kernel_deval(ui, &wi, &wi_dx);
+  kernel_deval(uj, &wj, &wj_dx);
+  const real delta_u_factor = (pi->u - pj->u) * r_inv;
+  pi->diffusion.laplace_u += pj->mass * delta_u_factor * wi_dx / pj->rho;
+  pj->diffusion.laplace_u -= pi->mass * delta_u_factor * wj_dx / pi->rho;
+  const real alpha_i = pi->viscosity.alpha;
+  const real alpha_j = pj->viscosity.alpha;
+  pi->force.alpha_visc_max_ngb = rmax(pi->force.alpha_visc_max_ngb, alpha_j);
+  pj->force.alpha_visc_max_ngb = rmax(pj->force.alpha_visc_max_ngb, alpha_i);
+}
+
+/* hydro_iact.h:276-329 */
+static inline void iact_nonsym_gradient(real r2, const real dx[3], real hi,
+                                        real hj, opart *pi, const opart *pj,
+                                        real a, real H) {
+  (void)hj;
+  const real r = SQRT(r2);
+  const real r_inv = r ? (real)1 / r : (real)0;
+  const real fac_mu = (real)1;
+  const real a2_Hubble = a * a * H;
+  const real dvdr = (pi->v[0] - pj->v[0]) * dx[0] + (pi->v[1] - pj->v[1]) * dx[1] +
+                    (pi->v[2] - pj->v[2]) * dx[2];
+  const real dvdr_Hubble = dvdr + a2_Hubble * r2;
+  const real omega_ij = rmin(dvdr_Hubble, (real)0);
+  const real mu_ij = fac_mu * r_inv * omega_ij;
+  const real new_v_sig = signal_velocity(pi, pj, mu_ij, (real)const_viscosity_beta);
+  pi->viscosity.v_sig = rmax(pi->viscosity.v_sig, new_v_sig);
+  real wi, wi_dx;
+  const real ui = r / hi;
+  kernel_deval(ui, &wi, &wi_dx);
+  const real delta_u_factor = (pi->u - pj->u) * r_inv;
+  pi->diffusion.laplace_u += pj->mass * delta_u_factor * wi_dx / pj->rho;
+  const real alpha_j = pj->viscosity.alpha;
+  pi->force.alpha_visc_max_ngb = rmax(pi->force.alpha_visc_max_ngb, alpha_j);
+}
+
+/* hydro_iact.h:343-474 */
+static inline void iact_force(real r2, const real dx[3], real hi, real hj,
+                              opart *pi, opart *pj, real a, real H) {
+  const real fac_mu = (real)1;
+  const real a2_Hubble = a * a * H;
+  const real r = SQRT(r2);
+  const real r_inv = r ? (real)1 / r : (real)0;
+  const real mj = pj->mass, mi = pi->mass;
+  const real rhoi = pi->rho, rhoj = pj->rho;
+  const real pressurei = pi->force.pressure, pressurej = pj->force.pressure;
+  const real hi_inv = (real)1 / hi;
+  const real hid_inv = pow_dimension_plus_one(hi_inv);
+  const real xi = r * hi_inv;
+  real wi, wi_dx;
+  kernel_deval(xi, &wi, &wi_dx);
+  const real wi_dr = hid_inv * wi_dx;
+  const real hj_inv = (real)1 / hj;
+  const real hjd_inv = pow_dimension_plus_one(hj_inv);
+  const real xj = r * hj_inv;
+  real wj, wj_dx;
+  kernel_deval(xj, &wj, &wj_dx);
+  const real wj_dr = hjd_inv * wj_dx;
+  const real dvdr = (pi->v[0] - pj->v[0]) * dx[0] + (pi->v[1] - pj->v[1]) * dx[1] +
+                    (pi->v[2] - pj->v[2]) * dx[2];
+  const real dvdr_Hubble = dvdr + a2_Hubble * r2;
+  const real omega_ij = rmin(dvdr_Hubble, (real)0);
+  const real mu_ij = fac_mu * r_inv * omega_ij;
+  const real v_sig = signal_velocity(pi, pj, mu_ij, (real)const_viscosity_beta);
+  const real f_ij = (real)1 - pi->force.f / mj;
+  const real f_ji = (real)1 - pj->force.f / mi;
+  const real balsara_i = pi->force.balsara, balsara_j = pj->force.balsara;
+  const real rho_ij = rhoi + rhoj;
+  const real alpha = pi->viscosity.alpha + pj->viscosity.alpha;
+  const real visc =
+      (real)-0.25f * alpha * v_sig * mu_ij * (balsara_i + balsara_j) / rho_ij;
+  const real visc_acc_term = (real)0.5f * visc * (wi_dr * f_ij + wj_dr * f_ji) * r_inv;
+  const real P_over_rho2_i = pressurei / (rhoi * rhoi) * f_ij;
+  const real P_over_rho2_j = pressurej / (rhoj * rhoj) * f_ji;
+  const real sph_acc_term = (P_over_rho2_i * wi_dr + P_over_rho2_j * wj_dr) * r_inv;
+  const real acc = sph_acc_term + visc_acc_term;
+  pi->a_hydro[0] -= mj * acc * dx[0];
+  pi->a_hydro[1] -= mj * acc * dx[1];
+  pi->a_hydro[2] -= mj * acc * dx[2];
+  pj->a_hydro[0] += mi * acc * dx[0];
+  pj->a_hydro[1] += mi * acc * dx[1];
+  pj->a_hydro[2] += mi * acc * dx[2];
+  const real sph_du_term_i = P_over_rho2_i * dvdr * r_inv * wi_dr;
+  const real sph_du_term_j = P_over_rho2_j * dvdr * r_inv * wj_dr;
+  const real visc_du_term = (real)0.5f * visc_acc_term * dvdr_Hubble;
+  const real alpha_diff =
+      (pressurei * pi->diffusion.alpha + pressurej * pj->diffusion.alpha) /
+      (pressurei + pressurej);
+  const real v_diff = alpha_diff * (real)0.5f *
+                      (SQRT((real)2.f * FABS(pressurei - pressurej) / rho_ij) +
+                       FABS(fac_mu * r_inv * dvdr_Hubble));
+  const real diff_du_term =
+      v_diff * (pi->u - pj->u) * (f_ij * wi_dr / rhoi + f_ji * wj_dr / rhoj);
+  const real du_dt_i = sph_du_term_i + visc_du_term + diff_du_term;
+  const real du_dt_j = sph_du_term_j + visc_du_term - diff_du_term;
+  pi->u_dt += du_dt_i * mj;
+  pj->u_dt += du_dt_j * mi;
+  pi->force.h_dt -= mj * dvdr * r_inv / rhoj * wi_dr;
+  pj->force.h_dt -= mi * dvdr * r_inv / rhoi * wj_dr;
+}
+
+/* hydro_iact.h:488-609 */
+static inline void iact_nonsym_force(real r2, const real dx[3], real hi, real hj,
+                                     opart *pi, const opart *pj, real a, real H) {
+  const real fac_mu = (real)1;
+  const real a2_Hubble = a * a * H;
+  const real r = SQRT(r2);
+  const real r_inv = r ? (real)1 / r : (real)0;
+  const real mi = pi->mass, mj = pj->mass;
+  const real rhoi = pi->rho, rhoj = pj->rho;
+  const real pressurei = pi->force.pressure, pressurej = pj->force.pressure;
+  const real hi_inv = (real)1 / hi;
+  const real hid_inv = pow_dimension_plus_one(hi_inv);
+  const real xi = r * hi_inv;
+  real wi, wi_dx;
+  kernel_deval(xi, &wi, &wi_dx);
+  const real wi_dr = hid_inv * wi_dx;
+  const real hj_inv = (real)1 / hj;
+  const real hjd_inv = pow_dimension_plus_one(hj_inv);
+  const real xj = r * hj_inv;
+  real wj, wj_dx;
+  kernel_deval(xj, &wj, &wj_dx);
+  const real wj_dr = hjd_inv * wj_dx;
+  const real dvdr = (pi->v[0] - pj->v[0]) * dx[0] + (pi->v[1] - pj->v[1]) * dx[1] +
+                    (pi->v[2] - pj->v[2]) * dx[2];
+  const real dvdr_Hubble = dvdr + a2_Hubble * r2;
+  const real omega_ij = rmin(dvdr_Hubble, (real)0);
+  const real mu_ij = fac_mu * r_inv * omega_ij;
+  const real v_sig = signal_velocity(pi, pj, mu_ij, (real)const_viscosity_beta);
+  const real f_ij = (real)1 - pi->force.f / mj;
+  const real f_ji = (real)1 - pj->force.f / mi;
+  const real balsara_i = pi->force.balsara, balsara_j = pj->force.balsara;
+  const real rho_ij = rhoi + rhoj;
+  const real alpha = pi->viscosity.alpha + pj->viscosity.alpha;
+  const real visc =
+      (real)-0.25f * alpha * v_sig * mu_ij * (balsara_i + balsara_j) / rho_ij;
+  const real visc_acc_term = (real)0.5f * visc * (wi_dr * f_ij + wj_dr * f_ji) * r_inv;
+  const real P_over_rho2_i = pressurei / (rhoi * rhoi) * f_ij;
+  const real P_over_rho2_j = pressurej / (rhoj * rhoj) * f_ji;
+  const real sph_acc_term = (P_over_rho2_i * wi_dr + P_over_rho2_j * wj_dr) * r_inv;
+  const real acc = sph_acc_term + visc_acc_term;
+  pi->a_hydro[0] -= mj * acc * dx[0];
+  pi->a_hydro[1] -= mj * acc * dx[1];
+  pi->a_hydro[2] -= mj * acc * dx[2];
+  const real sph_du_term_i = P_over_rho2_i * dvdr * r_inv * wi_dr;
+  const real visc_du_term = (real)0.5f * visc_acc_term * dvdr_Hubble;
+  const real alpha_diff =
+      (pressurei * pi->diffusion.alpha + pressurej * pj->diffusion.alpha) /
+      (pressurei + pressurej);
+  const real v_diff = alpha_diff * (real)0.5f *
+                      (SQRT((real)2.f * FABS(pressurei - pressurej) / rho_ij) +
+                       FABS(fac_mu * r_inv * dvdr_Hubble));
+  const real diff_du_term =
+      v_diff * (pi->u - pj->u) * (f_ij * wi_dr / rhoi + f_ji * wj_dr / rhoj);
+  const real du_dt_i = sph_du_term_i + visc_du_term + diff_du_term;
+  pi->u_dt += du_dt_i * mj;
+  pi->force.h_dt -= mj * dvdr * r_inv / rhoj * wi_dr;
+}
+
+/* src/timestep_limiter_iact.h:34-66 */
+static inline void iact_timebin(opart *pi, opart *pj) {
+  if (pj->time_bin > 0 && pj->time_bin < pi->limiter_data.min_ngb_time_bin)
+    pi->limiter_data.min_ngb_time_bin = pj->time_bin;
+  if (pi->time_bin > 0 && pi->time_bin < pj->limiter_data.min_ngb_time_bin)
+    pj->limiter_data.min_ngb_time_bin = pi->time_bin;
+}
+static inline void iact_nonsym_timebin(opart *pi, const opart *pj) {
+  if (pj->time_bin > 0 && pj->time_bin < pi->limiter_data.min_ngb_time_bin)
+    pi->limiter_data.min_ngb_time_bin = pj->time_bin;
+}
+
+/* Exported single-interaction entry points (testSymmetry-style checks). */
+API void PFX(iact_density)(real r2, const real *dx, real hi, real hj, opart *pi,
+                           opart *pj, real a, real H) {
+  iact_density(r2, dx, hi, hj, pi, pj, a, H);
+}
+API void PFX(iact_nonsym_density)(real r2, const real *dx, real hi, real hj,
+                                  opart *pi, const opart *pj, real a, real H) {
+  iact_nonsym_density(r2, dx, hi, hj, pi, pj, a, H);
+}
+API void PFX(iact_force)(real r2, const real *dx, real hi, real hj, opart *pi,
+                         opart *pj, real a, real H) {
+  iact_force(r2, dx, hi, hj, pi, pj, a, H);
+}
+API void PFX(iact_nonsym_force)(real r2, const real *dx, real hi, real hj,
+                                opart *pi, const opart *pj, real a, real H) {
+  iact_nonsym_force(r2, dx, hi, hj, pi, pj, a, H);
+}
+API void PFX(iact_gradient)(real r2, const real *dx, real hi, real hj, opart *pi,
+                            opart *pj, real a, real H) {
+  iact_gradient(r2, dx, hi, hj, pi, pj, a, H);
+}
+API void PFX(iact_nonsym_gradient)(real r2, const real *dx, real hi, real hj,
+                                   opart *pi, const opart *pj, real a, real H) {
+  iact_nonsym_gradient(r2, dx, hi, hj, pi, pj, a, H);
+}
+
+/* ======================================================================== */
+/* Per-particle operations — src/hydro/SPHENIX/hydro.h                      */
+/* ======================================================================== */
+
+/* The engine-side scalars the particle ops read (plain POD for ctypes). */
+struct oracle_params {
+  double a, H, a2_inv, a_factor_sound_speed, a_factor_Balsara_eps;
+  double time_base;
+  float eta_neighbours, h_tolerance, h_max, h_min;
+  int max_smoothing_iterations;
+  int use_mass_weighted_num_ngb;
+  float visc_alpha, visc_alpha_max, visc_alpha_min, visc_length;
+  float diff_alpha, diff_beta, diff_alpha_max, diff_alpha_min;
+  int max_active_bin;
+  int periodic;
+  double dim[3];
+};
+
+/* hydro.h:553-566 */
+static inline void hydro_init_part(opart *p) {
+  p->density.wcount = 0;
+  p->density.wcount_dh = 0;
+  p->rho = 0;
+  p->density.rho_dh = 0;
+  p->density.rot_v[0] = 0;
+  p->density.rot_v[1] = 0;
+  p->density.rot_v[2] = 0;
+  p->viscosity.div_v = 0;
+  p->diffusion.laplace_u = 0;
+}
+
+/* hydro.h:599-630 */
+static inline void hydro_end_density(opart *p, const struct oracle_params *P) {
+  const real h = p->h;
+  const real h_inv = (real)1 / h;
+  const real h_inv_dim = pow_dimension(h_inv);
+  const real h_inv_dim_plus_one = h_inv_dim * h_inv;
+  p->rho += p->mass * (real)kernel_root;
+  p->density.rho_dh -= (real)hydro_dimension * p->mass * (real)kernel_root;
+  p->density.wcount += (real)kernel_root;
+  p->density.wcount_dh -= (real)hydro_dimension * (real)kernel_root;
+  p->rho *= h_inv_dim;
+  p->density.rho_dh *= h_inv_dim_plus_one;
+  p->density.wcount *= h_inv_dim;
+  p->density.wcount_dh *= h_inv_dim_plus_one;
+  const real rho_inv = (real)1 / p->rho;
+  const real a_inv2 = (real)P->a2_inv;
+  p->density.rot_v[0] *= h_inv_dim_plus_one * a_inv2 * rho_inv;
+  p->density.rot_v[1] *= h_inv_dim_plus_one * a_inv2 * rho_inv;
+  p->density.rot_v[2] *= h_inv_dim_plus_one * a_inv2 * rho_inv;
+  p->viscosity.div_v *= h_inv_dim_plus_one * rho_inv * a_inv2;
+  p->viscosity.div_v += (real)P->H * (real)hydro_dimension;
+}
+
+/* src/equation_of_state/ideal_gas/equation_of_state.h:121,164 */
+static inline real gas_pressure_from_internal_energy(real density, real u) {
+  return (real)hydro_gamma_minus_one * u * density;
+}
+static inline real gas_soundspeed_from_pressure(real density, real Pr) {
+  return SQRT((real)hydro_gamma * Pr / density);
+}
+
+/* hydro.h:654-717 */
+static inline void hydro_prepare_gradient(opart *p, const struct oracle_params *P) {
+  const real fac_B = (real)P->a_factor_Balsara_eps;
+  const real curl_v = SQRT(p->density.rot_v[0] * p->density.rot_v[0] +
+                           p->density.rot_v[1] * p->density.rot_v[1] +
+                           p->density.rot_v[2] * p->density.rot_v[2]);
+  const real abs_div_v = FABS(p->viscosity.div_v);
+  const real pressure = gas_pressure_from_internal_energy(p->rho, p->u);
+  const real soundspeed = gas_soundspeed_from_pressure(p->rho, pressure);
+  const real balsara =
+      abs_div_v / (abs_div_v + curl_v + (real)0.0001f * soundspeed * fac_B / p->h);
+  const real common_factor = p->h * (real)hydro_dimension_inv / p->density.wcount;
+  real grad_h_term;
+  if (p->h > (real)0.9999f * (real)P->h_max) {
+    grad_h_term = 0;
+  } else {
+    const real grad_W_term = common_factor * p->density.wcount_dh;
+    if (grad_W_term < (real)-0.9999f)
+      grad_h_term = 0;
+    else
+      grad_h_term = common_factor * p->density.rho_dh / ((real)1 + grad_W_term);
+  }
+  p->force.f = grad_h_term;
+  p->force.pressure = pressure;
+  p->force.soundspeed = soundspeed;
+  p->force.balsara = balsara;
+}
+
+/* hydro.h:728-733 */
+static inline void hydro_reset_gradient(opart *p) {
+  p->viscosity.v_sig = (real)2 * p->force.soundspeed;
+  p->force.alpha_visc_max_ngb = p->viscosity.alpha;
+}
+
+/* hydro.h:745-757 */
+static inline void hydro_end_gradient(opart *p) {
+  const real h = p->h;
+  const real h_inv = (real)1 / h;
+  const real h_inv_dim = pow_dimension(h_inv);
+  const real h_inv_dim_plus_one = h_inv_dim * h_inv;
+  p->diffusion.laplace_u *= (real)2 * h_inv_dim_plus_one;
+}
+
+/* hydro.h:774-802 */
+static inline void hydro_part_has_no_neighbours(opart *p) {
+  const real h = p->h;
+  const real h_inv = (real)1 / h;
+  const real h_inv_dim = pow_dimension(h_inv);
+  p->rho = p->mass * (real)kernel_root * h_inv_dim;
+  p->viscosity.v_sig = 0;
+  p->density.wcount = (real)kernel_root * h_inv_dim;
+  p->density.rho_dh = 0;
+  p->density.wcount_dh = 0;
+  p->density.rot_v[0] = 0;
+  p->density.rot_v[1] = 0;
+  p->density.rot_v[2] = 0;
+  p->viscosity.div_v = 0;
+  p->diffusion.laplace_u = 0;
+}
+
+/* hydro.h:823-934 */
+static inline void hydro_prepare_force(opart *p, const struct oracle_params *P,
+                                       real dt_alpha) {
+  const real kernel_support_physical = p->h * (real)P->a * (real)kernel_gamma;
+  const real kernel_support_physical_inv = (real)1 / kernel_support_physical;
+  const real v_sig_physical = p->viscosity.v_sig * (real)P->a_factor_sound_speed;
+  const real pressure = gas_pressure_from_internal_energy(p->rho, p->u);
+  const real soundspeed_physical =
+      gas_soundspeed_from_pressure(p->rho, pressure) * (real)P->a_factor_sound_speed;
+  const real sound_crossing_time_inverse =
+      soundspeed_physical * kernel_support_physical_inv;
+  const real div_v_dt =
+      dt_alpha == (real)0
+          ? (real)0
+          : (p->viscosity.div_v - p->viscosity.div_v_previous_step) / dt_alpha;
+  const real S = p->viscosity.div_v < (real)0
+                     ? kernel_support_physical * kernel_support_physical *
+                           rmax((real)0, (real)-1 * div_v_dt)
+                     : (real)0;
+  const real soundspeed_square = soundspeed_physical * soundspeed_physical;
+  const real alpha_loc = (real)P->visc_alpha_max * S / (soundspeed_square + S);
+  if (alpha_loc > p->viscosity.alpha) {
+    p->viscosity.alpha = alpha_loc;
+  } else {
+    const real timescale_ratio =
+        dt_alpha * sound_crossing_time_inverse * (real)P->visc_length;
+    p->viscosity.alpha += alpha_loc * timescale_ratio;
+    p->viscosity.alpha /= ((real)1 + timescale_ratio);
+  }
+  p->viscosity.alpha = rmax(p->viscosity.alpha, (real)P->visc_alpha_min);
+  p->viscosity.div_v_previous_step = p->viscosity.div_v;
+  p->viscosity.div_v_dt = div_v_dt;
+  const real diffusion_timescale_physical_inverse =
+      v_sig_physical * kernel_support_physical_inv;
+  const real sqrt_u_inv = (real)1 / SQRT(p->u);
+  real alpha_diff_dt = (real)P->diff_beta * kernel_support_physical *
+                       p->diffusion.laplace_u * (real)P->a_factor_sound_speed *
+                       sqrt_u_inv * (real)P->a2_inv;
+  alpha_diff_dt -= (p->diffusion.alpha - (real)P->diff_alpha_min) *
+                   diffusion_timescale_physical_inverse;
+  real new_diffusion_alpha = p->diffusion.alpha;
+  new_diffusion_alpha += alpha_diff_dt * dt_alpha;
+  new_diffusion_alpha = rmax(new_diffusion_alpha, (real)P->diff_alpha_min);
+  const real viscous_diffusion_limit =
+      (real)P->diff_alpha_max *
+      ((real)1 - p->force.alpha_visc_max_ngb / (real)P->visc_alpha_max);
+  new_diffusion_alpha = rmin(new_diffusion_alpha, viscous_diffusion_limit);
+  p->diffusion.alpha = new_diffusion_alpha;
+}
+
+/* hydro.h:944-955 + src/timestep_limiter.h:35-39 */
+static inline void hydro_reset_acceleration(opart *p) {
+  p->a_hydro[0] = 0;
+  p->a_hydro[1] = 0;
+  p->a_hydro[2] = 0;
+  p->u_dt = 0;
+  p->force.h_dt = 0;
+}
+static inline void timestep_limiter_prepare_force(opart *p) {
+  p->limiter_data.min_ngb_time_bin = num_time_bins + 1;
+}
+
+/* hydro.h:1080-1084 */
+static inline void hydro_end_force(opart *p) {
+  p->force.h_dt *= p->h * (real)hydro_dimension_inv;
+}
+
+/* src/timeline.h:56-61,91-95: non-cosmological dt of a time-bin */
+static inline double get_timestep(timebin_t bin, double time_base) {
+  if (bin <= 0) return 0.;
+  return (double)(1LL << (bin + 1)) * time_base;
+}
+
+/* ======================================================================== */
+/* Grid-gather box loops: for each active i, visit the grid cells that      */
+/* overlap [x_i - R, x_i + R] and apply the non-symmetric interaction with  */
+/* every in-range j (nearest periodic image, as tools.c pairs_all_* do).    */
+/* This is exactly the interaction set of all SWIFT density/force tasks of  */
+/* a step (each active i meets every j within H_i, resp. max(H_i, H_j)).    */
+/* ======================================================================== */
+struct ogrid {
+  int cdim[3];
+  double w[3];
+  int ncell;
+  int *start; /* ncell+1 */
+  int *index; /* particle indices sorted by cell */
+};
+
+static void ogrid_build(struct ogrid *g, const opart *parts, long long N,
+                        const double dim[3], double min_width) {
+  for (int k = 0; k < 3; k++) {
+    int c = (int)floor(dim[k] / min_width);
+    if (c < 1) c = 1;
+    if (c > 256) c = 256;
+    g->cdim[k] = c;
+    g->w[k] = dim[k] / c;
+  }
+  g->ncell = g->cdim[0] * g->cdim[1] * g->cdim[2];
+  g->start = (int *)calloc((size_t)g->ncell + 1, sizeof(int));
+  g->index = (int *)malloc(sizeof(int) * (size_t)(N > 0 ? N : 1));
+  int *cellof = (int *)malloc(sizeof(int) * (size_t)(N > 0 ? N : 1));
+  for (long long i = 0; i < N; i++) {
+    int c[3];
+    for (int k = 0; k < 3; k++) {
+      double xx = parts[i].x[k];
+      xx -= floor(xx / dim[k]) * dim[k];
+      c[k] = (int)(xx / g->w[k]);
+      if (c[k] >= g->cdim[k]) c[k] = g->cdim[k] - 1;
+      if (c[k] < 0) c[k] = 0;
+    }
+    cellof[i] = (c[2] * g->cdim[1] + c[1]) * g->cdim[0] + c[0];
+    g->start[cellof[i] + 1]++;
+  }
+  for (int c = 0; c < g->ncell; c++) g->start[c + 1] += g->start[c];
+  int *fill = (int *)malloc(sizeof(int) * (size_t)g->ncell);
+  memcpy(fill, g->start, sizeof(int) * (size_t)g->ncell);
+  for (long long i = 0; i < N; i++) g->index[fill[cellof[i]]++] = (int)i;
+  free(fill);
+  free(cellof);
+}
+
+static void ogrid_free(struct ogrid *g) {
+  free(g->start);
+  free(g->index);
+}
+
+/* src/periodic.h:66-72 */
+static inline double nearest(double dx, double box) {
+  return ((dx > 0.5 * box) ? (dx - box) : ((dx < -0.5 * box) ? (dx + box) : dx));
+}
+
+enum { LOOP_DENSITY = 0, LOOP_GRADIENT = 1, LOOP_FORCE = 2 };
+
+/* Gather for one i over the grid; returns the number of interactions. */
+static long long gather_one(opart *parts, const struct ogrid *g, long long i,
+                            int loop, double reach, const struct oracle_params *P) {
+  opart *pi = &parts[i];
+  const real hi = pi->h;
+  const real hig2 = hi * hi * (real)kernel_gamma2;
+  const real a = (real)P->a, Hc = (real)P->H;
+  long long n = 0;
+  int lo[3], hi_c[3];
+  for (int k = 0; k < 3; k++) {
+    double xx = pi->x[k];
+    if (P->periodic) xx -= floor(xx / P->dim[k]) * P->dim[k];
+    lo[k] = (int)floor((xx - reach) / g->w[k]);
+    hi_c[k] = (int)floor((xx + reach) / g->w[k]);
+    if (!P->periodic) {
+      if (lo[k] < 0) lo[k] = 0;
+      if (hi_c[k] > g->cdim[k] - 1) hi_c[k] = g->cdim[k] - 1;
+    } else if (hi_c[k] - lo[k] + 1 > g->cdim[k]) {
+      lo[k] = 0;
+      hi_c[k] = g->cdim[k] - 1;
+    }
+  }
+  for (int cz = lo[2]; cz <= hi_c[2]; cz++) {
+    const int wz = ((cz % g->cdim[2]) + g->cdim[2]) % g->cdim[2];
+    for (int cy = lo[1]; cy <= hi_c[1]; cy++) {
+      const int wy = ((cy % g->cdim[1]) + g->cdim[1]) % g->cdim[1];
+      for (int cx = lo[0]; cx <= hi_c[0]; cx++) {
+        const int wx = ((cx % g->cdim[0]) + g->cdim[0]) % g->cdim[0];
+        const int c = (wz * g->cdim[1] + wy) * g->cdim[0] + wx;
+        for (int q = g->start[c]; q < g->start[c + 1]; q++) {
+          const int j = g->index[q];
+          if (j == i) continue;
+          opart *pj = &parts[j];
+          if (part_is_inhibited(pj)) continue;
+          real dx[3];
+          real r2 = 0;
+          for (int k = 0; k < 3; k++) {
+            double d = pi->x[k] - pj->x[k];
+            if (P->periodic) d = nearest(d, P->dim[k]);
+            dx[k] = (real)d;
+            r2 += dx[k] * dx[k];
+          }
+          const real hj = pj->h;
+          if (loop == LOOP_FORCE) {
+            const real hjg2 = hj * hj * (real)kernel_gamma2;
+            if (r2 < hig2 || r2 < hjg2) {
+              iact_nonsym_force(r2, dx, hi, hj, pi, pj, a, Hc);
+              iact_nonsym_timebin(pi, pj);
+              n++;
+            }
+          } else if (r2 < hig2) {
+            if (loop == LOOP_DENSITY)
+              iact_nonsym_density(r2, dx, hi, hj, pi, pj, a, Hc);
+            else
+              iact_nonsym_gradient(r2, dx, hi, hj, pi, pj, a, Hc);
+            n++;
+          }
+        }
+      }
+    }
+  }
+  return n;
+}
+
+/* Convert the ABI array to oracle records (no-op view in the f32 build). */
+static opart *to_oparts(struct part *parts, long long N, int phase) {
+#ifdef ORACLE_F32
+  (void)N; (void)phase;
+  return parts;
+#else
+  opart *o = (opart *)malloc(sizeof(opart) * (size_t)(N > 0 ? N : 1));
+  for (long long i = 0; i < N; i++) part_to_opart(&parts[i], &o[i], phase);
+  return o;
+#endif
+}
+static void from_oparts(opart *o, struct part *parts, long long N, int phase) {
+#ifdef ORACLE_F32
+  (void)o; (void)parts; (void)N; (void)phase;
+#else
+  for (long long i = 0; i < N; i++) opart_to_part(&o[i], &parts[i], phase);
+  free(o);
+#endif
+}
+
+static double max_h(const opart *o, long long N) {
+  double m = 0;
+  for (long long i = 0; i < N; i++)
+    if (!part_is_inhibited(&o[i]) && o[i].h > m) m = o[i].h;
+  return m;
+}
+
+/* Runs one loop over every active particle (subset = NULL) or over the
+ * index list `subset`. Per-particle interaction counts go to `counts`
+ * (optional). Returns the total number of directed interactions. */
+static long long box_loop(opart *o, long long N, const struct oracle_params *P,
+                          int loop, const int *subset, long long nsub,
+                          int *counts) {
+  const double hmax = max_h(o, N) * kernel_gamma;
+  struct ogrid g;
+  ogrid_build(&g, o, N, P->dim, hmax > 0 ? hmax : P->dim[0]);
+  const long long nit = subset ? nsub : N;
+  long long total = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : total)
+  for (long long t = 0; t < nit; t++) {
+    const long long i = subset ? subset[t] : t;
+    if (!part_is_active(&o[i], (timebin_t)P->max_active_bin)) continue;
+    if (part_is_inhibited(&o[i])) continue;
+    const double reach =
+        (loop == LOOP_FORCE) ? hmax : (double)o[i].h * kernel_gamma;
+    const long long n = gather_one(o, &g, i, loop, reach, P);
+    if (counts) counts[i] = (int)n;
+    total += n;
+  }
+  ogrid_free(&g);
+  return total;
+}
+
+/* Density loop over a periodic/non-periodic box (hydro_init_part is the
+ * caller's job, as in SWIFT where the drift/init precedes the loop). */
+API long long PFX(box_density)(struct part *parts, long long N,
+                               const struct oracle_params *P, int *counts) {
+  opart *o = to_oparts(parts, N, PHASE_DENSITY);
+  const long long n = box_loop(o, N, P, LOOP_DENSITY, NULL, 0, counts);
+  from_oparts(o, parts, N, PHASE_DENSITY);
+  return n;
+}
+
+API long long PFX(box_density_subset)(struct part *parts, long long N,
+                                      const struct oracle_params *P,
+                                      const int *subset, long long nsub) {
+  opart *o = to_oparts(parts, N, PHASE_DENSITY);
+  const long long n = box_loop(o, N, P, LOOP_DENSITY, subset, nsub, NULL);
+  from_oparts(o, parts, N, PHASE_DENSITY);
+  return n;
+}
+
+API long long PFX(box_gradient)(struct part *parts, long long N,
+                                const struct oracle_params *P, int *counts) {
+  opart *o = to_oparts(parts, N, PHASE_FORCE);
+  const long long n = box_loop(o, N, P, LOOP_GRADIENT, NULL, 0, counts);
+  from_oparts(o, parts, N, PHASE_FORCE);
+  return n;
+}
+
+API long long PFX(box_force)(struct part *parts, long long N,
+                             const struct oracle_params *P, int *counts) {
+  opart *o = to_oparts(parts, N, PHASE_FORCE);
+  const long long n = box_loop(o, N, P, LOOP_FORCE, NULL, 0, counts);
+  from_oparts(o, parts, N, PHASE_FORCE);
+  return n;
+}
+
+API void PFX(init_parts)(struct part *parts, long long N,
+                         const struct oracle_params *P) {
+  for (long long i = 0; i < N; i++) {
+    struct part *p = &parts[i];
+    if (p->time_bin > P->max_active_bin) continue;
+    p->density.wcount = 0.f;
+    p->density.wcount_dh = 0.f;
+    p->rho = 0.f;
+    p->density.rho_dh = 0.f;
+    p->density.rot_v[0] = p->density.rot_v[1] = p->density.rot_v[2] = 0.f;
+    p->viscosity.div_v = 0.f;
+    p->diffusion.laplace_u = 0.f;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Ghost: src/runner_ghost.c:1085-1596, SPHENIX branch (EXTRA_HYDRO_LOOP),   */
+/* non-cosmological, no mass-weighted neighbour number by default. The      */
+/* "subset reruns" of runner_ghost.c:1503-1546 become box_loop(subset).     */
+/* Returns the number of iterations; *n_failed = particles not converged.   */
+/* ------------------------------------------------------------------------ */
+API int PFX(box_ghost)(struct part *parts, long long N,
+                       const struct oracle_params *P, long long *n_failed) {
+  opart *o = to_oparts(parts, N, PHASE_DENSITY);
+  const real eps = (real)P->h_tolerance;
+  const real hydro_h_max = (real)P->h_max, hydro_h_min = (real)P->h_min;
+  const real eta = (real)P->eta_neighbours;
+  const real hydro_eta_dim = pow_dimension(eta);
+  int *pid = (int *)malloc(sizeof(int) * (size_t)(N > 0 ? N : 1));
+  real *left = (real *)malloc(sizeof(real) * (size_t)(N > 0 ? N : 1));
+  real *right = (real *)malloc(sizeof(real) * (size_t)(N > 0 ? N : 1));
+  long long count = 0;
+  for (long long k = 0; k < N; k++)
+    if (part_is_active(&o[k], (timebin_t)P->max_active_bin) &&
+        !part_is_inhibited(&o[k])) {
+      pid[count] = (int)k;
+      left[count] = 0;
+      right[count] = hydro_h_max;
+      count++;
+    }
+  int num_reruns;
+  for (num_reruns = 0; count > 0 && num_reruns < P->max_smoothing_iterations;
+       num_reruns++) {
+    long long redo = 0;
+    for (long long i = 0; i < count; i++) {
+      opart *p = &o[pid[i]];
+      const real h_old = p->h;
+      const real h_old_dim = pow_dimension(h_old);
+      const real h_old_dim_minus_one = pow_dimension_minus_one(h_old);
+      real h_new;
+      int has_no_neighbours = 0;
+      int done = 0;
+      if (p->density.wcount < (real)(1.e-5 * kernel_root)) {
+        has_no_neighbours = 1;
+        h_new = (real)2 * h_old;
+      } else {
+        hydro_end_density(p, P);
+        if (P->use_mass_weighted_num_ngb) {
+          const real inv_mass = (real)1 / p->mass;
+          p->density.wcount = p->rho * inv_mass;
+          p->density.wcount_dh = p->density.rho_dh * inv_mass;
+        }
+        const real n_sum = p->density.wcount * h_old_dim;
+        const real n_target = hydro_eta_dim;
+        const real f = n_sum - n_target;
+        const real f_prime = p->density.wcount_dh * h_old_dim +
+                             (real)hydro_dimension * p->density.wcount * h_old_dim_minus_one;
+        if (n_sum < n_target)
+          left[i] = rmax(left[i], h_old);
+        else if (n_sum > n_target)
+          right[i] = rmin(right[i], h_old);
+        if (((p->h >= hydro_h_max) && (f < (real)0)) ||
+            ((p->h <= hydro_h_min) && (f > (real)0))) {
+          done = 1; /* converged "by force": tidy up below */
+          h_new = h_old;
+        } else {
+          h_new = h_old - f / (f_prime + (real)FLT_MIN);
+          h_new = rmin(h_new, (real)2 * h_old);
+          h_new = rmax(h_new, (real)0.5f * h_old);
+          h_new = rmax(h_new, left[i]);
+          h_new = rmin(h_new, right[i]);
+        }
+      }
+      if (!done && FABS(h_new - h_old) > eps * h_old) {
+        if ((h_new == left[i] && h_old == right[i]) ||
+            (h_old == left[i] && h_new == right[i])) {
+#ifdef ORACLE_F32
+          p->h = cbrtf(0.5f * (pow_dimension(left[i]) + pow_dimension(right[i])));
+#else
+          p->h = cbrt(0.5 * (pow_dimension(left[i]) + pow_dimension(right[i])));
+#endif
+        } else {
+          p->h = h_new;
+        }
+        if (p->h < hydro_h_max && p->h > hydro_h_min) {
+          pid[redo] = pid[i];
+          left[redo] = left[i];
+          right[redo] = right[i];
+          redo++;
+          hydro_init_part(p);
+          continue;
+        } else if (p->h <= hydro_h_min) {
+          p->h = hydro_h_min;
+        } else if (p->h >= hydro_h_max) {
+          p->h = hydro_h_max;
+          if (has_no_neighbours) hydro_part_has_no_neighbours(p);
+        }
+      }
+      /* converged: prepare for the gradient loop (EXTRA_HYDRO_LOOP) */
+      hydro_prepare_gradient(p, P);
+      hydro_reset_gradient(p);
+    }
+    count = redo;
+    if (count > 0) box_loop(o, N, P, LOOP_DENSITY, pid, count, NULL);
+  }
+  if (n_failed) *n_failed = count;
+  free(pid);
+  free(left);
+  free(right);
+  /* After the ghost the force-side union members are live. */
+  from_oparts(o, parts, N, PHASE_FORCE);
+  return num_reruns;
+}
+
+/* runner_ghost.c:992-1083 (extra ghost) for every active particle */
+API void PFX(box_extra_ghost)(struct part *parts, long long N,
+                              const struct oracle_params *P) {
+  opart *o = to_oparts(parts, N, PHASE_FORCE);
+  for (long long i = 0; i < N; i++) {
+    opart *p = &o[i];
+    if (!part_is_active(p, (timebin_t)P->max_active_bin)) continue;
+    hydro_end_gradient(p);
+    const real dt_alpha = (real)get_timestep(p->time_bin, P->time_base);
+    hydro_prepare_force(p, P, dt_alpha);
+    timestep_limiter_prepare_force(p);
+    hydro_reset_acceleration(p);
+  }
+  from_oparts(o, parts, N, PHASE_FORCE);
+}
+
+/* src/runner_others.c:618 -> hydro_end_force */
+API void PFX(box_end_force)(struct part *parts, long long N,
+                            const struct oracle_params *P) {
+  opart *o = to_oparts(parts, N, PHASE_FORCE);
+  for (long long i = 0; i < N; i++)
+    if (part_is_active(&o[i], (timebin_t)P->max_active_bin)) hydro_end_force(&o[i]);
+  from_oparts(o, parts, N, PHASE_FORCE);
+}
+
+/* Exact count of directed in-range pairs (density: r < H_i; force:
+ * r < max(H_i, H_j)), active i only. Used as the metric's denominator. */
+API long long PFX(box_count_pairs)(struct part *parts, long long N,
+                                   const struct oracle_params *P, int force) {
+  opart *o = to_oparts(parts, N, PHASE_DENSITY);
+  const double hmax = max_h(o, N) * kernel_gamma;
+  struct ogrid g;
+  ogrid_build(&g, o, N, P->dim, hmax > 0 ? hmax : P->dim[0]);
+  long long total = 0;
+#pragma omp parallel for schedule(dynamic, 1024) reduction(+ : total)
+  for (long long i = 0; i < N; i++) {
+    const opart *pi = &o[i];
+    if (!part_is_active(pi, (timebin_t)P->max_active_bin)) continue;
+    const real hig2 = pi->h * pi->h * (real)kernel_gamma2;
+    const double reach = force ? hmax : (double)pi->h * kernel_gamma;
+    int lo[3], hc[3];
+    for (int k = 0; k < 3; k++) {
+      double xx = pi->x[k];
+      if (P->periodic) xx -= floor(xx / P->dim[k]) * P->dim[k];
+      lo[k] = (int)floor((xx - reach) / g.w[k]);
+      hc[k] = (int)floor((xx + reach) / g.w[k]);
+      if (!P->periodic) {
+        if (lo[k] < 0) lo[k] = 0;
+        if (hc[k] > g.cdim[k] - 1) hc[k] = g.cdim[k] - 1;
+      } else if (hc[k] - lo[k] + 1 > g.cdim[k]) {
+        lo[k] = 0;
+        hc[k] = g.cdim[k] - 1;
+      }
+    }
+    for (int cz = lo[2]; cz <= hc[2]; cz++)
+      for (int cy = lo[1]; cy <= hc[1]; cy++)
+        for (int cx = lo[0]; cx <= hc[0]; cx++) {
+          const int c = ((((cz % g.cdim[2]) + g.cdim[2]) % g.cdim[2]) * g.cdim[1] +
+                         (((cy % g.cdim[1]) + g.cdim[1]) % g.cdim[1])) * g.cdim[0] +
+                        (((cx % g.cdim[0]) + g.cdim[0]) % g.cdim[0]);
+          for (int q = g.start[c]; q < g.start[c + 1]; q++) {
+            const int j = g.index[q];
+            if (j == i) continue;
+            const opart *pj = &o[j];
+            real r2 = 0;
+            for (int k = 0; k < 3; k++) {
+              double d = pi->x[k] - pj->x[k];
+              if (P->periodic) d = nearest(d, P->dim[k]);
+              const real dd = (real)d;
+              r2 += dd * dd;
+            }
+            const real hjg2 = pj->h * pj->h * (real)kernel_gamma2;
+            if (r2 < hig2 || (force && r2 < hjg2)) total++;
+          }
+        }
+  }
+  ogrid_free(&g);
+#ifndef ORACLE_F32
+  free(o);
+#endif
+  return total;
+}
+
+#ifdef ORACLE_F32
+/* ======================================================================== */
+/* Cell-task loops (faithful float restatement of                          */
+/* src/runner_doiact_functions_hydro.h). These operate on SWIFT-style cells */
+/* (include/swift_compat.h) exactly as the runner does, including sorted    */
+/* pseudo-Verlet windows, activity masks and the ci/cj swap of              */
+/* space_getsid.                                                            */
+/* ======================================================================== */
+
+/* src/sort_part.h:42-92 */
+static const double runner_shift[13][3] = {
+    {5.773502691896258e-01, 5.773502691896258e-01, 5.773502691896258e-01},
+    {7.071067811865475e-01, 7.071067811865475e-01, 0.0},
+    {5.773502691896258e-01, 5.773502691896258e-01, -5.773502691896258e-01},
+    {7.071067811865475e-01, 0.0, 7.071067811865475e-01},
+    {1.0, 0.0, 0.0},
+    {7.071067811865475e-01, 0.0, -7.071067811865475e-01},
+    {5.773502691896258e-01, -5.773502691896258e-01, 5.773502691896258e-01},
+    {7.071067811865475e-01, -7.071067811865475e-01, 0.0},
+    {5.773502691896258e-01, -5.773502691896258e-01, -5.773502691896258e-01},
+    {0.0, 7.071067811865475e-01, 7.071067811865475e-01},
+    {0.0, 1.0, 0.0},
+    {0.0, 7.071067811865475e-01, -7.071067811865475e-01},
+    {0.0, 0.0, 1.0},
+};
+static const int runner_flip[27] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0,
+                                    0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+static const int sortlistID[27] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 0,
+                                   12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0};
+#define space_maxreldx 0.1f /* src/space.h:66 */
+
+static int cmp_sort_entry(const void *a, const void *b) {
+  const struct sort_entry *x = (const struct sort_entry *)a;
+  const struct sort_entry *y = (const struct sort_entry *)b;
+  if (x->d < y->d) return -1;
+  if (x->d > y->d) return 1;
+  return (x->i < y->i) ? -1 : (x->i > y->i);
+}
+
+/* src/runner_sort.c:352-391 (leaf branch): project on the 13 axes, add the
+ * FLT_MAX sentinel, sort ascending. Storage: caller-owned per-cell lists. */
+API void orf_cell_sort(struct cell *c, int flags) {
+  const int count = c->hydro.count;
+  for (int j = 0; j < 13; j++) {
+    if (!(flags & (1 << j))) continue;
+    if (c->hydro.sort[j] == NULL)
+      c->hydro.sort[j] =
+          (struct sort_entry *)malloc(sizeof(struct sort_entry) * (size_t)(count + 1));
+    struct sort_entry *e = c->hydro.sort[j];
+    for (int k = 0; k < count; k++) {
+      const double *px = c->hydro.parts[k].x;
+      e[k].i = k;
+      e[k].d = px[0] * runner_shift[j][0] + px[1] * runner_shift[j][1] +
+               px[2] * runner_shift[j][2];
+    }
+    e[count].d = FLT_MAX;
+    e[count].i = 0;
+    qsort(e, (size_t)count, sizeof(struct sort_entry), cmp_sort_entry);
+    c->hydro.sorted |= (uint16_t)(1 << j);
+  }
+  c->hydro.dx_max_sort = 0.f;
+  c->hydro.dx_max_sort_old = 0.f;
+}
+
+API void orf_cell_free_sorts(struct cell *c) {
+  for (int j = 0; j < 13; j++) {
+    free(c->hydro.sort[j]);
+    c->hydro.sort[j] = NULL;
+  }
+  c->hydro.sorted = 0;
+}
+
+/* src/space_getsid.h:46-82 */
+static int space_getsid(const struct space *s, struct cell **ci, struct cell **cj,
+                        double shift[3]) {
+  const int periodic = s->periodic;
+  double dx[3];
+  for (int k = 0; k < 3; k++) {
+    dx[k] = (*cj)->loc[k] - (*ci)->loc[k];
+    if (periodic && dx[k] < -s->dim[k] / 2)
+      shift[k] = s->dim[k];
+    else if (periodic && dx[k] > s->dim[k] / 2)
+      shift[k] = -s->dim[k];
+    else
+      shift[k] = 0.0;
+    dx[k] += shift[k];
+  }
+  int sid = 0;
+  for (int k = 0; k < 3; k++)
+    sid = 3 * sid + ((dx[k] < 0.0) ? 0 : ((dx[k] > 0.0) ? 2 : 1));
+  if (runner_flip[sid]) {
+    struct cell *temp = *ci;
+    *ci = *cj;
+    *cj = temp;
+    for (int k = 0; k < 3; k++) shift[k] = -shift[k];
+  }
+  return sortlistID[sid];
+}
+
+static inline int cell_is_active_hydro(const struct cell *c, const struct engine *e) {
+  return c->hydro.ti_end_min == e->ti_current; /* src/active.h:176-190 */
+}
+
+#define PA(p) part_is_active((p), e->max_active_bin)
+
+/* DOPAIR1, runner_doiact_functions_hydro.h:1068-1320; loop = density or
+ * gradient (both use the r < H_i criterion). */
+static void dopair1(const struct engine *e, struct cell *ci, struct cell *cj,
+                    const int sid, const double *shift, int loop) {
+  const float a = (float)e->cosmology->a, H = (float)e->cosmology->H;
+  double rshift = 0.0;
+  for (int k = 0; k < 3; k++) rshift += shift[k] * runner_shift[sid][k];
+  const struct sort_entry *sort_i = cell_get_hydro_sorts(ci, sid);
+  const struct sort_entry *sort_j = cell_get_hydro_sorts(cj, sid);
+  const double hi_max = ci->hydro.h_max * kernel_gamma - rshift;
+  const double hj_max = cj->hydro.h_max * kernel_gamma;
+  const int count_i = ci->hydro.count, count_j = cj->hydro.count;
+  struct part *parts_i = ci->hydro.parts, *parts_j = cj->hydro.parts;
+  const double di_max = sort_i[count_i - 1].d - rshift;
+  const double dj_min = sort_j[0].d;
+  const float dx_max = (ci->hydro.dx_max_sort + cj->hydro.dx_max_sort);
+
+  if (cell_is_active_hydro(ci, e)) {
+    for (int pid = count_i - 1;
+         pid >= 0 && sort_i[pid].d + hi_max + dx_max > dj_min; pid--) {
+      struct part *pi = &parts_i[sort_i[pid].i];
+      const float hi = pi->h;
+      if (!PA(pi)) continue;
+      const double di = sort_i[pid].d + hi * kernel_gamma + dx_max - rshift;
+      if (di < dj_min) continue;
+      const float hig2 = hi * hi * kernel_gamma2;
+      const float pix = pi->x[0] - (cj->loc[0] + shift[0]);
+      const float piy = pi->x[1] - (cj->loc[1] + shift[1]);
+      const float piz = pi->x[2] - (cj->loc[2] + shift[2]);
+      for (int pjd = 0; pjd < count_j && sort_j[pjd].d < di; pjd++) {
+        struct part *pj = &parts_j[sort_j[pjd].i];
+        if (part_is_inhibited(pj)) continue;
+        const float hj = pj->h;
+        const float pjx = pj->x[0] - cj->loc[0];
+        const float pjy = pj->x[1] - cj->loc[1];
+        const float pjz = pj->x[2] - cj->loc[2];
+        float dx[3] = {pix - pjx, piy - pjy, piz - pjz};
+        const float r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+        if (r2 < hig2) {
+          if (loop == LOOP_DENSITY)
+            iact_nonsym_density(r2, dx, hi, hj, pi, pj, a, H);
+          else
+            iact_nonsym_gradient(r2, dx, hi, hj, pi, pj, a, H);
+        }
+      }
+    }
+  }
+  if (cell_is_active_hydro(cj, e)) {
+    for (int pjd = 0; pjd < count_j && sort_j[pjd].d - hj_max - dx_max < di_max;
+         pjd++) {
+      struct part *pj = &parts_j[sort_j[pjd].i];
+      const float hj = pj->h;
+      if (!PA(pj)) continue;
+      const double dj = sort_j[pjd].d - hj * kernel_gamma - dx_max + rshift;
+      if (dj - rshift > di_max) continue;
+      const float hjg2 = hj * hj * kernel_gamma2;
+      const float pjx = pj->x[0] - cj->loc[0];
+      const float pjy = pj->x[1] - cj->loc[1];
+      const float pjz = pj->x[2] - cj->loc[2];
+      for (int pid = count_i - 1; pid >= 0 && sort_i[pid].d > dj; pid--) {
+        struct part *pi = &parts_i[sort_i[pid].i];
+        if (part_is_inhibited(pi)) continue;
+        const float hi = pi->h;
+        const float pix = pi->x[0] - (cj->loc[0] + shift[0]);
+        const float piy = pi->x[1] - (cj->loc[1] + shift[1]);
+        const float piz = pi->x[2] - (cj->loc[2] + shift[2]);
+        float dx[3] = {pjx - pix, pjy - piy, pjz - piz};
+        const float r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+        if (r2 < hjg2) {
+          if (loop == LOOP_DENSITY)
+            iact_nonsym_density(r2, dx, hj, hi, pj, pi, a, H);
+          else
+            iact_nonsym_gradient(r2, dx, hj, hi, pj, pi, a, H);
+        }
+      }
+    }
+  }
+}
+
+/* DOSELF1, runner_doiact_functions_hydro.h:2062-2261 */
+static void doself1(const struct engine *e, struct cell *c, int loop) {
+  const float a = (float)e->cosmology->a, H = (float)e->cosmology->H;
+  struct part *parts = c->hydro.parts;
+  const int count = c->hydro.count;
+  int *indt = (int *)malloc(sizeof(int) * (size_t)(count > 0 ? count : 1));
+  int countdt = 0, firstdt = 0;
+  for (int k = 0; k < count; k++)
+    if (PA(&parts[k])) indt[countdt++] = k;
+  for (int pid = 0; pid < count; pid++) {
+    struct part *pi = &parts[pid];
+    if (part_is_inhibited(pi)) continue;
+    double pix[3];
+    for (int k = 0; k < 3; k++) pix[k] = pi->x[k];
+    const float hi = pi->h;
+    const float hig2 = hi * hi * kernel_gamma2;
+    if (!PA(pi)) {
+      for (int pjd = firstdt; pjd < countdt; pjd++) {
+        struct part *pj = &parts[indt[pjd]];
+        const float hj = pj->h;
+        float r2 = 0.0f;
+        float dx[3];
+        for (int k = 0; k < 3; k++) {
+          dx[k] = pj->x[k] - pix[k];
+          r2 += dx[k] * dx[k];
+        }
+        if (r2 < hj * hj * kernel_gamma2) {
+          if (loop == LOOP_DENSITY)
+            iact_nonsym_density(r2, dx, hj, hi, pj, pi, a, H);
+          else
+            iact_nonsym_gradient(r2, dx, hj, hi, pj, pi, a, H);
+        }
+      }
+    } else {
+      firstdt += 1;
+      for (int pjd = pid + 1; pjd < count; pjd++) {
+        struct part *pj = &parts[pjd];
+        if (part_is_inhibited(pj)) continue;
+        const float hj = pj->h;
+        float r2 = 0.0f;
+        float dx[3];
+        for (int k = 0; k < 3; k++) {
+          dx[k] = pix[k] - pj->x[k];
+          r2 += dx[k] * dx[k];
+        }
+        const int doj = (PA(pj)) && (r2 < hj * hj * kernel_gamma2);
+        const int doi = (r2 < hig2);
+        if (doi || doj) {
+          if (doi && doj) {
+            if (loop == LOOP_DENSITY)
+              iact_density(r2, dx, hi, hj, pi, pj, a, H);
+            else
+              iact_gradient(r2, dx, hi, hj, pi, pj, a, H);
+          } else if (doi) {
+            if (loop == LOOP_DENSITY)
+              iact_nonsym_density(r2, dx, hi, hj, pi, pj, a, H);
+            else
+              iact_nonsym_gradient(r2, dx, hi, hj, pi, pj, a, H);
+          } else if (doj) {
+            dx[0] = -dx[0];
+            dx[1] = -dx[1];
+            dx[2] = -dx[2];
+            if (loop == LOOP_DENSITY)
+              iact_nonsym_density(r2, dx, hj, hi, pj, pi, a, H);
+            else
+              iact_nonsym_gradient(r2, dx, hj, hi, pj, pi, a, H);
+          }
+        }
+      }
+    }
+  }
+  free(indt);
+}
+
+/* DOPAIR2, runner_doiact_functions_hydro.h:1424-1961 (force) */
+static void dopair2(const struct engine *e, struct cell *ci, struct cell *cj,
+                    const int sid, const double *shift) {
+  const float a = (float)e->cosmology->a, H = (float)e->cosmology->H;
+  double rshift = 0.0;
+  for (int k = 0; k < 3; k++) rshift += shift[k] * runner_shift[sid][k];
+  struct sort_entry *sort_i = cell_get_hydro_sorts(ci, sid);
+  struct sort_entry *sort_j = cell_get_hydro_sorts(cj, sid);
+  const double hi_max = ci->hydro.h_max, hj_max = cj->hydro.h_max;
+  const int count_i = ci->hydro.count, count_j = cj->hydro.count;
+  struct part *parts_i = ci->hydro.parts, *parts_j = cj->hydro.parts;
+  const double dx_max = (ci->hydro.dx_max_sort + cj->hydro.dx_max_sort);
+  const double di_max = sort_i[count_i - 1].d;
+  const double dj_min = sort_j[0].d;
+  const double shift_i[3] = {cj->loc[0] + shift[0], cj->loc[1] + shift[1],
+                             cj->loc[2] + shift[2]};
+  const double shift_j[3] = {cj->loc[0], cj->loc[1], cj->loc[2]};
+  int count_active_i = 0, count_active_j = 0;
+  struct sort_entry *sort_active_i = NULL, *sort_active_j = NULL;
+  if (cell_is_active_hydro(ci, e)) {
+    sort_active_i = (struct sort_entry *)malloc(sizeof(struct sort_entry) * (size_t)count_i);
+    for (int k = 0; k < count_i; k++)
+      if (PA(&parts_i[sort_i[k].i])) sort_active_i[count_active_i++] = sort_i[k];
+  }
+  if (cell_is_active_hydro(cj, e)) {
+    sort_active_j = (struct sort_entry *)malloc(sizeof(struct sort_entry) * (size_t)count_j);
+    for (int k = 0; k < count_j; k++)
+      if (PA(&parts_j[sort_j[k].i])) sort_active_j[count_active_j++] = sort_j[k];
+  }
+  for (int pid = count_i - 1;
+       pid >= 0 && sort_i[pid].d + hi_max * kernel_gamma + dx_max - rshift > dj_min;
+       pid--) {
+    struct part *pi = &parts_i[sort_i[pid].i];
+    if (part_is_inhibited(pi)) continue;
+    const float hi = pi->h;
+    const double di = sort_i[pid].d + hi * kernel_gamma + dx_max - rshift;
+    if (di < dj_min) continue;
+    const float hig2 = hi * hi * kernel_gamma2;
+    const float pix = pi->x[0] - shift_i[0];
+    const float piy = pi->x[1] - shift_i[1];
+    const float piz = pi->x[2] - shift_i[2];
+    if (!PA(pi)) {
+      for (int pjd = 0; pjd < count_active_j && sort_active_j[pjd].d < di; pjd++) {
+        struct part *pj = &parts_j[sort_active_j[pjd].i];
+        if (part_is_inhibited(pj)) continue;
+        const float hj = pj->h;
+        const float pjx = pj->x[0] - shift_j[0];
+        const float pjy = pj->x[1] - shift_j[1];
+        const float pjz = pj->x[2] - shift_j[2];
+        const float dx[3] = {pjx - pix, pjy - piy, pjz - piz};
+        const float r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+        if (r2 < hig2) {
+          iact_nonsym_force(r2, dx, hj, hi, pj, pi, a, H);
+          iact_nonsym_timebin(pj, pi);
+        }
+      }
+    } else {
+      for (int pjd = 0; pjd < count_j && sort_j[pjd].d < di; pjd++) {
+        struct part *pj = &parts_j[sort_j[pjd].i];
+        if (part_is_inhibited(pj)) continue;
+        const float hj = pj->h;
+        const float pjx = pj->x[0] - shift_j[0];
+        const float pjy = pj->x[1] - shift_j[1];
+        const float pjz = pj->x[2] - shift_j[2];
+        const float dx[3] = {pix - pjx, piy - pjy, piz - pjz};
+        const float r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+        if (r2 < hig2) {
+          if (PA(pj)) {
+            iact_force(r2, dx, hi, hj, pi, pj, a, H);
+            iact_timebin(pi, pj);
+          } else {
+            iact_nonsym_force(r2, dx, hi, hj, pi, pj, a, H);
+            iact_nonsym_timebin(pi, pj);
+          }
+        }
+      }
+    }
+  }
+  for (int pjd = 0;
+       pjd < count_j && sort_j[pjd].d - hj_max * kernel_gamma - dx_max < di_max - rshift;
+       pjd++) {
+    struct part *pj = &parts_j[sort_j[pjd].i];
+    if (part_is_inhibited(pj)) continue;
+    const float hj = pj->h;
+    const double dj = sort_j[pjd].d - hj * kernel_gamma - dx_max;
+    if (dj > di_max - rshift) continue;
+    const float hjg2 = hj * hj * kernel_gamma2;
+    const float pjx = pj->x[0] - shift_j[0];
+    const float pjy = pj->x[1] - shift_j[1];
+    const float pjz = pj->x[2] - shift_j[2];
+    if (!PA(pj)) {
+      for (int pid = count_active_i - 1;
+           pid >= 0 && sort_active_i[pid].d - rshift > dj; pid--) {
+        struct part *pi = &parts_i[sort_active_i[pid].i];
+        if (part_is_inhibited(pi)) continue;
+        const float hi = pi->h;
+        const float hig2 = hi * hi * kernel_gamma2;
+        const float pix = pi->x[0] - shift_i[0];
+        const float piy = pi->x[1] - shift_i[1];
+        const float piz = pi->x[2] - shift_i[2];
+        const float dx[3] = {pix - pjx, piy - pjy, piz - pjz};
+        const float r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+        if (r2 < hjg2 && r2 >= hig2) {
+          iact_nonsym_force(r2, dx, hi, hj, pi, pj, a, H);
+          iact_nonsym_timebin(pi, pj);
+        }
+      }
+    } else {
+      for (int pid = count_i - 1; pid >= 0 && sort_i[pid].d - rshift > dj; pid--) {
+        struct part *pi = &parts_i[sort_i[pid].i];
+        if (part_is_inhibited(pi)) continue;
+        const float hi = pi->h;
+        const float hig2 = hi * hi * kernel_gamma2;
+        const float pix = pi->x[0] - shift_i[0];
+        const float piy = pi->x[1] - shift_i[1];
+        const float piz = pi->x[2] - shift_i[2];
+        const float dx[3] = {pjx - pix, pjy - piy, pjz - piz};
+        const float r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+        if (r2 < hjg2 && r2 >= hig2) {
+          if (PA(pi)) {
+            iact_force(r2, dx, hj, hi, pj, pi, a, H);
+            iact_timebin(pj, pi);
+          } else {
+            iact_nonsym_force(r2, dx, hj, hi, pj, pi, a, H);
+            iact_nonsym_timebin(pj, pi);
+          }
+        }
+      }
+    }
+  }
+  free(sort_active_i);
+  free(sort_active_j);
+}
+
+/* DOSELF2, runner_doiact_functions_hydro.h:2304-2476 (force) */
+static void doself2(const struct engine *e, struct cell *c) {
+  const float a = (float)e->cosmology->a, H = (float)e->cosmology->H;
+  struct part *parts = c->hydro.parts;
+  const int count = c->hydro.count;
+  int *indt = (int *)malloc(sizeof(int) * (size_t)(count > 0 ? count : 1));
+  int countdt = 0, firstdt = 0;
+  for (int k = 0; k < count; k++)
+    if (PA(&parts[k])) indt[countdt++] = k;
+  for (int pid = 0; pid < count; pid++) {
+    struct part *pi = &parts[pid];
+    if (part_is_inhibited(pi)) continue;
+    double pix[3];
+    for (int k = 0; k < 3; k++) pix[k] = pi->x[k];
+    const float hi = pi->h;
+    const float hig2 = hi * hi * kernel_gamma2;
+    if (!PA(pi)) {
+      for (int pjd = firstdt; pjd < countdt; pjd++) {
+        struct part *pj = &parts[indt[pjd]];
+        const float hj = pj->h;
+        float r2 = 0.0f;
+        float dx[3];
+        for (int k = 0; k < 3; k++) {
+          dx[k] = pj->x[k] - pix[k];
+          r2 += dx[k] * dx[k];
+        }
+        if (r2 < hig2 || r2 < hj * hj * kernel_gamma2) {
+          iact_nonsym_force(r2, dx, hj, hi, pj, pi, a, H);
+          iact_nonsym_timebin(pj, pi);
+        }
+      }
+    } else {
+      firstdt += 1;
+      for (int pjd = pid + 1; pjd < count; pjd++) {
+        struct part *pj = &parts[pjd];
+        if (part_is_inhibited(pj)) continue;
+        const float hj = pj->h;
+        float r2 = 0.0f;
+        float dx[3];
+        for (int k = 0; k < 3; k++) {
+          dx[k] = pix[k] - pj->x[k];
+          r2 += dx[k] * dx[k];
+        }
+        if (r2 < hig2 || r2 < hj * hj * kernel_gamma2) {
+          if (PA(pj)) {
+            iact_force(r2, dx, hi, hj, pi, pj, a, H);
+            iact_timebin(pi, pj);
+          } else {
+            iact_nonsym_force(r2, dx, hi, hj, pi, pj, a, H);
+            iact_nonsym_timebin(pi, pj);
+          }
+        }
+      }
+    }
+  }
+  free(indt);
+}
+
+static int check_pair(const struct engine *e, struct cell **ci, struct cell **cj,
+                      double shift[3], int *sid) {
+  if ((*ci)->hydro.count == 0 || (*cj)->hydro.count == 0) return 0;
+  if (!cell_is_active_hydro(*ci, e) && !cell_is_active_hydro(*cj, e)) return 0;
+  *sid = space_getsid(e->s, ci, cj, shift);
+  if (!((*ci)->hydro.sorted & (1 << *sid)) ||
+      (*ci)->hydro.dx_max_sort_old > space_maxreldx * (*ci)->dmin)
+    return -1;
+  if (!((*cj)->hydro.sorted & (1 << *sid)) ||
+      (*cj)->hydro.dx_max_sort_old > space_maxreldx * (*cj)->dmin)
+    return -1;
+  return 1;
+}
+
+/* DOPAIR1_BRANCH, runner_doiact_functions_hydro.h:1331-1413. Returns 0 on
+ * success, -1 for "Interacting unsorted cells". */
+API int orf_dopair1_branch(struct runner *r, struct cell *ci, struct cell *cj,
+                           int loop) {
+  double shift[3] = {0.0, 0.0, 0.0};
+  int sid;
+  const int ok = check_pair(r->e, &ci, &cj, shift, &sid);
+  if (ok <= 0) return ok;
+  dopair1(r->e, ci, cj, sid, shift, loop);
+  return 0;
+}
+API int orf_doself1_branch(struct runner *r, struct cell *c, int loop) {
+  const struct engine *e = r->e;
+  if (c->hydro.count == 0) return 0;
+  if (!cell_is_active_hydro(c, e)) return 0;
+  if (c->hydro.h_max_old * kernel_gamma > c->dmin) return -2;
+  doself1(e, c, loop);
+  return 0;
+}
+API int orf_dopair2_branch(struct runner *r, struct cell *ci, struct cell *cj) {
+  double shift[3] = {0.0, 0.0, 0.0};
+  int sid;
+  const int ok = check_pair(r->e, &ci, &cj, shift, &sid);
+  if (ok <= 0) return ok;
+  dopair2(r->e, ci, cj, sid, shift);
+  return 0;
+}
+API int orf_doself2_branch(struct runner *r, struct cell *c) {
+  const struct engine *e = r->e;
+  if (c->hydro.count == 0) return 0;
+  if (!cell_is_active_hydro(c, e)) return 0;
+  doself2(e, c);
+  return 0;
+}
+
+/* DOSELF_SUBSET, runner_doiact_functions_hydro.h:949-1036 (density) */
+API void orf_doself_subset(struct runner *r, struct cell *ci, struct part *parts,
+                           const int *ind, int count) {
+  const struct engine *e = r->e;
+  const float a = (float)e->cosmology->a, H = (float)e->cosmology->H;
+  const int count_i = ci->hydro.count;
+  struct part *parts_j = ci->hydro.parts;
+  for (int pid = 0; pid < count; pid++) {
+    struct part *pi = &parts[ind[pid]];
+    const float pix[3] = {(float)(pi->x[0] - ci->loc[0]), (float)(pi->x[1] - ci->loc[1]),
+                          (float)(pi->x[2] - ci->loc[2])};
+    const float hi = pi->h;
+    const float hig2 = hi * hi * kernel_gamma2;
+    for (int pjd = 0; pjd < count_i; pjd++) {
+      struct part *pj = &parts_j[pjd];
+      if (pi == pj) continue;
+      if (part_is_inhibited(pj)) continue;
+      const float hj = pj->h;
+      const float pjx[3] = {(float)(pj->x[0] - ci->loc[0]), (float)(pj->x[1] - ci->loc[1]),
+                            (float)(pj->x[2] - ci->loc[2])};
+      float dx[3] = {pix[0] - pjx[0], pix[1] - pjx[1], pix[2] - pjx[2]};
+      const float r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+      if (r2 < hig2) iact_nonsym_density(r2, dx, hi, hj, pi, pj, a, H);
+    }
+  }
+}
+
+/* DOPAIR_SUBSET_NAIVE semantics (runner_doiact_functions_hydro.h:608-694):
+ * every j of cj, periodic shift from the cell offsets. The sorted variant
+ * (710-870) visits a superset window of the same in-range set. */
+API void orf_dopair_subset(struct runner *r, struct cell *ci, struct part *parts_i,
+                           const int *ind, int count, struct cell *cj) {
+  const struct engine *e = r->e;
+  const float a = (float)e->cosmology->a, H = (float)e->cosmology->H;
+  if (cj->hydro.count == 0) return;
+  double shift[3] = {0.0, 0.0, 0.0};
+  for (int k = 0; k < 3; k++) {
+    if (cj->loc[k] - ci->loc[k] < -e->s->dim[k] / 2)
+      shift[k] = e->s->dim[k];
+    else if (cj->loc[k] - ci->loc[k] > e->s->dim[k] / 2)
+      shift[k] = -e->s->dim[k];
+  }
+  const int count_j = cj->hydro.count;
+  struct part *parts_j = cj->hydro.parts;
+  for (int pid = 0; pid < count; pid++) {
+    struct part *pi = &parts_i[ind[pid]];
+    const double pix = pi->x[0] - shift[0];
+    const double piy = pi->x[1] - shift[1];
+    const double piz = pi->x[2] - shift[2];
+    const float hi = pi->h;
+    const float hig2 = hi * hi * kernel_gamma2;
+    for (int pjd = 0; pjd < count_j; pjd++) {
+      struct part *pj = &parts_j[pjd];
+      if (part_is_inhibited(pj)) continue;
+      const float hj = pj->h;
+      float dx[3] = {(float)(pix - pj->x[0]), (float)(piy - pj->x[1]),
+                     (float)(piz - pj->x[2])};
+      const float r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+      if (r2 < hig2) iact_nonsym_density(r2, dx, hi, hj, pi, pj, a, H);
+    }
+  }
+}
+
+/* Brute-force oracles of the reference's tests, src/tools.c:198-700. */
+API void orf_pairs_all_density(struct runner *r, struct cell *ci, struct cell *cj) {
+  const struct engine *e = r->e;
+  const double dim[3] = {e->s->dim[0], e->s->dim[1], e->s->dim[2]};
+  const float a = (float)e->cosmology->a, H = (float)e->cosmology->H;
+  for (int i = 0; i < ci->hydro.count; ++i) {
+    struct part *pi = &ci->hydro.parts[i];
+    const float hi = pi->h, hig2 = hi * hi * kernel_gamma2;
+    if (!PA(pi)) continue;
+    for (int j = 0; j < cj->hydro.count; ++j) {
+      struct part *pj = &cj->hydro.parts[j];
+      float r2 = 0.0f, dx[3];
+      for (int k = 0; k < 3; k++) {
+        dx[k] = ci->hydro.parts[i].x[k] - cj->hydro.parts[j].x[k];
+        dx[k] = nearest(dx[k], dim[k]);
+        r2 += dx[k] * dx[k];
+      }
+      if (r2 < hig2 && !part_is_inhibited(pj))
+        iact_nonsym_density(r2, dx, hi, pj->h, pi, pj, a, H);
+    }
+  }
+  for (int j = 0; j < cj->hydro.count; ++j) {
+    struct part *pj = &cj->hydro.parts[j];
+    const float hj = pj->h, hjg2 = hj * hj * kernel_gamma2;
+    if (!PA(pj)) continue;
+    for (int i = 0; i < ci->hydro.count; ++i) {
+      struct part *pi = &ci->hydro.parts[i];
+      float r2 = 0.0f, dx[3];
+      for (int k = 0; k < 3; k++) {
+        dx[k] = cj->hydro.parts[j].x[k] - ci->hydro.parts[i].x[k];
+        dx[k] = nearest(dx[k], dim[k]);
+        r2 += dx[k] * dx[k];
+      }
+      if (r2 < hjg2 && !part_is_inhibited(pi))
+        iact_nonsym_density(r2, dx, hj, pi->h, pj, pi, a, H);
+    }
+  }
+}
+
+API void orf_self_all_density(struct runner *r, struct cell *ci) {
+  const struct engine *e = r->e;
+  const float a = (float)e->cosmology->a, H = (float)e->cosmology->H;
+  for (int i = 0; i < ci->hydro.count; ++i) {
+    struct part *pi = &ci->hydro.parts[i];
+    const float hi = pi->h, hig2 = hi * hi * kernel_gamma2;
+    for (int j = i + 1; j < ci->hydro.count; ++j) {
+      struct part *pj = &ci->hydro.parts[j];
+      const float hj = pj->h, hjg2 = hj * hj * kernel_gamma2;
+      float r2 = 0.0f, dxi[3];
+      for (int k = 0; k < 3; k++) {
+        dxi[k] = ci->hydro.parts[i].x[k] - ci->hydro.parts[j].x[k];
+        r2 += dxi[k] * dxi[k];
+      }
+      if (r2 < hig2 && PA(pi) && !part_is_inhibited(pj))
+        iact_nonsym_density(r2, dxi, hi, hj, pi, pj, a, H);
+      if (r2 < hjg2 && PA(pj) && !part_is_inhibited(pi)) {
+        dxi[0] = -dxi[0];
+        dxi[1] = -dxi[1];
+        dxi[2] = -dxi[2];
+        iact_nonsym_density(r2, dxi, hj, hi, pj, pi, a, H);
+      }
+    }
+  }
+}
+
+API void orf_pairs_all_force(struct runner *r, struct cell *ci, struct cell *cj) {
+  const struct engine *e = r->e;
+  const double dim[3] = {e->s->dim[0], e->s->dim[1], e->s->dim[2]};
+  const float a = (float)e->cosmology->a, H = (float)e->cosmology->H;
+  for (int i = 0; i < ci->hydro.count; ++i) {
+    struct part *pi = &ci->hydro.parts[i];
+    const float hi = pi->h, hig2 = hi * hi * kernel_gamma2;
+    if (!PA(pi)) continue;
+    for (int j = 0; j < cj->hydro.count; ++j) {
+      struct part *pj = &cj->hydro.parts[j];
+      const float hj = pj->h, hjg2 = hj * hj * kernel_gamma2;
+      float r2 = 0.0f, dx[3];
+      for (int k = 0; k < 3; k++) {
+        dx[k] = ci->hydro.parts[i].x[k] - cj->hydro.parts[j].x[k];
+        dx[k] = nearest(dx[k], dim[k]);
+        r2 += dx[k] * dx[k];
+      }
+      if (r2 < hig2 || r2 < hjg2) {
+        iact_nonsym_force(r2, dx, hi, hj, pi, pj, a, H);
+        iact_nonsym_timebin(pi, pj);
+      }
+    }
+  }
+  for (int j = 0; j < cj->hydro.count; ++j) {
+    struct part *pj = &cj->hydro.parts[j];
+    const float hj = pj->h, hjg2 = hj * hj * kernel_gamma2;
+    if (!PA(pj)) continue;
+    for (int i = 0; i < ci->hydro.count; ++i) {
+      struct part *pi = &ci->hydro.parts[i];
+      const float hi = pi->h, hig2 = hi * hi * kernel_gamma2;
+      float r2 = 0.0f, dx[3];
+      for (int k = 0; k < 3; k++) {
+        dx[k] = cj->hydro.parts[j].x[k] - ci->hydro.parts[i].x[k];
+        dx[k] = nearest(dx[k], dim[k]);
+        r2 += dx[k] * dx[k];
+      }
+      if (r2 < hjg2 || r2 < hig2) {
+        iact_nonsym_force(r2, dx, hj, hi, pj, pi, a, H);
+        iact_nonsym_timebin(pj, pi);
+      }
+    }
+  }
+}
+
+API void orf_self_all_force(struct runner *r, struct cell *ci) {
+  const struct engine *e = r->e;
+  const float a = (float)e->cosmology->a, H = (float)e->cosmology->H;
+  for (int i = 0; i < ci->hydro.count; ++i) {
+    struct part *pi = &ci->hydro.parts[i];
+    const float hi = pi->h, hig2 = hi * hi * kernel_gamma2;
+    for (int j = i + 1; j < ci->hydro.count; ++j) {
+      struct part *pj = &ci->hydro.parts[j];
+      const float hj = pj->h, hjg2 = hj * hj * kernel_gamma2;
+      float r2 = 0.0f, dxi[3];
+      for (int k = 0; k < 3; k++) {
+        dxi[k] = ci->hydro.parts[i].x[k] - ci->hydro.parts[j].x[k];
+        r2 += dxi[k] * dxi[k];
+      }
+      if (r2 < hig2 || r2 < hjg2) {
+        if (PA(pi) && PA(pj)) {
+          iact_force(r2, dxi, hi, hj, pi, pj, a, H);
+          iact_timebin(pi, pj);
+        } else if (PA(pi)) {
+          iact_nonsym_force(r2, dxi, hi, hj, pi, pj, a, H);
+          iact_nonsym_timebin(pi, pj);
+        } else if (PA(pj)) {
+          dxi[0] = -dxi[0];
+          dxi[1] = -dxi[1];
+          dxi[2] = -dxi[2];
+          iact_nonsym_force(r2, dxi, hj, hi, pj, pi, a, H);
+          iact_nonsym_timebin(pj, pi);
+        }
+      }
+    }
+  }
+}
+
+/* Per-particle ops exposed for the cell-level tests (test125cells chain). */
+API void orf_part_end_density(struct part *p, const struct oracle_params *P) {
+  hydro_end_density(p, P);
+}
+API void orf_part_prepare_gradient(struct part *p, const struct oracle_params *P) {
+  hydro_prepare_gradient(p, P);
+  hydro_reset_gradient(p);
+}
+API void orf_part_extra_ghost(struct part *p, const struct oracle_params *P) {
+  hydro_end_gradient(p);
+  hydro_prepare_force(p, P, (float)get_timestep(p->time_bin, P->time_base));
+  timestep_limiter_prepare_force(p);
+  hydro_reset_acceleration(p);
+}
+API void orf_part_end_force(struct part *p) { hydro_end_force(p); }
+API void orf_part_init(struct part *p) { hydro_init_part(p); }
+
+/* ------------------------------------------------------------------------ */
+/* CPU baseline: the float restatement of DOSELF1/DOPAIR1 (density) and     */
+/* DOSELF2/DOPAIR2 (force) over a periodic top-level cell grid, multi-      */
+/* threaded with conflict-free scheduling: all self tasks in parallel; then */
+/* for each of the 13 pair directions and each of the 8 parity classes of  */
+/* the left cell, all pairs in parallel (two pairs of one (direction,      */
+/* parity) group never share a cell when cdim is even).                    */
+/* ------------------------------------------------------------------------ */
+struct orf_cellgrid {
+  int cdim;
+  struct cell *cells;
+  struct part *parts; /* cell-ordered copy */
+  long long N;
+};
+
+static const int pair_dirs[13][3] = {{1, 1, 1}, {1, 1, 0}, {1, 1, -1}, {1, 0, 1},
+                                     {1, 0, 0}, {1, 0, -1}, {1, -1, 1}, {1, -1, 0},
+                                     {1, -1, -1}, {0, 1, 1}, {0, 1, 0}, {0, 1, -1},
+                                     {0, 0, 1}};
+
+/* Build a cdim^3 periodic grid of cells over a copy of the particles,
+ * sorted in all 13 directions. */
+API struct orf_cellgrid *orf_cellgrid_new(const struct part *parts, long long N,
+                                          double box, int cdim) {
+  struct orf_cellgrid *g = (struct orf_cellgrid *)calloc(1, sizeof(*g));
+  g->cdim = cdim;
+  g->N = N;
+  const int nc = cdim * cdim * cdim;
+  g->cells = (struct cell *)calloc((size_t)nc, sizeof(struct cell));
+  g->parts = (struct part *)aligned_alloc(32, sizeof(struct part) * (size_t)(N > 0 ? N : 1));
+  int *cnt = (int *)calloc((size_t)nc + 1, sizeof(int));
+  int *cof = (int *)malloc(sizeof(int) * (size_t)(N > 0 ? N : 1));
+  const double w = box / cdim;
+  for (long long i = 0; i < N; i++) {
+    int c[3];
+    for (int k = 0; k < 3; k++) {
+      double xx = parts[i].x[k] - floor(parts[i].x[k] / box) * box;
+      c[k] = (int)(xx / w);
+      if (c[k] >= cdim) c[k] = cdim - 1;
+    }
+    cof[i] = (c[0] * cdim + c[1]) * cdim + c[2];
+    cnt[cof[i] + 1]++;
+  }
+  for (int c = 0; c < nc; c++) cnt[c + 1] += cnt[c];
+  int *fill = (int *)malloc(sizeof(int) * (size_t)nc);
+  memcpy(fill, cnt, sizeof(int) * (size_t)nc);
+  for (long long i = 0; i < N; i++) g->parts[fill[cof[i]]++] = parts[i];
+  for (int cx = 0; cx < cdim; cx++)
+    for (int cy = 0; cy < cdim; cy++)
+      for (int cz = 0; cz < cdim; cz++) {
+        const int id = (cx * cdim + cy) * cdim + cz;
+        struct cell *c = &g->cells[id];
+        c->loc[0] = cx * w;
+        c->loc[1] = cy * w;
+        c->loc[2] = cz * w;
+        c->width[0] = c->width[1] = c->width[2] = w;
+        c->dmin = (float)w;
+        c->hydro.parts = g->parts + cnt[id];
+        c->hydro.count = cnt[id + 1] - cnt[id];
+        float hmax = 0.f;
+        for (int k = 0; k < c->hydro.count; k++)
+          if (c->hydro.parts[k].h > hmax) hmax = c->hydro.parts[k].h;
+        c->hydro.h_max = c->hydro.h_max_old = c->hydro.h_max_active = hmax;
+        c->hydro.ti_end_min = 8;
+        c->hydro.ti_old_part = 8;
+      }
+#pragma omp parallel for schedule(dynamic, 8)
+  for (int id = 0; id < nc; id++) orf_cell_sort(&g->cells[id], 0x1FFF);
+  free(fill);
+  free(cnt);
+  free(cof);
+  return g;
+}
+
+API void orf_cellgrid_free(struct orf_cellgrid *g) {
+  const int nc = g->cdim * g->cdim * g->cdim;
+  for (int id = 0; id < nc; id++) orf_cell_free_sorts(&g->cells[id]);
+  free(g->cells);
+  free(g->parts);
+  free(g);
+}
+
+API struct part *orf_cellgrid_parts(struct orf_cellgrid *g) { return g->parts; }
+
+/* Runs the full density (loop=0) or force (loop=2) pass over the grid with
+ * `nthreads` threads. Returns elapsed wall seconds. */
+API double orf_cellgrid_run(struct orf_cellgrid *g, struct runner *r, int loop,
+                            int nthreads) {
+  const int cdim = g->cdim;
+  const int nc = cdim * cdim * cdim;
+  struct timespec t0, t1;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+  (void)nthreads;
+#endif
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+#pragma omp parallel
+  {
+#pragma omp for schedule(dynamic, 4)
+    for (int id = 0; id < nc; id++) {
+      if (loop == LOOP_FORCE)
+        orf_doself2_branch(r, &g->cells[id]);
+      else
+        orf_doself1_branch(r, &g->cells[id], loop);
+    }
+    for (int d = 0; d < 13; d++) {
+      for (int par = 0; par < 8; par++) {
+        const int px = par & 1, py = (par >> 1) & 1, pz = (par >> 2) & 1;
+        const int h = cdim / 2;
+#pragma omp for schedule(dynamic, 4)
+        for (int t = 0; t < h * h * h; t++) {
+          const int cx = 2 * (t / (h * h)) + px;
+          const int cy = 2 * ((t / h) % h) + py;
+          const int cz = 2 * (t % h) + pz;
+          const int nx = (cx + pair_dirs[d][0] + cdim) % cdim;
+          const int ny = (cy + pair_dirs[d][1] + cdim) % cdim;
+          const int nz = (cz + pair_dirs[d][2] + cdim) % cdim;
+          struct cell *ci = &g->cells[(cx * cdim + cy) * cdim + cz];
+          struct cell *cj = &g->cells[(nx * cdim + ny) * cdim + nz];
+          if (loop == LOOP_FORCE)
+            orf_dopair2_branch(r, ci, cj);
+          else
+            orf_dopair1_branch(r, ci, cj, loop);
+        }
+      }
+    }
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+}
+#endif /* ORACLE_F32 */
+
+/* ======================================================================== */
+/* Gravity P2P — src/runner_doiact_grav.c, src/gravity/MultiSoftening/      */
+/* gravity_iact.h, src/kernel_gravity.h, src/kernel_long_gravity.h,         */
+/* src/gravity_cache.h. Float restatement in the f32 build; the f64 build   */
+/* promotes every temporary.                                                */
+/* ======================================================================== */
+
+/* kernel_gravity.h:48-70 (Wendland-C2) */
+static inline real kernel_grav_pot_eval(real u) {
+  real W = (real)3.f * u - (real)15.f;
+  W = W * u + (real)28.f;
+  W = W * u - (real)21.f;
+  W = W * u;
+  W = W * u + (real)7.f;
+  W = W * u;
+  W = W * u - (real)3.f;
+  return W;
+}
+/* kernel_gravity.h:79-100 */
+static inline real kernel_grav_force_eval(real u) {
+  real W = (real)21.f * u - (real)90.f;
+  W = W * u + (real)140.f;
+  W = W * u - (real)84.f;
+  W = W * u;
+  W = W * u + (real)14.f;
+  return W;
+}
+/* kernel_long_gravity.h:204-262 (default branch) */
+static inline void kernel_long_grav_eval(real r_over_r_s, real *corr_f, real *corr_pot) {
+  const real x = (real)2.f * r_over_r_s;
+  const real exp_x = EXP(x);
+  const real alpha = (real)1.f / ((real)1.f + exp_x);
+  real W = (real)1.f - alpha * exp_x;
+  W = W * (real)2.f;
+  *corr_pot = W;
+  W = (real)1.f - alpha;
+  W = W * x - exp_x;
+  W = W * alpha + (real)1.f;
+  W = W * (real)2.f;
+  *corr_f = W;
+}
+/* gravity_iact.h:47-81 */
+static inline void iact_grav_pp_full(real r2, real h2, real h_inv, real h_inv3,
+                                     real mass, real *f_ij, real *pot_ij) {
+  const real r_inv = (real)1.f / SQRT(r2 + (real)FLT_MIN);
+  if (r2 >= h2) {
+    *f_ij = mass * r_inv * r_inv * r_inv;
+    *pot_ij = -mass * r_inv;
+  } else {
+    const real r = r2 * r_inv;
+    const real ui = r * h_inv;
+    *f_ij = mass * h_inv3 * kernel_grav_force_eval(ui);
+    *pot_ij = mass * h_inv * kernel_grav_pot_eval(ui);
+  }
+}
+/* gravity_iact.h:91-135 */
+static inline void iact_grav_pp_truncated(real r2, real h2, real h_inv, real h_inv3,
+                                          real mass, real r_s_inv, real *f_ij,
+                                          real *pot_ij) {
+  const real r_inv = (real)1.f / SQRT(r2 + (real)FLT_MIN);
+  const real r = r2 * r_inv;
+  if (r2 >= h2) {
+    *f_ij = mass * r_inv * r_inv * r_inv;
+    *pot_ij = -mass * r_inv;
+  } else {
+    const real ui = r * h_inv;
+    *f_ij = mass * h_inv3 * kernel_grav_force_eval(ui);
+    *pot_ij = mass * h_inv * kernel_grav_pot_eval(ui);
+  }
+  const real u_lr = r * r_s_inv;
+  real corr_f_lr, corr_pot_lr;
+  kernel_long_grav_eval(u_lr, &corr_f_lr, &corr_pot_lr);
+  *f_ij *= corr_f_lr;
+  *pot_ij *= corr_pot_lr;
+}
+
+static inline real nearest_r(real dx, real box) {
+  return ((dx > (real)0.5f * box) ? (dx - box)
+                                  : ((dx < (real)-0.5f * box) ? (dx + box) : dx));
+}
+
+struct oracle_grav_params {
+  int periodic;        /* e->mesh->periodic */
+  float dim[3];        /* e->mesh->dim */
+  float r_s_inv;       /* e->mesh->r_s_inv */
+  double r_cut_min;    /* e->mesh->r_cut_min */
+  int max_active_bin;
+};
+
+/* P2P of the (active) particles of gi against all of gj (no multipoles):
+ * runner_dopair_grav_pp_full / _truncated (runner_doiact_grav.c:584-760),
+ * on gravity caches (gravity_cache.h:310-379): positions relative to `shift`
+ * cast to float, inhibited -> mass 0 / inactive; truncated selects the
+ * erfc-like long-range factor. self: j == i skipped
+ * (runner_doself_grav_pp_full, runner_doiact_grav.c:1500-1622). */
+static long long grav_pp(struct gpart *gi, int ni, const struct gpart *gj, int nj,
+                         int self, int truncated, const double shift_i[3],
+                         const double shift_j[3], const struct oracle_grav_params *G) {
+  long long n = 0;
+  const real dim[3] = {(real)G->dim[0], (real)G->dim[1], (real)G->dim[2]};
+  for (int pid = 0; pid < ni; pid++) {
+    struct gpart *gp = &gi[pid];
+    if (gp->time_bin == time_bin_inhibited) continue;
+    if (gp->time_bin > G->max_active_bin) continue;
+    const real x_i = (real)(gp->x[0] - shift_i[0]);
+    const real y_i = (real)(gp->x[1] - shift_i[1]);
+    const real z_i = (real)(gp->x[2] - shift_i[2]);
+    const real h_i = gp->epsilon;
+    real a_x = 0, a_y = 0, a_z = 0, pot = 0;
+    for (int pjd = 0; pjd < nj; pjd++) {
+      if (self && pid == pjd) continue;
+      const struct gpart *gq = &gj[pjd];
+      const real mass_j = (gq->time_bin == time_bin_inhibited) ? (real)0 : (real)gq->mass;
+      real dx = (real)(gq->x[0] - shift_j[0]) - x_i;
+      real dy = (real)(gq->x[1] - shift_j[1]) - y_i;
+      real dz = (real)(gq->x[2] - shift_j[2]) - z_i;
+      if (G->periodic && !self) {
+        dx = nearest_r(dx, dim[0]);
+        dy = nearest_r(dy, dim[1]);
+        dz = nearest_r(dz, dim[2]);
+      }
+      const real r2 = dx * dx + dy * dy + dz * dz;
+      const real h = rmax(h_i, (real)gq->epsilon);
+      const real h2 = h * h;
+      const real h_inv = (real)1.f / h;
+      const real h_inv_3 = h_inv * h_inv * h_inv;
+      real f_ij, pot_ij;
+      if (truncated)
+        iact_grav_pp_truncated(r2, h2, h_inv, h_inv_3, mass_j, (real)G->r_s_inv, &f_ij,
+                               &pot_ij);
+      else
+        iact_grav_pp_full(r2, h2, h_inv, h_inv_3, mass_j, &f_ij, &pot_ij);
+      a_x += f_ij * dx;
+      a_y += f_ij * dy;
+      a_z += f_ij * dz;
+      pot += pot_ij;
+      n++;
+    }
+    /* gravity_cache_write_back (gravity_cache.h:488-511): a_grav += cache */
+    gp->a_grav[0] += (float)a_x;
+    gp->a_grav[1] += (float)a_y;
+    gp->a_grav[2] += (float)a_z;
+    gp->potential += (float)pot;
+  }
+  return n;
+}
+
+/* runner_doself_grav_pp (runner_doiact_grav.c:1788-1871): cache frame =
+ * cell centre; truncated iff periodic && 2*r_max > r_cut_min. */
+API long long PFX(grav_self_pp)(struct gpart *g, int n, const double loc[3],
+                                const double width[3], double r_max,
+                                const struct oracle_grav_params *G) {
+  const double c[3] = {loc[0] + 0.5 * width[0], loc[1] + 0.5 * width[1],
+                       loc[2] + 0.5 * width[2]};
+  const int truncated = G->periodic && (2. * r_max > G->r_cut_min);
+  return grav_pp(g, n, g, n, 1, truncated, c, c, G);
+}
+
+/* runner_dopair_grav_pp with allow_mpole = 0 (runner_doiact_grav.c:1202-1425):
+ * absolute float positions, nearest-image dx when periodic; truncated iff
+ * periodic && |CoM_i - CoM_j| + rmax_i + rmax_j > r_cut_min. Updates gi (and
+ * gj when symmetric). */
+API long long PFX(grav_pair_pp)(struct gpart *gi, int ni, struct gpart *gj, int nj,
+                                const double CoM_i[3], const double CoM_j[3],
+                                double rmax_i, double rmax_j, int symmetric,
+                                const struct oracle_grav_params *G) {
+  const double zero[3] = {0., 0., 0.};
+  int truncated = 0;
+  if (G->periodic) {
+    double dx[3];
+    for (int k = 0; k < 3; k++) {
+      dx[k] = (float)CoM_j[k] - (float)CoM_i[k];
+      dx[k] = nearest_r((real)dx[k], (real)G->dim[k]);
+    }
+    const double r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+    truncated = (sqrt(r2) + rmax_i + rmax_j) > G->r_cut_min;
+  }
+  long long n = grav_pp(gi, ni, gj, nj, 0, truncated, zero, zero, G);
+  if (symmetric) n += grav_pp(gj, nj, gi, ni, 0, truncated, zero, zero, G);
+  return n;
+}

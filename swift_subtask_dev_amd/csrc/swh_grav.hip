@@ -1,0 +1,323 @@
+// swh_grav.hip — batch leaf-leaf P2P gravity (runner_doself_grav_pp /
+// runner_dopair_grav_pp, src/runner_doiact_grav.c:1500-1871 and 584-760) on a
+// device-resident gpart set.
+//
+// One 256-thread workgroup per i-leaf; each thread keeps up to kIPer i-particle
+// accumulators in registers (fp64). Source leaves of the i-leaf's CSR list
+// are streamed through LDS in 256-particle tiles (x,y,z fp64 + eps, mass);
+// every lane reads the same tile entry (LDS broadcast), so the inner loop is
+// pure FMA work: the compute-bound P2P roofline (fp64 vector, no MFMA — this
+// is a gather/FMA path, not a dense contraction).
+#include "swh_internal.h"
+#include "swh_physics.h"
+
+namespace swh {
+
+constexpr int kGravBlock = 256;
+constexpr int kIPer = 2;  // i-particles per thread per pass (leaves up to 512 in one pass)
+
+struct GSoA {
+  double4* pos;  // x, y, z, epsilon
+  float* mass;   // 0 for inhibited
+  int8_t* active;
+  double4* acc;  // a_x, a_y, a_z, potential
+};
+
+__global__ void gunpack_kernel(GLayout L, const char* __restrict__ aos, int64_t n, GSoA g,
+                               int max_active_bin) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const char* r = aos + i * L.stride;
+  const double* x = reinterpret_cast<const double*>(r + L.x);
+  const float eps = *reinterpret_cast<const float*>(r + L.epsilon);
+  g.pos[i] = make_double4(x[0], x[1], x[2], (double)eps);
+  const int tb = *reinterpret_cast<const int8_t*>(r + L.time_bin);
+  const bool inhibited = tb == kTimeBinInhibited;
+  g.mass[i] = inhibited ? 0.f : *reinterpret_cast<const float*>(r + L.mass);
+  g.active[i] = (!inhibited && tb <= max_active_bin) ? 1 : 0;
+  g.acc[i] = make_double4(0., 0., 0., 0.);
+}
+
+__global__ void gpack_kernel(GLayout L, char* __restrict__ aos, int64_t n, GSoA g) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !g.active[i]) return;
+  char* r = aos + i * L.stride;
+  float* a = reinterpret_cast<float*>(r + L.a_grav);
+  const double4 ac = g.acc[i];
+  a[0] += (float)ac.x;
+  a[1] += (float)ac.y;
+  a[2] += (float)ac.z;
+  *reinterpret_cast<float*>(r + L.potential) += (float)ac.w;
+  g.acc[i] = make_double4(0., 0., 0., 0.);  // a second download adds nothing
+}
+
+template <typename T>
+__global__ __launch_bounds__(kGravBlock) void p2p_kernel(
+    GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
+    const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
+    double dimz, T r_s_inv, unsigned long long* counter) {
+  __shared__ double sx[kGravBlock], sy[kGravBlock], sz[kGravBlock];
+  __shared__ float se[kGravBlock], sm[kGravBlock];
+  const int li = blockIdx.x;
+  const swh_leaf L = leaves[li];
+  const int p0 = pair_off[li], p1 = pair_off[li + 1];
+  unsigned long long nint = 0;
+  for (int ibase = 0; ibase < L.count; ibase += kGravBlock * kIPer) {
+    int gi[kIPer];
+    double xi[kIPer], yi[kIPer], zi[kIPer];
+    T hi[kIPer], ax[kIPer], ay[kIPer], az[kIPer], pot[kIPer];
+    bool act[kIPer];
+#pragma unroll
+    for (int k = 0; k < kIPer; k++) {
+      const int local = ibase + k * kGravBlock + (int)threadIdx.x;
+      gi[k] = L.start + local;
+      act[k] = local < L.count && g.active[gi[k]];
+      const double4 p = act[k] ? g.pos[gi[k]] : make_double4(0., 0., 0., 1.);
+      xi[k] = p.x; yi[k] = p.y; zi[k] = p.z;
+      hi[k] = (T)p.w;
+      ax[k] = ay[k] = az[k] = pot[k] = (T)0;
+    }
+    for (int q = p0; q < p1; q++) {
+      const swh_leaf_pair pr = pairs[q];
+      const swh_leaf J = leaves[pr.j];
+      for (int jbase = 0; jbase < J.count; jbase += kGravBlock) {
+        const int nt = min(kGravBlock, J.count - jbase);
+        __syncthreads();
+        if ((int)threadIdx.x < nt) {
+          const int gj = J.start + jbase + (int)threadIdx.x;
+          const double4 p = g.pos[gj];
+          sx[threadIdx.x] = p.x;
+          sy[threadIdx.x] = p.y;
+          sz[threadIdx.x] = p.z;
+          se[threadIdx.x] = (float)p.w;
+          sm[threadIdx.x] = g.mass[gj];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kIPer; k++) {
+          if (!act[k]) continue;
+          const int self_local = gi[k] - (J.start + jbase);  // skip j == i
+          if (pr.truncated) {
+            for (int t = 0; t < nt; t++) {
+              if (t == self_local) continue;
+              double dxd = sx[t] - xi[k], dyd = sy[t] - yi[k], dzd = sz[t] - zi[k];
+              if (periodic) {
+                dxd = dxd > 0.5 * dimx ? dxd - dimx : (dxd < -0.5 * dimx ? dxd + dimx : dxd);
+                dyd = dyd > 0.5 * dimy ? dyd - dimy : (dyd < -0.5 * dimy ? dyd + dimy : dyd);
+                dzd = dzd > 0.5 * dimz ? dzd - dimz : (dzd < -0.5 * dimz ? dzd + dimz : dzd);
+              }
+              const T dx = (T)dxd, dy = (T)dyd, dz = (T)dzd;
+              const T r2 = dx * dx + dy * dy + dz * dz;
+              const T h = tmax(hi[k], (T)se[t]);
+              const T h_inv = (T)1 / h;
+              T f, pt;
+              iact_grav_pp<T, true>(r2, h * h, h_inv, h_inv * h_inv * h_inv, (T)sm[t], r_s_inv,
+                                    f, pt);
+              ax[k] += f * dx; ay[k] += f * dy; az[k] += f * dz; pot[k] += pt;
+            }
+          } else {
+            for (int t = 0; t < nt; t++) {
+              if (t == self_local) continue;
+              double dxd = sx[t] - xi[k], dyd = sy[t] - yi[k], dzd = sz[t] - zi[k];
+              if (periodic) {
+                dxd = dxd > 0.5 * dimx ? dxd - dimx : (dxd < -0.5 * dimx ? dxd + dimx : dxd);
+                dyd = dyd > 0.5 * dimy ? dyd - dimy : (dyd < -0.5 * dimy ? dyd + dimy : dyd);
+                dzd = dzd > 0.5 * dimz ? dzd - dimz : (dzd < -0.5 * dimz ? dzd + dimz : dzd);
+              }
+              const T dx = (T)dxd, dy = (T)dyd, dz = (T)dzd;
+              const T r2 = dx * dx + dy * dy + dz * dz;
+              const T h = tmax(hi[k], (T)se[t]);
+              const T h_inv = (T)1 / h;
+              T f, pt;
+              iact_grav_pp<T, false>(r2, h * h, h_inv, h_inv * h_inv * h_inv, (T)sm[t],
+                                     r_s_inv, f, pt);
+              ax[k] += f * dx; ay[k] += f * dy; az[k] += f * dz; pot[k] += pt;
+            }
+          }
+          nint += (unsigned long long)(nt - ((self_local >= 0 && self_local < nt) ? 1 : 0));
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kIPer; k++) {
+      if (!act[k]) continue;
+      double4 a = g.acc[gi[k]];
+      a.x += (double)ax[k];
+      a.y += (double)ay[k];
+      a.z += (double)az[k];
+      a.w += (double)pot[k];
+      g.acc[gi[k]] = a;
+    }
+  }
+  if (counter) {
+    for (int o = 32; o > 0; o >>= 1) nint += __shfl_xor(nint, o);
+    if ((threadIdx.x & 63) == 0 && nint) atomicAdd(counter, nint);
+  }
+}
+
+static GSoA gsoa_of(swh_gspace* g) {
+  GSoA s;
+  s.pos = g->pos.as<double4>();
+  s.mass = g->mass.as<float>();
+  s.active = g->active.as<int8_t>();
+  s.acc = g->accel.as<double4>();
+  return s;
+}
+
+}  // namespace swh
+
+using namespace swh;
+
+extern "C" {
+
+swh_status swh_gspace_create(swh_context* ctx, swh_gspace** out) {
+  if (!ctx || !out) return SWH_ERR_ARG;
+  SWH_HIP(hipSetDevice(ctx->device));
+  auto* g = new swh_gspace();
+  g->ctx = ctx;
+  if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete g;
+    return SWH_ERR_HIP;
+  }
+  *out = g;
+  return SWH_OK;
+}
+
+swh_status swh_gspace_destroy(swh_gspace* g) {
+  if (!g) return SWH_OK;
+  (void)hipSetDevice(g->ctx->device);
+  (void)hipStreamSynchronize(g->stream);
+  DevBuf* bufs[] = {&g->aos, &g->pos, &g->mass, &g->active, &g->accel,
+                    &g->leaves, &g->pair_off, &g->pairs, &g->counter};
+  for (DevBuf* b : bufs) b->release();
+  (void)hipStreamDestroy(g->stream);
+  delete g;
+  return SWH_OK;
+}
+
+// The activity mask needs max_active_bin: it is (re)derived in
+// swh_grav_pp_batch from the AoS image, so upload only stages the records.
+swh_status swh_gspace_upload(swh_gspace* g, const void* gparts, int64_t count,
+                             const swh_gpart_layout* GL, int on_device) {
+  if (!g || (count > 0 && !gparts) || count < 0 || count > INT32_MAX / 2 || !GL)
+    return SWH_ERR_ARG;
+  GLayout L;
+  SWH_TRY(make_glayout(GL, &L));
+  SWH_HIP(hipSetDevice(g->ctx->device));
+  g->layout = L;
+  g->n = count;
+  if (count == 0) return SWH_OK;
+  SWH_TRY(g->aos.reserve((size_t)count * L.stride));
+  SWH_TRY(g->pos.reserve((size_t)count * sizeof(double4)));
+  SWH_TRY(g->mass.reserve((size_t)count * sizeof(float)));
+  SWH_TRY(g->active.reserve((size_t)count));
+  SWH_TRY(g->accel.reserve((size_t)count * sizeof(double4)));
+  SWH_HIP(hipMemcpyAsync(g->aos.ptr, gparts, (size_t)count * L.stride,
+                         on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                         g->stream));
+  if (!on_device) SWH_HIP(hipStreamSynchronize(g->stream));
+  return SWH_OK;
+}
+
+swh_status swh_gspace_set_leaves(swh_gspace* g, const swh_leaf* leaves, int32_t nleaves,
+                                 const int32_t* pair_offset, const swh_leaf_pair* pairs,
+                                 int32_t npairs) {
+  if (!g || nleaves < 0 || npairs < 0 || (nleaves > 0 && (!leaves || !pair_offset)) ||
+      (npairs > 0 && !pairs))
+    return SWH_ERR_ARG;
+  int32_t maxc = 0;
+  for (int i = 0; i < nleaves; i++) {
+    if (leaves[i].start < 0 || leaves[i].count < 0 || leaves[i].start + leaves[i].count > g->n) {
+      set_error("leaf %d [%d,+%d) outside the gpart set of %lld", i, leaves[i].start,
+                leaves[i].count, (long long)g->n);
+      return SWH_ERR_ARG;
+    }
+    maxc = std::max(maxc, leaves[i].count);
+  }
+  if (nleaves > 0 && (pair_offset[0] != 0 || pair_offset[nleaves] != npairs)) {
+    set_error("pair_offset must run 0..npairs");
+    return SWH_ERR_ARG;
+  }
+  for (int q = 0; q < npairs; q++)
+    if (pairs[q].j < 0 || pairs[q].j >= nleaves) {
+      set_error("pair %d names leaf %d of %d", q, pairs[q].j, nleaves);
+      return SWH_ERR_ARG;
+    }
+  SWH_HIP(hipSetDevice(g->ctx->device));
+  SWH_TRY(g->leaves.reserve((size_t)std::max(1, nleaves) * sizeof(swh_leaf)));
+  SWH_TRY(g->pair_off.reserve((size_t)(nleaves + 1) * sizeof(int32_t)));
+  SWH_TRY(g->pairs.reserve((size_t)std::max(1, npairs) * sizeof(swh_leaf_pair)));
+  if (nleaves > 0) {
+    SWH_HIP(hipMemcpyAsync(g->leaves.ptr, leaves, nleaves * sizeof(swh_leaf),
+                           hipMemcpyHostToDevice, g->stream));
+    SWH_HIP(hipMemcpyAsync(g->pair_off.ptr, pair_offset, (nleaves + 1) * sizeof(int32_t),
+                           hipMemcpyHostToDevice, g->stream));
+  }
+  if (npairs > 0)
+    SWH_HIP(hipMemcpyAsync(g->pairs.ptr, pairs, npairs * sizeof(swh_leaf_pair),
+                           hipMemcpyHostToDevice, g->stream));
+  SWH_HIP(hipStreamSynchronize(g->stream));
+  g->nleaves = nleaves;
+  g->npairs = npairs;
+  g->max_leaf = maxc;
+  return SWH_OK;
+}
+
+swh_status swh_grav_pp_batch(swh_gspace* g, const swh_grav_params* G, int64_t* n_int) {
+  if (!g || !G) return SWH_ERR_ARG;
+  if (g->n == 0 || g->nleaves == 0) {
+    if (n_int) *n_int = 0;
+    return SWH_OK;
+  }
+  SWH_HIP(hipSetDevice(g->ctx->device));
+  const int block = 256;
+  hipLaunchKernelGGL(gunpack_kernel, dim3((int)((g->n + block - 1) / block)), dim3(block), 0,
+                     g->stream, g->layout, g->aos.as<const char>(), g->n, gsoa_of(g),
+                     G->max_active_bin);
+  SWH_HIP(hipGetLastError());
+  SWH_TRY(g->counter.reserve(sizeof(unsigned long long)));
+  unsigned long long* ctr = n_int ? g->counter.as<unsigned long long>() : nullptr;
+  if (ctr) SWH_HIP(hipMemsetAsync(ctr, 0, sizeof(unsigned long long), g->stream));
+  if (g->ctx->precision == SWH_PRECISION_F64)
+    hipLaunchKernelGGL(p2p_kernel<double>, dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
+                       gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
+                       g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
+                       (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, ctr);
+  else
+    hipLaunchKernelGGL(p2p_kernel<float>, dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
+                       gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
+                       g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
+                       (double)G->dim[1], (double)G->dim[2], (float)G->r_s_inv, ctr);
+  SWH_HIP(hipGetLastError());
+  if (n_int) {
+    unsigned long long h = 0;
+    SWH_HIP(hipMemcpyAsync(&h, ctr, sizeof(h), hipMemcpyDeviceToHost, g->stream));
+    SWH_HIP(hipStreamSynchronize(g->stream));
+    *n_int = (int64_t)h;
+  }
+  return SWH_OK;
+}
+
+swh_status swh_gspace_download(swh_gspace* g, void* gparts, const swh_gpart_layout* GL,
+                               int on_device) {
+  if (!g || (g->n > 0 && !gparts) || !GL) return SWH_ERR_ARG;
+  if (g->n == 0) return SWH_OK;
+  SWH_HIP(hipSetDevice(g->ctx->device));
+  const int block = 256;
+  hipLaunchKernelGGL(gpack_kernel, dim3((int)((g->n + block - 1) / block)), dim3(block), 0,
+                     g->stream, g->layout, g->aos.as<char>(), g->n, gsoa_of(g));
+  SWH_HIP(hipGetLastError());
+  SWH_HIP(hipMemcpyAsync(gparts, g->aos.ptr, (size_t)g->n * g->layout.stride,
+                         on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                         g->stream));
+  SWH_HIP(hipStreamSynchronize(g->stream));
+  return SWH_OK;
+}
+
+swh_status swh_gspace_sync(swh_gspace* g) {
+  if (!g) return SWH_ERR_ARG;
+  SWH_HIP(hipStreamSynchronize(g->stream));
+  return SWH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,707 @@
+// swh_hydro.hip — batch hydro loops of libswifthip on a device-resident
+// swh_space: one launch per loop replaces every density / gradient / force
+// task of a step (src/runner_doiact_functions_hydro.h DOSELF*/DOPAIR*/DOSUB*),
+// plus the ghost h-iteration (src/runner_ghost.c:1085-1596), the extra ghost
+// (:992-1083) and runner_do_end_hydro_force (src/runner_others.c:618).
+//
+// Gather formulation: one thread owns one active i-particle and visits the
+// grid rows overlapping [x_i - R, x_i + R] (R = H_i for density/gradient,
+// max over all H for force), each row one contiguous j range of the
+// cell-sorted SoA. Every directed pair (i <- j) is evaluated exactly once, with
+// the non-symmetric iact (hydro_iact.h:130,276,488), so the sums are
+// deterministic and need no atomics.
+#include "swh_internal.h"
+#include "swh_physics.h"
+#include "swh_space.h"
+
+namespace swh {
+
+enum { LOOP_DENSITY = 0, LOOP_GRADIENT = 1, LOOP_FORCE = 2 };
+
+__device__ __forceinline__ double wrap_nearest(double d, double box) {
+  return d > 0.5 * box ? d - box : (d < -0.5 * box ? d + box : d);
+}
+
+// ---------------------------------------------------------------------------
+// Per-loop gather states. visit() receives a candidate j with its (periodic
+// image) separation dx = x_i - x_j.
+// ---------------------------------------------------------------------------
+template <typename T>
+struct DensityState {
+  int self;
+  T hig2, hi_inv, vix, viy, viz;
+  DensityAcc<T> A;
+  int n;
+  __device__ __forceinline__ void visit(const SoA& a, int j, const double4& pj, T dx, T dy,
+                                        T dz) {
+    const T r2 = dx * dx + dy * dy + dz * dz;
+    if (r2 < hig2 && j != self) {
+      const float4 v = a.vm[j];
+      iact_nonsym_density<T>(r2, dx, dy, dz, hi_inv, vix, viy, viz, (T)v.w, (T)v.x, (T)v.y,
+                             (T)v.z, A);
+      n++;
+    }
+  }
+};
+
+template <typename T>
+struct GradientState {
+  int self;
+  T hi, hig2, vix, viy, viz, ui, ci, a2H;
+  GradientAcc<T> A;
+  int n;
+  __device__ __forceinline__ void visit(const SoA& a, int j, const double4& pj, T dx, T dy,
+                                        T dz) {
+    const T r2 = dx * dx + dy * dy + dz * dz;
+    if (r2 < hig2 && j != self) {
+      const float4 v = a.vm[j];
+      const float4 t = a.th[j];
+      iact_nonsym_gradient<T>(r2, dx, dy, dz, hi, vix, viy, viz, ui, ci, (T)v.w, (T)v.x,
+                              (T)v.y, (T)v.z, (T)t.x, (T)t.y, (T)t.w, (T)a.fc[j].z, a2H, A);
+      n++;
+    }
+  }
+};
+
+template <typename T>
+struct ForceState {
+  int self;
+  T hig2, hi_inv, hid_inv, a2H;
+  ForceIn<T> I;
+  ForceAcc<T> A;
+  int n;
+  __device__ __forceinline__ void visit(const SoA& a, int j, const double4& pj, T dx, T dy,
+                                        T dz) {
+    const T r2 = dx * dx + dy * dy + dz * dz;
+    const T hj = (T)pj.w;
+    const T hjg2 = hj * hj * (T)kGamma2;
+    if ((r2 < hig2 || r2 < hjg2) && j != self) {
+      ForceIn<T> J;
+      const float4 v = a.vm[j];
+      const float4 t = a.th[j];
+      const float4 c = a.fc[j];
+      J.vx = v.x; J.vy = v.y; J.vz = v.z; J.m = v.w;
+      J.h = hj;
+      J.u = t.x; J.rho = t.y; J.P = t.z; J.c = t.w;
+      J.f = c.x; J.balsara = c.y; J.alpha_visc = c.z; J.alpha_diff = c.w;
+      iact_nonsym_force<T>(r2, dx, dy, dz, I, hid_inv, hi_inv, J, a2H, A);
+      const int tbj = a.tb[j];
+      if (tbj > 0 && tbj < A.min_ngb_time_bin) A.min_ngb_time_bin = tbj;
+      n++;
+    }
+  }
+};
+
+// Visit every j in the grid cells overlapping the cube of half-width `reach`
+// around (xi,yi,zi). Rows along x are contiguous; a periodic wrap splits a
+// row into two ranges with an image shift. Dimensions whose range covers the
+// whole box fall back to the nearest-image convention (tools.c pairs_all_*).
+template <typename T, class S>
+__device__ __forceinline__ void gather_grid(const GridDev& g, const int* __restrict__ cs,
+                                            const SoA& a, double xi, double yi, double zi,
+                                            double reach, S& st) {
+  const double xs[3] = {xi, yi, zi};
+  int lo[3], hi[3];
+  bool full[3];
+  for (int k = 0; k < 3; k++) {
+    const double rel = xs[k] - g.origin[k];
+    lo[k] = (int)floor((rel - reach) * g.inv_w[k]);
+    hi[k] = (int)floor((rel + reach) * g.inv_w[k]);
+    if (g.periodic) {
+      full[k] = (hi[k] - lo[k] + 1 >= g.cdim[k]);
+      if (full[k]) {
+        lo[k] = 0;
+        hi[k] = g.cdim[k] - 1;
+      }
+    } else {
+      full[k] = false;
+      lo[k] = lo[k] < 0 ? 0 : lo[k];
+      hi[k] = hi[k] > g.cdim[k] - 1 ? g.cdim[k] - 1 : hi[k];
+    }
+  }
+  for (int cz = lo[2]; cz <= hi[2]; cz++) {
+    int wz = cz;
+    double sz = 0.;
+    if (g.periodic && !full[2]) {
+      if (cz < 0) { wz += g.cdim[2]; sz = -g.dim[2]; }
+      else if (cz >= g.cdim[2]) { wz -= g.cdim[2]; sz = g.dim[2]; }
+    }
+    for (int cy = lo[1]; cy <= hi[1]; cy++) {
+      int wy = cy;
+      double sy = 0.;
+      if (g.periodic && !full[1]) {
+        if (cy < 0) { wy += g.cdim[1]; sy = -g.dim[1]; }
+        else if (cy >= g.cdim[1]) { wy -= g.cdim[1]; sy = g.dim[1]; }
+      }
+      const int row = (wz * g.cdim[1] + wy) * g.cdim[0];
+      int seg_lo[2], seg_hi[2];
+      double seg_sx[2];
+      int nseg;
+      if (!g.periodic || full[0] || (lo[0] >= 0 && hi[0] < g.cdim[0])) {
+        nseg = 1; seg_lo[0] = lo[0]; seg_hi[0] = hi[0]; seg_sx[0] = 0.;
+      } else if (lo[0] < 0) {
+        nseg = 2;
+        seg_lo[0] = lo[0] + g.cdim[0]; seg_hi[0] = g.cdim[0] - 1; seg_sx[0] = -g.dim[0];
+        seg_lo[1] = 0; seg_hi[1] = hi[0]; seg_sx[1] = 0.;
+      } else {
+        nseg = 2;
+        seg_lo[0] = lo[0]; seg_hi[0] = g.cdim[0] - 1; seg_sx[0] = 0.;
+        seg_lo[1] = 0; seg_hi[1] = hi[0] - g.cdim[0]; seg_sx[1] = g.dim[0];
+      }
+      for (int sgi = 0; sgi < nseg; sgi++) {
+        const int j0 = cs[row + seg_lo[sgi]];
+        const int j1 = cs[row + seg_hi[sgi] + 1];
+        const double sx = seg_sx[sgi];
+        for (int j = j0; j < j1; j++) {
+          const double4 pj = a.pos[j];
+          double dx = xi - (pj.x + sx);
+          double dy = yi - (pj.y + sy);
+          double dz = zi - (pj.z + sz);
+          if (full[0]) dx = wrap_nearest(dx, g.dim[0]);
+          if (full[1]) dy = wrap_nearest(dy, g.dim[1]);
+          if (full[2]) dz = wrap_nearest(dz, g.dim[2]);
+          st.visit(a, j, pj, (T)dx, (T)dy, (T)dz);
+        }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void count_add(int n, unsigned long long* counter) {
+  unsigned long long v = (unsigned long long)n;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(counter, v);
+}
+
+template <int LOOP, typename T>
+__global__ __launch_bounds__(256) void loop_kernel(GridDev g, const int* __restrict__ cs,
+                                                   SoA a, const int* __restrict__ subset,
+                                                   int nitems, int max_active_bin, T a2H,
+                                                   const unsigned int* __restrict__ hmax_bits,
+                                                   unsigned long long* counter,
+                                                   int* __restrict__ ncount) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  int n = 0;
+  const int i = (t < nitems) ? (subset ? subset[t] : t) : -1;
+  if (i >= 0 && a.tb[i] <= max_active_bin) {
+    const double4 pi = a.pos[i];
+    const T hi = (T)pi.w;
+    const T hig2 = hi * hi * (T)kGamma2;
+    const float4 vmi = a.vm[i];
+    if (LOOP == LOOP_DENSITY) {
+      DensityState<T> st;
+      st.self = i;
+      st.hig2 = hig2;
+      st.hi_inv = (T)1 / hi;
+      st.vix = vmi.x; st.viy = vmi.y; st.viz = vmi.z;
+      st.A.zero();
+      st.n = 0;
+      gather_grid<T>(g, cs, a, pi.x, pi.y, pi.z, (double)pi.w * (double)kGamma, st);
+      float4 d = a.dens[i];
+      float4 r = a.rot[i];
+      a.th[i].y = (float)((T)a.th[i].y + st.A.rho);
+      d.x = (float)((T)d.x + st.A.rho_dh);
+      d.y = (float)((T)d.y + st.A.wcount);
+      d.z = (float)((T)d.z + st.A.wcount_dh);
+      d.w = (float)((T)d.w + st.A.div_v);
+      r.x = (float)((T)r.x + st.A.rot_x);
+      r.y = (float)((T)r.y + st.A.rot_y);
+      r.z = (float)((T)r.z + st.A.rot_z);
+      a.dens[i] = d;
+      a.rot[i] = r;
+      n = st.n;
+    } else if (LOOP == LOOP_GRADIENT) {
+      GradientState<T> st;
+      const float4 thi = a.th[i];
+      const float4 gi = a.grad[i];
+      st.self = i;
+      st.hi = hi;
+      st.hig2 = hig2;
+      st.vix = vmi.x; st.viy = vmi.y; st.viz = vmi.z;
+      st.ui = thi.x;
+      st.ci = thi.w;
+      st.a2H = a2H;
+      st.A.v_sig = gi.x;
+      st.A.alpha_visc_max_ngb = gi.y;
+      st.A.laplace_u = 0;
+      st.n = 0;
+      gather_grid<T>(g, cs, a, pi.x, pi.y, pi.z, (double)pi.w * (double)kGamma, st);
+      a.grad[i] = make_float4((float)st.A.v_sig, (float)st.A.alpha_visc_max_ngb, gi.z, gi.w);
+      a.rot[i].w = (float)((T)a.rot[i].w + st.A.laplace_u);
+      n = st.n;
+    } else {
+      ForceState<T> st;
+      const float4 thi = a.th[i];
+      const float4 fci = a.fc[i];
+      st.self = i;
+      st.hig2 = hig2;
+      st.hi_inv = (T)1 / hi;
+      const T hi2 = st.hi_inv * st.hi_inv;
+      st.hid_inv = hi2 * hi2;
+      st.a2H = a2H;
+      st.I.vx = vmi.x; st.I.vy = vmi.y; st.I.vz = vmi.z; st.I.m = vmi.w;
+      st.I.h = hi;
+      st.I.u = thi.x; st.I.rho = thi.y; st.I.P = thi.z; st.I.c = thi.w;
+      st.I.f = fci.x; st.I.balsara = fci.y; st.I.alpha_visc = fci.z; st.I.alpha_diff = fci.w;
+      st.A.ax = st.A.ay = st.A.az = st.A.u_dt = st.A.h_dt = (T)0;
+      st.A.min_ngb_time_bin = a.mintb[i];
+      st.n = 0;
+      const double hmax = (double)__uint_as_float(*hmax_bits) * (double)kGamma;
+      const double reach = fmax(hmax, (double)pi.w * (double)kGamma);
+      gather_grid<T>(g, cs, a, pi.x, pi.y, pi.z, reach, st);
+      float4 ac = a.acc[i];
+      ac.x = (float)((T)ac.x + st.A.ax);
+      ac.y = (float)((T)ac.y + st.A.ay);
+      ac.z = (float)((T)ac.z + st.A.az);
+      ac.w = (float)((T)ac.w + st.A.u_dt);
+      a.acc[i] = ac;
+      a.hdt[i] = (float)((T)a.hdt[i] + st.A.h_dt);
+      a.mintb[i] = (int8_t)st.A.min_ngb_time_bin;
+      n = st.n;
+    }
+    if (ncount) ncount[i] = n;
+  }
+  if (counter) count_add(n, counter);
+}
+
+// hydro_init_part (src/hydro/SPHENIX/hydro.h:553-566) on active particles.
+__global__ void init_kernel(SoA a, int64_t n, int max_active_bin) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || a.tb[i] > max_active_bin) return;
+  a.th[i].y = 0.f;
+  a.dens[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  a.rot[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// ---------------------------------------------------------------------------
+// Ghost (runner_ghost.c:1085-1596, EXTRA_HYDRO_LOOP branch, non-cosmological
+// time-steps). One thread per particle still iterating; particles whose h
+// moved by more than h_tolerance are re-initialised and appended to the redo
+// list (the subset reruns of runner_ghost.c:1503-1546 become one subset launch
+// of loop_kernel per iteration).
+// ---------------------------------------------------------------------------
+struct GhostParams {
+  float h_max, h_min, eta_dim, eps;
+  int use_mass_weighted;
+  double a2_inv, H, fac_B;
+};
+
+template <typename T>
+__global__ void ghost_init_kernel(SoA a, int64_t n, int max_active_bin, float h_max,
+                                  float* left, float* right, int* list, int* count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || a.tb[i] > max_active_bin) return;
+  left[i] = 0.f;
+  right[i] = h_max;
+  const int slot = atomicAdd(count, 1);
+  list[slot] = (int)i;
+}
+
+template <typename T>
+__global__ void ghost_kernel(SoA a, const int* __restrict__ list, int count,
+                             int* __restrict__ redo, int* __restrict__ nredo, float* left,
+                             float* right, GhostParams gp, unsigned int* hmax_bits) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= count) return;
+  const int i = list[t];
+  double4 pos = a.pos[i];
+  const T h_old = (T)(float)pos.w;
+  const T h_old_dim = h_old * h_old * h_old;
+  const T h_old_dim_minus_one = h_old * h_old;
+  float4 th = a.th[i];
+  float4 d = a.dens[i];   // rho_dh, wcount, wcount_dh, div_v
+  float4 r = a.rot[i];    // rot_v, laplace_u
+  const float4 vm = a.vm[i];
+  T rho = th.y, rho_dh = d.x, wcount = d.y, wcount_dh = d.z, div_v = d.w;
+  T rot_x = r.x, rot_y = r.y, rot_z = r.z;
+  T h_new;
+  bool has_no_neighbours = false;
+  bool tidy = false;  // converged-by-clamp branch (runner_ghost.c:1272-1300)
+  float lft = left[i], rgt = right[i];
+  if (wcount < (T)(1.e-5 * kRoot)) {
+    has_no_neighbours = true;
+    h_new = (T)2 * h_old;
+  } else {
+    // hydro_end_density (hydro.h:599-630)
+    const T h_inv = (T)1 / h_old;
+    const T h_inv_dim = h_inv * h_inv * h_inv;
+    const T h_inv_dim_plus_one = h_inv_dim * h_inv;
+    const T m = vm.w;
+    rho += m * (T)kRoot;
+    rho_dh -= (T)kDim * m * (T)kRoot;
+    wcount += (T)kRoot;
+    wcount_dh -= (T)kDim * (T)kRoot;
+    rho *= h_inv_dim;
+    rho_dh *= h_inv_dim_plus_one;
+    wcount *= h_inv_dim;
+    wcount_dh *= h_inv_dim_plus_one;
+    const T rho_inv = (T)1 / rho;
+    const T a_inv2 = (T)gp.a2_inv;
+    rot_x *= h_inv_dim_plus_one * a_inv2 * rho_inv;
+    rot_y *= h_inv_dim_plus_one * a_inv2 * rho_inv;
+    rot_z *= h_inv_dim_plus_one * a_inv2 * rho_inv;
+    div_v *= h_inv_dim_plus_one * rho_inv * a_inv2;
+    div_v += (T)gp.H * (T)kDim;
+    if (gp.use_mass_weighted) {
+      const T inv_mass = (T)1 / m;
+      wcount = rho * inv_mass;
+      wcount_dh = rho_dh * inv_mass;
+    }
+    const T n_sum = wcount * h_old_dim;
+    const T n_target = (T)gp.eta_dim;
+    const T f = n_sum - n_target;
+    const T f_prime = wcount_dh * h_old_dim + (T)kDim * wcount * h_old_dim_minus_one;
+    if (n_sum < n_target) lft = (float)tmax((T)lft, h_old);
+    else if (n_sum > n_target) rgt = (float)tmin((T)rgt, h_old);
+    if ((h_old >= (T)gp.h_max && f < (T)0) || (h_old <= (T)gp.h_min && f > (T)0)) {
+      tidy = true;
+      h_new = h_old;
+    } else {
+      h_new = h_old - f / (f_prime + (T)FLT_MIN);
+      h_new = tmin(h_new, (T)2 * h_old);
+      h_new = tmax(h_new, (T)0.5 * h_old);
+      h_new = tmax(h_new, (T)lft);
+      h_new = tmin(h_new, (T)rgt);
+    }
+  }
+  T h_final = h_old;
+  if (!tidy && fabs(h_new - h_old) > (T)gp.eps * h_old) {
+    T hset;
+    if ((h_new == (T)lft && h_old == (T)rgt) || (h_old == (T)lft && h_new == (T)rgt)) {
+      const T l3 = (T)lft * (T)lft * (T)lft, r3 = (T)rgt * (T)rgt * (T)rgt;
+      hset = cbrt((T)0.5 * (l3 + r3));
+    } else {
+      hset = h_new;
+    }
+    const float hf = (float)hset;
+    if (hf < gp.h_max && hf > gp.h_min) {
+      // redo: store h, re-initialise (hydro_init_part), queue for the rerun
+      pos.w = (double)hf;
+      a.pos[i] = pos;
+      a.th[i].y = 0.f;
+      a.dens[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      a.rot[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      left[i] = lft;
+      right[i] = rgt;
+      redo[atomicAdd(nredo, 1)] = i;
+      atomicMax(hmax_bits, __float_as_uint(hf));
+      return;
+    } else if (hf <= gp.h_min) {
+      h_final = (T)gp.h_min;
+    } else {
+      h_final = (T)gp.h_max;
+      if (has_no_neighbours) {
+        // hydro_part_has_no_neighbours (hydro.h:774-802)
+        const T hinv = (T)1 / h_final;
+        const T hid = hinv * hinv * hinv;
+        rho = (T)vm.w * (T)kRoot * hid;
+        wcount = (T)kRoot * hid;
+        rho_dh = wcount_dh = rot_x = rot_y = rot_z = div_v = (T)0;
+        r.w = 0.f;  // laplace_u
+      }
+    }
+  }
+  const float hf = (float)h_final;
+  pos.w = (double)hf;
+  a.pos[i] = pos;
+  atomicMax(hmax_bits, __float_as_uint(hf));
+  // converged: hydro_prepare_gradient + hydro_reset_gradient (hydro.h:654-733)
+  const T hh = (T)hf;
+  const T curl_v = tsqrt(rot_x * rot_x + rot_y * rot_y + rot_z * rot_z);
+  const T abs_div_v = fabs(div_v);
+  const T pressure = (T)kHydroGammaMinusOne * (T)th.x * rho;
+  const T soundspeed = tsqrt((T)kHydroGamma * pressure / rho);
+  const T balsara =
+      abs_div_v / (abs_div_v + curl_v + (T)0.0001f * soundspeed * (T)gp.fac_B / hh);
+  const T common_factor = hh * (T)kDimInv / wcount;
+  T grad_h_term;
+  if (hh > (T)0.9999f * (T)gp.h_max) {
+    grad_h_term = (T)0;
+  } else {
+    const T grad_W_term = common_factor * wcount_dh;
+    grad_h_term = (grad_W_term < (T)-0.9999f)
+                      ? (T)0
+                      : common_factor * rho_dh / ((T)1 + grad_W_term);
+  }
+  th.y = (float)rho;
+  th.z = (float)pressure;
+  th.w = (float)soundspeed;
+  a.th[i] = th;
+  a.dens[i] = make_float4((float)rho_dh, (float)wcount, (float)wcount_dh, (float)div_v);
+  r.x = (float)rot_x; r.y = (float)rot_y; r.z = (float)rot_z;
+  a.rot[i] = r;
+  float4 fc = a.fc[i];
+  fc.x = (float)grad_h_term;
+  fc.y = (float)balsara;
+  a.fc[i] = fc;
+  float4 g = a.grad[i];
+  g.x = (float)((T)2 * soundspeed);  // v_sig
+  g.y = fc.z;                        // alpha_visc_max_ngb = alpha_visc
+  a.grad[i] = g;
+}
+
+// runner_do_extra_ghost (runner_ghost.c:992-1083): hydro_end_gradient,
+// hydro_prepare_force (hydro.h:823-934), timestep_limiter_prepare_force,
+// hydro_reset_acceleration.
+struct ForcePrepParams {
+  double a, a_factor_sound_speed, a2_inv, time_base;
+  float visc_alpha_max, visc_alpha_min, visc_length;
+  float diff_beta, diff_alpha_max, diff_alpha_min;
+};
+
+template <typename T>
+__global__ void extra_ghost_kernel(SoA a, int64_t n, int max_active_bin, ForcePrepParams fp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int tb = a.tb[i];
+  if (tb > max_active_bin) return;
+  const T h = (T)(float)a.pos[i].w;
+  const T h_inv = (T)1 / h;
+  const T h_inv_dim = h_inv * h_inv * h_inv;
+  const T h_inv_dim_plus_one = h_inv_dim * h_inv;
+  float4 r = a.rot[i];
+  const T laplace_u = (T)r.w * (T)2 * h_inv_dim_plus_one;
+  r.w = (float)laplace_u;
+  a.rot[i] = r;
+  const T dt_alpha =
+      (T)((tb <= 0) ? 0. : (double)(1LL << (tb + 1)) * fp.time_base);  // get_timestep
+  const float4 th = a.th[i];
+  float4 g = a.grad[i];     // v_sig, avmn, div_v_prev, div_v_dt
+  float4 fc = a.fc[i];      // f, balsara, alpha_visc, alpha_diff
+  const T div_v = (T)a.dens[i].w;
+  const T kernel_support_physical = h * (T)fp.a * (T)kGamma;
+  const T kernel_support_physical_inv = (T)1 / kernel_support_physical;
+  const T v_sig_physical = (T)g.x * (T)fp.a_factor_sound_speed;
+  const T pressure = (T)kHydroGammaMinusOne * (T)th.x * (T)th.y;
+  const T soundspeed_physical =
+      tsqrt((T)kHydroGamma * pressure / (T)th.y) * (T)fp.a_factor_sound_speed;
+  const T sound_crossing_time_inverse = soundspeed_physical * kernel_support_physical_inv;
+  const T div_v_dt = dt_alpha == (T)0 ? (T)0 : (div_v - (T)g.z) / dt_alpha;
+  const T S = div_v < (T)0 ? kernel_support_physical * kernel_support_physical *
+                                 tmax((T)0, (T)-1 * div_v_dt)
+                           : (T)0;
+  const T soundspeed_square = soundspeed_physical * soundspeed_physical;
+  const T alpha_loc = (T)fp.visc_alpha_max * S / (soundspeed_square + S);
+  T alpha = fc.z;
+  if (alpha_loc > alpha) {
+    alpha = alpha_loc;
+  } else {
+    const T timescale_ratio = dt_alpha * sound_crossing_time_inverse * (T)fp.visc_length;
+    alpha += alpha_loc * timescale_ratio;
+    alpha /= ((T)1 + timescale_ratio);
+  }
+  alpha = tmax(alpha, (T)fp.visc_alpha_min);
+  g.z = (float)div_v;
+  g.w = (float)div_v_dt;
+  const T diffusion_timescale_physical_inverse = v_sig_physical * kernel_support_physical_inv;
+  const T sqrt_u_inv = (T)1 / tsqrt((T)th.x);
+  T alpha_diff_dt = (T)fp.diff_beta * kernel_support_physical * laplace_u *
+                    (T)fp.a_factor_sound_speed * sqrt_u_inv * (T)fp.a2_inv;
+  alpha_diff_dt -= ((T)fc.w - (T)fp.diff_alpha_min) * diffusion_timescale_physical_inverse;
+  T new_diffusion_alpha = (T)fc.w;
+  new_diffusion_alpha += alpha_diff_dt * dt_alpha;
+  new_diffusion_alpha = tmax(new_diffusion_alpha, (T)fp.diff_alpha_min);
+  const T viscous_diffusion_limit =
+      (T)fp.diff_alpha_max * ((T)1 - (T)g.y / (T)fp.visc_alpha_max);
+  new_diffusion_alpha = tmin(new_diffusion_alpha, viscous_diffusion_limit);
+  fc.z = (float)alpha;
+  fc.w = (float)new_diffusion_alpha;
+  a.fc[i] = fc;
+  a.grad[i] = g;
+  a.mintb[i] = (int8_t)(kNumTimeBins + 1);
+  a.acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  a.hdt[i] = 0.f;
+}
+
+__global__ void end_force_kernel(SoA a, int64_t n, int max_active_bin) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || a.tb[i] > max_active_bin) return;
+  a.hdt[i] = a.hdt[i] * ((float)a.pos[i].w * kDimInv);  // hydro.h:1080-1084
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+static swh_status check_built(swh_space* s) {
+  if (!s) return SWH_ERR_ARG;
+  if (!s->built) {
+    swh::set_error("swh_space_rebuild must precede the loops");
+    return SWH_ERR_STATE;
+  }
+  return SWH_OK;
+}
+
+static unsigned long long* counter_slot(swh_space* s) {
+  return s->counters.as<unsigned long long>();  // slot 0: interactions
+}
+static unsigned int* hmax_slot(swh_space* s) { return s->counters.as<unsigned int>() + 2; }
+
+template <int LOOP>
+static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const int* subset,
+                              int nitems, bool count) {
+  if (nitems <= 0) return SWH_OK;
+  const GridDev gd = grid_dev(s->grid);
+  const int block = 256;
+  const int grid = (nitems + block - 1) / block;
+  const double a2H = P->a * P->a * P->H;
+  unsigned long long* ctr = count ? counter_slot(s) : nullptr;
+  int* ncount = count ? s->ncount.as<int>() : nullptr;
+  if (s->ctx->precision == SWH_PRECISION_F64)
+    hipLaunchKernelGGL((loop_kernel<LOOP, double>), dim3(grid), dim3(block), 0, s->stream, gd,
+                       s->cell_start.as<const int>(), soa_of(s), subset, nitems,
+                       P->max_active_bin, a2H, hmax_slot(s), ctr, ncount);
+  else
+    hipLaunchKernelGGL((loop_kernel<LOOP, float>), dim3(grid), dim3(block), 0, s->stream, gd,
+                       s->cell_start.as<const int>(), soa_of(s), subset, nitems,
+                       P->max_active_bin, (float)a2H, hmax_slot(s), ctr, ncount);
+  SWH_HIP(hipGetLastError());
+  return SWH_OK;
+}
+
+template <int LOOP>
+static swh_status run_loop(swh_space* s, const swh_hydro_params* P, int64_t* n_out) {
+  SWH_TRY(check_built(s));
+  if (!P) return SWH_ERR_ARG;
+  SWH_HIP(hipSetDevice(s->ctx->device));
+  if (n_out) SWH_HIP(hipMemsetAsync(counter_slot(s), 0, sizeof(unsigned long long), s->stream));
+  SWH_TRY(launch_loop<LOOP>(s, P, nullptr, (int)s->n, n_out != nullptr));
+  if (n_out) {
+    unsigned long long h = 0;
+    SWH_HIP(hipMemcpyAsync(&h, counter_slot(s), sizeof(h), hipMemcpyDeviceToHost, s->stream));
+    SWH_HIP(hipStreamSynchronize(s->stream));
+    *n_out = (int64_t)h;
+  }
+  return SWH_OK;
+}
+
+}  // namespace swh
+
+using namespace swh;
+
+extern "C" {
+
+swh_status swh_space_init_parts(swh_space* s, const swh_hydro_params* P) {
+  if (!s || !P) return SWH_ERR_ARG;
+  if (s->n == 0) return SWH_OK;
+  SWH_HIP(hipSetDevice(s->ctx->device));
+  const int block = 256;
+  hipLaunchKernelGGL(init_kernel, dim3((int)((s->n + block - 1) / block)), dim3(block), 0,
+                     s->stream, soa_of(s), s->n, P->max_active_bin);
+  SWH_HIP(hipGetLastError());
+  return SWH_OK;
+}
+
+swh_status swh_density_loop(swh_space* s, const swh_hydro_params* P, int64_t* n) {
+  return run_loop<LOOP_DENSITY>(s, P, n);
+}
+swh_status swh_gradient_loop(swh_space* s, const swh_hydro_params* P, int64_t* n) {
+  return run_loop<LOOP_GRADIENT>(s, P, n);
+}
+swh_status swh_force_loop(swh_space* s, const swh_hydro_params* P, int64_t* n) {
+  return run_loop<LOOP_FORCE>(s, P, n);
+}
+
+swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iterations,
+                     int64_t* n_unconverged) {
+  SWH_TRY(check_built(s));
+  if (!P) return SWH_ERR_ARG;
+  if (iterations) *iterations = 0;
+  if (n_unconverged) *n_unconverged = 0;
+  const int64_t n = s->n;
+  if (n == 0) return SWH_OK;
+  SWH_HIP(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->stream;
+  SWH_TRY(s->ghost_left.reserve(n * sizeof(float)));
+  SWH_TRY(s->ghost_right.reserve(n * sizeof(float)));
+  SWH_TRY(s->ghost_list.reserve(n * sizeof(int)));
+  SWH_TRY(s->ghost_list2.reserve(n * sizeof(int)));
+  int* cnt = s->counters.as<int>() + 4;  // slots 4,5: list counts
+  SWH_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(int), st));
+  const int block = 256;
+  const int nblk = (int)((n + block - 1) / block);
+  hipLaunchKernelGGL(ghost_init_kernel<double>, dim3(nblk), dim3(block), 0, st, soa_of(s), n,
+                     P->max_active_bin, P->h_max, s->ghost_left.as<float>(),
+                     s->ghost_right.as<float>(), s->ghost_list.as<int>(), cnt);
+  SWH_HIP(hipGetLastError());
+  int count = 0;
+  SWH_HIP(hipMemcpyAsync(&count, cnt, sizeof(int), hipMemcpyDeviceToHost, st));
+  SWH_HIP(hipStreamSynchronize(st));
+  GhostParams gp;
+  gp.h_max = P->h_max;
+  gp.h_min = P->h_min;
+  gp.eta_dim = P->eta_neighbours * P->eta_neighbours * P->eta_neighbours;
+  gp.eps = P->h_tolerance;
+  gp.use_mass_weighted = P->use_mass_weighted_num_ngb;
+  gp.a2_inv = P->a2_inv;
+  gp.H = P->H;
+  gp.fac_B = P->a_factor_Balsara_eps;
+  int* list = s->ghost_list.as<int>();
+  int* list2 = s->ghost_list2.as<int>();
+  int it = 0;
+  for (; count > 0 && it < P->max_smoothing_iterations; it++) {
+    SWH_HIP(hipMemsetAsync(cnt + 1, 0, sizeof(int), st));
+    const int g = (count + block - 1) / block;
+    if (s->ctx->precision == SWH_PRECISION_F64)
+      hipLaunchKernelGGL(ghost_kernel<double>, dim3(g), dim3(block), 0, st, soa_of(s), list,
+                         count, list2, cnt + 1, s->ghost_left.as<float>(),
+                         s->ghost_right.as<float>(), gp, hmax_slot(s));
+    else
+      hipLaunchKernelGGL(ghost_kernel<float>, dim3(g), dim3(block), 0, st, soa_of(s), list,
+                         count, list2, cnt + 1, s->ghost_left.as<float>(),
+                         s->ghost_right.as<float>(), gp, hmax_slot(s));
+    SWH_HIP(hipGetLastError());
+    SWH_HIP(hipMemcpyAsync(&count, cnt + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+    SWH_HIP(hipStreamSynchronize(st));
+    std::swap(list, list2);
+    if (count > 0) SWH_TRY(launch_loop<LOOP_DENSITY>(s, P, list, count, false));
+  }
+  if (iterations) *iterations = it;
+  if (n_unconverged) *n_unconverged = count;
+  if (count > 0) {
+    swh::set_error("Smoothing length failed to converge on %d particles.", count);
+    return SWH_ERR_NOT_CONVERGED;
+  }
+  return SWH_OK;
+}
+
+swh_status swh_extra_ghost(swh_space* s, const swh_hydro_params* P) {
+  SWH_TRY(check_built(s));
+  if (!P) return SWH_ERR_ARG;
+  if (s->n == 0) return SWH_OK;
+  SWH_HIP(hipSetDevice(s->ctx->device));
+  ForcePrepParams fp;
+  fp.a = P->a;
+  fp.a_factor_sound_speed = P->a_factor_sound_speed;
+  fp.a2_inv = P->a2_inv;
+  fp.time_base = P->time_base;
+  fp.visc_alpha_max = P->visc_alpha_max;
+  fp.visc_alpha_min = P->visc_alpha_min;
+  fp.visc_length = P->visc_length;
+  fp.diff_beta = P->diff_beta;
+  fp.diff_alpha_max = P->diff_alpha_max;
+  fp.diff_alpha_min = P->diff_alpha_min;
+  const int block = 256;
+  const int g = (int)((s->n + block - 1) / block);
+  if (s->ctx->precision == SWH_PRECISION_F64)
+    hipLaunchKernelGGL(extra_ghost_kernel<double>, dim3(g), dim3(block), 0, s->stream,
+                       soa_of(s), s->n, P->max_active_bin, fp);
+  else
+    hipLaunchKernelGGL(extra_ghost_kernel<float>, dim3(g), dim3(block), 0, s->stream,
+                       soa_of(s), s->n, P->max_active_bin, fp);
+  SWH_HIP(hipGetLastError());
+  return SWH_OK;
+}
+
+swh_status swh_end_force(swh_space* s, const swh_hydro_params* P) {
+  SWH_TRY(check_built(s));
+  if (!P) return SWH_ERR_ARG;
+  if (s->n == 0) return SWH_OK;
+  SWH_HIP(hipSetDevice(s->ctx->device));
+  const int block = 256;
+  hipLaunchKernelGGL(end_force_kernel, dim3((int)((s->n + block - 1) / block)), dim3(block),
+                     0, s->stream, soa_of(s), s->n, P->max_active_bin);
+  SWH_HIP(hipGetLastError());
+  return SWH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,194 @@
+// swh_internal.h — host/device shared internals of libswifthip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "swifthip.h"
+
+namespace swh {
+
+// ---------------------------------------------------------------------------
+// Errors: thread-local message + status codes, no aborts.
+// ---------------------------------------------------------------------------
+void set_error(const char* fmt, ...);
+
+#define SWH_HIP(call)                                                           \
+  do {                                                                          \
+    hipError_t _e = (call);                                                     \
+    if (_e != hipSuccess) {                                                     \
+      ::swh::set_error("%s failed: %s (%s:%d)", #call, hipGetErrorString(_e),   \
+                       __FILE__, __LINE__);                                     \
+      return (_e == hipErrorOutOfMemory) ? SWH_ERR_OOM : SWH_ERR_HIP;           \
+    }                                                                           \
+  } while (0)
+
+#define SWH_TRY(expr)                      \
+  do {                                     \
+    swh_status _s = (expr);                \
+    if (_s != SWH_OK) return _s;           \
+  } while (0)
+
+// Growable device buffer (never shrinks; reused across calls so the loops do
+// no allocation once warm).
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  swh_status reserve(size_t b) {
+    if (b <= bytes) return SWH_OK;
+    if (ptr) {
+      hipError_t e = hipFree(ptr);
+      (void)e;
+      ptr = nullptr;
+      bytes = 0;
+    }
+    size_t nb = b < 256 ? 256 : b;
+    hipError_t e = hipMalloc(&ptr, nb);
+    if (e != hipSuccess) {
+      set_error("hipMalloc(%zu) failed: %s", nb, hipGetErrorString(e));
+      return SWH_ERR_OOM;
+    }
+    bytes = nb;
+    return SWH_OK;
+  }
+  void release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+  }
+  template <typename T>
+  T* as() const { return reinterpret_cast<T*>(ptr); }
+};
+
+// Pinned host staging buffer.
+struct HostBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  swh_status reserve(size_t b) {
+    if (b <= bytes) return SWH_OK;
+    if (ptr) (void)hipHostFree(ptr);
+    ptr = nullptr;
+    size_t nb = b < 4096 ? 4096 : b;
+    hipError_t e = hipHostMalloc(&ptr, nb, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      set_error("hipHostMalloc(%zu) failed: %s", nb, hipGetErrorString(e));
+      bytes = 0;
+      return SWH_ERR_OOM;
+    }
+    bytes = nb;
+    return SWH_OK;
+  }
+  void release() {
+    if (ptr) (void)hipHostFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+  }
+};
+
+// Device copy of the AoS layout (offsets), passed by value to kernels.
+struct Layout {
+  int stride;
+  int id, x, v, a_hydro, mass, h, u, u_dt, rho;
+  int div_v, div_v_dt, div_v_prev, visc_alpha, v_sig;
+  int laplace_u, diff_alpha;
+  int wcount, wcount_dh, rho_dh, rot_v;
+  int f, pressure, soundspeed, h_dt, balsara, avmn;
+  int time_bin, min_tb;
+};
+swh_status make_layout(const swh_part_layout* L, Layout* out);
+
+struct GLayout {
+  int stride, x, a_grav, potential, mass, epsilon, time_bin;
+};
+swh_status make_glayout(const swh_gpart_layout* L, GLayout* out);
+
+// Per-task worker: one stream + staging buffers, leased per host thread.
+struct TaskWorker {
+  hipStream_t stream = nullptr;
+  DevBuf dparts, dparts2, dind, dself, dcount;
+  HostBuf hstage, hstage2;
+  std::mutex busy;
+};
+
+}  // namespace swh
+
+struct swh_context {
+  int device = 0;
+  swh_precision precision = SWH_PRECISION_F64;
+  int num_cus = 256;
+  std::mutex lease_mutex;
+  std::vector<swh::TaskWorker*> workers;
+  swh::TaskWorker* lease();
+  void unlease(swh::TaskWorker* w);
+};
+
+// Neighbour grid of the batch path.
+struct SwhGrid {
+  int cdim[3] = {0, 0, 0};
+  double w[3] = {0, 0, 0};       // cell widths
+  double origin[3] = {0, 0, 0};  // lower corner of the gridded domain
+  double dim[3] = {0, 0, 0};     // box (periodic) or domain extent
+  int periodic = 0;
+  int ncell = 0;
+  double hmax = 0;  // max H = gamma*h over all particles at rebuild
+};
+
+// Device-resident particle set, sorted by grid cell (x fastest).
+struct swh_space {
+  swh_context* ctx = nullptr;
+  hipStream_t stream = nullptr;
+  bool own_stream = true;
+  int64_t n = 0;
+  bool built = false;
+  SwhGrid grid;
+  swh_tuning tuning{1, 0};
+
+  // AoS image of the caller's records (for write-back of untouched fields)
+  swh::DevBuf aos;
+  swh::Layout layout{};
+
+  // sorted SoA (j-records packed for gathers)
+  swh::DevBuf pos;   // double4 x,y,z,h
+  swh::DevBuf vm;    // float4 vx,vy,vz,m
+  swh::DevBuf th;    // float4 u,rho,P,c
+  swh::DevBuf fc;    // float4 f,balsara,alpha_visc,alpha_diff
+  swh::DevBuf tb;    // int8 time_bin
+  // i-side state/outputs (sorted order), float unless noted
+  swh::DevBuf dens;  // float4 rho_dh, wcount, wcount_dh, div_v
+  swh::DevBuf rot;   // float4 rot_x, rot_y, rot_z, laplace_u
+  swh::DevBuf grad;  // float4 v_sig, alpha_visc_max_ngb, div_v_prev, div_v_dt
+  swh::DevBuf acc;   // float4 ax, ay, az, u_dt
+  swh::DevBuf hdt;   // float h_dt
+  swh::DevBuf mintb; // int8 min_ngb_time_bin
+  swh::DevBuf perm;  // int32 sorted index -> caller index
+  swh::DevBuf ncount;  // int32 per-particle interaction count (diagnostic)
+  // grid
+  swh::DevBuf cell_start;  // int32[ncell+1]
+  // scratch
+  swh::DevBuf keys, keys2, idx, idx2, sort_tmp, scan_tmp, counters;
+  swh::DevBuf tmp_soa;     // staging for permutation gathers
+  swh::DevBuf ghost_left, ghost_right, ghost_list, ghost_list2, ghost_flag;
+  swh::HostBuf hstage;
+};
+
+struct swh_gspace {
+  swh_context* ctx = nullptr;
+  hipStream_t stream = nullptr;
+  int64_t n = 0;
+  swh::DevBuf aos;
+  swh::GLayout layout{};
+  swh::DevBuf pos;     // double4 x,y,z,eps
+  swh::DevBuf mass;    // float  mass (0 for inhibited)
+  swh::DevBuf active;  // int8
+  swh::DevBuf accel;   // double4 ax, ay, az, pot (accumulated this call)
+  swh::DevBuf leaves, pair_off, pairs;
+  int32_t nleaves = 0, npairs = 0;
+  int32_t max_leaf = 0;
+  swh::DevBuf counter;
+};

@@ -1,0 +1,257 @@
+// swh_physics.h — device-side SPHENIX / cubic-spline / Wendland-C2 physics,
+// templated on the arithmetic type T (double = the fp64 path, float = the
+// reference's own precision). Constants are the reference's float values
+// (same expressions as the macros they cite), promoted to T.
+//
+// References (/root/reference/src):
+//   kernel_hydro.h:45-64,195-284   cubic spline, kernel_deval
+//   hydro/SPHENIX/hydro_iact.h     runner_iact_nonsym_{density,gradient,force}
+//   hydro/SPHENIX/hydro.h          end_density / prepare_gradient / prepare_force ...
+//   kernel_gravity.h:48-100, kernel_long_gravity.h:204-262, gravity/MultiSoftening/gravity_iact.h
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cfloat>
+#include <cstdint>
+
+namespace swh {
+
+// --- constants: cubic spline, 3D, gamma = 5/3 -----------------------------
+constexpr double kPi = 3.14159265358979323846;
+constexpr float kGamma = (float)(1.825742);
+constexpr float kGammaInv = (float)(1. / kGamma);
+constexpr float kGamma2 = kGamma * kGamma;
+constexpr float kConstant = (float)(16. * (1. / kPi));
+constexpr float kGammaInvDim = (float)(1. / (kGamma * kGamma * kGamma));
+constexpr float kGammaInvDimPlusOne = (float)(1. / (kGamma * kGamma * kGamma * kGamma));
+constexpr float kRoot = 0.5f * kConstant * kGammaInvDim;  // W(0)
+constexpr float kDim = 3.f;
+constexpr float kDimInv = 0.3333333333f;
+constexpr float kHydroGamma = 1.66666666666666667f;
+constexpr float kHydroGammaMinusOne = 0.66666666666666667f;
+constexpr float kViscBeta = 3.0f;
+constexpr int kNumTimeBins = 56;
+constexpr int kTimeBinInhibited = kNumTimeBins + 2;
+
+template <typename T>
+__device__ __forceinline__ T tmax(T a, T b) { return a > b ? a : b; }
+template <typename T>
+__device__ __forceinline__ T tmin(T a, T b) { return a < b ? a : b; }
+
+template <typename T> __device__ __forceinline__ T tsqrt(T x);
+template <> __device__ __forceinline__ double tsqrt<double>(double x) { return sqrt(x); }
+template <> __device__ __forceinline__ float tsqrt<float>(float x) { return sqrtf(x); }
+
+// kernel_deval (kernel_hydro.h:257-284). Branch 0: u/H < 1/2, branch 1: < 1,
+// branch 2 (outside support): all-zero coefficients. Coefficients are picked
+// with selects instead of a table load.
+template <typename T>
+__device__ __forceinline__ void kernel_deval(T u, T& W, T& dW_dx) {
+  const T x = u * (T)kGammaInv;
+  const int temp = (int)(x * (T)2);
+  const int ind = temp > 2 ? 2 : temp;
+  const T c0 = ind == 0 ? (T)3 : (ind == 1 ? (T)-1 : (T)0);
+  const T c1 = ind == 0 ? (T)-3 : (ind == 1 ? (T)3 : (T)0);
+  const T c2 = ind == 0 ? (T)0 : (ind == 1 ? (T)-3 : (T)0);
+  const T c3 = ind == 0 ? (T)0.5 : (ind == 1 ? (T)1 : (T)0);
+  T w = c0 * x + c1;
+  T dw = c0;
+  dw = dw * x + w;
+  w = x * w + c2;
+  dw = dw * x + w;
+  w = x * w + c3;
+  w = tmax(w, (T)0);
+  dw = tmin(dw, (T)0);
+  W = w * (T)kConstant * (T)kGammaInvDim;
+  dW_dx = dw * (T)kConstant * (T)kGammaInvDimPlusOne;
+}
+
+// ---------------------------------------------------------------------------
+// Accumulators of one i-particle for each loop (registers for the duration of
+// the gather).
+// ---------------------------------------------------------------------------
+template <typename T>
+struct DensityAcc {
+  T rho, rho_dh, wcount, wcount_dh, div_v, rot_x, rot_y, rot_z;
+  __device__ void zero() { rho = rho_dh = wcount = wcount_dh = div_v = rot_x = rot_y = rot_z = (T)0; }
+};
+
+// runner_iact_nonsym_density (hydro_iact.h:130-178). dx = x_i - x_j.
+template <typename T>
+__device__ __forceinline__ void iact_nonsym_density(T r2, T dx, T dy, T dz, T hi_inv,
+                                                    T vix, T viy, T viz, T mj, T vjx,
+                                                    T vjy, T vjz, DensityAcc<T>& A) {
+  const T r = tsqrt(r2);
+  const T ui = r * hi_inv;
+  T wi, wi_dx;
+  kernel_deval(ui, wi, wi_dx);
+  A.rho += mj * wi;
+  A.rho_dh -= mj * ((T)kDim * wi + ui * wi_dx);
+  A.wcount += wi;
+  A.wcount_dh -= ((T)kDim * wi + ui * wi_dx);
+  const T r_inv = r > (T)0 ? (T)1 / r : (T)0;
+  const T faci = mj * wi_dx * r_inv;
+  const T dvx = vix - vjx, dvy = viy - vjy, dvz = viz - vjz;
+  const T dvdr = dvx * dx + dvy * dy + dvz * dz;
+  A.div_v -= faci * dvdr;
+  A.rot_x += faci * (dvy * dz - dvz * dy);
+  A.rot_y += faci * (dvz * dx - dvx * dz);
+  A.rot_z += faci * (dvx * dy - dvy * dx);
+}
+
+template <typename T>
+struct GradientAcc {
+  T v_sig, laplace_u, alpha_visc_max_ngb;
+};
+
+// runner_iact_nonsym_gradient (hydro_iact.h:276-329); signal velocity
+// hydro.h:490-498 with beta = const_viscosity_beta; gamma=5/3 -> fac_mu = 1.
+template <typename T>
+__device__ __forceinline__ void iact_nonsym_gradient(T r2, T dx, T dy, T dz, T hi,
+                                                     T vix, T viy, T viz, T ui_energy,
+                                                     T ci, T mj, T vjx, T vjy, T vjz,
+                                                     T uj_energy, T rhoj, T cj,
+                                                     T alphaj, T a2_Hubble,
+                                                     GradientAcc<T>& A) {
+  const T r = tsqrt(r2);
+  const T r_inv = r > (T)0 ? (T)1 / r : (T)0;
+  const T dvdr = (vix - vjx) * dx + (viy - vjy) * dy + (viz - vjz) * dz;
+  const T dvdr_Hubble = dvdr + a2_Hubble * r2;
+  const T omega_ij = tmin(dvdr_Hubble, (T)0);
+  const T mu_ij = r_inv * omega_ij;
+  const T new_v_sig = ci + cj - (T)kViscBeta * mu_ij;
+  A.v_sig = tmax(A.v_sig, new_v_sig);
+  T wi, wi_dx;
+  const T ui = r / hi;
+  kernel_deval(ui, wi, wi_dx);
+  const T delta_u_factor = (ui_energy - uj_energy) * r_inv;
+  A.laplace_u += mj * delta_u_factor * wi_dx / rhoj;
+  A.alpha_visc_max_ngb = tmax(A.alpha_visc_max_ngb, alphaj);
+}
+
+// Per-particle force-side inputs (i or j).
+template <typename T>
+struct ForceIn {
+  T m, h, rho, P, c, f, balsara, alpha_visc, alpha_diff, u;
+  T vx, vy, vz;
+};
+
+template <typename T>
+struct ForceAcc {
+  T ax, ay, az, u_dt, h_dt;
+  int min_ngb_time_bin;
+};
+
+// runner_iact_nonsym_force (hydro_iact.h:488-609). dx = x_i - x_j.
+template <typename T>
+__device__ __forceinline__ void iact_nonsym_force(T r2, T dx, T dy, T dz,
+                                                  const ForceIn<T>& I, T hid_inv,
+                                                  T hi_inv, const ForceIn<T>& J,
+                                                  T a2_Hubble, ForceAcc<T>& A) {
+  const T r = tsqrt(r2);
+  const T r_inv = r > (T)0 ? (T)1 / r : (T)0;
+  const T mi = I.m, mj = J.m;
+  const T rhoi = I.rho, rhoj = J.rho;
+  const T pressurei = I.P, pressurej = J.P;
+  const T xi = r * hi_inv;
+  T wi, wi_dx;
+  kernel_deval(xi, wi, wi_dx);
+  const T wi_dr = hid_inv * wi_dx;
+  const T hj_inv = (T)1 / J.h;
+  const T hj2 = hj_inv * hj_inv;
+  const T hjd_inv = hj2 * hj2;
+  const T xj = r * hj_inv;
+  T wj, wj_dx;
+  kernel_deval(xj, wj, wj_dx);
+  const T wj_dr = hjd_inv * wj_dx;
+  const T dvdr = (I.vx - J.vx) * dx + (I.vy - J.vy) * dy + (I.vz - J.vz) * dz;
+  const T dvdr_Hubble = dvdr + a2_Hubble * r2;
+  const T omega_ij = tmin(dvdr_Hubble, (T)0);
+  const T mu_ij = r_inv * omega_ij;
+  const T v_sig = I.c + J.c - (T)kViscBeta * mu_ij;
+  const T f_ij = (T)1 - I.f / mj;
+  const T f_ji = (T)1 - J.f / mi;
+  const T rho_ij = rhoi + rhoj;
+  const T alpha = I.alpha_visc + J.alpha_visc;
+  const T visc = (T)-0.25 * alpha * v_sig * mu_ij * (I.balsara + J.balsara) / rho_ij;
+  const T visc_acc_term = (T)0.5 * visc * (wi_dr * f_ij + wj_dr * f_ji) * r_inv;
+  const T P_over_rho2_i = pressurei / (rhoi * rhoi) * f_ij;
+  const T P_over_rho2_j = pressurej / (rhoj * rhoj) * f_ji;
+  const T sph_acc_term = (P_over_rho2_i * wi_dr + P_over_rho2_j * wj_dr) * r_inv;
+  const T acc = sph_acc_term + visc_acc_term;
+  A.ax -= mj * acc * dx;
+  A.ay -= mj * acc * dy;
+  A.az -= mj * acc * dz;
+  const T sph_du_term_i = P_over_rho2_i * dvdr * r_inv * wi_dr;
+  const T visc_du_term = (T)0.5 * visc_acc_term * dvdr_Hubble;
+  const T alpha_diff = (pressurei * I.alpha_diff + pressurej * J.alpha_diff) /
+                       (pressurei + pressurej);
+  const T v_diff = alpha_diff * (T)0.5 *
+                   (tsqrt((T)2 * fabs(pressurei - pressurej) / rho_ij) +
+                    fabs(r_inv * dvdr_Hubble));
+  const T diff_du_term =
+      v_diff * (I.u - J.u) * (f_ij * wi_dr / rhoi + f_ji * wj_dr / rhoj);
+  const T du_dt_i = sph_du_term_i + visc_du_term + diff_du_term;
+  A.u_dt += du_dt_i * mj;
+  A.h_dt -= mj * dvdr * r_inv / rhoj * wi_dr;
+}
+
+// ---------------------------------------------------------------------------
+// Gravity (Wendland-C2 softening, erfc-like long-range truncation)
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T grav_pot_eval(T u) {  // kernel_gravity.h:48-70
+  T W = (T)3 * u - (T)15;
+  W = W * u + (T)28;
+  W = W * u - (T)21;
+  W = W * u;
+  W = W * u + (T)7;
+  W = W * u;
+  W = W * u - (T)3;
+  return W;
+}
+template <typename T>
+__device__ __forceinline__ T grav_force_eval(T u) {  // kernel_gravity.h:79-100
+  T W = (T)21 * u - (T)90;
+  W = W * u + (T)140;
+  W = W * u - (T)84;
+  W = W * u;
+  W = W * u + (T)14;
+  return W;
+}
+
+template <typename T> __device__ __forceinline__ T texp(T x);
+template <> __device__ __forceinline__ double texp<double>(double x) { return exp(x); }
+template <> __device__ __forceinline__ float texp<float>(float x) { return expf(x); }
+
+// runner_iact_grav_pp_full / _truncated (gravity_iact.h:47-135)
+template <typename T, bool TRUNC>
+__device__ __forceinline__ void iact_grav_pp(T r2, T h2, T h_inv, T h_inv3, T mass,
+                                             T r_s_inv, T& f_ij, T& pot_ij) {
+  const T r_inv = (T)1 / tsqrt(r2 + (T)FLT_MIN);
+  if (r2 >= h2) {
+    f_ij = mass * r_inv * r_inv * r_inv;
+    pot_ij = -mass * r_inv;
+  } else {
+    const T r = r2 * r_inv;
+    const T ui = r * h_inv;
+    f_ij = mass * h_inv3 * grav_force_eval(ui);
+    pot_ij = mass * h_inv * grav_pot_eval(ui);
+  }
+  if (TRUNC) {
+    const T r = r2 * r_inv;
+    const T x = (T)2 * (r * r_s_inv);
+    const T exp_x = texp(x);
+    const T alpha = (T)1 / ((T)1 + exp_x);
+    T W = (T)1 - alpha * exp_x;
+    const T corr_pot = W * (T)2;
+    W = (T)1 - alpha;
+    W = W * x - exp_x;
+    W = W * alpha + (T)1;
+    const T corr_f = W * (T)2;
+    f_ij *= corr_f;
+    pot_ij *= corr_pot;
+  }
+}
+
+}  // namespace swh

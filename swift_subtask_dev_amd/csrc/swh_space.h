@@ -1,0 +1,50 @@
+// swh_space.h — device views of the batch-path particle set and grid.
+#pragma once
+
+#include "swh_internal.h"
+
+namespace swh {
+
+// Sorted SoA arrays of a swh_space (device pointers, passed by value).
+struct SoA {
+  double4* pos;   // x, y, z, h
+  float4* vm;     // vx, vy, vz, mass
+  float4* th;     // u, rho, pressure, soundspeed
+  float4* fc;     // f (grad-h), balsara, alpha_visc, alpha_diff
+  int8_t* tb;     // time_bin
+  float4* dens;   // rho_dh, wcount, wcount_dh, div_v
+  float4* rot;    // rot_v[3], laplace_u
+  float4* grad;   // v_sig, alpha_visc_max_ngb, div_v_previous_step, div_v_dt
+  float4* acc;    // a_hydro[3], u_dt
+  float* hdt;     // h_dt
+  int8_t* mintb;  // limiter min_ngb_time_bin
+  int* perm;      // sorted index -> caller index
+};
+
+struct GridDev {
+  int cdim[3];
+  int periodic;
+  double w[3];
+  double inv_w[3];
+  double origin[3];
+  double dim[3];
+};
+
+inline GridDev grid_dev(const SwhGrid& g) {
+  GridDev d;
+  for (int k = 0; k < 3; k++) {
+    d.cdim[k] = g.cdim[k];
+    d.w[k] = g.w[k];
+    d.inv_w[k] = 1.0 / g.w[k];
+    d.origin[k] = g.origin[k];
+    d.dim[k] = g.dim[k];
+  }
+  d.periodic = g.periodic;
+  return d;
+}
+
+SoA soa_of(swh_space* s);
+// Recompute max h over the set into the device slot counters[2] (float bits).
+swh_status space_hmax_to_device(swh_space* s);
+
+}  // namespace swh

@@ -1,0 +1,507 @@
+// swh_space.hip — device-resident particle set of the batch path:
+// AoS <-> SoA marshalling (the caller keeps SWIFT's struct part layout), and
+// the neighbour-grid rebuild that replaces space_rebuild + runner_do_hydro_sort
+// (src/space.c, src/runner_sort.c:201-431) for this path: particles are
+// binned into a uniform grid of cells of width >= max(H)/cell_factor and
+// stably radix-sorted by cell index (x fastest), so every grid row is one
+// contiguous range of the SoA arrays.
+#include <hipcub/hipcub.hpp>
+
+#include "swh_internal.h"
+#include "swh_physics.h"
+#include "swh_space.h"
+
+namespace swh {
+
+__device__ __forceinline__ float aos_f(const char* r, int off) {
+  return off >= 0 ? *reinterpret_cast<const float*>(r + off) : 0.f;
+}
+
+__global__ void unpack_kernel(Layout L, const char* __restrict__ aos, int64_t n, SoA a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const char* r = aos + i * L.stride;
+  const double* x = reinterpret_cast<const double*>(r + L.x);
+  a.pos[i] = make_double4(x[0], x[1], x[2], (double)aos_f(r, L.h));
+  a.vm[i] = make_float4(aos_f(r, L.v), aos_f(r, L.v + 4), aos_f(r, L.v + 8), aos_f(r, L.mass));
+  a.th[i] = make_float4(aos_f(r, L.u), aos_f(r, L.rho), aos_f(r, L.pressure),
+                        aos_f(r, L.soundspeed));
+  a.fc[i] = make_float4(aos_f(r, L.f), aos_f(r, L.balsara), aos_f(r, L.visc_alpha),
+                        aos_f(r, L.diff_alpha));
+  a.tb[i] = *reinterpret_cast<const int8_t*>(r + L.time_bin);
+  a.dens[i] = make_float4(aos_f(r, L.rho_dh), aos_f(r, L.wcount), aos_f(r, L.wcount_dh),
+                          aos_f(r, L.div_v));
+  a.rot[i] = make_float4(aos_f(r, L.rot_v), aos_f(r, L.rot_v + 4), aos_f(r, L.rot_v + 8),
+                         aos_f(r, L.laplace_u));
+  a.grad[i] = make_float4(aos_f(r, L.v_sig), aos_f(r, L.avmn), aos_f(r, L.div_v_prev),
+                          aos_f(r, L.div_v_dt));
+  a.acc[i] = make_float4(aos_f(r, L.a_hydro), aos_f(r, L.a_hydro + 4),
+                         aos_f(r, L.a_hydro + 8), aos_f(r, L.u_dt));
+  a.hdt[i] = aos_f(r, L.h_dt);
+  a.mintb[i] = L.min_tb >= 0 ? *reinterpret_cast<const int8_t*>(r + L.min_tb) : (int8_t)0;
+  a.perm[i] = (int)i;
+}
+
+__device__ __forceinline__ void put_f(char* r, int off, float v) {
+  if (off >= 0) *reinterpret_cast<float*>(r + off) = v;
+}
+
+__global__ void pack_kernel(Layout L, char* __restrict__ aos, int64_t n, SoA a, int fields) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  char* r = aos + (int64_t)a.perm[s] * L.stride;
+  const double4 p = a.pos[s];
+  const float4 th = a.th[s];
+  if (fields & SWH_FIELDS_DENSITY) {
+    const float4 d = a.dens[s];
+    const float4 rt = a.rot[s];
+    put_f(r, L.h, (float)p.w);
+    put_f(r, L.rho, th.y);
+    put_f(r, L.rho_dh, d.x);
+    put_f(r, L.wcount, d.y);
+    put_f(r, L.wcount_dh, d.z);
+    put_f(r, L.div_v, d.w);
+    put_f(r, L.rot_v, rt.x);
+    put_f(r, L.rot_v + 4, rt.y);
+    put_f(r, L.rot_v + 8, rt.z);
+    put_f(r, L.laplace_u, rt.w);
+  }
+  if (fields & SWH_FIELDS_GRADIENT) {
+    const float4 d = a.dens[s];
+    const float4 rt = a.rot[s];
+    const float4 g = a.grad[s];
+    const float4 fc = a.fc[s];
+    put_f(r, L.h, (float)p.w);
+    put_f(r, L.rho, th.y);
+    put_f(r, L.div_v, d.w);
+    put_f(r, L.laplace_u, rt.w);
+    put_f(r, L.v_sig, g.x);
+    put_f(r, L.avmn, g.y);
+    put_f(r, L.div_v_prev, g.z);
+    put_f(r, L.div_v_dt, g.w);
+    put_f(r, L.f, fc.x);
+    put_f(r, L.balsara, fc.y);
+    put_f(r, L.visc_alpha, fc.z);
+    put_f(r, L.diff_alpha, fc.w);
+    put_f(r, L.pressure, th.z);
+    put_f(r, L.soundspeed, th.w);
+  }
+  if (fields & SWH_FIELDS_FORCE) {
+    const float4 ac = a.acc[s];
+    put_f(r, L.a_hydro, ac.x);
+    put_f(r, L.a_hydro + 4, ac.y);
+    put_f(r, L.a_hydro + 8, ac.z);
+    put_f(r, L.u_dt, ac.w);
+    put_f(r, L.h_dt, a.hdt[s]);
+    if (L.min_tb >= 0) *reinterpret_cast<int8_t*>(r + L.min_tb) = a.mintb[s];
+  }
+}
+
+// Per-block partial bounding box + max h over non-inhibited particles.
+__global__ void bbox_kernel(const double4* __restrict__ pos, const int8_t* __restrict__ tb,
+                            int64_t n, double* out) {
+  __shared__ double red[7][256];
+  double v[7] = {1e300, 1e300, 1e300, -1e300, -1e300, -1e300, 0.};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (tb[i] == kTimeBinInhibited) continue;
+    const double4 p = pos[i];
+    v[0] = fmin(v[0], p.x); v[1] = fmin(v[1], p.y); v[2] = fmin(v[2], p.z);
+    v[3] = fmax(v[3], p.x); v[4] = fmax(v[4], p.y); v[5] = fmax(v[5], p.z);
+    v[6] = fmax(v[6], p.w);
+  }
+  for (int k = 0; k < 7; k++) red[k][threadIdx.x] = v[k];
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      for (int k = 0; k < 3; k++)
+        red[k][threadIdx.x] = fmin(red[k][threadIdx.x], red[k][threadIdx.x + s]);
+      for (int k = 3; k < 7; k++)
+        red[k][threadIdx.x] = fmax(red[k][threadIdx.x], red[k][threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 7; k++) out[blockIdx.x * 7 + k] = red[k][0];
+}
+
+// Inhibited particles get key = ncell: they sort behind every cell and are
+// never visited as neighbours (the loops' part_is_inhibited skip).
+__global__ void key_kernel(GridDev g, double4* __restrict__ pos, const int8_t* __restrict__ tb,
+                           int64_t n, int ncell, uint32_t* __restrict__ keys,
+                           int* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  idx[i] = (int)i;
+  if (tb[i] == kTimeBinInhibited) {
+    keys[i] = (uint32_t)ncell;
+    return;
+  }
+  double4 p = pos[i];
+  if (g.periodic) {  // box-wrap as space_rebuild does
+    p.x -= floor(p.x / g.dim[0]) * g.dim[0];
+    p.y -= floor(p.y / g.dim[1]) * g.dim[1];
+    p.z -= floor(p.z / g.dim[2]) * g.dim[2];
+    if (p.x >= g.dim[0]) p.x = 0.;
+    if (p.y >= g.dim[1]) p.y = 0.;
+    if (p.z >= g.dim[2]) p.z = 0.;
+    pos[i] = p;
+  }
+  int c[3];
+  const double xs[3] = {p.x, p.y, p.z};
+  for (int k = 0; k < 3; k++) {
+    int ck = (int)floor((xs[k] - g.origin[k]) * g.inv_w[k]);
+    ck = ck < 0 ? 0 : (ck >= g.cdim[k] ? g.cdim[k] - 1 : ck);
+    c[k] = ck;
+  }
+  keys[i] = (uint32_t)((c[2] * g.cdim[1] + c[1]) * g.cdim[0] + c[0]);
+}
+
+// Gather every SoA array through the sort permutation (src -> dst).
+__global__ void permute_kernel(SoA src, SoA dst, const int* __restrict__ idx, int64_t n) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const int i = idx[s];
+  dst.pos[s] = src.pos[i];
+  dst.vm[s] = src.vm[i];
+  dst.th[s] = src.th[i];
+  dst.fc[s] = src.fc[i];
+  dst.tb[s] = src.tb[i];
+  dst.dens[s] = src.dens[i];
+  dst.rot[s] = src.rot[i];
+  dst.grad[s] = src.grad[i];
+  dst.acc[s] = src.acc[i];
+  dst.hdt[s] = src.hdt[i];
+  dst.mintb[s] = src.mintb[i];
+  dst.perm[s] = src.perm[i];
+}
+
+// cell_start[c] = first sorted index with key >= c (c in [0, ncell]).
+__global__ void cell_start_kernel(const uint32_t* __restrict__ keys, int64_t n, int ncell,
+                                  int* __restrict__ start) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  const int64_t prev = (i == 0) ? -1 : (int64_t)keys[i - 1];
+  const int64_t cur = (i == n) ? (int64_t)ncell : (int64_t)keys[i];
+  for (int64_t c = prev + 1; c <= cur; c++) start[c] = (int)i;
+}
+
+__global__ void hmax_kernel(const double4* __restrict__ pos, const int8_t* __restrict__ tb,
+                            int64_t n, unsigned int* out_bits) {
+  float m = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    if (tb[i] != kTimeBinInhibited) m = fmaxf(m, (float)pos[i].w);
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(out_bits, __float_as_uint(m));
+}
+
+}  // namespace swh
+
+using namespace swh;
+
+// ---------------------------------------------------------------------------
+// SoA views
+// ---------------------------------------------------------------------------
+namespace swh {
+
+SoA soa_of(swh_space* s) {
+  SoA a;
+  a.pos = s->pos.as<double4>();
+  a.vm = s->vm.as<float4>();
+  a.th = s->th.as<float4>();
+  a.fc = s->fc.as<float4>();
+  a.tb = s->tb.as<int8_t>();
+  a.dens = s->dens.as<float4>();
+  a.rot = s->rot.as<float4>();
+  a.grad = s->grad.as<float4>();
+  a.acc = s->acc.as<float4>();
+  a.hdt = s->hdt.as<float>();
+  a.mintb = s->mintb.as<int8_t>();
+  a.perm = s->perm.as<int>();
+  return a;
+}
+
+static size_t soa_bytes_per_part() {
+  return sizeof(double4) + 7 * sizeof(float4) + sizeof(float) + 2 * sizeof(int8_t) +
+         sizeof(int);
+}
+
+// Carve a SoA view out of one contiguous scratch buffer.
+static SoA soa_carve(char* base, int64_t n) {
+  SoA a;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* p = base + off;
+    off += (bytes + 255) & ~size_t(255);
+    return p;
+  };
+  a.pos = reinterpret_cast<double4*>(take(n * sizeof(double4)));
+  a.vm = reinterpret_cast<float4*>(take(n * sizeof(float4)));
+  a.th = reinterpret_cast<float4*>(take(n * sizeof(float4)));
+  a.fc = reinterpret_cast<float4*>(take(n * sizeof(float4)));
+  a.dens = reinterpret_cast<float4*>(take(n * sizeof(float4)));
+  a.rot = reinterpret_cast<float4*>(take(n * sizeof(float4)));
+  a.grad = reinterpret_cast<float4*>(take(n * sizeof(float4)));
+  a.acc = reinterpret_cast<float4*>(take(n * sizeof(float4)));
+  a.hdt = reinterpret_cast<float*>(take(n * sizeof(float)));
+  a.perm = reinterpret_cast<int*>(take(n * sizeof(int)));
+  a.tb = reinterpret_cast<int8_t*>(take(n));
+  a.mintb = reinterpret_cast<int8_t*>(take(n));
+  return a;
+}
+
+static swh_status copy_soa(const SoA& src, swh_space* s, hipStream_t st) {
+  const int64_t n = s->n;
+  SWH_HIP(hipMemcpyAsync(s->pos.ptr, src.pos, n * sizeof(double4), hipMemcpyDeviceToDevice, st));
+  SWH_HIP(hipMemcpyAsync(s->vm.ptr, src.vm, n * sizeof(float4), hipMemcpyDeviceToDevice, st));
+  SWH_HIP(hipMemcpyAsync(s->th.ptr, src.th, n * sizeof(float4), hipMemcpyDeviceToDevice, st));
+  SWH_HIP(hipMemcpyAsync(s->fc.ptr, src.fc, n * sizeof(float4), hipMemcpyDeviceToDevice, st));
+  SWH_HIP(hipMemcpyAsync(s->tb.ptr, src.tb, n, hipMemcpyDeviceToDevice, st));
+  SWH_HIP(hipMemcpyAsync(s->dens.ptr, src.dens, n * sizeof(float4), hipMemcpyDeviceToDevice, st));
+  SWH_HIP(hipMemcpyAsync(s->rot.ptr, src.rot, n * sizeof(float4), hipMemcpyDeviceToDevice, st));
+  SWH_HIP(hipMemcpyAsync(s->grad.ptr, src.grad, n * sizeof(float4), hipMemcpyDeviceToDevice, st));
+  SWH_HIP(hipMemcpyAsync(s->acc.ptr, src.acc, n * sizeof(float4), hipMemcpyDeviceToDevice, st));
+  SWH_HIP(hipMemcpyAsync(s->hdt.ptr, src.hdt, n * sizeof(float), hipMemcpyDeviceToDevice, st));
+  SWH_HIP(hipMemcpyAsync(s->mintb.ptr, src.mintb, n, hipMemcpyDeviceToDevice, st));
+  SWH_HIP(hipMemcpyAsync(s->perm.ptr, src.perm, n * sizeof(int), hipMemcpyDeviceToDevice, st));
+  return SWH_OK;
+}
+
+static swh_status reserve_soa(swh_space* s, int64_t n) {
+  SWH_TRY(s->pos.reserve(n * sizeof(double4)));
+  SWH_TRY(s->vm.reserve(n * sizeof(float4)));
+  SWH_TRY(s->th.reserve(n * sizeof(float4)));
+  SWH_TRY(s->fc.reserve(n * sizeof(float4)));
+  SWH_TRY(s->tb.reserve(n));
+  SWH_TRY(s->dens.reserve(n * sizeof(float4)));
+  SWH_TRY(s->rot.reserve(n * sizeof(float4)));
+  SWH_TRY(s->grad.reserve(n * sizeof(float4)));
+  SWH_TRY(s->acc.reserve(n * sizeof(float4)));
+  SWH_TRY(s->hdt.reserve(n * sizeof(float)));
+  SWH_TRY(s->mintb.reserve(n));
+  SWH_TRY(s->perm.reserve(n * sizeof(int)));
+  SWH_TRY(s->ncount.reserve(n * sizeof(int)));
+  return SWH_OK;
+}
+
+swh_status space_hmax_to_device(swh_space* s) {
+  SWH_TRY(s->counters.reserve(64));
+  unsigned int* hb = s->counters.as<unsigned int>() + 2;  // slot 2: hmax bits
+  SWH_HIP(hipMemsetAsync(hb, 0, sizeof(unsigned int), s->stream));
+  hipLaunchKernelGGL(hmax_kernel, dim3(1024), dim3(256), 0, s->stream, s->pos.as<double4>(),
+                     s->tb.as<int8_t>(), s->n, hb);
+  SWH_HIP(hipGetLastError());
+  return SWH_OK;
+}
+
+}  // namespace swh
+
+extern "C" {
+
+swh_status swh_space_create(swh_context* ctx, swh_space** out) {
+  if (!ctx || !out) return SWH_ERR_ARG;
+  SWH_HIP(hipSetDevice(ctx->device));
+  auto* s = new swh_space();
+  s->ctx = ctx;
+  hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete s;
+    set_error("hipStreamCreate failed: %s", hipGetErrorString(e));
+    return SWH_ERR_HIP;
+  }
+  *out = s;
+  return SWH_OK;
+}
+
+swh_status swh_space_destroy(swh_space* s) {
+  if (!s) return SWH_OK;
+  (void)hipSetDevice(s->ctx->device);
+  (void)hipStreamSynchronize(s->stream);
+  DevBuf* bufs[] = {&s->aos, &s->pos, &s->vm, &s->th, &s->fc, &s->tb, &s->dens, &s->rot,
+                    &s->grad, &s->acc, &s->hdt, &s->mintb, &s->perm, &s->ncount,
+                    &s->cell_start, &s->keys, &s->keys2, &s->idx, &s->idx2, &s->sort_tmp,
+                    &s->scan_tmp, &s->counters, &s->tmp_soa, &s->ghost_left,
+                    &s->ghost_right, &s->ghost_list, &s->ghost_list2, &s->ghost_flag};
+  for (DevBuf* b : bufs) b->release();
+  s->hstage.release();
+  if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+  return SWH_OK;
+}
+
+swh_status swh_space_set_stream(swh_space* s, void* stream) {
+  if (!s) return SWH_ERR_ARG;
+  if (stream) {
+    if (s->own_stream && s->stream) {
+      (void)hipStreamSynchronize(s->stream);
+      (void)hipStreamDestroy(s->stream);
+    }
+    s->stream = reinterpret_cast<hipStream_t>(stream);
+    s->own_stream = false;
+  }
+  return SWH_OK;
+}
+
+swh_status swh_space_set_tuning(swh_space* s, const swh_tuning* t) {
+  if (!s || !t || t->cell_factor < 1 || t->cell_factor > 4) return SWH_ERR_ARG;
+  s->tuning = *t;
+  s->built = false;
+  return SWH_OK;
+}
+
+int64_t swh_space_count(const swh_space* s) { return s ? s->n : 0; }
+
+swh_status swh_space_sync(swh_space* s) {
+  if (!s) return SWH_ERR_ARG;
+  SWH_HIP(hipStreamSynchronize(s->stream));
+  return SWH_OK;
+}
+
+swh_status swh_space_upload_parts(swh_space* s, const void* parts, int64_t count,
+                                  const swh_part_layout* PL, int on_device) {
+  if (!s || (count > 0 && !parts) || count < 0 || count > INT32_MAX / 2 || !PL)
+    return SWH_ERR_ARG;
+  Layout L;
+  SWH_TRY(make_layout(PL, &L));
+  SWH_HIP(hipSetDevice(s->ctx->device));
+  s->layout = L;
+  s->n = count;
+  s->built = false;
+  if (count == 0) return SWH_OK;
+  const size_t bytes = (size_t)count * L.stride;
+  SWH_TRY(s->aos.reserve(bytes));
+  SWH_TRY(reserve_soa(s, count));
+  SWH_HIP(hipMemcpyAsync(s->aos.ptr, parts, bytes,
+                         on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                         s->stream));
+  const int block = 256;
+  const int grid = (int)((count + block - 1) / block);
+  hipLaunchKernelGGL(unpack_kernel, dim3(grid), dim3(block), 0, s->stream, L,
+                     s->aos.as<const char>(), count, soa_of(s));
+  SWH_HIP(hipGetLastError());
+  if (!on_device) SWH_HIP(hipStreamSynchronize(s->stream));  // caller may reuse `parts`
+  return SWH_OK;
+}
+
+swh_status swh_space_download_parts(swh_space* s, void* parts, const swh_part_layout* PL,
+                                    int fields, int on_device) {
+  if (!s || (s->n > 0 && !parts) || !PL) return SWH_ERR_ARG;
+  Layout L;
+  SWH_TRY(make_layout(PL, &L));
+  if (L.stride != s->layout.stride) {
+    set_error("download layout stride differs from upload");
+    return SWH_ERR_ARG;
+  }
+  if (s->n == 0) return SWH_OK;
+  SWH_HIP(hipSetDevice(s->ctx->device));
+  const int block = 256;
+  const int grid = (int)((s->n + block - 1) / block);
+  hipLaunchKernelGGL(pack_kernel, dim3(grid), dim3(block), 0, s->stream, L,
+                     s->aos.as<char>(), s->n, soa_of(s), fields);
+  SWH_HIP(hipGetLastError());
+  SWH_HIP(hipMemcpyAsync(parts, s->aos.ptr, (size_t)s->n * L.stride,
+                         on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                         s->stream));
+  SWH_HIP(hipStreamSynchronize(s->stream));
+  return SWH_OK;
+}
+
+swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min_cell_width) {
+  if (!s || !P) return SWH_ERR_ARG;
+  const int64_t n = s->n;
+  if (n == 0) {
+    s->built = true;
+    return SWH_OK;
+  }
+  SWH_HIP(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->stream;
+  // 1. bounding box + max h
+  const int nb = 512;
+  SWH_TRY(s->scan_tmp.reserve(nb * 7 * sizeof(double)));
+  SWH_TRY(s->hstage.reserve(nb * 7 * sizeof(double)));
+  hipLaunchKernelGGL(bbox_kernel, dim3(nb), dim3(256), 0, st, s->pos.as<double4>(),
+                     s->tb.as<int8_t>(), n, s->scan_tmp.as<double>());
+  SWH_HIP(hipGetLastError());
+  SWH_HIP(hipMemcpyAsync(s->hstage.ptr, s->scan_tmp.ptr, nb * 7 * sizeof(double),
+                         hipMemcpyDeviceToHost, st));
+  SWH_HIP(hipStreamSynchronize(st));
+  const double* hb = static_cast<const double*>(s->hstage.ptr);
+  double bb[7] = {1e300, 1e300, 1e300, -1e300, -1e300, -1e300, 0.};
+  for (int b = 0; b < nb; b++) {
+    for (int k = 0; k < 3; k++) bb[k] = std::min(bb[k], hb[b * 7 + k]);
+    for (int k = 3; k < 7; k++) bb[k] = std::max(bb[k], hb[b * 7 + k]);
+  }
+  SwhGrid& g = s->grid;
+  g.periodic = P->periodic;
+  g.hmax = bb[6] * (double)kGamma;
+  double width = min_cell_width > 0 ? min_cell_width
+                                    : g.hmax / (double)std::max(1, s->tuning.cell_factor);
+  if (!(width > 0)) width = 1.0;
+  int64_t total = 1;
+  for (int k = 0; k < 3; k++) {
+    if (g.periodic) {
+      g.origin[k] = 0.;
+      g.dim[k] = P->dim[k];
+    } else {
+      const double ext = std::max(bb[k + 3] - bb[k], 1e-300);
+      g.origin[k] = bb[k];
+      g.dim[k] = ext * (1. + 1e-12) + 1e-300;
+    }
+    int c = (int)std::floor(g.dim[k] / width);
+    c = std::max(1, std::min(c, 1024));
+    g.cdim[k] = c;
+    total *= c;
+  }
+  // keep the cell count bounded (memory and scan cost)
+  while (total > std::max<int64_t>(64, 8 * n) && total > 27) {
+    total = 1;
+    for (int k = 0; k < 3; k++) {
+      g.cdim[k] = std::max(1, g.cdim[k] * 3 / 4);
+      total *= g.cdim[k];
+    }
+  }
+  for (int k = 0; k < 3; k++) g.w[k] = g.dim[k] / g.cdim[k];
+  g.ncell = (int)total;
+  GridDev gd = grid_dev(g);
+  // 2. keys + stable radix sort by cell
+  SWH_TRY(s->keys.reserve(n * sizeof(uint32_t)));
+  SWH_TRY(s->keys2.reserve(n * sizeof(uint32_t)));
+  SWH_TRY(s->idx.reserve(n * sizeof(int)));
+  SWH_TRY(s->idx2.reserve(n * sizeof(int)));
+  const int block = 256;
+  const int grid = (int)((n + block - 1) / block);
+  hipLaunchKernelGGL(key_kernel, dim3(grid), dim3(block), 0, st, gd, s->pos.as<double4>(),
+                     s->tb.as<const int8_t>(), n, g.ncell, s->keys.as<uint32_t>(),
+                     s->idx.as<int>());
+  SWH_HIP(hipGetLastError());
+  int end_bit = 1;
+  while ((1LL << end_bit) <= (int64_t)g.ncell) end_bit++;
+  size_t tmp_bytes = 0;
+  SWH_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, s->keys.as<uint32_t>(),
+                                             s->keys2.as<uint32_t>(), s->idx.as<int>(),
+                                             s->idx2.as<int>(), (int)n, 0, end_bit, st));
+  SWH_TRY(s->sort_tmp.reserve(tmp_bytes));
+  SWH_HIP(hipcub::DeviceRadixSort::SortPairs(s->sort_tmp.ptr, tmp_bytes,
+                                             s->keys.as<uint32_t>(), s->keys2.as<uint32_t>(),
+                                             s->idx.as<int>(), s->idx2.as<int>(), (int)n, 0,
+                                             end_bit, st));
+  // 3. permute SoA into cell order
+  SWH_TRY(s->tmp_soa.reserve((size_t)n * soa_bytes_per_part() + 16 * 256));
+  SoA tmp = soa_carve(s->tmp_soa.as<char>(), n);
+  hipLaunchKernelGGL(permute_kernel, dim3(grid), dim3(block), 0, st, soa_of(s), tmp,
+                     s->idx2.as<const int>(), n);
+  SWH_HIP(hipGetLastError());
+  SWH_TRY(copy_soa(tmp, s, st));
+  // 4. cell starts
+  SWH_TRY(s->cell_start.reserve(((size_t)g.ncell + 1) * sizeof(int)));
+  hipLaunchKernelGGL(cell_start_kernel, dim3((int)((n + 1 + block - 1) / block)), dim3(block),
+                     0, st, s->keys2.as<const uint32_t>(), n, g.ncell,
+                     s->cell_start.as<int>());
+  SWH_HIP(hipGetLastError());
+  SWH_TRY(space_hmax_to_device(s));
+  s->built = true;
+  return SWH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,197 @@
+"""Synthetic initial conditions for the benchmark configurations and tests.
+
+The real SWIFT ICs (glassCube_64.hdf5, EAGLE_ICs_6.hdf5, SmallCosmoVolume)
+are `wget`-only and unavailable offline; these generators build
+inputs of the same shape from recipes cited per function. Every generator is
+deterministic (numpy PCG64 with a recorded seed).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import abi
+
+GAMMA = 5.0 / 3.0
+
+
+def _rng(seed: int) -> np.random.Generator:
+    return np.random.Generator(np.random.PCG64(seed))
+
+
+def perturbed_lattice(n: int, box: float = 1.0, pert: float = 0.1, seed: int = 0x5EED):
+    """n^3 lattice points (i+0.5)/n*box, each coordinate displaced by
+    uniform(-0.5, 0.5)*pert/n*box (tests/test27cells.c make_cell, -d pert)."""
+    rng = _rng(seed)
+    g = (np.arange(n) + 0.5) / n
+    x, y, z = np.meshgrid(g, g, g, indexing="ij")
+    pos = np.stack([x.ravel(), y.ravel(), z.ravel()], axis=1)
+    pos = pos + rng.uniform(-0.5, 0.5, size=pos.shape) * pert / n
+    pos = np.mod(pos * box, box)
+    return pos
+
+
+def sedov_box(n: int, eta: float = 1.2348, pert: float = 0.1, seed: int = 0x5EED,
+              velocity: str = "zero", rho0: float = 1.0, P0: float = 1.0e-6, E0: float = 1.0,
+              n_inject: int = 15) -> np.ndarray:
+    """SedovBlast_3D-like periodic unit box of n^3 gas particles
+    (examples/HydroTests/SedovBlast_3D/makeIC.py: rho0=1, P0=1e-6, E0=1 into
+    the 15 particles closest to the centre; sedov.yml resolution_eta=1.2348).
+    The glass file is replaced by a 10%-perturbed lattice; h = eta * L / n.
+    velocity: "zero" (Sedov) or "divergent" (v = x - 0.5, test27cells.c:138)."""
+    N = n ** 3
+    pos = perturbed_lattice(n, 1.0, pert, seed)
+    p = abi.new_parts(N)
+    p["id"] = np.arange(1, N + 1)
+    p["x"] = pos
+    m = rho0 * 1.0 / N
+    p["mass"] = m
+    p["h"] = eta / n
+    u = np.full(N, P0 / (rho0 * (GAMMA - 1.0)), dtype=np.float64)
+    r = np.sqrt(((pos - 0.5) ** 2).sum(axis=1))
+    idx = np.argsort(r, kind="stable")[:n_inject]
+    u[idx] = E0 / (n_inject * m)
+    p["u"] = u
+    if velocity == "divergent":
+        p["v"] = (pos - 0.5).astype(np.float32)
+    elif velocity == "random":
+        p["v"] = _rng(seed + 1).uniform(-0.05, 0.05, size=(N, 3)).astype(np.float32)
+    p["time_bin"] = 1
+    p["visc_alpha"] = 0.1
+    p["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
+    return p
+
+
+def clustered_box(n_bg: int, n_clumps: int = 8, per_clump: int = 4096, seed: int = 6,
+                  eta: float = 1.2348) -> np.ndarray:
+    """EAGLE_6-like stand-in: a uniform background lattice plus
+    Plummer-sphere clumps, so smoothing lengths span more than an order of
+    magnitude after the ghost converges them. Periodic unit box."""
+    rng = _rng(seed)
+    bg = perturbed_lattice(n_bg, 1.0, 0.3, seed)
+    clumps = []
+    for _ in range(n_clumps):
+        c = rng.uniform(0.15, 0.85, 3)
+        a = rng.uniform(0.01, 0.03)
+        # Plummer radii: r = a / sqrt(u^(-2/3) - 1)
+        uu = rng.uniform(0.05, 0.9, per_clump)
+        rr = a / np.sqrt(uu ** (-2.0 / 3.0) - 1.0)
+        d = rng.normal(size=(per_clump, 3))
+        d /= np.linalg.norm(d, axis=1)[:, None]
+        clumps.append(np.mod(c + d * rr[:, None], 1.0))
+    pos = np.concatenate([bg] + clumps)
+    N = len(pos)
+    p = abi.new_parts(N)
+    p["id"] = np.arange(1, N + 1)
+    p["x"] = pos
+    p["mass"] = 1.0 / N
+    p["h"] = eta / n_bg  # the ghost adapts it
+    p["u"] = 1.0
+    p["v"] = rng.normal(scale=0.01, size=(N, 3)).astype(np.float32)
+    p["time_bin"] = 1
+    p["visc_alpha"] = 0.1
+    return p
+
+
+def make_cell(n: int, offset, size: float, h: float, density: float, first_id: int,
+              pert: float, vel: str, h_pert: float, rng: np.random.Generator,
+              shuffle: bool = True) -> np.ndarray:
+    """tests/test27cells.c make_cell:95-211 — n^3 particles on a (perturbed)
+    lattice in one cell; h = size*h*U(1, h_pert)/n; mass = rho V / count;
+    velocity fields zero / random / divergent (about 1.5*size) / rotating."""
+    count = n ** 3
+    p = abi.new_parts(count)
+    k = 0
+    pos = np.empty((count, 3))
+    for ix in range(n):
+        for iy in range(n):
+            for iz in range(n):
+                r = rng.uniform(-0.5, 0.5, 3) * pert
+                pos[k] = [offset[0] + size * (ix + 0.5 + r[0]) / n,
+                          offset[1] + size * (iy + 0.5 + r[1]) / n,
+                          offset[2] + size * (iz + 0.5 + r[2]) / n]
+                k += 1
+    p["x"] = pos
+    if vel == "zero":
+        p["v"] = 0.0
+    elif vel == "random":
+        p["v"] = rng.uniform(-0.05, 0.05, (count, 3)).astype(np.float32)
+    elif vel == "divergent":
+        p["v"] = (pos - 1.5 * size).astype(np.float32)
+    elif vel == "rotating":
+        v = np.zeros((count, 3))
+        v[:, 0] = pos[:, 1]
+        v[:, 1] = -pos[:, 0]
+        p["v"] = v.astype(np.float32)
+    if h_pert:
+        p["h"] = size * h * rng.uniform(1.0, h_pert, count) / n
+    else:
+        p["h"] = size * h / n
+    p["id"] = np.arange(first_id + 1, first_id + count + 1)
+    p["mass"] = density * size ** 3 / count
+    p["time_bin"] = 1
+    if shuffle:
+        p[:] = p[rng.permutation(count)]
+    return p
+
+
+def uniform_gravity_box(n: int, epsilon: float = 0.001, seed: int = 256) -> np.ndarray:
+    """GravityTests uniform DM box stand-in (examples/GravityTests/Gravity_glass:
+    L=1, rho=1; uniform_DM_box.yml comoving_softening 0.001): n^3 uniform
+    random gparts of mass 1/N."""
+    rng = _rng(seed)
+    N = n ** 3
+    g = abi.new_gparts(N)
+    g["id_or_neg_offset"] = np.arange(1, N + 1)
+    g["x"] = rng.uniform(0.0, 1.0, (N, 3))
+    g["mass"] = 1.0 / N
+    g["epsilon"] = epsilon
+    g["time_bin"] = 1
+    g["type"] = 1
+    return g
+
+
+def leaf_cells(gparts: np.ndarray, cdim: int, box: float = 1.0):
+    """Sort gparts into a cdim^3 grid of leaves; returns (sorted gparts,
+    leaves[start,count], cell coords). Used for P2P over neighbouring leaves."""
+    x = np.mod(gparts["x"], box)
+    c = np.minimum((x / (box / cdim)).astype(np.int64), cdim - 1)
+    key = (c[:, 0] * cdim + c[:, 1]) * cdim + c[:, 2]
+    order = np.argsort(key, kind="stable")
+    g = gparts[order].copy()
+    key = key[order]
+    counts = np.bincount(key, minlength=cdim ** 3)
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    leaves = np.zeros(cdim ** 3, dtype=abi.LEAF_DTYPE)
+    leaves["start"] = starts
+    leaves["count"] = counts
+    return g, leaves
+
+
+def neighbour_pairs(cdim: int, periodic: bool = True, truncated: int = 0):
+    """CSR list: every leaf interacts with itself and its 26 neighbours."""
+    offs = []
+    pairs = []
+    for cx in range(cdim):
+        for cy in range(cdim):
+            for cz in range(cdim):
+                offs.append(len(pairs))
+                seen = set()
+                for dx in (-1, 0, 1):
+                    for dy in (-1, 0, 1):
+                        for dz in (-1, 0, 1):
+                            nx, ny, nz = cx + dx, cy + dy, cz + dz
+                            if periodic:
+                                nx, ny, nz = nx % cdim, ny % cdim, nz % cdim
+                            elif not (0 <= nx < cdim and 0 <= ny < cdim and 0 <= nz < cdim):
+                                continue
+                            j = (nx * cdim + ny) * cdim + nz
+                            if j in seen:
+                                continue
+                            seen.add(j)
+                            pairs.append((j, truncated))
+    offs.append(len(pairs))
+    arr = np.zeros(len(pairs), dtype=abi.LEAF_PAIR_DTYPE)
+    if pairs:
+        arr["j"] = [p[0] for p in pairs]
+        arr["truncated"] = [p[1] for p in pairs]
+    return np.asarray(offs, dtype=np.int32), arr

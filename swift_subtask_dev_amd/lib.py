@@ -1,0 +1,362 @@
+"""ctypes bindings of libswifthip (include/swifthip.h) and the SWIFT-signature
+adapter (include/swifthip_swift.h).
+
+The product path is the HIP library: if ``libswifthip.so`` is missing this
+module raises immediately — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+from . import abi
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "libswifthip.so"
+ADAPTER_PATH = PKG / "libswifthip_swift.so"
+
+STATUS = {
+    0: "ok", 1: "invalid argument", 2: "HIP runtime error", 3: "Interacting unsorted cells.",
+    4: "Cell smaller than smoothing length", 5: "Smoothing length failed to converge",
+    6: "no usable gfx950 device", 7: "device out of memory", 8: "call out of order",
+}
+
+# Every symbol include/swifthip.h declares (checked by tests/test_abi.py).
+HIP_SYMBOLS = [
+    "swh_part_layout_sphenix", "swh_gpart_layout_multisoftening", "swh_init", "swh_finalize",
+    "swh_set_precision", "swh_status_string", "swh_last_error", "swh_abi_version",
+    "swh_doself_density", "swh_dopair_density", "swh_doself_gradient", "swh_dopair_gradient",
+    "swh_doself_force", "swh_dopair_force", "swh_doself_subset_density",
+    "swh_dopair_subset_density", "swh_grav_self_pp", "swh_grav_pair_pp", "swh_space_create",
+    "swh_space_destroy", "swh_space_set_stream", "swh_space_upload_parts",
+    "swh_space_download_parts", "swh_space_count", "swh_space_rebuild", "swh_space_init_parts",
+    "swh_density_loop", "swh_ghost", "swh_gradient_loop", "swh_extra_ghost", "swh_force_loop",
+    "swh_end_force", "swh_space_sync", "swh_space_set_tuning", "swh_gspace_create",
+    "swh_gspace_destroy", "swh_gspace_upload", "swh_gspace_set_leaves", "swh_grav_pp_batch",
+    "swh_gspace_download", "swh_gspace_sync",
+]
+ADAPTER_SYMBOLS = [
+    "swifthip_swift_init", "swifthip_swift_finalize", "swifthip_swift_last_error",
+    "swifthip_swift_clear_error", "runner_doself1_branch_density",
+    "runner_dopair1_branch_density", "runner_doself1_branch_gradient",
+    "runner_dopair1_branch_gradient", "runner_doself2_branch_force",
+    "runner_dopair2_branch_force", "runner_doself_subset_branch_density",
+    "runner_dopair_subset_branch_density", "runner_doself_grav_pp", "runner_dopair_grav_pp",
+]
+
+
+class SwhError(RuntimeError):
+    def __init__(self, status: int, where: str, detail: str = ""):
+        self.status = status
+        super().__init__(f"{where}: {STATUS.get(status, status)} {detail}".strip())
+
+
+_lib = None
+_adapter = None
+
+
+def load() -> C.CDLL:
+    """Load libswifthip.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -m swift_subtask_dev_amd.build` "
+            "(the HIP library is the only implementation of this path)")
+    lib = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
+    vp, i32, i64, dp = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+    P = C.POINTER
+    sigs = {
+        "swh_part_layout_sphenix": (None, [P(abi.PartLayout)]),
+        "swh_gpart_layout_multisoftening": (None, [P(abi.GPartLayout)]),
+        "swh_init": (C.c_int, [P(vp), C.c_int]),
+        "swh_finalize": (C.c_int, [vp]),
+        "swh_set_precision": (C.c_int, [vp, C.c_int]),
+        "swh_status_string": (C.c_char_p, [C.c_int]),
+        "swh_last_error": (C.c_char_p, []),
+        "swh_abi_version": (C.c_int, []),
+        "swh_doself_density": (C.c_int, [vp, P(abi.CellView), P(abi.PartLayout), P(abi.HydroParams)]),
+        "swh_doself_gradient": (C.c_int, [vp, P(abi.CellView), P(abi.PartLayout), P(abi.HydroParams)]),
+        "swh_doself_force": (C.c_int, [vp, P(abi.CellView), P(abi.PartLayout), P(abi.HydroParams)]),
+        "swh_dopair_density": (C.c_int, [vp, P(abi.CellView), P(abi.CellView), P(dp), P(abi.PartLayout), P(abi.HydroParams)]),
+        "swh_dopair_gradient": (C.c_int, [vp, P(abi.CellView), P(abi.CellView), P(dp), P(abi.PartLayout), P(abi.HydroParams)]),
+        "swh_dopair_force": (C.c_int, [vp, P(abi.CellView), P(abi.CellView), P(dp), P(abi.PartLayout), P(abi.HydroParams)]),
+        "swh_doself_subset_density": (C.c_int, [vp, P(abi.CellView), vp, P(i32), i32, P(abi.PartLayout), P(abi.HydroParams)]),
+        "swh_dopair_subset_density": (C.c_int, [vp, P(abi.CellView), vp, P(i32), i32, P(abi.CellView), P(dp), P(abi.PartLayout), P(abi.HydroParams)]),
+        "swh_grav_self_pp": (C.c_int, [vp, P(abi.GCellView), P(abi.GPartLayout), P(abi.GravParams)]),
+        "swh_grav_pair_pp": (C.c_int, [vp, P(abi.GCellView), P(abi.GCellView), C.c_int, P(abi.GPartLayout), P(abi.GravParams)]),
+        "swh_space_create": (C.c_int, [vp, P(vp)]),
+        "swh_space_destroy": (C.c_int, [vp]),
+        "swh_space_set_stream": (C.c_int, [vp, vp]),
+        "swh_space_upload_parts": (C.c_int, [vp, vp, i64, P(abi.PartLayout), C.c_int]),
+        "swh_space_download_parts": (C.c_int, [vp, vp, P(abi.PartLayout), C.c_int, C.c_int]),
+        "swh_space_count": (i64, [vp]),
+        "swh_space_rebuild": (C.c_int, [vp, P(abi.HydroParams), dp]),
+        "swh_space_init_parts": (C.c_int, [vp, P(abi.HydroParams)]),
+        "swh_density_loop": (C.c_int, [vp, P(abi.HydroParams), P(i64)]),
+        "swh_ghost": (C.c_int, [vp, P(abi.HydroParams), P(i32), P(i64)]),
+        "swh_gradient_loop": (C.c_int, [vp, P(abi.HydroParams), P(i64)]),
+        "swh_extra_ghost": (C.c_int, [vp, P(abi.HydroParams)]),
+        "swh_force_loop": (C.c_int, [vp, P(abi.HydroParams), P(i64)]),
+        "swh_end_force": (C.c_int, [vp, P(abi.HydroParams)]),
+        "swh_space_sync": (C.c_int, [vp]),
+        "swh_space_set_tuning": (C.c_int, [vp, P(abi.Tuning)]),
+        "swh_gspace_create": (C.c_int, [vp, P(vp)]),
+        "swh_gspace_destroy": (C.c_int, [vp]),
+        "swh_gspace_upload": (C.c_int, [vp, vp, i64, P(abi.GPartLayout), C.c_int]),
+        "swh_gspace_set_leaves": (C.c_int, [vp, vp, i32, P(i32), vp, i32]),
+        "swh_grav_pp_batch": (C.c_int, [vp, P(abi.GravParams), P(i64)]),
+        "swh_gspace_download": (C.c_int, [vp, vp, P(abi.GPartLayout), C.c_int]),
+        "swh_gspace_sync": (C.c_int, [vp]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def load_adapter() -> C.CDLL:
+    global _adapter
+    if _adapter is not None:
+        return _adapter
+    load()
+    if not ADAPTER_PATH.exists():
+        raise ImportError(f"{ADAPTER_PATH} is missing: run the build")
+    ad = C.CDLL(str(ADAPTER_PATH))
+    vp, P = C.c_void_p, C.POINTER
+    ad.swifthip_swift_init.restype = C.c_int
+    ad.swifthip_swift_init.argtypes = [C.c_int, C.c_int]
+    ad.swifthip_swift_finalize.restype = None
+    ad.swifthip_swift_last_error.restype = C.c_char_p
+    ad.swifthip_swift_clear_error.restype = None
+    for n in ("runner_doself1_branch_density", "runner_doself1_branch_gradient",
+              "runner_doself2_branch_force", "runner_doself_grav_pp"):
+        getattr(ad, n).argtypes = [vp, vp]
+        getattr(ad, n).restype = None
+    for n in ("runner_dopair1_branch_density", "runner_dopair1_branch_gradient",
+              "runner_dopair2_branch_force"):
+        getattr(ad, n).argtypes = [vp, vp, vp]
+        getattr(ad, n).restype = None
+    ad.runner_doself_subset_branch_density.argtypes = [vp, vp, vp, P(C.c_int), C.c_int]
+    ad.runner_doself_subset_branch_density.restype = None
+    ad.runner_dopair_subset_branch_density.argtypes = [vp, vp, vp, P(C.c_int), C.c_int, vp]
+    ad.runner_dopair_subset_branch_density.restype = None
+    ad.runner_dopair_grav_pp.argtypes = [vp, vp, vp, C.c_int, C.c_int]
+    ad.runner_dopair_grav_pp.restype = None
+    _adapter = ad
+    return ad
+
+
+def _check(status: int, where: str) -> None:
+    if status != 0:
+        detail = (load().swh_last_error() or b"").decode(errors="replace")
+        raise SwhError(status, where, detail)
+
+
+def part_layout() -> abi.PartLayout:
+    L = abi.PartLayout()
+    load().swh_part_layout_sphenix(C.byref(L))
+    return L
+
+
+def gpart_layout() -> abi.GPartLayout:
+    L = abi.GPartLayout()
+    load().swh_gpart_layout_multisoftening(C.byref(L))
+    return L
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+class Context:
+    """One swh_context (device + per-task streams)."""
+
+    def __init__(self, device: int = 0, precision: str = "f64"):
+        lib = load()
+        self._lib = lib
+        h = C.c_void_p()
+        _check(lib.swh_init(C.byref(h), device), "swh_init")
+        self.handle = h
+        self.set_precision(precision)
+        self.L = part_layout()
+        self.GL = gpart_layout()
+
+    def set_precision(self, precision: str) -> None:
+        _check(self._lib.swh_set_precision(self.handle, 0 if precision == "f64" else 1),
+               "swh_set_precision")
+        self.precision = precision
+
+    def close(self) -> None:
+        if self.handle:
+            self._lib.swh_finalize(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- per-task -------------------------------------------------------
+    def cell_view(self, parts: np.ndarray, loc, width, active=True) -> abi.CellView:
+        v = abi.CellView()
+        v.parts = _ptr(parts)
+        v.count = len(parts)
+        v.active = 1 if active else 0
+        for k in range(3):
+            v.loc[k] = loc[k]
+            v.width[k] = width[k]
+        return v
+
+    def doself(self, loop: str, view: abi.CellView, P: abi.HydroParams) -> None:
+        fn = {"density": self._lib.swh_doself_density, "gradient": self._lib.swh_doself_gradient,
+              "force": self._lib.swh_doself_force}[loop]
+        _check(fn(self.handle, C.byref(view), C.byref(self.L), C.byref(P)), f"doself_{loop}")
+
+    def dopair(self, loop: str, vi, vj, shift, P) -> None:
+        fn = {"density": self._lib.swh_dopair_density, "gradient": self._lib.swh_dopair_gradient,
+              "force": self._lib.swh_dopair_force}[loop]
+        sh = (C.c_double * 3)(*shift)
+        _check(fn(self.handle, C.byref(vi), C.byref(vj), sh, C.byref(self.L), C.byref(P)),
+               f"dopair_{loop}")
+
+
+class HydroSpace:
+    """Device-resident particle set (swh_space): the batch loops."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self._lib = ctx._lib
+        h = C.c_void_p()
+        _check(self._lib.swh_space_create(ctx.handle, C.byref(h)), "swh_space_create")
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            self._lib.swh_space_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_tuning(self, cell_factor=1, loop_variant=0):
+        t = abi.Tuning(cell_factor, loop_variant)
+        _check(self._lib.swh_space_set_tuning(self.handle, C.byref(t)), "set_tuning")
+
+    def upload(self, parts, count=None, on_device=False):
+        """parts: numpy PART_DTYPE array (host) or a device pointer (int) with count."""
+        if on_device:
+            _check(self._lib.swh_space_upload_parts(self.handle, C.c_void_p(parts), count,
+                                                    C.byref(self.ctx.L), 1), "upload")
+        else:
+            _check(self._lib.swh_space_upload_parts(self.handle, _ptr(parts), len(parts),
+                                                    C.byref(self.ctx.L), 0), "upload")
+
+    def download(self, parts: np.ndarray, fields=abi.FIELDS_ALL):
+        _check(self._lib.swh_space_download_parts(self.handle, _ptr(parts), C.byref(self.ctx.L),
+                                                  fields, 0), "download")
+
+    def rebuild(self, P, min_cell_width=0.0):
+        _check(self._lib.swh_space_rebuild(self.handle, C.byref(P), min_cell_width), "rebuild")
+
+    def init_parts(self, P):
+        _check(self._lib.swh_space_init_parts(self.handle, C.byref(P)), "init_parts")
+
+    def _loop(self, fn, P, count):
+        n = C.c_int64(0)
+        _check(fn(self.handle, C.byref(P), C.byref(n) if count else None), fn.__name__)
+        return n.value if count else None
+
+    def density(self, P, count=True):
+        return self._loop(self._lib.swh_density_loop, P, count)
+
+    def gradient(self, P, count=True):
+        return self._loop(self._lib.swh_gradient_loop, P, count)
+
+    def force(self, P, count=True):
+        return self._loop(self._lib.swh_force_loop, P, count)
+
+    def ghost(self, P):
+        it = C.c_int32(0)
+        nu = C.c_int64(0)
+        _check(self._lib.swh_ghost(self.handle, C.byref(P), C.byref(it), C.byref(nu)), "ghost")
+        return it.value, nu.value
+
+    def extra_ghost(self, P):
+        _check(self._lib.swh_extra_ghost(self.handle, C.byref(P)), "extra_ghost")
+
+    def end_force(self, P):
+        _check(self._lib.swh_end_force(self.handle, C.byref(P)), "end_force")
+
+    def sync(self):
+        _check(self._lib.swh_space_sync(self.handle), "sync")
+
+    def hydro_step(self, P):
+        """The full SPHENIX hydro chain of one step:
+        density -> ghost -> gradient -> extra ghost -> force -> end force."""
+        self.init_parts(P)
+        nd = self.density(P)
+        it, _ = self.ghost(P)
+        ng = self.gradient(P)
+        self.extra_ghost(P)
+        nf = self.force(P)
+        self.end_force(P)
+        return {"density": nd, "gradient": ng, "force": nf, "ghost_iterations": it}
+
+
+class GravSpace:
+    """Device-resident gpart set for batch P2P (swh_gspace)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self._lib = ctx._lib
+        h = C.c_void_p()
+        _check(self._lib.swh_gspace_create(ctx.handle, C.byref(h)), "swh_gspace_create")
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            self._lib.swh_gspace_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, gparts: np.ndarray):
+        _check(self._lib.swh_gspace_upload(self.handle, _ptr(gparts), len(gparts),
+                                           C.byref(self.ctx.GL), 0), "gspace_upload")
+
+    def set_leaves(self, leaves: np.ndarray, pair_offset: np.ndarray, pairs: np.ndarray):
+        leaves = np.ascontiguousarray(leaves, dtype=abi.LEAF_DTYPE)
+        pair_offset = np.ascontiguousarray(pair_offset, dtype=np.int32)
+        pairs = np.ascontiguousarray(pairs, dtype=abi.LEAF_PAIR_DTYPE)
+        self._keep = (leaves, pair_offset, pairs)
+        _check(self._lib.swh_gspace_set_leaves(
+            self.handle, _ptr(leaves), len(leaves),
+            pair_offset.ctypes.data_as(C.POINTER(C.c_int32)), _ptr(pairs), len(pairs)),
+            "set_leaves")
+
+    def pp(self, G: abi.GravParams, count=True):
+        n = C.c_int64(0)
+        _check(self._lib.swh_grav_pp_batch(self.handle, C.byref(G), C.byref(n) if count else None),
+               "grav_pp_batch")
+        return n.value if count else None
+
+    def download(self, gparts: np.ndarray):
+        _check(self._lib.swh_gspace_download(self.handle, _ptr(gparts), C.byref(self.ctx.GL), 0),
+               "gspace_download")
+
+    def sync(self):
+        _check(self._lib.swh_gspace_sync(self.handle), "gspace_sync")

@@ -1,0 +1,271 @@
+#!/usr/bin/env python
+"""bench.py — directed particle-pair interactions/s (density + force loops)
+on a SedovBlast_3D-like 128^3 box, MI355X, fp64, 1..N GPUs.
+
+One step = one density loop + one force loop over every active particle of
+the (per-GPU) 128^3 sub-volume — the two loops the metric names (SURVEY 8d:
+"density + force; gradient reported separately"). Inputs are resident in HBM
+before the timed region: a full SPHENIX chain (density, ghost h-iteration,
+gradient, extra ghost, force) prepares converged smoothing lengths and the
+force-loop inputs in an untimed setup. Timed per step, on the library's HIP
+stream: hydro_init_part + density gather, hydro_reset_acceleration + force
+gather.
+
+Multi-GPU (weak scaling): the periodic box is N unit Sedov cubes along x,
+one x-slab per rank; each rank holds its slab + a read-only halo and runs the
+loops for its own particles — no collective in the data path
+(swift_subtask_dev_amd/decomp.py).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       torchrun ... bench.py --gpus N   (one process per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import statistics
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "particle-pair interactions/s (density+force) on SedovBlast_3D 128³; 1/2/4/8 GPU"
+HBM_PEAK = 8.0e12       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_PEAK = 78.6e12     # MI355X fp64 vector
+S_IN_DENSITY, S_OUT_DENSITY = 45, 32   # SURVEY 8d algorithmic bytes per particle
+S_IN_FORCE, S_OUT_FORCE = 77, 21
+FLOPS_DENSITY, FLOPS_FORCE = 65, 146   # SURVEY 8d flops per directed interaction
+
+
+def log(msg):
+    print(msg, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(parts, P, n_density, n_force, runs=3, threads=None):
+    """The oracle's float restatement of DOSELF1/DOPAIR1 + DOSELF2/DOPAIR2
+    (sorted pseudo-Verlet loops) over a cdim=20 periodic cell grid, timed on
+    the host cores (kind "port"; the reference's own build is unavailable)."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib as O
+    from swift_subtask_dev_amd import abi
+
+    threads = threads or min(16, os.cpu_count() or 1)
+    eb = abi.EngineBundle(dim=tuple(P.dim), periodic=True, params=P, max_active_bin=P.max_active_bin)
+    new = O.fn("f32", "cellgrid_new")
+    run = O.fn("f32", "cellgrid_run")
+    free = O.fn("f32", "cellgrid_free")
+    # separate copies: struct part's density/force union must keep the force
+    # inputs intact for the force loop
+    gd = new(parts.ctypes.data, len(parts), float(P.dim[0]), 20)
+    gf = new(parts.ctypes.data, len(parts), float(P.dim[0]), 20)
+    times = []
+    try:
+        for r in range(runs + 1):  # first run = warm-up
+            td = run(gd, C.addressof(eb.runner), 0, threads)
+            tf = run(gf, C.addressof(eb.runner), 2, threads)
+            if r > 0:
+                times.append(td + tf)
+    finally:
+        free(gd)
+        free(gf)
+    t = statistics.median(times)
+    return {
+        "value": (n_density + n_force) / t,
+        "unit": "interactions/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"full 128^3 box, density+force loops (float restatement of DOSELF1/DOPAIR1/"
+                  f"DOSELF2/DOPAIR2, cdim=20 cells), median of {runs} runs after 1 warm-up, "
+                  f"{t:.3f} s per step",
+        "seconds_per_step": t,
+    }
+
+
+def load_traffic():
+    path = ROOT / "profiles" / "traffic_density.json"
+    if path.exists():
+        try:
+            return json.loads(path.read_text())
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=128, help="particles per dimension per GPU")
+    ap.add_argument("--cell-factor", type=int, default=int(os.environ.get("SWH_CELL_FACTOR", "2")))
+    ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-runs", type=int, default=3)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from swift_subtask_dev_amd import abi, decomp, ics, lib
+
+    n = args.n
+    t_setup = time.time()
+    parts = ics.sedov_slabs(n, world)
+    box = (float(world), 1.0, 1.0)
+    P = abi.default_hydro_params(box, True)
+    P.max_active_bin = 1
+    ctx = lib.Context(local_rank, args.precision)
+
+    # ---- untimed setup: the full SPHENIX chain on the whole box ----------
+    sp = lib.HydroSpace(ctx)
+    sp.set_tuning(args.cell_factor)
+    sp.upload(parts)
+    sp.rebuild(P)
+    chain = sp.hydro_step(P)
+    sp.download(parts, abi.FIELDS_ALL)
+    sp.close()
+    hmax = float(parts["h"].max()) * 1.825742
+
+    local, n_owned = decomp.slab_local_set(parts, rank, world, box[0], 1.02 * hmax)
+    del parts
+    sp = lib.HydroSpace(ctx)
+    sp.set_tuning(args.cell_factor)
+    # a dedicated (non-NULL) stream: the library's kernels and the timing
+    # events share it, so the events bracket exactly the loop kernels
+    stream = torch.cuda.Stream()
+    sp.set_stream(stream.cuda_stream)
+    sp.upload(local)
+    sp.rebuild(P)
+    # exact interaction counts of one step (same work every step: h is fixed)
+    sp.init_parts(P)
+    n_density = sp.density(P)
+    sp.reset_acceleration(P)
+    n_force = sp.force(P)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s: {n_owned} owned + "
+        f"{len(local) - n_owned} halo parts, {n_density} density + {n_force} force "
+        f"interactions/step, chain ghost iterations {chain['ghost_iterations']}")
+
+    def step(ev=None):
+        sp.init_parts(P)
+        if ev:
+            ev[0].record(stream)
+        sp.density(P, count=False)
+        if ev:
+            ev[1].record(stream)
+        sp.reset_acceleration(P)
+        if ev:
+            ev[2].record(stream)
+        sp.force(P, count=False)
+        if ev:
+            ev[3].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t_dens = [e[0].elapsed_time(e[1]) * 1e-3 for e in events]
+    t_force = [e[2].elapsed_time(e[3]) * 1e-3 for e in events]
+
+    tot = torch.tensor([float(n_density + n_force) * args.steps, float(n_owned)],
+                       dtype=torch.float64, device="cuda")
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    total_interactions, total_owned = tot.tolist()
+    elapsed_max = tmax.item()
+
+    if rank == 0:
+        td = statistics.mean(t_dens)
+        tf = statistics.mean(t_force)
+        b_dens = n_owned * (27 * S_IN_DENSITY + S_OUT_DENSITY)
+        b_force = n_owned * (27 * S_IN_FORCE + S_OUT_FORCE)
+        achieved = b_dens / td
+        traffic = load_traffic()
+        out = {
+            "metric": METRIC,
+            "value": total_interactions / elapsed_max,
+            "unit": "interactions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64" if args.precision == "f64" else "f32",
+            "data": "synthetic (SedovBlast_3D-like perturbed lattice, eta=1.2348; glass IC unavailable offline)",
+            "config": {
+                "workload": f"SedovBlast_3D {n}^3 per GPU: density + force loops (SPHENIX, cubic spline)",
+                "particles_per_gpu": n_owned,
+                "global_particles": int(total_owned),
+                "decomposition": f"{world} x-slab(s) + read-only halo, no data-path collective",
+                "density_interactions_per_step": n_density,
+                "force_interactions_per_step": n_force,
+                "cell_factor": args.cell_factor,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "density gather (loop_kernel<DENSITY,double>)",
+                "achieved": achieved / 1e9,
+                "peak": HBM_PEAK / 1e9,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK,
+                "traffic": traffic.get("bytes_per_launch") if traffic else None,
+                "bytes_model": f"N*(27*{S_IN_DENSITY}+{S_OUT_DENSITY}) = {b_dens} B per launch",
+                "launch_ms": td * 1e3,
+            },
+            "kernels": {
+                "density_ms": td * 1e3,
+                "force_ms": tf * 1e3,
+                "force_algorithmic_GBps": b_force / tf / 1e9,
+                "density_fp64_frac": n_density * FLOPS_DENSITY / td / FP64_PEAK,
+                "force_fp64_frac": n_force * FLOPS_FORCE / tf / FP64_PEAK,
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            # the CPU path times the same loops on the same (prepared) inputs
+            sp.download(local, abi.FIELDS_ALL)
+            try:
+                out["cpu_baseline"] = cpu_baseline(local, P, n_density, n_force, args.cpu_runs)
+                out["gpu_over_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+            except Exception as e:  # report, never fake
+                log(f"cpu baseline failed: {e}")
+        print(json.dumps(out), flush=True)
+    sp.close()
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

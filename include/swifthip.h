@@ -232,6 +232,9 @@ SWH_API swh_status swh_space_rebuild(swh_space *s, const swh_hydro_params *P,
 /* Loops over all active particles. n_interactions (optional) receives the
  * number of directed interactions evaluated (r < H_i, resp. max(H_i,H_j)). */
 SWH_API swh_status swh_space_init_parts(swh_space *s, const swh_hydro_params *P);
+/* hydro_reset_acceleration + timestep_limiter_prepare_force on active parts
+ * (what the extra ghost does before the force loop). */
+SWH_API swh_status swh_space_reset_acceleration(swh_space *s, const swh_hydro_params *P);
 SWH_API swh_status swh_density_loop(swh_space *s, const swh_hydro_params *P, int64_t *n_interactions);
 SWH_API swh_status swh_ghost(swh_space *s, const swh_hydro_params *P, int32_t *iterations,
                      int64_t *n_unconverged);

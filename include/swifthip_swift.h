@@ -42,6 +42,8 @@ extern "C" {
  * the first task, e.g. from engine_config). Precision: 0 = fp64, 1 = fp32. */
 SWHS_API int swifthip_swift_init(int device, int precision);
 SWHS_API void swifthip_swift_finalize(void);
+/* Switch the arithmetic of subsequent tasks: 0 = fp64, 1 = fp32. */
+SWHS_API int swifthip_swift_set_precision(int precision);
 /* Last adapter error ("Interacting unsorted cells." ...) or "" . */
 SWHS_API const char *swifthip_swift_last_error(void);
 SWHS_API void swifthip_swift_clear_error(void);

@@ -161,7 +161,7 @@ typedef struct opart {
 /* Which union member is live when converting f64 records <-> ABI parts. */
 enum { PHASE_DENSITY = 0, PHASE_FORCE = 1 };
 
-static void part_to_opart(const struct part *p, opart *o, int phase) {
+__attribute__((unused)) static void part_to_opart(const struct part *p, opart *o, int phase) {
 #ifdef ORACLE_F32
   (void)phase;
   *o = *p;
@@ -198,7 +198,7 @@ static void part_to_opart(const struct part *p, opart *o, int phase) {
 #endif
 }
 
-static void opart_to_part(const opart *o, struct part *p, int phase) {
+__attribute__((unused)) static void opart_to_part(const opart *o, struct part *p, int phase) {
 #ifdef ORACLE_F32
   (void)phase;
   *p = *o;
@@ -2150,6 +2150,66 @@ static long long grav_pp(struct gpart *gi, int ni, const struct gpart *gj, int n
     gp->potential += (float)pot;
   }
   return n;
+}
+
+/* All P2P tasks of a step over leaf cells at once: leaves[i] = {start,count}
+ * ranges of `g`; for i-leaf l the source leaves are pairs[off[l]..off[l+1])
+ * as {j, truncated}. Each active i accumulates over every source leaf in
+ * `real` and is written back once (the per-task float write-back of
+ * gravity_cache_write_back would add float rounding of every partial sum).
+ * Positions: direct differences, nearest image when periodic. */
+API long long PFX(grav_pp_leaves)(struct gpart *g, const int *leaves, int nleaves,
+                                  const int *off, const int *pairs,
+                                  const struct oracle_grav_params *G) {
+  long long total = 0;
+  const real dim[3] = {(real)G->dim[0], (real)G->dim[1], (real)G->dim[2]};
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total)
+  for (int l = 0; l < nleaves; l++) {
+    const int s = leaves[2 * l], c = leaves[2 * l + 1];
+    for (int pid = s; pid < s + c; pid++) {
+      struct gpart *gp = &g[pid];
+      if (gp->time_bin == time_bin_inhibited || gp->time_bin > G->max_active_bin) continue;
+      real a_x = 0, a_y = 0, a_z = 0, pot = 0;
+      const real h_i = gp->epsilon;
+      for (int q = off[l]; q < off[l + 1]; q++) {
+        const int jl = pairs[2 * q], trunc = pairs[2 * q + 1];
+        const int sj = leaves[2 * jl], cj = leaves[2 * jl + 1];
+        for (int pjd = sj; pjd < sj + cj; pjd++) {
+          if (pjd == pid) continue;
+          const struct gpart *gq = &g[pjd];
+          const real mass_j = (gq->time_bin == time_bin_inhibited) ? (real)0 : (real)gq->mass;
+          real dx = (real)(gq->x[0] - gp->x[0]);
+          real dy = (real)(gq->x[1] - gp->x[1]);
+          real dz = (real)(gq->x[2] - gp->x[2]);
+          if (G->periodic) {
+            dx = nearest_r(dx, dim[0]);
+            dy = nearest_r(dy, dim[1]);
+            dz = nearest_r(dz, dim[2]);
+          }
+          const real r2 = dx * dx + dy * dy + dz * dz;
+          const real h = rmax(h_i, (real)gq->epsilon);
+          const real h_inv = (real)1.f / h;
+          const real h_inv_3 = h_inv * h_inv * h_inv;
+          real f_ij, pot_ij;
+          if (trunc)
+            iact_grav_pp_truncated(r2, h * h, h_inv, h_inv_3, mass_j, (real)G->r_s_inv,
+                                   &f_ij, &pot_ij);
+          else
+            iact_grav_pp_full(r2, h * h, h_inv, h_inv_3, mass_j, &f_ij, &pot_ij);
+          a_x += f_ij * dx;
+          a_y += f_ij * dy;
+          a_z += f_ij * dz;
+          pot += pot_ij;
+          total++;
+        }
+      }
+      gp->a_grav[0] += (float)a_x;
+      gp->a_grav[1] += (float)a_y;
+      gp->a_grav[2] += (float)a_z;
+      gp->potential += (float)pot;
+    }
+  }
+  return total;
 }
 
 /* runner_doself_grav_pp (runner_doiact_grav.c:1788-1871): cache frame =

@@ -513,6 +513,15 @@ __global__ void extra_ghost_kernel(SoA a, int64_t n, int max_active_bin, ForcePr
   a.hdt[i] = 0.f;
 }
 
+// hydro_reset_acceleration (hydro.h:944-955) + timestep_limiter_prepare_force.
+__global__ void reset_acc_kernel(SoA a, int64_t n, int max_active_bin) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || a.tb[i] > max_active_bin) return;
+  a.acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  a.hdt[i] = 0.f;
+  a.mintb[i] = (int8_t)(kNumTimeBins + 1);
+}
+
 __global__ void end_force_kernel(SoA a, int64_t n, int max_active_bin) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n || a.tb[i] > max_active_bin) return;
@@ -688,6 +697,17 @@ swh_status swh_extra_ghost(swh_space* s, const swh_hydro_params* P) {
   else
     hipLaunchKernelGGL(extra_ghost_kernel<float>, dim3(g), dim3(block), 0, s->stream,
                        soa_of(s), s->n, P->max_active_bin, fp);
+  SWH_HIP(hipGetLastError());
+  return SWH_OK;
+}
+
+swh_status swh_space_reset_acceleration(swh_space* s, const swh_hydro_params* P) {
+  if (!s || !P) return SWH_ERR_ARG;
+  if (s->n == 0) return SWH_OK;
+  SWH_HIP(hipSetDevice(s->ctx->device));
+  const int block = 256;
+  hipLaunchKernelGGL(reset_acc_kernel, dim3((int)((s->n + block - 1) / block)), dim3(block),
+                     0, s->stream, soa_of(s), s->n, P->max_active_bin);
   SWH_HIP(hipGetLastError());
   return SWH_OK;
 }

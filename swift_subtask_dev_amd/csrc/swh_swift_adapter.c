@@ -47,6 +47,14 @@ int swifthip_swift_init(int device, int precision) {
   return 0;
 }
 
+int swifthip_swift_set_precision(int precision) {
+  if (!swhs_ctx) return -1;
+  return swh_set_precision(swhs_ctx, precision ? SWH_PRECISION_F32 : SWH_PRECISION_F64) ==
+                 SWH_OK
+             ? 0
+             : -1;
+}
+
 void swifthip_swift_finalize(void) {
   if (swhs_ctx) swh_finalize(swhs_ctx);
   swhs_ctx = NULL;

@@ -30,6 +30,41 @@ def perturbed_lattice(n: int, box: float = 1.0, pert: float = 0.1, seed: int = 0
     return pos
 
 
+def sedov_slabs(n: int, nslab: int, eta: float = 1.2348, pert: float = 0.1,
+                seed: int = 0x5EED, rho0: float = 1.0, P0: float = 1.0e-6, E0: float = 1.0,
+                n_inject: int = 15) -> np.ndarray:
+    """`nslab` unit Sedov cubes side by side along x: a periodic (nslab, 1, 1)
+    box of (n*nslab) x n x n perturbed-lattice particles, the blast in the
+    centre of the whole box. nslab = 1 is exactly sedov_box(n)'s recipe.
+    Used for the weak-scaling decomposition (one unit slab per GPU)."""
+    rng = _rng(seed)
+    N = n ** 3 * nslab
+    p = abi.new_parts(N)
+    gx = (np.arange(n * nslab) + 0.5) / n
+    g = (np.arange(n) + 0.5) / n
+    # chunked fill keeps peak host memory at ~one slab of temporaries
+    for s in range(nslab):
+        x, y, z = np.meshgrid(gx[s * n:(s + 1) * n], g, g, indexing="ij")
+        pos = np.stack([x.ravel(), y.ravel(), z.ravel()], axis=1)
+        pos += rng.uniform(-0.5, 0.5, size=pos.shape) * pert / n
+        pos[:, 0] = np.mod(pos[:, 0], nslab)
+        pos[:, 1:] = np.mod(pos[:, 1:], 1.0)
+        p["x"][s * n ** 3:(s + 1) * n ** 3] = pos
+    p["id"] = np.arange(1, N + 1)
+    m = rho0 * nslab / N
+    p["mass"] = m
+    p["h"] = eta / n
+    p["u"] = P0 / (rho0 * (GAMMA - 1.0))
+    c = np.array([0.5 * nslab, 0.5, 0.5])
+    r2 = ((p["x"] - c) ** 2).sum(axis=1)
+    idx = np.argpartition(r2, n_inject)[:n_inject]
+    p["u"][idx] = E0 / (n_inject * m)
+    p["time_bin"] = 1
+    p["visc_alpha"] = 0.1
+    p["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
+    return p
+
+
 def sedov_box(n: int, eta: float = 1.2348, pert: float = 0.1, seed: int = 0x5EED,
               velocity: str = "zero", rho0: float = 1.0, P0: float = 1.0e-6, E0: float = 1.0,
               n_inject: int = 15) -> np.ndarray:

@@ -32,6 +32,7 @@ HIP_SYMBOLS = [
     "swh_dopair_subset_density", "swh_grav_self_pp", "swh_grav_pair_pp", "swh_space_create",
     "swh_space_destroy", "swh_space_set_stream", "swh_space_upload_parts",
     "swh_space_download_parts", "swh_space_count", "swh_space_rebuild", "swh_space_init_parts",
+    "swh_space_reset_acceleration",
     "swh_density_loop", "swh_ghost", "swh_gradient_loop", "swh_extra_ghost", "swh_force_loop",
     "swh_end_force", "swh_space_sync", "swh_space_set_tuning", "swh_gspace_create",
     "swh_gspace_destroy", "swh_gspace_upload", "swh_gspace_set_leaves", "swh_grav_pp_batch",
@@ -39,6 +40,7 @@ HIP_SYMBOLS = [
 ]
 ADAPTER_SYMBOLS = [
     "swifthip_swift_init", "swifthip_swift_finalize", "swifthip_swift_last_error",
+    "swifthip_swift_set_precision",
     "swifthip_swift_clear_error", "runner_doself1_branch_density",
     "runner_dopair1_branch_density", "runner_doself1_branch_gradient",
     "runner_dopair1_branch_gradient", "runner_doself2_branch_force",
@@ -96,6 +98,7 @@ def load() -> C.CDLL:
         "swh_space_count": (i64, [vp]),
         "swh_space_rebuild": (C.c_int, [vp, P(abi.HydroParams), dp]),
         "swh_space_init_parts": (C.c_int, [vp, P(abi.HydroParams)]),
+        "swh_space_reset_acceleration": (C.c_int, [vp, P(abi.HydroParams)]),
         "swh_density_loop": (C.c_int, [vp, P(abi.HydroParams), P(i64)]),
         "swh_ghost": (C.c_int, [vp, P(abi.HydroParams), P(i32), P(i64)]),
         "swh_gradient_loop": (C.c_int, [vp, P(abi.HydroParams), P(i64)]),
@@ -132,6 +135,8 @@ def load_adapter() -> C.CDLL:
     ad.swifthip_swift_init.restype = C.c_int
     ad.swifthip_swift_init.argtypes = [C.c_int, C.c_int]
     ad.swifthip_swift_finalize.restype = None
+    ad.swifthip_swift_set_precision.restype = C.c_int
+    ad.swifthip_swift_set_precision.argtypes = [C.c_int]
     ad.swifthip_swift_last_error.restype = C.c_char_p
     ad.swifthip_swift_clear_error.restype = None
     for n in ("runner_doself1_branch_density", "runner_doself1_branch_gradient",
@@ -270,6 +275,14 @@ class HydroSpace:
 
     def init_parts(self, P):
         _check(self._lib.swh_space_init_parts(self.handle, C.byref(P)), "init_parts")
+
+    def reset_acceleration(self, P):
+        _check(self._lib.swh_space_reset_acceleration(self.handle, C.byref(P)),
+               "reset_acceleration")
+
+    def set_stream(self, stream_ptr: int):
+        """Bind a HIP stream (e.g. torch.cuda.current_stream().cuda_stream)."""
+        _check(self._lib.swh_space_set_stream(self.handle, C.c_void_p(stream_ptr)), "set_stream")
 
     def _loop(self, fn, P, count):
         n = C.c_int64(0)

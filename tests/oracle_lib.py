@@ -38,8 +38,8 @@ def load(prec: str = "f32") -> C.CDLL:
     if prec in _libs:
         return _libs[prec]
     path = F32 if prec == "f32" else F64
-    if not path.exists():
-        build()
+    if not _libs:
+        build()  # incremental make: picks up oracle.c edits
     lib = C.CDLL(str(path))
     pfx = "orf_" if prec == "f32" else "ord_"
     vp, i64, P = C.c_void_p, C.c_longlong, C.POINTER
@@ -66,6 +66,7 @@ def load(prec: str = "f32") -> C.CDLL:
                               P(abi.GravParams)])
     sig("grav_pair_pp", i64, [vp, C.c_int, vp, C.c_int, P(C.c_double), P(C.c_double),
                               C.c_double, C.c_double, C.c_int, P(abi.GravParams)])
+    sig("grav_pp_leaves", i64, [vp, vp, C.c_int, vp, vp, P(abi.GravParams)])
     if prec == "f32":
         for n in ("iact_density", "iact_force", "iact_gradient"):
             sig(n, None, [real, P(real), real, real, vp, vp, real, real])

@@ -104,6 +104,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=128, help="particles per dimension per GPU")
     ap.add_argument("--cell-factor", type=int, default=int(os.environ.get("SWH_CELL_FACTOR", "2")))
+    ap.add_argument("--loop-variant", type=int, default=int(os.environ.get("SWH_LOOP_VARIANT", "0")),
+                    help="0 default (two-phase), 1 direct gather, 2 two-phase gather")
+    ap.add_argument("--group-size", type=int, default=int(os.environ.get("SWH_GROUP_SIZE", "0")),
+                    help="tile i-group size / row width: 0 (default 16), 16, 32, 64")
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-runs", type=int, default=3)
@@ -145,7 +149,7 @@ def main():
     local, n_owned = decomp.slab_local_set(parts, rank, world, box[0], 1.02 * hmax)
     del parts
     sp = lib.HydroSpace(ctx)
-    sp.set_tuning(args.cell_factor)
+    sp.set_tuning(args.cell_factor, args.loop_variant, args.group_size)
     # a dedicated (non-NULL) stream: the library's kernels and the timing
     # events share it, so the events bracket exactly the loop kernels
     stream = torch.cuda.Stream()
@@ -158,6 +162,8 @@ def main():
     sp.reset_acceleration(P)
     n_force = sp.force(P)
     torch.cuda.synchronize()
+    info = sp.info()
+    log(f"[rank {rank}] grid {info}")
     log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s: {n_owned} owned + "
         f"{len(local) - n_owned} halo parts, {n_density} density + {n_force} force "
         f"interactions/step, chain ghost iterations {chain['ghost_iterations']}")
@@ -231,10 +237,16 @@ def main():
                 "density_interactions_per_step": n_density,
                 "force_interactions_per_step": n_force,
                 "cell_factor": args.cell_factor,
+                "loop_variant": args.loop_variant,
+                "group_size": args.group_size or 16,
+                "grid_cdim": info["cdim"],
+                "i_groups": info["ngroups"],
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "density gather (loop_kernel<DENSITY,double>)",
+                "kernel": {0: "tile_kernel<DENSITY,double>", 3: "tile_kernel<DENSITY,double>",
+                           1: "loop_kernel<DENSITY,double,1>",
+                           2: "loop_kernel<DENSITY,double,2>"}[args.loop_variant],
                 "achieved": achieved / 1e9,
                 "peak": HBM_PEAK / 1e9,
                 "unit": "GB/s",

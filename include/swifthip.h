@@ -248,9 +248,22 @@ SWH_API swh_status swh_space_sync(swh_space *s);
 /* Kernel-tuning knobs of the batch loops (bench/diagnostics). */
 typedef struct swh_tuning {
   int32_t cell_factor;  /* neighbour-grid cells per H_max (1..4) */
-  int32_t loop_variant; /* 0 = default */
+  int32_t loop_variant; /* 0 = default (3); 1 = per-particle direct gather, 2 = per-particle
+                           two-phase gather, 3 = tile (i-groups in 16/32/64-lane rows) */
+  int32_t group_size;   /* tile i-group size = row width: 0 (default 16), 16, 32, 64 */
 } swh_tuning;
 SWH_API swh_status swh_space_set_tuning(swh_space *s, const swh_tuning *t);
+
+/* Neighbour-grid diagnostics of the last rebuild. */
+typedef struct swh_space_info {
+  int32_t cdim[3];  /* grid cells per dimension */
+  int32_t ncell;
+  int32_t ngroups;  /* i-groups of the tile loops (octree leaves, <= 64 parts) */
+  int32_t reserved;
+  double cell_width[3];
+  double h_max;     /* max gamma*h at rebuild */
+} swh_space_info;
+SWH_API swh_status swh_space_get_info(const swh_space *s, swh_space_info *info);
 
 /* Batch P2P gravity over leaf cells of a device-resident gpart set. Leaves
  * are contiguous [start, start+count) ranges; for each i-leaf, the CSR list

@@ -10,162 +10,15 @@
 // cell-sorted SoA. Every directed pair (i <- j) is evaluated exactly once, with
 // the non-symmetric iact (hydro_iact.h:130,276,488), so the sums are
 // deterministic and need no atomics.
+#include "swh_gather.h"
 #include "swh_internal.h"
-#include "swh_physics.h"
-#include "swh_space.h"
+#include "swh_tile.h"
 
 namespace swh {
 
-enum { LOOP_DENSITY = 0, LOOP_GRADIENT = 1, LOOP_FORCE = 2 };
-
-__device__ __forceinline__ double wrap_nearest(double d, double box) {
-  return d > 0.5 * box ? d - box : (d < -0.5 * box ? d + box : d);
-}
-
-// ---------------------------------------------------------------------------
-// Per-loop gather states. visit() receives a candidate j with its (periodic
-// image) separation dx = x_i - x_j.
-// ---------------------------------------------------------------------------
-template <typename T>
-struct DensityState {
-  int self;
-  T hig2, hi_inv, vix, viy, viz;
-  DensityAcc<T> A;
-  int n;
-  __device__ __forceinline__ void visit(const SoA& a, int j, const double4& pj, T dx, T dy,
-                                        T dz) {
-    const T r2 = dx * dx + dy * dy + dz * dz;
-    if (r2 < hig2 && j != self) {
-      const float4 v = a.vm[j];
-      iact_nonsym_density<T>(r2, dx, dy, dz, hi_inv, vix, viy, viz, (T)v.w, (T)v.x, (T)v.y,
-                             (T)v.z, A);
-      n++;
-    }
-  }
-};
-
-template <typename T>
-struct GradientState {
-  int self;
-  T hi, hig2, vix, viy, viz, ui, ci, a2H;
-  GradientAcc<T> A;
-  int n;
-  __device__ __forceinline__ void visit(const SoA& a, int j, const double4& pj, T dx, T dy,
-                                        T dz) {
-    const T r2 = dx * dx + dy * dy + dz * dz;
-    if (r2 < hig2 && j != self) {
-      const float4 v = a.vm[j];
-      const float4 t = a.th[j];
-      iact_nonsym_gradient<T>(r2, dx, dy, dz, hi, vix, viy, viz, ui, ci, (T)v.w, (T)v.x,
-                              (T)v.y, (T)v.z, (T)t.x, (T)t.y, (T)t.w, (T)a.fc[j].z, a2H, A);
-      n++;
-    }
-  }
-};
-
-template <typename T>
-struct ForceState {
-  int self;
-  T hig2, hi_inv, hid_inv, a2H;
-  ForceIn<T> I;
-  ForceAcc<T> A;
-  int n;
-  __device__ __forceinline__ void visit(const SoA& a, int j, const double4& pj, T dx, T dy,
-                                        T dz) {
-    const T r2 = dx * dx + dy * dy + dz * dz;
-    const T hj = (T)pj.w;
-    const T hjg2 = hj * hj * (T)kGamma2;
-    if ((r2 < hig2 || r2 < hjg2) && j != self) {
-      ForceIn<T> J;
-      const float4 v = a.vm[j];
-      const float4 t = a.th[j];
-      const float4 c = a.fc[j];
-      J.vx = v.x; J.vy = v.y; J.vz = v.z; J.m = v.w;
-      J.h = hj;
-      J.u = t.x; J.rho = t.y; J.P = t.z; J.c = t.w;
-      J.f = c.x; J.balsara = c.y; J.alpha_visc = c.z; J.alpha_diff = c.w;
-      iact_nonsym_force<T>(r2, dx, dy, dz, I, hid_inv, hi_inv, J, a2H, A);
-      const int tbj = a.tb[j];
-      if (tbj > 0 && tbj < A.min_ngb_time_bin) A.min_ngb_time_bin = tbj;
-      n++;
-    }
-  }
-};
-
-// Visit every j in the grid cells overlapping the cube of half-width `reach`
-// around (xi,yi,zi). Rows along x are contiguous; a periodic wrap splits a
-// row into two ranges with an image shift. Dimensions whose range covers the
-// whole box fall back to the nearest-image convention (tools.c pairs_all_*).
-template <typename T, class S>
-__device__ __forceinline__ void gather_grid(const GridDev& g, const int* __restrict__ cs,
-                                            const SoA& a, double xi, double yi, double zi,
-                                            double reach, S& st) {
-  const double xs[3] = {xi, yi, zi};
-  int lo[3], hi[3];
-  bool full[3];
-  for (int k = 0; k < 3; k++) {
-    const double rel = xs[k] - g.origin[k];
-    lo[k] = (int)floor((rel - reach) * g.inv_w[k]);
-    hi[k] = (int)floor((rel + reach) * g.inv_w[k]);
-    if (g.periodic) {
-      full[k] = (hi[k] - lo[k] + 1 >= g.cdim[k]);
-      if (full[k]) {
-        lo[k] = 0;
-        hi[k] = g.cdim[k] - 1;
-      }
-    } else {
-      full[k] = false;
-      lo[k] = lo[k] < 0 ? 0 : lo[k];
-      hi[k] = hi[k] > g.cdim[k] - 1 ? g.cdim[k] - 1 : hi[k];
-    }
-  }
-  for (int cz = lo[2]; cz <= hi[2]; cz++) {
-    int wz = cz;
-    double sz = 0.;
-    if (g.periodic && !full[2]) {
-      if (cz < 0) { wz += g.cdim[2]; sz = -g.dim[2]; }
-      else if (cz >= g.cdim[2]) { wz -= g.cdim[2]; sz = g.dim[2]; }
-    }
-    for (int cy = lo[1]; cy <= hi[1]; cy++) {
-      int wy = cy;
-      double sy = 0.;
-      if (g.periodic && !full[1]) {
-        if (cy < 0) { wy += g.cdim[1]; sy = -g.dim[1]; }
-        else if (cy >= g.cdim[1]) { wy -= g.cdim[1]; sy = g.dim[1]; }
-      }
-      const int row = (wz * g.cdim[1] + wy) * g.cdim[0];
-      int seg_lo[2], seg_hi[2];
-      double seg_sx[2];
-      int nseg;
-      if (!g.periodic || full[0] || (lo[0] >= 0 && hi[0] < g.cdim[0])) {
-        nseg = 1; seg_lo[0] = lo[0]; seg_hi[0] = hi[0]; seg_sx[0] = 0.;
-      } else if (lo[0] < 0) {
-        nseg = 2;
-        seg_lo[0] = lo[0] + g.cdim[0]; seg_hi[0] = g.cdim[0] - 1; seg_sx[0] = -g.dim[0];
-        seg_lo[1] = 0; seg_hi[1] = hi[0]; seg_sx[1] = 0.;
-      } else {
-        nseg = 2;
-        seg_lo[0] = lo[0]; seg_hi[0] = g.cdim[0] - 1; seg_sx[0] = 0.;
-        seg_lo[1] = 0; seg_hi[1] = hi[0] - g.cdim[0]; seg_sx[1] = g.dim[0];
-      }
-      for (int sgi = 0; sgi < nseg; sgi++) {
-        const int j0 = cs[row + seg_lo[sgi]];
-        const int j1 = cs[row + seg_hi[sgi] + 1];
-        const double sx = seg_sx[sgi];
-        for (int j = j0; j < j1; j++) {
-          const double4 pj = a.pos[j];
-          double dx = xi - (pj.x + sx);
-          double dy = yi - (pj.y + sy);
-          double dz = zi - (pj.z + sz);
-          if (full[0]) dx = wrap_nearest(dx, g.dim[0]);
-          if (full[1]) dy = wrap_nearest(dy, g.dim[1]);
-          if (full[2]) dz = wrap_nearest(dz, g.dim[2]);
-          st.visit(a, j, pj, (T)dx, (T)dy, (T)dz);
-        }
-      }
-    }
-  }
-}
+// Per-lane hit-list capacity of the two-phase gather (LDS: 4 waves x CAP x 64
+// x 4 B = 48 KiB per 256-thread block).
+constexpr int kHitCap = 48;
 
 __device__ __forceinline__ void count_add(int n, unsigned long long* counter) {
   unsigned long long v = (unsigned long long)n;
@@ -173,95 +26,49 @@ __device__ __forceinline__ void count_add(int n, unsigned long long* counter) {
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(counter, v);
 }
 
-template <int LOOP, typename T>
-__global__ __launch_bounds__(256) void loop_kernel(GridDev g, const int* __restrict__ cs,
-                                                   SoA a, const int* __restrict__ subset,
+// One thread per i-particle (item t of the launch, or subset[t]); inactive
+// and padding lanes still take part in the wave-level drains of variant 2.
+template <int LOOP, typename T, int VARIANT>
+__global__ __launch_bounds__(256) void loop_kernel(GridDev g, SoA a,
+                                                   const int* __restrict__ subset,
                                                    int nitems, int max_active_bin, T a2H,
                                                    const unsigned int* __restrict__ hmax_bits,
                                                    unsigned long long* counter,
                                                    int* __restrict__ ncount) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  int n = 0;
   const int i = (t < nitems) ? (subset ? subset[t] : t) : -1;
-  if (i >= 0 && a.tb[i] <= max_active_bin) {
-    const double4 pi = a.pos[i];
-    const T hi = (T)pi.w;
-    const T hig2 = hi * hi * (T)kGamma2;
-    const float4 vmi = a.vm[i];
-    if (LOOP == LOOP_DENSITY) {
-      DensityState<T> st;
-      st.self = i;
-      st.hig2 = hig2;
-      st.hi_inv = (T)1 / hi;
-      st.vix = vmi.x; st.viy = vmi.y; st.viz = vmi.z;
-      st.A.zero();
-      st.n = 0;
-      gather_grid<T>(g, cs, a, pi.x, pi.y, pi.z, (double)pi.w * (double)kGamma, st);
-      float4 d = a.dens[i];
-      float4 r = a.rot[i];
-      a.th[i].y = (float)((T)a.th[i].y + st.A.rho);
-      d.x = (float)((T)d.x + st.A.rho_dh);
-      d.y = (float)((T)d.y + st.A.wcount);
-      d.z = (float)((T)d.z + st.A.wcount_dh);
-      d.w = (float)((T)d.w + st.A.div_v);
-      r.x = (float)((T)r.x + st.A.rot_x);
-      r.y = (float)((T)r.y + st.A.rot_y);
-      r.z = (float)((T)r.z + st.A.rot_z);
-      a.dens[i] = d;
-      a.rot[i] = r;
-      n = st.n;
-    } else if (LOOP == LOOP_GRADIENT) {
-      GradientState<T> st;
-      const float4 thi = a.th[i];
-      const float4 gi = a.grad[i];
-      st.self = i;
-      st.hi = hi;
-      st.hig2 = hig2;
-      st.vix = vmi.x; st.viy = vmi.y; st.viz = vmi.z;
-      st.ui = thi.x;
-      st.ci = thi.w;
-      st.a2H = a2H;
-      st.A.v_sig = gi.x;
-      st.A.alpha_visc_max_ngb = gi.y;
-      st.A.laplace_u = 0;
-      st.n = 0;
-      gather_grid<T>(g, cs, a, pi.x, pi.y, pi.z, (double)pi.w * (double)kGamma, st);
-      a.grad[i] = make_float4((float)st.A.v_sig, (float)st.A.alpha_visc_max_ngb, gi.z, gi.w);
-      a.rot[i].w = (float)((T)a.rot[i].w + st.A.laplace_u);
-      n = st.n;
-    } else {
-      ForceState<T> st;
-      const float4 thi = a.th[i];
-      const float4 fci = a.fc[i];
-      st.self = i;
-      st.hig2 = hig2;
-      st.hi_inv = (T)1 / hi;
-      const T hi2 = st.hi_inv * st.hi_inv;
-      st.hid_inv = hi2 * hi2;
-      st.a2H = a2H;
-      st.I.vx = vmi.x; st.I.vy = vmi.y; st.I.vz = vmi.z; st.I.m = vmi.w;
-      st.I.h = hi;
-      st.I.u = thi.x; st.I.rho = thi.y; st.I.P = thi.z; st.I.c = thi.w;
-      st.I.f = fci.x; st.I.balsara = fci.y; st.I.alpha_visc = fci.z; st.I.alpha_diff = fci.w;
-      st.A.ax = st.A.ay = st.A.az = st.A.u_dt = st.A.h_dt = (T)0;
-      st.A.min_ngb_time_bin = a.mintb[i];
-      st.n = 0;
-      const double hmax = (double)__uint_as_float(*hmax_bits) * (double)kGamma;
-      const double reach = fmax(hmax, (double)pi.w * (double)kGamma);
-      gather_grid<T>(g, cs, a, pi.x, pi.y, pi.z, reach, st);
-      float4 ac = a.acc[i];
-      ac.x = (float)((T)ac.x + st.A.ax);
-      ac.y = (float)((T)ac.y + st.A.ay);
-      ac.z = (float)((T)ac.z + st.A.az);
-      ac.w = (float)((T)ac.w + st.A.u_dt);
-      a.acc[i] = ac;
-      a.hdt[i] = (float)((T)a.hdt[i] + st.A.h_dt);
-      a.mintb[i] = (int8_t)st.A.min_ngb_time_bin;
-      n = st.n;
-    }
-    if (ncount) ncount[i] = n;
+  const bool act = i >= 0 && a.tb[i] <= max_active_bin;
+  LoopState<LOOP, T> st;
+  st.n = 0;
+  double4 pi = make_double4(0., 0., 0., 0.);
+  if (act) {
+    st.load_i(a, i, a2H, hmax_bits);
+    pi = a.pos[i];
   }
-  if (counter) count_add(n, counter);
+  if (VARIANT == 2) {
+    __shared__ int hits[4][kHitCap * 64];
+    gather_two_phase<kHitCap, T>(g, a, pi, act, st, hits[threadIdx.x >> 6], threadIdx.x & 63);
+  } else if (act) {
+    gather_direct<T>(g, a, pi, st);
+  }
+  if (act) {
+    st.store(a, i);
+    if (ncount) ncount[i] = st.n;
+  }
+  if (counter) count_add(act ? st.n : 0, counter);
+}
+
+// Variant 3: NS = 64/SG i-groups per 64-lane wave (swh_tile.h).
+template <int LOOP, typename T, int SG>
+__global__ __launch_bounds__(64) void tile_kernel(GridDev g, SoA a,
+                                                  const int2* __restrict__ groups, int ngroups,
+                                                  int max_active_bin, T a2H,
+                                                  const unsigned int* __restrict__ hmax_bits,
+                                                  unsigned long long* counter,
+                                                  int* __restrict__ ncount) {
+  __shared__ TileLds<SG, TileSlots<LOOP>::value, LoopState<LOOP, T>::kPay> lds;
+  tile_loop<LOOP, T, SG>(g, a, groups, ngroups, max_active_bin, a2H, hmax_bits, counter, ncount,
+                         lds);
 }
 
 // hydro_init_part (src/hydro/SPHENIX/hydro.h:553-566) on active particles.
@@ -545,24 +352,54 @@ static unsigned long long* counter_slot(swh_space* s) {
 }
 static unsigned int* hmax_slot(swh_space* s) { return s->counters.as<unsigned int>() + 2; }
 
+template <int LOOP, typename T>
+static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int nitems,
+                         int max_active_bin, T a2H, unsigned long long* ctr, int* ncount) {
+  // the tile loop needs the rebuild's compact i-groups: subsets (ghost reruns)
+  // take the per-particle direct gather
+  const int v = s->tuning.loop_variant == 0 ? 3 : s->tuning.loop_variant;
+  if (v == 3 && !subset) {
+    const int sg = s->tuning.group_size > 0 ? s->tuning.group_size : 16;
+    const int nw = (s->ngroups + 64 / sg - 1) / (64 / sg);
+    const int2* grp = s->groups.as<const int2>();
+    if (sg == 16)
+      hipLaunchKernelGGL((tile_kernel<LOOP, T, 16>), dim3(nw), dim3(64), 0, s->stream, gd,
+                         soa_of(s), grp, s->ngroups, max_active_bin, a2H, hmax_slot(s), ctr,
+                         ncount);
+    else if (sg == 32)
+      hipLaunchKernelGGL((tile_kernel<LOOP, T, 32>), dim3(nw), dim3(64), 0, s->stream, gd,
+                         soa_of(s), grp, s->ngroups, max_active_bin, a2H, hmax_slot(s), ctr,
+                         ncount);
+    else
+      hipLaunchKernelGGL((tile_kernel<LOOP, T, 64>), dim3(nw), dim3(64), 0, s->stream, gd,
+                         soa_of(s), grp, s->ngroups, max_active_bin, a2H, hmax_slot(s), ctr,
+                         ncount);
+    return;
+  }
+  const int block = 256;
+  const int grid = (nitems + block - 1) / block;
+  if (v == 2)
+    hipLaunchKernelGGL((loop_kernel<LOOP, T, 2>), dim3(grid), dim3(block), 0, s->stream, gd,
+                       soa_of(s), subset, nitems, max_active_bin, a2H, hmax_slot(s), ctr, ncount);
+  else
+    hipLaunchKernelGGL((loop_kernel<LOOP, T, 1>), dim3(grid), dim3(block), 0, s->stream, gd,
+                       soa_of(s), subset, nitems, max_active_bin, a2H, hmax_slot(s), ctr, ncount);
+}
+
 template <int LOOP>
 static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const int* subset,
                               int nitems, bool count) {
   if (nitems <= 0) return SWH_OK;
-  const GridDev gd = grid_dev(s->grid);
-  const int block = 256;
-  const int grid = (nitems + block - 1) / block;
+  if (!subset && s->ngroups <= 0) return SWH_OK;
+  const GridDev gd = grid_dev(s);
   const double a2H = P->a * P->a * P->H;
   unsigned long long* ctr = count ? counter_slot(s) : nullptr;
   int* ncount = count ? s->ncount.as<int>() : nullptr;
   if (s->ctx->precision == SWH_PRECISION_F64)
-    hipLaunchKernelGGL((loop_kernel<LOOP, double>), dim3(grid), dim3(block), 0, s->stream, gd,
-                       s->cell_start.as<const int>(), soa_of(s), subset, nitems,
-                       P->max_active_bin, a2H, hmax_slot(s), ctr, ncount);
+    launch_typed<LOOP, double>(s, gd, subset, nitems, P->max_active_bin, a2H, ctr, ncount);
   else
-    hipLaunchKernelGGL((loop_kernel<LOOP, float>), dim3(grid), dim3(block), 0, s->stream, gd,
-                       s->cell_start.as<const int>(), soa_of(s), subset, nitems,
-                       P->max_active_bin, (float)a2H, hmax_slot(s), ctr, ncount);
+    launch_typed<LOOP, float>(s, gd, subset, nitems, P->max_active_bin, (float)a2H, ctr,
+                              ncount);
   SWH_HIP(hipGetLastError());
   return SWH_OK;
 }

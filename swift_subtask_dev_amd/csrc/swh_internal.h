@@ -139,7 +139,8 @@ struct SwhGrid {
   double hmax = 0;  // max H = gamma*h over all particles at rebuild
 };
 
-// Device-resident particle set, sorted by grid cell (x fastest).
+// Device-resident particle set, sorted by grid cell in Morton order of the
+// cells (cell_rank maps a linear x-fastest cell index to its Morton rank).
 struct swh_space {
   swh_context* ctx = nullptr;
   hipStream_t stream = nullptr;
@@ -147,7 +148,7 @@ struct swh_space {
   int64_t n = 0;
   bool built = false;
   SwhGrid grid;
-  swh_tuning tuning{1, 0};
+  swh_tuning tuning{1, 0, 0};
 
   // AoS image of the caller's records (for write-back of untouched fields)
   swh::DevBuf aos;
@@ -169,7 +170,14 @@ struct swh_space {
   swh::DevBuf perm;  // int32 sorted index -> caller index
   swh::DevBuf ncount;  // int32 per-particle interaction count (diagnostic)
   // grid
-  swh::DevBuf cell_start;  // int32[ncell+1]
+  swh::DevBuf cell_start;  // int32[ncell+1], indexed by Morton rank
+  swh::DevBuf cell_rank;   // int32[ncell]: linear cell -> Morton rank
+  swh::DevBuf cell_code;   // uint32[ncell]: Morton code of each rank (ascending)
+  swh::DevBuf cell_span;   // int2[ncell]: linear cell -> sorted range
+  int rank_cdim[3] = {0, 0, 0};  // grid the rank table was built for
+  swh::DevBuf groups;      // int2[ngroups]: i-groups (start, count) of the tile loops
+  swh::DevBuf seg_groups, seg_off;
+  int32_t ngroups = 0;
   // scratch
   swh::DevBuf keys, keys2, idx, idx2, sort_tmp, scan_tmp, counters;
   swh::DevBuf tmp_soa;     // staging for permutation gathers

@@ -28,10 +28,18 @@ struct GridDev {
   double inv_w[3];
   double origin[3];
   double dim[3];
+  const int2* span;  // linear (x-fastest) cell -> its sorted range [x, y)
 };
 
-inline GridDev grid_dev(const SwhGrid& g) {
+// Sorted range of grid cell (cx, cy, cz) (already wrapped into the grid).
+__device__ __forceinline__ int2 cell_range_of(const GridDev& g, int cx, int cy, int cz) {
+  return g.span[(cz * g.cdim[1] + cy) * g.cdim[0] + cx];
+}
+
+inline GridDev grid_dev(const swh_space* s) {
+  const SwhGrid& g = s->grid;
   GridDev d;
+  d.span = s->cell_span.as<const int2>();
   for (int k = 0; k < 3; k++) {
     d.cdim[k] = g.cdim[k];
     d.w[k] = g.w[k];

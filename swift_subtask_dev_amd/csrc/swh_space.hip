@@ -3,9 +3,14 @@
 // the neighbour-grid rebuild that replaces space_rebuild + runner_do_hydro_sort
 // (src/space.c, src/runner_sort.c:201-431) for this path: particles are
 // binned into a uniform grid of cells of width >= max(H)/cell_factor and
-// stably radix-sorted by cell index (x fastest), so every grid row is one
-// contiguous range of the SoA arrays.
+// stably radix-sorted by the Morton rank of their cell, so every cell is one
+// contiguous range of the SoA arrays and consecutive cells are close in space.
+// The tile loops' i-groups are cut from that order the way SWIFT splits its
+// cell tree into leaves (space_split, cell.c): runs of consecutive cells of
+// one aligned Morton block holding <= 64 particles.
 #include <hipcub/hipcub.hpp>
+
+#include <cstring>
 
 #include "swh_internal.h"
 #include "swh_physics.h"
@@ -127,9 +132,9 @@ __global__ void bbox_kernel(const double4* __restrict__ pos, const int8_t* __res
 
 // Inhibited particles get key = ncell: they sort behind every cell and are
 // never visited as neighbours (the loops' part_is_inhibited skip).
-__global__ void key_kernel(GridDev g, double4* __restrict__ pos, const int8_t* __restrict__ tb,
-                           int64_t n, int ncell, uint32_t* __restrict__ keys,
-                           int* __restrict__ idx) {
+__global__ void key_kernel(GridDev g, const int* __restrict__ rank, double4* __restrict__ pos,
+                           const int8_t* __restrict__ tb, int64_t n, int ncell,
+                           uint32_t* __restrict__ keys, int* __restrict__ idx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   idx[i] = (int)i;
@@ -154,7 +159,139 @@ __global__ void key_kernel(GridDev g, double4* __restrict__ pos, const int8_t* _
     ck = ck < 0 ? 0 : (ck >= g.cdim[k] ? g.cdim[k] - 1 : ck);
     c[k] = ck;
   }
-  keys[i] = (uint32_t)((c[2] * g.cdim[1] + c[1]) * g.cdim[0] + c[0]);
+  keys[i] = (uint32_t)rank[(c[2] * g.cdim[1] + c[1]) * g.cdim[0] + c[0]];
+}
+
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 10 bits -> every 3rd bit
+  v &= 0x3ffu;
+  v = (v | (v << 16)) & 0x030000ffu;
+  v = (v | (v << 8)) & 0x0300f00fu;
+  v = (v | (v << 4)) & 0x030c30c3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+
+// Morton code of every linear cell (cdim <= 1024 per dimension).
+__global__ void morton_kernel(int cx, int cy, int ncell, uint32_t* __restrict__ code,
+                              int* __restrict__ lin) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncell) return;
+  const uint32_t x = c % cx, y = (c / cx) % cy, z = c / (cx * cy);
+  code[c] = spread3(x) | (spread3(y) << 1) | (spread3(z) << 2);
+  lin[c] = c;
+}
+
+__global__ void span_kernel(const int* __restrict__ rank, const int* __restrict__ cs, int ncell,
+                            int2* __restrict__ span) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncell) return;
+  const int r = rank[c];
+  span[c] = make_int2(cs[r], cs[r + 1]);
+}
+
+__global__ void rank_scatter_kernel(const int* __restrict__ sorted_lin, int ncell,
+                                    int* __restrict__ rank) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < ncell) rank[sorted_lin[k]] = k;
+}
+
+// i-groups of the tile loops: the leaves of the octree over the Morton-ordered
+// cells with at most kGroupMax (= the tile row width) particles (space_split's rule with
+// space_splitsize = kGroupMax), consecutive sibling leaves merged while they
+// fit. A block at level L = the aligned 2^L-cube of cells sharing code >> 3L;
+// its cells are one contiguous rank range (ranks sorted by code). One thread
+// per cell; the first cell of a leaf block emits its group. Cells holding more
+// than kGroupMax particles are split into chunks of kGroupMax.
+constexpr int kMaxLevel = 10;  // 30-bit codes
+
+__device__ __forceinline__ int lower_bound_u32(const uint32_t* __restrict__ a, int n,
+                                               uint32_t v) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+struct BlockSpan {
+  int r0, r1;  // rank range
+  int count;   // particles
+};
+
+__device__ __forceinline__ BlockSpan block_span(const uint32_t* __restrict__ code,
+                                                const int* __restrict__ cs, int ncell,
+                                                uint32_t lo_code, int level) {
+  BlockSpan b;
+  const uint64_t hi_code = (uint64_t)lo_code + (1ull << (3 * level));
+  b.r0 = lower_bound_u32(code, ncell, lo_code);
+  b.r1 = hi_code > 0xffffffffull ? ncell : lower_bound_u32(code, ncell, (uint32_t)hi_code);
+  b.count = cs[b.r1] - cs[b.r0];
+  return b;
+}
+
+template <bool WRITE>
+__global__ void group_kernel(const uint32_t* __restrict__ code, const int* __restrict__ cs,
+                             int ncell, int kGroupMax, int* __restrict__ ngroup,
+                             const int* __restrict__ off, int2* __restrict__ out) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= ncell) return;
+  const uint32_t c = code[r];
+  int ng = 0;
+  const int n0 = cs[r + 1] - cs[r];
+  auto emit = [&](int start, int count) {
+    if (WRITE) out[off[r] + ng] = make_int2(start, count);
+    ng++;
+  };
+  if (n0 > kGroupMax) {  // oversized cell: chunks
+    for (int s = 0; s < n0; s += kGroupMax) emit(cs[r] + s, min(kGroupMax, n0 - s));
+  } else {
+    int L = 0;  // largest level whose block holds <= kGroupMax particles
+    BlockSpan leaf;
+    leaf.r0 = r;
+    leaf.r1 = r + 1;
+    leaf.count = n0;
+    for (int l = 1; l <= kMaxLevel; l++) {
+      const BlockSpan b = block_span(code, cs, ncell, (c >> (3 * l)) << (3 * l), l);
+      if (b.count > kGroupMax) break;
+      L = l;
+      leaf = b;
+    }
+    if (leaf.r0 == r && leaf.count > 0) {  // head of a non-empty leaf
+      if (L == kMaxLevel) {
+        emit(cs[leaf.r0], leaf.count);
+      } else {
+        // greedy merge over the parent's children, in order; a child holding
+        // more than kGroupMax particles (split further) breaks the run
+        const int mine = (int)((c >> (3 * L)) & 7u);
+        const uint32_t parent = (c >> (3 * (L + 1))) << (3 * (L + 1));
+        int run_start = -1, run_r0 = 0, sum = 0;
+        for (int o = 0; o < 8; o++) {
+          const BlockSpan ch = block_span(code, cs, ncell, parent + ((uint32_t)o << (3 * L)), L);
+          if (ch.count > kGroupMax) {
+            if (run_start == mine) emit(cs[run_r0], sum);
+            run_start = -1;
+            sum = 0;
+            continue;
+          }
+          if (ch.count == 0) continue;
+          if (run_start >= 0 && sum + ch.count > kGroupMax) {
+            if (run_start == mine) emit(cs[run_r0], sum);
+            run_start = -1;
+            sum = 0;
+          }
+          if (run_start < 0) {
+            run_start = o;
+            run_r0 = ch.r0;
+          }
+          sum += ch.count;
+        }
+        if (run_start == mine) emit(cs[run_r0], sum);
+      }
+    }
+  }
+  if (!WRITE) ngroup[r] = ng;
 }
 
 // Gather every SoA array through the sort permutation (src -> dst).
@@ -195,6 +332,7 @@ __global__ void hmax_kernel(const double4* __restrict__ pos, const int8_t* __res
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   if ((threadIdx.x & 63) == 0) atomicMax(out_bits, __float_as_uint(m));
 }
+
 
 }  // namespace swh
 
@@ -320,7 +458,8 @@ swh_status swh_space_destroy(swh_space* s) {
   (void)hipStreamSynchronize(s->stream);
   DevBuf* bufs[] = {&s->aos, &s->pos, &s->vm, &s->th, &s->fc, &s->tb, &s->dens, &s->rot,
                     &s->grad, &s->acc, &s->hdt, &s->mintb, &s->perm, &s->ncount,
-                    &s->cell_start, &s->keys, &s->keys2, &s->idx, &s->idx2, &s->sort_tmp,
+                    &s->cell_start, &s->cell_rank, &s->cell_code, &s->cell_span, &s->groups, &s->seg_groups,
+                    &s->seg_off, &s->keys, &s->keys2, &s->idx, &s->idx2, &s->sort_tmp,
                     &s->scan_tmp, &s->counters, &s->tmp_soa, &s->ghost_left,
                     &s->ghost_right, &s->ghost_list, &s->ghost_list2, &s->ghost_flag};
   for (DevBuf* b : bufs) b->release();
@@ -344,13 +483,29 @@ swh_status swh_space_set_stream(swh_space* s, void* stream) {
 }
 
 swh_status swh_space_set_tuning(swh_space* s, const swh_tuning* t) {
-  if (!s || !t || t->cell_factor < 1 || t->cell_factor > 4) return SWH_ERR_ARG;
+  if (!s || !t || t->cell_factor < 1 || t->cell_factor > 4 || t->loop_variant < 0 ||
+      t->loop_variant > 3 ||
+      (t->group_size != 0 && t->group_size != 16 && t->group_size != 32 && t->group_size != 64))
+    return SWH_ERR_ARG;
   s->tuning = *t;
   s->built = false;
   return SWH_OK;
 }
 
 int64_t swh_space_count(const swh_space* s) { return s ? s->n : 0; }
+
+swh_status swh_space_get_info(const swh_space* s, swh_space_info* info) {
+  if (!s || !info) return SWH_ERR_ARG;
+  std::memset(info, 0, sizeof(*info));
+  for (int k = 0; k < 3; k++) {
+    info->cdim[k] = s->grid.cdim[k];
+    info->cell_width[k] = s->grid.w[k];
+  }
+  info->ncell = s->grid.ncell;
+  info->ngroups = s->ngroups;
+  info->h_max = s->grid.hmax;
+  return SWH_OK;
+}
 
 swh_status swh_space_sync(swh_space* s) {
   if (!s) return SWH_ERR_ARG;
@@ -463,15 +618,42 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
   }
   for (int k = 0; k < 3; k++) g.w[k] = g.dim[k] / g.cdim[k];
   g.ncell = (int)total;
-  GridDev gd = grid_dev(g);
-  // 2. keys + stable radix sort by cell
-  SWH_TRY(s->keys.reserve(n * sizeof(uint32_t)));
-  SWH_TRY(s->keys2.reserve(n * sizeof(uint32_t)));
-  SWH_TRY(s->idx.reserve(n * sizeof(int)));
-  SWH_TRY(s->idx2.reserve(n * sizeof(int)));
   const int block = 256;
+  const int64_t nsort = std::max<int64_t>(n, g.ncell);
+  SWH_TRY(s->keys.reserve(nsort * sizeof(uint32_t)));
+  SWH_TRY(s->keys2.reserve(nsort * sizeof(uint32_t)));
+  SWH_TRY(s->idx.reserve(nsort * sizeof(int)));
+  SWH_TRY(s->idx2.reserve(nsort * sizeof(int)));
+  // 2a. Morton rank of every cell (cached per grid shape)
+  if (s->rank_cdim[0] != g.cdim[0] || s->rank_cdim[1] != g.cdim[1] ||
+      s->rank_cdim[2] != g.cdim[2]) {
+    SWH_TRY(s->cell_rank.reserve((size_t)g.ncell * sizeof(int)));
+    const int cg = (g.ncell + block - 1) / block;
+    hipLaunchKernelGGL(morton_kernel, dim3(cg), dim3(block), 0, st, g.cdim[0], g.cdim[1],
+                       g.ncell, s->keys.as<uint32_t>(), s->idx.as<int>());
+    SWH_HIP(hipGetLastError());
+    size_t mb = 0;
+    SWH_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, mb, s->keys.as<uint32_t>(),
+                                               s->keys2.as<uint32_t>(), s->idx.as<int>(),
+                                               s->idx2.as<int>(), g.ncell, 0, 30, st));
+    SWH_TRY(s->sort_tmp.reserve(mb));
+    SWH_HIP(hipcub::DeviceRadixSort::SortPairs(s->sort_tmp.ptr, mb, s->keys.as<uint32_t>(),
+                                               s->keys2.as<uint32_t>(), s->idx.as<int>(),
+                                               s->idx2.as<int>(), g.ncell, 0, 30, st));
+    hipLaunchKernelGGL(rank_scatter_kernel, dim3(cg), dim3(block), 0, st,
+                       s->idx2.as<const int>(), g.ncell, s->cell_rank.as<int>());
+    SWH_HIP(hipGetLastError());
+    SWH_TRY(s->cell_code.reserve((size_t)g.ncell * sizeof(uint32_t)));
+    SWH_HIP(hipMemcpyAsync(s->cell_code.ptr, s->keys2.ptr, (size_t)g.ncell * sizeof(uint32_t),
+                           hipMemcpyDeviceToDevice, st));
+    for (int k = 0; k < 3; k++) s->rank_cdim[k] = g.cdim[k];
+  }
+  SWH_TRY(s->cell_start.reserve(((size_t)g.ncell + 1) * sizeof(int)));
+  GridDev gd = grid_dev(s);
+  // 2b. keys (Morton rank of the cell) + stable radix sort
   const int grid = (int)((n + block - 1) / block);
-  hipLaunchKernelGGL(key_kernel, dim3(grid), dim3(block), 0, st, gd, s->pos.as<double4>(),
+  hipLaunchKernelGGL(key_kernel, dim3(grid), dim3(block), 0, st, gd,
+                     s->cell_rank.as<const int>(), s->pos.as<double4>(),
                      s->tb.as<const int8_t>(), n, g.ncell, s->keys.as<uint32_t>(),
                      s->idx.as<int>());
   SWH_HIP(hipGetLastError());
@@ -494,10 +676,42 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
   SWH_HIP(hipGetLastError());
   SWH_TRY(copy_soa(tmp, s, st));
   // 4. cell starts
-  SWH_TRY(s->cell_start.reserve(((size_t)g.ncell + 1) * sizeof(int)));
   hipLaunchKernelGGL(cell_start_kernel, dim3((int)((n + 1 + block - 1) / block)), dim3(block),
                      0, st, s->keys2.as<const uint32_t>(), n, g.ncell,
                      s->cell_start.as<int>());
+  SWH_HIP(hipGetLastError());
+  // 4b. per-linear-cell span table (one load per cell lookup in the loops)
+  SWH_TRY(s->cell_span.reserve((size_t)g.ncell * sizeof(int2)));
+  hipLaunchKernelGGL(span_kernel, dim3((g.ncell + block - 1) / block), dim3(block), 0, st,
+                     s->cell_rank.as<const int>(), s->cell_start.as<const int>(), g.ncell,
+                     s->cell_span.as<int2>());
+  SWH_HIP(hipGetLastError());
+  // 5. i-groups of the tile loops
+  const int nc = g.ncell;
+  const int gmax = s->tuning.group_size > 0 ? s->tuning.group_size : 16;
+  SWH_TRY(s->seg_groups.reserve(((size_t)nc + 1) * sizeof(int)));
+  SWH_TRY(s->seg_off.reserve(((size_t)nc + 1) * sizeof(int)));
+  const int cgrid = (nc + block - 1) / block;
+  hipLaunchKernelGGL(group_kernel<false>, dim3(cgrid), dim3(block), 0, st,
+                     s->cell_code.as<const uint32_t>(), s->cell_start.as<const int>(), nc,
+                     gmax, s->seg_groups.as<int>(), nullptr, nullptr);
+  SWH_HIP(hipGetLastError());
+  SWH_HIP(hipMemsetAsync(s->seg_groups.as<int>() + nc, 0, sizeof(int), st));
+  size_t sb = 0;
+  SWH_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, sb, s->seg_groups.as<int>(),
+                                           s->seg_off.as<int>(), nc + 1, st));
+  SWH_TRY(s->scan_tmp.reserve(std::max(sb, (size_t)nb * 7 * sizeof(double))));
+  SWH_HIP(hipcub::DeviceScan::ExclusiveSum(s->scan_tmp.ptr, sb, s->seg_groups.as<int>(),
+                                           s->seg_off.as<int>(), nc + 1, st));
+  int ng = 0;
+  SWH_HIP(hipMemcpyAsync(&ng, s->seg_off.as<int>() + nc, sizeof(int), hipMemcpyDeviceToHost,
+                         st));
+  SWH_HIP(hipStreamSynchronize(st));
+  s->ngroups = ng;
+  SWH_TRY(s->groups.reserve(((size_t)ng + 1) * sizeof(int2)));
+  hipLaunchKernelGGL(group_kernel<true>, dim3(cgrid), dim3(block), 0, st,
+                     s->cell_code.as<const uint32_t>(), s->cell_start.as<const int>(), nc,
+                     gmax, nullptr, s->seg_off.as<const int>(), s->groups.as<int2>());
   SWH_HIP(hipGetLastError());
   SWH_TRY(space_hmax_to_device(s));
   s->built = true;

@@ -34,7 +34,8 @@ HIP_SYMBOLS = [
     "swh_space_download_parts", "swh_space_count", "swh_space_rebuild", "swh_space_init_parts",
     "swh_space_reset_acceleration",
     "swh_density_loop", "swh_ghost", "swh_gradient_loop", "swh_extra_ghost", "swh_force_loop",
-    "swh_end_force", "swh_space_sync", "swh_space_set_tuning", "swh_gspace_create",
+    "swh_end_force", "swh_space_sync", "swh_space_set_tuning", "swh_space_get_info",
+    "swh_gspace_create",
     "swh_gspace_destroy", "swh_gspace_upload", "swh_gspace_set_leaves", "swh_grav_pp_batch",
     "swh_gspace_download", "swh_gspace_sync",
 ]
@@ -107,6 +108,7 @@ def load() -> C.CDLL:
         "swh_end_force": (C.c_int, [vp, P(abi.HydroParams)]),
         "swh_space_sync": (C.c_int, [vp]),
         "swh_space_set_tuning": (C.c_int, [vp, P(abi.Tuning)]),
+        "swh_space_get_info": (C.c_int, [vp, P(abi.SpaceInfo)]),
         "swh_gspace_create": (C.c_int, [vp, P(vp)]),
         "swh_gspace_destroy": (C.c_int, [vp]),
         "swh_gspace_upload": (C.c_int, [vp, vp, i64, P(abi.GPartLayout), C.c_int]),
@@ -253,9 +255,15 @@ class HydroSpace:
         except Exception:
             pass
 
-    def set_tuning(self, cell_factor=1, loop_variant=0):
-        t = abi.Tuning(cell_factor, loop_variant)
+    def set_tuning(self, cell_factor=1, loop_variant=0, group_size=0):
+        t = abi.Tuning(cell_factor, loop_variant, group_size)
         _check(self._lib.swh_space_set_tuning(self.handle, C.byref(t)), "set_tuning")
+
+    def info(self) -> dict:
+        i = abi.SpaceInfo()
+        _check(self._lib.swh_space_get_info(self.handle, C.byref(i)), "get_info")
+        return {"cdim": list(i.cdim), "ncell": i.ncell, "ngroups": i.ngroups,
+                "cell_width": list(i.cell_width), "h_max": i.h_max}
 
     def upload(self, parts, count=None, on_device=False):
         """parts: numpy PART_DTYPE array (host) or a device pointer (int) with count."""

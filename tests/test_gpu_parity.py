@@ -245,11 +245,16 @@ def test_125cells_chain_vs_f64(gpu_ctx):
     assert_close(gr["main"]["a_hydro"], orc["main"]["a_hydro"], 1e-5, 1e-3, "a_hydro")
 
 
-def box_chain_gpu(ctx, parts, P, cell_factor=1):
+# loop_variant 1 = per-particle direct gather, 2 = per-particle two-phase,
+# 3 = tile (one wave per i-group; the default)
+VARIANTS = [1, 2, 3]
+
+
+def box_chain_gpu(ctx, parts, P, cell_factor=1, variant=0, group_size=0):
     from swift_subtask_dev_amd import lib
     g = abi.copy_parts(parts)
     sp = lib.HydroSpace(ctx)
-    sp.set_tuning(cell_factor)
+    sp.set_tuning(cell_factor, variant, group_size)
     sp.upload(g)
     sp.rebuild(P)
     res = sp.hydro_step(P)
@@ -275,8 +280,9 @@ def box_chain_oracle(parts, P, prec="f64"):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("variant,group_size", [(1, 0), (2, 0), (3, 16), (3, 32), (3, 64)])
 @pytest.mark.parametrize("cell_factor", [1, 2, 3])
-def test_box_density_vs_f64(gpu_ctx, cell_factor):
+def test_box_density_vs_f64(gpu_ctx, cell_factor, variant, group_size):
     """Batch density loop on a periodic Sedov-like box vs the fp64 oracle;
     identical interaction count; every grid refinement gives the same sums."""
     from swift_subtask_dev_amd import lib
@@ -284,7 +290,7 @@ def test_box_density_vs_f64(gpu_ctx, cell_factor):
     parts = ics.sedov_box(20, velocity="divergent", seed=11)
     g = abi.copy_parts(parts)
     sp = lib.HydroSpace(gpu_ctx)
-    sp.set_tuning(cell_factor)
+    sp.set_tuning(cell_factor, variant, group_size)
     sp.upload(g)
     sp.rebuild(P)
     sp.init_parts(P)
@@ -298,14 +304,15 @@ def test_box_density_vs_f64(gpu_ctx, cell_factor):
 
 
 @pytest.mark.gpu
-def test_box_chain_vs_f64(gpu_ctx):
+@pytest.mark.parametrize("variant,group_size", [(1, 0), (2, 0), (3, 16), (3, 64)])
+def test_box_chain_vs_f64(gpu_ctx, variant, group_size):
     """Full SPHENIX chain (density, ghost with h iteration, gradient, extra
     ghost, force, end force) on a perturbed box with h off-target so the
     ghost iterates."""
     P = abi.default_hydro_params()
     parts = ics.sedov_box(16, velocity="divergent", pert=0.3, seed=5)
     parts["h"] *= np.random.Generator(np.random.PCG64(1)).uniform(0.8, 1.25, len(parts))
-    g, rg = box_chain_gpu(gpu_ctx, parts, P)
+    g, rg = box_chain_gpu(gpu_ctx, parts, P, variant=variant, group_size=group_size)
     o, ro = box_chain_oracle(parts, P)
     assert rg["ghost_iterations"] >= 2
     # Chain tolerance: the GPU keeps struct-part (float) storage between the
@@ -315,8 +322,11 @@ def test_box_chain_vs_f64(gpu_ctx):
     for f in ("rho", "pressure", "soundspeed", "balsara", "v_sig", "laplace_u",
               "visc_alpha", "diff_alpha"):
         assert_close(g[f], o[f], 5e-5, 1e-4, f)
-    # grad-h term: f enters only as f/m_j (f_ij = 1 - f_i/m_j): floor at 1e-5 m
-    e = np.abs(g["f"] - o["f"]) / np.maximum(np.abs(o["f"]), 1e-5 * o["mass"])
+    # grad-h term: f is a cancelling rho_dh sum and enters the force only as
+    # f_ij = 1 - f_i/m_j (~1): floor |f| at 1e-3 m, i.e. an absolute error of
+    # 5e-8 in f_ij (float epsilon). The f32 oracle differs from the f64 one by
+    # 1.9e-2 under the 1e-5 m floor on this case; the GPU's fp64 path by 4e-4.
+    e = np.abs(g["f"] - o["f"]) / np.maximum(np.abs(o["f"]), 1e-3 * o["mass"])
     assert e.max() < 5e-5, e.max()
     assert_close(g["a_hydro"], o["a_hydro"], 5e-5, 1e-4, "a_hydro")
     assert_close(g["u_dt"], o["u_dt"], 5e-5, 1e-4, "u_dt")
@@ -355,10 +365,11 @@ def test_box_active_mask_and_inhibited(gpu_ctx):
 
 
 @pytest.mark.gpu
-def test_non_periodic_box(gpu_ctx):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_non_periodic_box(gpu_ctx, variant):
     P = abi.default_hydro_params(periodic=False)
     parts = ics.sedov_box(14, velocity="divergent", seed=21)
-    g, rg = box_chain_gpu(gpu_ctx, parts, P)
+    g, rg = box_chain_gpu(gpu_ctx, parts, P, variant=variant)
     o, ro = box_chain_oracle(parts, P)
     assert rg["density"] == ro["density"]
     assert_close(g["rho"], o["rho"], 1e-5, what="rho")
@@ -366,11 +377,13 @@ def test_non_periodic_box(gpu_ctx):
 
 
 @pytest.mark.gpu
-def test_clustered_box_chain(gpu_ctx):
-    """EAGLE-like stand-in: smoothing lengths spanning >10x after the ghost."""
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_clustered_box_chain(gpu_ctx, variant):
+    """EAGLE-like stand-in: smoothing lengths spanning >10x after the ghost
+    (dense clumps overflow the two-phase hit lists mid-row)."""
     P = abi.default_hydro_params()
     parts = ics.clustered_box(12, n_clumps=3, per_clump=600, seed=4)
-    g, rg = box_chain_gpu(gpu_ctx, parts, P)
+    g, rg = box_chain_gpu(gpu_ctx, parts, P, variant=variant)
     o, ro = box_chain_oracle(parts, P)
     assert g["h"].max() / g["h"].min() > 5
     assert_close(g["h"], o["h"], 1e-5, what="h")
@@ -440,10 +453,15 @@ def test_force_pair_self_adapter(adapter):
     assert not errs, "\n".join(errs)
     assert np.array_equal(g["min_ngb_time_bin"][s:e], b["min_ngb_time_bin"][s:e])
     cg.free_sorts()
-    # fp64 GPU vs fp64 oracle (all 27 cells' force loop, main cell compared)
+    # fp64 GPU vs fp64 oracle (all 27 cells' force loop, main cell compared).
+    # Per-task mode writes each task's fp64 partial sum back into struct
+    # part's float fields (26 pair tasks + 1 self task, as SWIFT's runners
+    # do), so a cancelling sum carries ~27 float roundings of partial sums
+    # up to ~100x the final value: rel 1e-4 (observed 5.5e-5), not TIGHT.
+    # The batch loops, which sum in fp64 across all tasks, are held to TIGHT.
     o = abi.copy_parts(parts)
     O.fn("f64", "box_force")(o.ctypes.data, len(o), C.byref(P), None)
-    assert_close(cols(g[s:e]), cols(o[s:e]), TIGHT, 1e-6, "force f64")
+    assert_close(cols(g[s:e]), cols(o[s:e]), 1e-4, 1e-6, "force f64 (per-task)")
     assert np.array_equal(g["min_ngb_time_bin"][s:e], o["min_ngb_time_bin"][s:e])
 
 

@@ -103,9 +103,13 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=128, help="particles per dimension per GPU")
-    ap.add_argument("--cell-factor", type=int, default=int(os.environ.get("SWH_CELL_FACTOR", "2")))
+    ap.add_argument("--cell-factor", type=int, default=int(os.environ.get("SWH_CELL_FACTOR", "1")))
     ap.add_argument("--loop-variant", type=int, default=int(os.environ.get("SWH_LOOP_VARIANT", "0")),
                     help="0 default (two-phase), 1 direct gather, 2 two-phase gather")
+    ap.add_argument("--cell-scale", type=float, default=float(os.environ.get("SWH_CELL_SCALE", "0")),
+                    help="grid cells per H_max as a real number (overrides --cell-factor)")
+    ap.add_argument("--diag-mode", type=int, default=0,
+                    help="profiling only, results invalid: 1 tile staging only, 2 + candidate tests")
     ap.add_argument("--group-size", type=int, default=int(os.environ.get("SWH_GROUP_SIZE", "0")),
                     help="tile i-group size / row width: 0 (default 16), 16, 32, 64")
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
@@ -149,7 +153,8 @@ def main():
     local, n_owned = decomp.slab_local_set(parts, rank, world, box[0], 1.02 * hmax)
     del parts
     sp = lib.HydroSpace(ctx)
-    sp.set_tuning(args.cell_factor, args.loop_variant, args.group_size)
+    sp.set_tuning(args.cell_factor, args.loop_variant, args.group_size, args.cell_scale,
+                  args.diag_mode)
     # a dedicated (non-NULL) stream: the library's kernels and the timing
     # events share it, so the events bracket exactly the loop kernels
     stream = torch.cuda.Stream()
@@ -236,7 +241,7 @@ def main():
                 "decomposition": f"{world} x-slab(s) + read-only halo, no data-path collective",
                 "density_interactions_per_step": n_density,
                 "force_interactions_per_step": n_force,
-                "cell_factor": args.cell_factor,
+                "cell_factor": args.cell_scale or args.cell_factor,
                 "loop_variant": args.loop_variant,
                 "group_size": args.group_size or 16,
                 "grid_cdim": info["cdim"],

@@ -251,6 +251,9 @@ typedef struct swh_tuning {
   int32_t loop_variant; /* 0 = default (3); 1 = per-particle direct gather, 2 = per-particle
                            two-phase gather, 3 = tile (i-groups in 16/32/64-lane rows) */
   int32_t group_size;   /* tile i-group size = row width: 0 (default 16), 16, 32, 64 */
+  float cell_scale;     /* if > 0: cells per H_max as a real number (overrides cell_factor) */
+  int32_t diag_mode;    /* 0; profiling only (results invalid): 1 = tile staging only,
+                           2 = staging + candidate tests, no interactions */
 } swh_tuning;
 SWH_API swh_status swh_space_set_tuning(swh_space *s, const swh_tuning *t);
 

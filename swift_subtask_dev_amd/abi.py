@@ -165,7 +165,7 @@ class SpaceInfo(C.Structure):
 class Tuning(C.Structure):
     """swh_tuning (include/swifthip.h)."""
     _fields_ = [("cell_factor", C.c_int32), ("loop_variant", C.c_int32),
-                ("group_size", C.c_int32)]
+                ("group_size", C.c_int32), ("cell_scale", C.c_float), ("diag_mode", C.c_int32)]
 
 
 class Leaf(C.Structure):

@@ -36,6 +36,13 @@ __device__ __forceinline__ double wrap_nearest(double d, double box) {
 template <int LOOP, typename T>
 struct LoopState;
 
+// j-side record of a loop as staged by the tile loop.
+template <int N>
+struct JRec {
+  float4 p[N];
+  int meta;
+};
+
 template <typename T>
 struct LoopState<LOOP_DENSITY, T> {
   int self, n;
@@ -55,7 +62,7 @@ struct LoopState<LOOP_DENSITY, T> {
     A.zero();
   }
   __device__ __forceinline__ bool accept(int j, const double4&, T r2) const {
-    return r2 < hig2 && j != self;
+    return (r2 < hig2) & (j != self);
   }
   __device__ __forceinline__ void interact(const SoA& a, int j, const double4&, T dx, T dy,
                                            T dz, T r2) {
@@ -65,9 +72,11 @@ struct LoopState<LOOP_DENSITY, T> {
     n++;
   }
   static constexpr int kPay = 1;
-  __device__ static __forceinline__ void load_j(const SoA& a, int j, float4* p, int& meta) {
-    p[0] = a.vm[j];
-    meta = 0;
+  __device__ static __forceinline__ JRec<1> load_j(const SoA& a, int j) {
+    JRec<1> r;
+    r.p[0] = a.vm[j];
+    r.meta = 0;
+    return r;
   }
   __device__ __forceinline__ void interact_staged(const float4* p, int, const double4&, T dx,
                                                   T dy, T dz, T r2) {
@@ -119,7 +128,7 @@ struct LoopState<LOOP_GRADIENT, T> {
     gw = g.w;
   }
   __device__ __forceinline__ bool accept(int j, const double4&, T r2) const {
-    return r2 < hig2 && j != self;
+    return (r2 < hig2) & (j != self);
   }
   __device__ __forceinline__ void interact(const SoA& a, int j, const double4&, T dx, T dy,
                                            T dz, T r2) {
@@ -130,11 +139,13 @@ struct LoopState<LOOP_GRADIENT, T> {
     n++;
   }
   static constexpr int kPay = 2;
-  __device__ static __forceinline__ void load_j(const SoA& a, int j, float4* p, int& meta) {
+  __device__ static __forceinline__ JRec<2> load_j(const SoA& a, int j) {
     const float4 t = a.th[j];
-    p[0] = a.vm[j];
-    p[1] = make_float4(t.x, t.y, t.w, a.fc[j].z);  // u, rho, c, alpha_visc
-    meta = 0;
+    JRec<2> r;
+    r.p[0] = a.vm[j];
+    r.p[1] = make_float4(t.x, t.y, t.w, a.fc[j].z);  // u, rho, c, alpha_visc
+    r.meta = 0;
+    return r;
   }
   __device__ __forceinline__ void interact_staged(const float4* p, int, const double4&, T dx,
                                                   T dy, T dz, T r2) {
@@ -181,7 +192,7 @@ struct LoopState<LOOP_FORCE, T> {
   }
   __device__ __forceinline__ bool accept(int j, const double4& pj, T r2) const {
     const T hj = (T)pj.w;
-    return (r2 < hig2 || r2 < hj * hj * (T)kGamma2) && j != self;
+    return ((r2 < hig2) | (r2 < hj * hj * (T)kGamma2)) & (j != self);
   }
   __device__ __forceinline__ void interact(const SoA& a, int j, const double4& pj, T dx, T dy,
                                            T dz, T r2) {
@@ -199,11 +210,13 @@ struct LoopState<LOOP_FORCE, T> {
     n++;
   }
   static constexpr int kPay = 3;
-  __device__ static __forceinline__ void load_j(const SoA& a, int j, float4* p, int& meta) {
-    p[0] = a.vm[j];
-    p[1] = a.th[j];
-    p[2] = a.fc[j];
-    meta = a.tb[j];
+  __device__ static __forceinline__ JRec<3> load_j(const SoA& a, int j) {
+    JRec<3> r;
+    r.p[0] = a.vm[j];
+    r.p[1] = a.th[j];
+    r.p[2] = a.fc[j];
+    r.meta = a.tb[j];
+    return r;
   }
   __device__ __forceinline__ void interact_staged(const float4* p, int tbj, const double4& pj,
                                                   T dx, T dy, T dz, T r2) {

@@ -65,10 +65,10 @@ __global__ __launch_bounds__(64) void tile_kernel(GridDev g, SoA a,
                                                   int max_active_bin, T a2H,
                                                   const unsigned int* __restrict__ hmax_bits,
                                                   unsigned long long* counter,
-                                                  int* __restrict__ ncount) {
+                                                  int* __restrict__ ncount, int diag) {
   __shared__ TileLds<SG, TileSlots<LOOP>::value, LoopState<LOOP, T>::kPay> lds;
   tile_loop<LOOP, T, SG>(g, a, groups, ngroups, max_active_bin, a2H, hmax_bits, counter, ncount,
-                         lds);
+                         diag, lds);
 }
 
 // hydro_init_part (src/hydro/SPHENIX/hydro.h:553-566) on active particles.
@@ -365,15 +365,15 @@ static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int
     if (sg == 16)
       hipLaunchKernelGGL((tile_kernel<LOOP, T, 16>), dim3(nw), dim3(64), 0, s->stream, gd,
                          soa_of(s), grp, s->ngroups, max_active_bin, a2H, hmax_slot(s), ctr,
-                         ncount);
+                         ncount, s->tuning.diag_mode);
     else if (sg == 32)
       hipLaunchKernelGGL((tile_kernel<LOOP, T, 32>), dim3(nw), dim3(64), 0, s->stream, gd,
                          soa_of(s), grp, s->ngroups, max_active_bin, a2H, hmax_slot(s), ctr,
-                         ncount);
+                         ncount, s->tuning.diag_mode);
     else
       hipLaunchKernelGGL((tile_kernel<LOOP, T, 64>), dim3(nw), dim3(64), 0, s->stream, gd,
                          soa_of(s), grp, s->ngroups, max_active_bin, a2H, hmax_slot(s), ctr,
-                         ncount);
+                         ncount, s->tuning.diag_mode);
     return;
   }
   const int block = 256;

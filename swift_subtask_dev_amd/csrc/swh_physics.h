@@ -42,11 +42,67 @@ template <typename T> __device__ __forceinline__ T tsqrt(T x);
 template <> __device__ __forceinline__ double tsqrt<double>(double x) { return sqrt(x); }
 template <> __device__ __forceinline__ float tsqrt<float>(float x) { return sqrtf(x); }
 
+// fp64 reciprocal and reciprocal square root: the hardware approximation
+// (v_rcp_f64 / v_rsq_f64) refined by two Newton steps to ~1 ulp, a third of
+// the instructions of an IEEE division / sqrt. The float path keeps the
+// reference's own operations (it is compared with the float oracle).
+__device__ __forceinline__ double rcp_f64(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+__device__ __forceinline__ double rsqrt_f64(double x) {  // x > 0
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  double e = fma(-h * y, y, 0.5);
+  y = fma(y, e, y);
+  e = fma(-h * y, y, 0.5);
+  return fma(y, e, y);
+}
+// a / b: fp64 through rcp_f64, float as the reference writes it.
+template <typename T> __device__ __forceinline__ T tdiv(T a, T b);
+template <> __device__ __forceinline__ double tdiv<double>(double a, double b) {
+  return a * rcp_f64(b);
+}
+template <> __device__ __forceinline__ float tdiv<float>(float a, float b) { return a / b; }
+
+// r = |dx| and 1/r (0 for r = 0, as the loops' r > 0 guard).
+template <typename T> __device__ __forceinline__ void r_and_inv(T r2, T& r, T& r_inv);
+template <>
+__device__ __forceinline__ void r_and_inv<double>(double r2, double& r, double& r_inv) {
+  r_inv = r2 > 0. ? rsqrt_f64(r2) : 0.;
+  r = r2 * r_inv;
+}
+template <>
+__device__ __forceinline__ void r_and_inv<float>(float r2, float& r, float& r_inv) {
+  r = sqrtf(r2);
+  r_inv = r > 0.f ? 1.f / r : 0.f;
+}
+
 // kernel_deval (kernel_hydro.h:257-284). Branch 0: u/H < 1/2, branch 1: < 1,
 // branch 2 (outside support): all-zero coefficients. Coefficients are picked
 // with selects instead of a table load.
 template <typename T>
-__device__ __forceinline__ void kernel_deval(T u, T& W, T& dW_dx) {
+__device__ __forceinline__ void kernel_deval(T u, T& W, T& dW_dx);
+
+// fp64: the same piecewise cubic in closed form, w = (1-x)^3_+ - 4 (1/2-x)^3_+
+// (equal to the table's Horner forms on [0,1/2) and [1/2,1), zero beyond),
+// without the index selects.
+template <>
+__device__ __forceinline__ void kernel_deval<double>(double u, double& W, double& dW_dx) {
+  const double x = u * (double)kGammaInv;
+  const double t = fmax(1. - x, 0.);
+  const double q = fmax(0.5 - x, 0.);
+  const double t2 = t * t, q2 = q * q;
+  W = fma(-4. * q2, q, t2 * t) * ((double)kConstant * (double)kGammaInvDim);
+  dW_dx = fma(12., q2, -3. * t2) * ((double)kConstant * (double)kGammaInvDimPlusOne);
+}
+
+template <>
+__device__ __forceinline__ void kernel_deval<float>(float u, float& W, float& dW_dx) {
+  using T = float;
   const T x = u * (T)kGammaInv;
   const int temp = (int)(x * (T)2);
   const int ind = temp > 2 ? 2 : temp;
@@ -81,7 +137,8 @@ template <typename T>
 __device__ __forceinline__ void iact_nonsym_density(T r2, T dx, T dy, T dz, T hi_inv,
                                                     T vix, T viy, T viz, T mj, T vjx,
                                                     T vjy, T vjz, DensityAcc<T>& A) {
-  const T r = tsqrt(r2);
+  T r, r_inv;
+  r_and_inv(r2, r, r_inv);
   const T ui = r * hi_inv;
   T wi, wi_dx;
   kernel_deval(ui, wi, wi_dx);
@@ -89,7 +146,6 @@ __device__ __forceinline__ void iact_nonsym_density(T r2, T dx, T dy, T dz, T hi
   A.rho_dh -= mj * ((T)kDim * wi + ui * wi_dx);
   A.wcount += wi;
   A.wcount_dh -= ((T)kDim * wi + ui * wi_dx);
-  const T r_inv = r > (T)0 ? (T)1 / r : (T)0;
   const T faci = mj * wi_dx * r_inv;
   const T dvx = vix - vjx, dvy = viy - vjy, dvz = viz - vjz;
   const T dvdr = dvx * dx + dvy * dy + dvz * dz;
@@ -113,8 +169,8 @@ __device__ __forceinline__ void iact_nonsym_gradient(T r2, T dx, T dy, T dz, T h
                                                      T uj_energy, T rhoj, T cj,
                                                      T alphaj, T a2_Hubble,
                                                      GradientAcc<T>& A) {
-  const T r = tsqrt(r2);
-  const T r_inv = r > (T)0 ? (T)1 / r : (T)0;
+  T r, r_inv;
+  r_and_inv(r2, r, r_inv);
   const T dvdr = (vix - vjx) * dx + (viy - vjy) * dy + (viz - vjz) * dz;
   const T dvdr_Hubble = dvdr + a2_Hubble * r2;
   const T omega_ij = tmin(dvdr_Hubble, (T)0);
@@ -122,10 +178,10 @@ __device__ __forceinline__ void iact_nonsym_gradient(T r2, T dx, T dy, T dz, T h
   const T new_v_sig = ci + cj - (T)kViscBeta * mu_ij;
   A.v_sig = tmax(A.v_sig, new_v_sig);
   T wi, wi_dx;
-  const T ui = r / hi;
+  const T ui = tdiv(r, hi);
   kernel_deval(ui, wi, wi_dx);
   const T delta_u_factor = (ui_energy - uj_energy) * r_inv;
-  A.laplace_u += mj * delta_u_factor * wi_dx / rhoj;
+  A.laplace_u += tdiv(mj * delta_u_factor * wi_dx, rhoj);
   A.alpha_visc_max_ngb = tmax(A.alpha_visc_max_ngb, alphaj);
 }
 
@@ -148,8 +204,8 @@ __device__ __forceinline__ void iact_nonsym_force(T r2, T dx, T dy, T dz,
                                                   const ForceIn<T>& I, T hid_inv,
                                                   T hi_inv, const ForceIn<T>& J,
                                                   T a2_Hubble, ForceAcc<T>& A) {
-  const T r = tsqrt(r2);
-  const T r_inv = r > (T)0 ? (T)1 / r : (T)0;
+  T r, r_inv;
+  r_and_inv(r2, r, r_inv);
   const T mi = I.m, mj = J.m;
   const T rhoi = I.rho, rhoj = J.rho;
   const T pressurei = I.P, pressurej = J.P;
@@ -157,7 +213,7 @@ __device__ __forceinline__ void iact_nonsym_force(T r2, T dx, T dy, T dz,
   T wi, wi_dx;
   kernel_deval(xi, wi, wi_dx);
   const T wi_dr = hid_inv * wi_dx;
-  const T hj_inv = (T)1 / J.h;
+  const T hj_inv = tdiv((T)1, J.h);
   const T hj2 = hj_inv * hj_inv;
   const T hjd_inv = hj2 * hj2;
   const T xj = r * hj_inv;
@@ -169,14 +225,14 @@ __device__ __forceinline__ void iact_nonsym_force(T r2, T dx, T dy, T dz,
   const T omega_ij = tmin(dvdr_Hubble, (T)0);
   const T mu_ij = r_inv * omega_ij;
   const T v_sig = I.c + J.c - (T)kViscBeta * mu_ij;
-  const T f_ij = (T)1 - I.f / mj;
-  const T f_ji = (T)1 - J.f / mi;
+  const T f_ij = (T)1 - tdiv(I.f, mj);
+  const T f_ji = (T)1 - tdiv(J.f, mi);
   const T rho_ij = rhoi + rhoj;
   const T alpha = I.alpha_visc + J.alpha_visc;
-  const T visc = (T)-0.25 * alpha * v_sig * mu_ij * (I.balsara + J.balsara) / rho_ij;
+  const T visc = tdiv((T)-0.25 * alpha * v_sig * mu_ij * (I.balsara + J.balsara), rho_ij);
   const T visc_acc_term = (T)0.5 * visc * (wi_dr * f_ij + wj_dr * f_ji) * r_inv;
-  const T P_over_rho2_i = pressurei / (rhoi * rhoi) * f_ij;
-  const T P_over_rho2_j = pressurej / (rhoj * rhoj) * f_ji;
+  const T P_over_rho2_i = tdiv(pressurei, rhoi * rhoi) * f_ij;
+  const T P_over_rho2_j = tdiv(pressurej, rhoj * rhoj) * f_ji;
   const T sph_acc_term = (P_over_rho2_i * wi_dr + P_over_rho2_j * wj_dr) * r_inv;
   const T acc = sph_acc_term + visc_acc_term;
   A.ax -= mj * acc * dx;
@@ -184,16 +240,16 @@ __device__ __forceinline__ void iact_nonsym_force(T r2, T dx, T dy, T dz,
   A.az -= mj * acc * dz;
   const T sph_du_term_i = P_over_rho2_i * dvdr * r_inv * wi_dr;
   const T visc_du_term = (T)0.5 * visc_acc_term * dvdr_Hubble;
-  const T alpha_diff = (pressurei * I.alpha_diff + pressurej * J.alpha_diff) /
-                       (pressurei + pressurej);
+  const T alpha_diff = tdiv(pressurei * I.alpha_diff + pressurej * J.alpha_diff,
+                            pressurei + pressurej);
   const T v_diff = alpha_diff * (T)0.5 *
-                   (tsqrt((T)2 * fabs(pressurei - pressurej) / rho_ij) +
+                   (tsqrt(tdiv((T)2 * fabs(pressurei - pressurej), rho_ij)) +
                     fabs(r_inv * dvdr_Hubble));
   const T diff_du_term =
-      v_diff * (I.u - J.u) * (f_ij * wi_dr / rhoi + f_ji * wj_dr / rhoj);
+      v_diff * (I.u - J.u) * (tdiv(f_ij * wi_dr, rhoi) + tdiv(f_ji * wj_dr, rhoj));
   const T du_dt_i = sph_du_term_i + visc_du_term + diff_du_term;
   A.u_dt += du_dt_i * mj;
-  A.h_dt -= mj * dvdr * r_inv / rhoj * wi_dr;
+  A.h_dt -= tdiv(mj * dvdr * r_inv, rhoj) * wi_dr;
 }
 
 // ---------------------------------------------------------------------------

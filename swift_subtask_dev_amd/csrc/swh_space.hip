@@ -485,7 +485,8 @@ swh_status swh_space_set_stream(swh_space* s, void* stream) {
 swh_status swh_space_set_tuning(swh_space* s, const swh_tuning* t) {
   if (!s || !t || t->cell_factor < 1 || t->cell_factor > 4 || t->loop_variant < 0 ||
       t->loop_variant > 3 ||
-      (t->group_size != 0 && t->group_size != 16 && t->group_size != 32 && t->group_size != 64))
+      (t->group_size != 0 && t->group_size != 16 && t->group_size != 32 && t->group_size != 64) ||
+      t->cell_scale < 0.f || t->cell_scale > 4.f || t->diag_mode < 0 || t->diag_mode > 2)
     return SWH_ERR_ARG;
   s->tuning = *t;
   s->built = false;
@@ -590,8 +591,9 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
   SwhGrid& g = s->grid;
   g.periodic = P->periodic;
   g.hmax = bb[6] * (double)kGamma;
-  double width = min_cell_width > 0 ? min_cell_width
-                                    : g.hmax / (double)std::max(1, s->tuning.cell_factor);
+  const double cells_per_h = s->tuning.cell_scale > 0.f ? (double)s->tuning.cell_scale
+                                                       : (double)std::max(1, s->tuning.cell_factor);
+  double width = min_cell_width > 0 ? min_cell_width : g.hmax / cells_per_h;
   if (!(width > 0)) width = 1.0;
   int64_t total = 1;
   for (int k = 0; k < 3; k++) {

@@ -255,8 +255,9 @@ class HydroSpace:
         except Exception:
             pass
 
-    def set_tuning(self, cell_factor=1, loop_variant=0, group_size=0):
-        t = abi.Tuning(cell_factor, loop_variant, group_size)
+    def set_tuning(self, cell_factor=1, loop_variant=0, group_size=0, cell_scale=0.0,
+                   diag_mode=0):
+        t = abi.Tuning(cell_factor, loop_variant, group_size, cell_scale, diag_mode)
         _check(self._lib.swh_space_set_tuning(self.handle, C.byref(t)), "set_tuning")
 
     def info(self) -> dict:

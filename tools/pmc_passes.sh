@@ -1,0 +1,21 @@
+#!/bin/bash
+# PMC passes over a short bench run (one counter group per pass, kernel-trace
+# only; no runtime/sys trace domains are combined with --pmc).
+# usage: tools/pmc_passes.sh <outdir> [bench args...]
+out="$1"; shift
+mkdir -p "$out"
+rocprofv3 -L > "$out/counters_list.txt" 2>&1 || true
+run() {
+  local name="$1"; shift
+  timeout -k 10 240 rocprofv3 --pmc "$@" --kernel-include-regex "tile_kernel|loop_kernel|p2p_kernel" \
+    -d "$out/$name" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline $BENCH_ARGS \
+    > "$out/$name.log" 2>&1
+  local rc=$?
+  echo "pass $name rc=$rc"
+  return $rc
+}
+run sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU || exit $?
+run sq2 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH || exit $?
+run tcc1 FETCH_SIZE || exit $?
+run tcc2 WRITE_SIZE || exit $?
+run tcc3 TCC_HIT_sum TCC_MISS_sum || exit $?

@@ -105,13 +105,15 @@ def main():
     ap.add_argument("--n", type=int, default=128, help="particles per dimension per GPU")
     ap.add_argument("--cell-factor", type=int, default=int(os.environ.get("SWH_CELL_FACTOR", "1")))
     ap.add_argument("--loop-variant", type=int, default=int(os.environ.get("SWH_LOOP_VARIANT", "0")),
-                    help="0 default (two-phase), 1 direct gather, 2 two-phase gather")
+                    help="0 default, 1 direct gather, 2 two-phase gather, 3 tile, 4 tile + fp32 tests")
     ap.add_argument("--cell-scale", type=float, default=float(os.environ.get("SWH_CELL_SCALE", "0")),
                     help="grid cells per H_max as a real number (overrides --cell-factor)")
     ap.add_argument("--diag-mode", type=int, default=0,
                     help="profiling only, results invalid: 1 tile staging only, 2 + candidate tests")
     ap.add_argument("--group-size", type=int, default=int(os.environ.get("SWH_GROUP_SIZE", "0")),
                     help="tile i-group size / row width: 0 (default 16), 16, 32, 64")
+    ap.add_argument("--group-mode", type=int, default=int(os.environ.get("SWH_GROUP_MODE", "0")),
+                    help="tile i-groups: 0 octree leaves, 1 consecutive runs of group-size parts")
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-runs", type=int, default=3)
@@ -154,7 +156,7 @@ def main():
     del parts
     sp = lib.HydroSpace(ctx)
     sp.set_tuning(args.cell_factor, args.loop_variant, args.group_size, args.cell_scale,
-                  args.diag_mode)
+                  args.diag_mode, args.group_mode)
     # a dedicated (non-NULL) stream: the library's kernels and the timing
     # events share it, so the events bracket exactly the loop kernels
     stream = torch.cuda.Stream()
@@ -244,6 +246,7 @@ def main():
                 "cell_factor": args.cell_scale or args.cell_factor,
                 "loop_variant": args.loop_variant,
                 "group_size": args.group_size or 16,
+                "group_mode": args.group_mode,
                 "grid_cdim": info["cdim"],
                 "i_groups": info["ngroups"],
             },
@@ -251,7 +254,8 @@ def main():
                 "bound": "hbm",
                 "kernel": {0: "tile_kernel<DENSITY,double>", 3: "tile_kernel<DENSITY,double>",
                            1: "loop_kernel<DENSITY,double,1>",
-                           2: "loop_kernel<DENSITY,double,2>"}[args.loop_variant],
+                           2: "loop_kernel<DENSITY,double,2>",
+                           4: "tile4_kernel<DENSITY,double>"}[args.loop_variant],
                 "achieved": achieved / 1e9,
                 "peak": HBM_PEAK / 1e9,
                 "unit": "GB/s",

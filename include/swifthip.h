@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SWH_ABI_VERSION 1
+#define SWH_ABI_VERSION 2
 
 #if defined(__GNUC__)
 #define SWH_API __attribute__((visibility("default")))
@@ -249,11 +249,14 @@ SWH_API swh_status swh_space_sync(swh_space *s);
 typedef struct swh_tuning {
   int32_t cell_factor;  /* neighbour-grid cells per H_max (1..4) */
   int32_t loop_variant; /* 0 = default (3); 1 = per-particle direct gather, 2 = per-particle
-                           two-phase gather, 3 = tile (i-groups in 16/32/64-lane rows) */
+                           two-phase gather, 3 = tile (i-groups in 16/32/64-lane rows),
+                           4 = tile with fp32 candidate tests + exact fp64 re-test */
   int32_t group_size;   /* tile i-group size = row width: 0 (default 16), 16, 32, 64 */
   float cell_scale;     /* if > 0: cells per H_max as a real number (overrides cell_factor) */
   int32_t diag_mode;    /* 0; profiling only (results invalid): 1 = tile staging only,
                            2 = staging + candidate tests, no interactions */
+  int32_t group_mode;   /* tile i-groups: 0 = octree leaves of the Morton-ordered cells,
+                           1 = consecutive runs of group_size sorted particles (full rows) */
 } swh_tuning;
 SWH_API swh_status swh_space_set_tuning(swh_space *s, const swh_tuning *t);
 
@@ -265,6 +268,8 @@ typedef struct swh_space_info {
   int32_t reserved;
   double cell_width[3];
   double h_max;     /* max gamma*h at rebuild */
+  int64_t loop_stats[4]; /* last counted tile loop (variant 4): candidates loaded, staged,
+                            phase-A wave steps, phase-B wave steps */
 } swh_space_info;
 SWH_API swh_status swh_space_get_info(const swh_space *s, swh_space_info *info);
 

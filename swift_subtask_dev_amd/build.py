@@ -19,7 +19,8 @@ LIB = PKG / "libswifthip.so"
 ADAPTER = PKG / "libswifthip_swift.so"
 
 HIP_SOURCES = ["swh_api.hip", "swh_tasks.hip", "swh_space.hip", "swh_hydro.hip", "swh_grav.hip"]
-HIP_HEADERS = ["swh_internal.h", "swh_physics.h", "swh_space.h"]
+HIP_HEADERS = ["swh_internal.h", "swh_physics.h", "swh_space.h", "swh_gather.h", "swh_tile.h",
+               "swh_tile4.h"]
 
 
 def _hipcc() -> str:

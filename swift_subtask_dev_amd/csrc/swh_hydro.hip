@@ -13,6 +13,7 @@
 #include "swh_gather.h"
 #include "swh_internal.h"
 #include "swh_tile.h"
+#include "swh_tile4.h"
 
 namespace swh {
 
@@ -69,6 +70,19 @@ __global__ __launch_bounds__(64) void tile_kernel(GridDev g, SoA a,
   __shared__ TileLds<SG, TileSlots<LOOP>::value, LoopState<LOOP, T>::kPay> lds;
   tile_loop<LOOP, T, SG>(g, a, groups, ngroups, max_active_bin, a2H, hmax_bits, counter, ncount,
                          diag, lds);
+}
+
+// Variant 4: the tile loop with fp32 candidate tests (swh_tile4.h).
+template <int LOOP, typename T, int SG>
+__global__ __launch_bounds__(64) void tile4_kernel(GridDev g, SoA a,
+                                                   const int2* __restrict__ groups, int ngroups,
+                                                   int max_active_bin, T a2H,
+                                                   const unsigned int* __restrict__ hmax_bits,
+                                                   unsigned long long* counter,
+                                                   int* __restrict__ ncount, int diag) {
+  __shared__ Tile4Lds<SG, TileSlots<LOOP>::value> lds;
+  tile4_loop<LOOP, T, SG>(g, a, groups, ngroups, max_active_bin, a2H, hmax_bits, counter,
+                          ncount, diag, lds);
 }
 
 // hydro_init_part (src/hydro/SPHENIX/hydro.h:553-566) on active particles.
@@ -358,22 +372,23 @@ static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int
   // the tile loop needs the rebuild's compact i-groups: subsets (ghost reruns)
   // take the per-particle direct gather
   const int v = s->tuning.loop_variant == 0 ? 3 : s->tuning.loop_variant;
-  if (v == 3 && !subset) {
+  if ((v == 3 || v == 4) && !subset) {
     const int sg = s->tuning.group_size > 0 ? s->tuning.group_size : 16;
     const int nw = (s->ngroups + 64 / sg - 1) / (64 / sg);
     const int2* grp = s->groups.as<const int2>();
-    if (sg == 16)
-      hipLaunchKernelGGL((tile_kernel<LOOP, T, 16>), dim3(nw), dim3(64), 0, s->stream, gd,
-                         soa_of(s), grp, s->ngroups, max_active_bin, a2H, hmax_slot(s), ctr,
-                         ncount, s->tuning.diag_mode);
-    else if (sg == 32)
-      hipLaunchKernelGGL((tile_kernel<LOOP, T, 32>), dim3(nw), dim3(64), 0, s->stream, gd,
-                         soa_of(s), grp, s->ngroups, max_active_bin, a2H, hmax_slot(s), ctr,
-                         ncount, s->tuning.diag_mode);
-    else
-      hipLaunchKernelGGL((tile_kernel<LOOP, T, 64>), dim3(nw), dim3(64), 0, s->stream, gd,
-                         soa_of(s), grp, s->ngroups, max_active_bin, a2H, hmax_slot(s), ctr,
-                         ncount, s->tuning.diag_mode);
+#define SWH_TILE_LAUNCH(K)                                                                   \
+  hipLaunchKernelGGL((K), dim3(nw), dim3(64), 0, s->stream, gd, soa_of(s), grp, s->ngroups, \
+                     max_active_bin, a2H, hmax_slot(s), ctr, ncount, s->tuning.diag_mode)
+    if (v == 4) {
+      if (sg == 16) SWH_TILE_LAUNCH((tile4_kernel<LOOP, T, 16>));
+      else if (sg == 32) SWH_TILE_LAUNCH((tile4_kernel<LOOP, T, 32>));
+      else SWH_TILE_LAUNCH((tile4_kernel<LOOP, T, 64>));
+    } else {
+      if (sg == 16) SWH_TILE_LAUNCH((tile_kernel<LOOP, T, 16>));
+      else if (sg == 32) SWH_TILE_LAUNCH((tile_kernel<LOOP, T, 32>));
+      else SWH_TILE_LAUNCH((tile_kernel<LOOP, T, 64>));
+    }
+#undef SWH_TILE_LAUNCH
     return;
   }
   const int block = 256;
@@ -409,13 +424,19 @@ static swh_status run_loop(swh_space* s, const swh_hydro_params* P, int64_t* n_o
   SWH_TRY(check_built(s));
   if (!P) return SWH_ERR_ARG;
   SWH_HIP(hipSetDevice(s->ctx->device));
-  if (n_out) SWH_HIP(hipMemsetAsync(counter_slot(s), 0, sizeof(unsigned long long), s->stream));
+  // counted launch: slot 0 = interactions, slots 4-7 = tile work counters
+  unsigned long long* ctr = counter_slot(s);
+  if (n_out) {
+    SWH_HIP(hipMemsetAsync(ctr, 0, sizeof(unsigned long long), s->stream));
+    SWH_HIP(hipMemsetAsync(ctr + 4, 0, 4 * sizeof(unsigned long long), s->stream));
+  }
   SWH_TRY(launch_loop<LOOP>(s, P, nullptr, (int)s->n, n_out != nullptr));
   if (n_out) {
-    unsigned long long h = 0;
-    SWH_HIP(hipMemcpyAsync(&h, counter_slot(s), sizeof(h), hipMemcpyDeviceToHost, s->stream));
+    unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    SWH_HIP(hipMemcpyAsync(h, ctr, sizeof(h), hipMemcpyDeviceToHost, s->stream));
     SWH_HIP(hipStreamSynchronize(s->stream));
-    *n_out = (int64_t)h;
+    *n_out = (int64_t)h[0];
+    for (int k = 0; k < 4; k++) s->loop_stats[k] = (int64_t)h[4 + k];
   }
   return SWH_OK;
 }

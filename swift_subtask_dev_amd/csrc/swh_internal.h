@@ -148,7 +148,7 @@ struct swh_space {
   int64_t n = 0;
   bool built = false;
   SwhGrid grid;
-  swh_tuning tuning{1, 0, 0, 0.f, 0};
+  swh_tuning tuning{1, 0, 0, 0.f, 0, 0};
 
   // AoS image of the caller's records (for write-back of untouched fields)
   swh::DevBuf aos;
@@ -178,6 +178,7 @@ struct swh_space {
   swh::DevBuf groups;      // int2[ngroups]: i-groups (start, count) of the tile loops
   swh::DevBuf seg_groups, seg_off;
   int32_t ngroups = 0;
+  int64_t loop_stats[4] = {0, 0, 0, 0};  // work counters of the last counted tile loop
   // scratch
   swh::DevBuf keys, keys2, idx, idx2, sort_tmp, scan_tmp, counters;
   swh::DevBuf tmp_soa;     // staging for permutation gathers

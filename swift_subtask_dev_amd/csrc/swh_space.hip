@@ -294,6 +294,15 @@ __global__ void group_kernel(const uint32_t* __restrict__ code, const int* __res
   if (!WRITE) ngroup[r] = ng;
 }
 
+// i-groups as consecutive runs of kGroupMax sorted particles (tuning
+// group_mode 1): every row is full; a run may straddle a Morton jump.
+__global__ void chunk_group_kernel(int64_t n, int kGroupMax, int ng, int2* __restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= ng) return;
+  const int64_t s = (int64_t)k * kGroupMax;
+  out[k] = make_int2((int)s, (int)min((int64_t)kGroupMax, n - s));
+}
+
 // Gather every SoA array through the sort permutation (src -> dst).
 __global__ void permute_kernel(SoA src, SoA dst, const int* __restrict__ idx, int64_t n) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -484,7 +493,7 @@ swh_status swh_space_set_stream(swh_space* s, void* stream) {
 
 swh_status swh_space_set_tuning(swh_space* s, const swh_tuning* t) {
   if (!s || !t || t->cell_factor < 1 || t->cell_factor > 4 || t->loop_variant < 0 ||
-      t->loop_variant > 3 ||
+      t->loop_variant > 4 || t->group_mode < 0 || t->group_mode > 1 ||
       (t->group_size != 0 && t->group_size != 16 && t->group_size != 32 && t->group_size != 64) ||
       t->cell_scale < 0.f || t->cell_scale > 4.f || t->diag_mode < 0 || t->diag_mode > 2)
     return SWH_ERR_ARG;
@@ -505,6 +514,7 @@ swh_status swh_space_get_info(const swh_space* s, swh_space_info* info) {
   info->ncell = s->grid.ncell;
   info->ngroups = s->ngroups;
   info->h_max = s->grid.hmax;
+  for (int k = 0; k < 4; k++) info->loop_stats[k] = s->loop_stats[k];
   return SWH_OK;
 }
 
@@ -691,6 +701,17 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
   // 5. i-groups of the tile loops
   const int nc = g.ncell;
   const int gmax = s->tuning.group_size > 0 ? s->tuning.group_size : 16;
+  if (s->tuning.group_mode == 1) {
+    const int ng = (int)((n + gmax - 1) / gmax);
+    s->ngroups = ng;
+    SWH_TRY(s->groups.reserve(((size_t)ng + 1) * sizeof(int2)));
+    hipLaunchKernelGGL(chunk_group_kernel, dim3((ng + block - 1) / block), dim3(block), 0, st,
+                       n, gmax, ng, s->groups.as<int2>());
+    SWH_HIP(hipGetLastError());
+    SWH_TRY(space_hmax_to_device(s));
+    s->built = true;
+    return SWH_OK;
+  }
   SWH_TRY(s->seg_groups.reserve(((size_t)nc + 1) * sizeof(int)));
   SWH_TRY(s->seg_off.reserve(((size_t)nc + 1) * sizeof(int)));
   const int cgrid = (nc + block - 1) / block;

@@ -256,15 +256,16 @@ class HydroSpace:
             pass
 
     def set_tuning(self, cell_factor=1, loop_variant=0, group_size=0, cell_scale=0.0,
-                   diag_mode=0):
-        t = abi.Tuning(cell_factor, loop_variant, group_size, cell_scale, diag_mode)
+                   diag_mode=0, group_mode=0):
+        t = abi.Tuning(cell_factor, loop_variant, group_size, cell_scale, diag_mode, group_mode)
         _check(self._lib.swh_space_set_tuning(self.handle, C.byref(t)), "set_tuning")
 
     def info(self) -> dict:
         i = abi.SpaceInfo()
         _check(self._lib.swh_space_get_info(self.handle, C.byref(i)), "get_info")
         return {"cdim": list(i.cdim), "ncell": i.ncell, "ngroups": i.ngroups,
-                "cell_width": list(i.cell_width), "h_max": i.h_max}
+                "cell_width": list(i.cell_width), "h_max": i.h_max,
+                "loop_stats": list(i.loop_stats)}
 
     def upload(self, parts, count=None, on_device=False):
         """parts: numpy PART_DTYPE array (host) or a device pointer (int) with count."""

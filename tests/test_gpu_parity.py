@@ -246,15 +246,15 @@ def test_125cells_chain_vs_f64(gpu_ctx):
 
 
 # loop_variant 1 = per-particle direct gather, 2 = per-particle two-phase,
-# 3 = tile (one wave per i-group; the default)
-VARIANTS = [1, 2, 3]
+# 3 = tile (one wave per i-group), 4 = tile with fp32 candidate tests
+VARIANTS = [1, 2, 3, 4]
 
 
-def box_chain_gpu(ctx, parts, P, cell_factor=1, variant=0, group_size=0):
+def box_chain_gpu(ctx, parts, P, cell_factor=1, variant=0, group_size=0, group_mode=0):
     from swift_subtask_dev_amd import lib
     g = abi.copy_parts(parts)
     sp = lib.HydroSpace(ctx)
-    sp.set_tuning(cell_factor, variant, group_size)
+    sp.set_tuning(cell_factor, variant, group_size, group_mode=group_mode)
     sp.upload(g)
     sp.rebuild(P)
     res = sp.hydro_step(P)
@@ -280,9 +280,11 @@ def box_chain_oracle(parts, P, prec="f64"):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant,group_size", [(1, 0), (2, 0), (3, 16), (3, 32), (3, 64)])
+@pytest.mark.parametrize("variant,group_size,group_mode",
+                         [(1, 0, 0), (2, 0, 0), (3, 16, 0), (3, 32, 0), (3, 64, 0), (4, 16, 0),
+                          (4, 32, 0), (4, 64, 0), (3, 16, 1), (4, 16, 1), (4, 32, 1)])
 @pytest.mark.parametrize("cell_factor", [1, 2, 3])
-def test_box_density_vs_f64(gpu_ctx, cell_factor, variant, group_size):
+def test_box_density_vs_f64(gpu_ctx, cell_factor, variant, group_size, group_mode):
     """Batch density loop on a periodic Sedov-like box vs the fp64 oracle;
     identical interaction count; every grid refinement gives the same sums."""
     from swift_subtask_dev_amd import lib
@@ -290,7 +292,7 @@ def test_box_density_vs_f64(gpu_ctx, cell_factor, variant, group_size):
     parts = ics.sedov_box(20, velocity="divergent", seed=11)
     g = abi.copy_parts(parts)
     sp = lib.HydroSpace(gpu_ctx)
-    sp.set_tuning(cell_factor, variant, group_size)
+    sp.set_tuning(cell_factor, variant, group_size, group_mode=group_mode)
     sp.upload(g)
     sp.rebuild(P)
     sp.init_parts(P)
@@ -304,15 +306,18 @@ def test_box_density_vs_f64(gpu_ctx, cell_factor, variant, group_size):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant,group_size", [(1, 0), (2, 0), (3, 16), (3, 64)])
-def test_box_chain_vs_f64(gpu_ctx, variant, group_size):
+@pytest.mark.parametrize("variant,group_size,group_mode",
+                         [(1, 0, 0), (2, 0, 0), (3, 16, 0), (3, 64, 0), (4, 16, 0), (4, 64, 0),
+                          (4, 16, 1)])
+def test_box_chain_vs_f64(gpu_ctx, variant, group_size, group_mode):
     """Full SPHENIX chain (density, ghost with h iteration, gradient, extra
     ghost, force, end force) on a perturbed box with h off-target so the
     ghost iterates."""
     P = abi.default_hydro_params()
     parts = ics.sedov_box(16, velocity="divergent", pert=0.3, seed=5)
     parts["h"] *= np.random.Generator(np.random.PCG64(1)).uniform(0.8, 1.25, len(parts))
-    g, rg = box_chain_gpu(gpu_ctx, parts, P, variant=variant, group_size=group_size)
+    g, rg = box_chain_gpu(gpu_ctx, parts, P, variant=variant, group_size=group_size,
+                          group_mode=group_mode)
     o, ro = box_chain_oracle(parts, P)
     assert rg["ghost_iterations"] >= 2
     # Chain tolerance: the GPU keeps struct-part (float) storage between the

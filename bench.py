@@ -105,7 +105,8 @@ def main():
     ap.add_argument("--n", type=int, default=128, help="particles per dimension per GPU")
     ap.add_argument("--cell-factor", type=int, default=int(os.environ.get("SWH_CELL_FACTOR", "1")))
     ap.add_argument("--loop-variant", type=int, default=int(os.environ.get("SWH_LOOP_VARIANT", "0")),
-                    help="0 default, 1 direct gather, 2 two-phase gather, 3 tile, 4 tile + fp32 tests")
+                    help="0 default, 1 direct gather, 2 two-phase gather, 3 tile, 4 tile + fp32 tests, "
+                         "5 one group per wave")
     ap.add_argument("--cell-scale", type=float, default=float(os.environ.get("SWH_CELL_SCALE", "0")),
                     help="grid cells per H_max as a real number (overrides --cell-factor)")
     ap.add_argument("--diag-mode", type=int, default=0,
@@ -166,8 +167,10 @@ def main():
     # exact interaction counts of one step (same work every step: h is fixed)
     sp.init_parts(P)
     n_density = sp.density(P)
+    stats_density = list(sp.info()["loop_stats"])
     sp.reset_acceleration(P)
     n_force = sp.force(P)
+    stats_force = list(sp.info()["loop_stats"])
     torch.cuda.synchronize()
     info = sp.info()
     log(f"[rank {rank}] grid {info}")
@@ -255,7 +258,8 @@ def main():
                 "kernel": {0: "tile_kernel<DENSITY,double>", 3: "tile_kernel<DENSITY,double>",
                            1: "loop_kernel<DENSITY,double,1>",
                            2: "loop_kernel<DENSITY,double,2>",
-                           4: "tile4_kernel<DENSITY,double>"}[args.loop_variant],
+                           4: "tile4_kernel<DENSITY,double>",
+                           5: "tile5_kernel<DENSITY,double>"}[args.loop_variant],
                 "achieved": achieved / 1e9,
                 "peak": HBM_PEAK / 1e9,
                 "unit": "GB/s",
@@ -270,6 +274,10 @@ def main():
                 "force_algorithmic_GBps": b_force / tf / 1e9,
                 "density_fp64_frac": n_density * FLOPS_DENSITY / td / FP64_PEAK,
                 "force_fp64_frac": n_force * FLOPS_FORCE / tf / FP64_PEAK,
+                # tile-loop work counters (variants 4, 5): candidates loaded, staged,
+                # phase-A and phase-B wave steps
+                "density_loop_stats": stats_density,
+                "force_loop_stats": stats_force,
             },
             "cpu_baseline": None,
         }

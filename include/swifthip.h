@@ -250,7 +250,9 @@ typedef struct swh_tuning {
   int32_t cell_factor;  /* neighbour-grid cells per H_max (1..4) */
   int32_t loop_variant; /* 0 = default (3); 1 = per-particle direct gather, 2 = per-particle
                            two-phase gather, 3 = tile (i-groups in 16/32/64-lane rows),
-                           4 = tile with fp32 candidate tests + exact fp64 re-test */
+                           4 = tile with fp32 candidate tests + exact fp64 re-test,
+                           5 = as 4 with one i-group per wave, 64/group_size lanes
+                               per particle */
   int32_t group_size;   /* tile i-group size = row width: 0 (default 16), 16, 32, 64 */
   float cell_scale;     /* if > 0: cells per H_max as a real number (overrides cell_factor) */
   int32_t diag_mode;    /* 0; profiling only (results invalid): 1 = tile staging only,
@@ -268,7 +270,7 @@ typedef struct swh_space_info {
   int32_t reserved;
   double cell_width[3];
   double h_max;     /* max gamma*h at rebuild */
-  int64_t loop_stats[4]; /* last counted tile loop (variant 4): candidates loaded, staged,
+  int64_t loop_stats[4]; /* last counted tile loop (variants 4, 5): candidates loaded, staged,
                             phase-A wave steps, phase-B wave steps */
 } swh_space_info;
 SWH_API swh_status swh_space_get_info(const swh_space *s, swh_space_info *info);

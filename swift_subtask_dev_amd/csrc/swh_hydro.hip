@@ -14,6 +14,7 @@
 #include "swh_internal.h"
 #include "swh_tile.h"
 #include "swh_tile4.h"
+#include "swh_tile5.h"
 
 namespace swh {
 
@@ -83,6 +84,19 @@ __global__ __launch_bounds__(64) void tile4_kernel(GridDev g, SoA a,
   __shared__ Tile4Lds<SG, TileSlots<LOOP>::value> lds;
   tile4_loop<LOOP, T, SG>(g, a, groups, ngroups, max_active_bin, a2H, hmax_bits, counter,
                           ncount, diag, lds);
+}
+
+// Variant 5: one i-group per wave, LPI lanes per i-particle (swh_tile5.h).
+template <int LOOP, typename T, int LPI>
+__global__ __launch_bounds__(64) void tile5_kernel(GridDev g, SoA a,
+                                                   const int2* __restrict__ groups, int ngroups,
+                                                   int max_active_bin, T a2H,
+                                                   const unsigned int* __restrict__ hmax_bits,
+                                                   unsigned long long* counter,
+                                                   int* __restrict__ ncount, int diag) {
+  __shared__ Tile5Lds<LPI> lds;
+  tile5_loop<LOOP, T, LPI>(g, a, groups, ngroups, max_active_bin, a2H, hmax_bits, counter,
+                           ncount, diag, lds);
 }
 
 // hydro_init_part (src/hydro/SPHENIX/hydro.h:553-566) on active particles.
@@ -372,14 +386,19 @@ static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int
   // the tile loop needs the rebuild's compact i-groups: subsets (ghost reruns)
   // take the per-particle direct gather
   const int v = s->tuning.loop_variant == 0 ? 3 : s->tuning.loop_variant;
-  if ((v == 3 || v == 4) && !subset) {
+  if (v >= 3 && !subset) {
     const int sg = s->tuning.group_size > 0 ? s->tuning.group_size : 16;
-    const int nw = (s->ngroups + 64 / sg - 1) / (64 / sg);
+    // variants 3/4 pack 64/sg groups into a wave, variant 5 gives each group a wave
+    const int nw = v == 5 ? s->ngroups : (s->ngroups + 64 / sg - 1) / (64 / sg);
     const int2* grp = s->groups.as<const int2>();
 #define SWH_TILE_LAUNCH(K)                                                                   \
   hipLaunchKernelGGL((K), dim3(nw), dim3(64), 0, s->stream, gd, soa_of(s), grp, s->ngroups, \
                      max_active_bin, a2H, hmax_slot(s), ctr, ncount, s->tuning.diag_mode)
-    if (v == 4) {
+    if (v == 5) {
+      if (sg == 16) SWH_TILE_LAUNCH((tile5_kernel<LOOP, T, 4>));
+      else if (sg == 32) SWH_TILE_LAUNCH((tile5_kernel<LOOP, T, 2>));
+      else SWH_TILE_LAUNCH((tile5_kernel<LOOP, T, 1>));
+    } else if (v == 4) {
       if (sg == 16) SWH_TILE_LAUNCH((tile4_kernel<LOOP, T, 16>));
       else if (sg == 32) SWH_TILE_LAUNCH((tile4_kernel<LOOP, T, 32>));
       else SWH_TILE_LAUNCH((tile4_kernel<LOOP, T, 64>));

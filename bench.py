@@ -106,7 +106,7 @@ def main():
     ap.add_argument("--cell-factor", type=int, default=int(os.environ.get("SWH_CELL_FACTOR", "1")))
     ap.add_argument("--loop-variant", type=int, default=int(os.environ.get("SWH_LOOP_VARIANT", "0")),
                     help="0 default, 1 direct gather, 2 two-phase gather, 3 tile, 4 tile + fp32 tests, "
-                         "5 one group per wave")
+                         "5 one group per wave, 6 tile + fp32 tests + balanced phase B")
     ap.add_argument("--cell-scale", type=float, default=float(os.environ.get("SWH_CELL_SCALE", "0")),
                     help="grid cells per H_max as a real number (overrides --cell-factor)")
     ap.add_argument("--diag-mode", type=int, default=0,
@@ -225,7 +225,10 @@ def main():
         b_dens = n_owned * (27 * S_IN_DENSITY + S_OUT_DENSITY)
         b_force = n_owned * (27 * S_IN_FORCE + S_OUT_FORCE)
         achieved = b_dens / td
-        traffic = load_traffic()
+        # PMC traffic was measured on the default configuration only
+        default_cfg = (args.loop_variant == 0 and args.group_size == 0 and args.group_mode == 0
+                       and args.cell_factor == 1 and args.cell_scale == 0 and args.n == 128)
+        traffic = load_traffic() if default_cfg else None
         out = {
             "metric": METRIC,
             "value": total_interactions / elapsed_max,
@@ -255,11 +258,12 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": {0: "tile_kernel<DENSITY,double>", 3: "tile_kernel<DENSITY,double>",
+                "kernel": {0: "tile5_kernel<DENSITY,double>", 3: "tile_kernel<DENSITY,double>",
                            1: "loop_kernel<DENSITY,double,1>",
                            2: "loop_kernel<DENSITY,double,2>",
                            4: "tile4_kernel<DENSITY,double>",
-                           5: "tile5_kernel<DENSITY,double>"}[args.loop_variant],
+                           5: "tile5_kernel<DENSITY,double>",
+                           6: "tile6_kernel<DENSITY,double>"}[args.loop_variant],
                 "achieved": achieved / 1e9,
                 "peak": HBM_PEAK / 1e9,
                 "unit": "GB/s",

@@ -252,7 +252,9 @@ typedef struct swh_tuning {
                            two-phase gather, 3 = tile (i-groups in 16/32/64-lane rows),
                            4 = tile with fp32 candidate tests + exact fp64 re-test,
                            5 = as 4 with one i-group per wave, 64/group_size lanes
-                               per particle */
+                               per particle,
+                           6 = as 4 (16-lane rows) with the hits of a drain dealt
+                               out evenly over the wave (balanced phase B) */
   int32_t group_size;   /* tile i-group size = row width: 0 (default 16), 16, 32, 64 */
   float cell_scale;     /* if > 0: cells per H_max as a real number (overrides cell_factor) */
   int32_t diag_mode;    /* 0; profiling only (results invalid): 1 = tile staging only,

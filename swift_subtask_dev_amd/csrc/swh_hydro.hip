@@ -15,6 +15,7 @@
 #include "swh_tile.h"
 #include "swh_tile4.h"
 #include "swh_tile5.h"
+#include "swh_tile6.h"
 
 namespace swh {
 
@@ -60,9 +61,20 @@ __global__ __launch_bounds__(256) void loop_kernel(GridDev g, SoA a,
   if (counter) count_add(act ? st.n : 0, counter);
 }
 
+// Occupancy of the tile kernels: SWH_TILE_WPE > 0 asks the compiler for at
+// least that many waves per SIMD (it caps the VGPR budget accordingly).
+#ifndef SWH_TILE_WPE
+#define SWH_TILE_WPE 0
+#endif
+#if SWH_TILE_WPE > 0
+#define SWH_TILE_BOUNDS __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SWH_TILE_WPE)))
+#else
+#define SWH_TILE_BOUNDS __launch_bounds__(64)
+#endif
+
 // Variant 3: NS = 64/SG i-groups per 64-lane wave (swh_tile.h).
 template <int LOOP, typename T, int SG>
-__global__ __launch_bounds__(64) void tile_kernel(GridDev g, SoA a,
+__global__ SWH_TILE_BOUNDS void tile_kernel(GridDev g, SoA a,
                                                   const int2* __restrict__ groups, int ngroups,
                                                   int max_active_bin, T a2H,
                                                   const unsigned int* __restrict__ hmax_bits,
@@ -75,20 +87,41 @@ __global__ __launch_bounds__(64) void tile_kernel(GridDev g, SoA a,
 
 // Variant 4: the tile loop with fp32 candidate tests (swh_tile4.h).
 template <int LOOP, typename T, int SG>
-__global__ __launch_bounds__(64) void tile4_kernel(GridDev g, SoA a,
+__global__ SWH_TILE_BOUNDS void tile4_kernel(GridDev g, SoA a,
                                                    const int2* __restrict__ groups, int ngroups,
                                                    int max_active_bin, T a2H,
                                                    const unsigned int* __restrict__ hmax_bits,
                                                    unsigned long long* counter,
                                                    int* __restrict__ ncount, int diag) {
   __shared__ Tile4Lds<SG, TileSlots<LOOP>::value> lds;
-  tile4_loop<LOOP, T, SG>(g, a, groups, ngroups, max_active_bin, a2H, hmax_bits, counter,
-                          ncount, diag, lds);
+  tile4_loop<LOOP, T, SG, false>(g, a, groups, ngroups, max_active_bin, a2H, hmax_bits, counter,
+                                 ncount, diag, lds);
+}
+
+// Variant 6: variant 4 with the balanced phase B of swh_tile6.h.
+template <int LOOP, typename T, int SG>
+__global__ SWH_TILE_BOUNDS void tile6_kernel(GridDev g, SoA a,
+                                             const int2* __restrict__ groups, int ngroups,
+                                             int max_active_bin, T a2H,
+                                             const unsigned int* __restrict__ hmax_bits,
+                                             unsigned long long* counter,
+                                             int* __restrict__ ncount, int diag) {
+  __shared__ Tile6Lds<SG, TileSlots<LOOP>::value, decltype(LoopState<LOOP, T>::A)> lds;
+  tile4_loop<LOOP, T, SG, true>(g, a, groups, ngroups, max_active_bin, a2H, hmax_bits, counter,
+                                ncount, diag, lds);
 }
 
 // Variant 5: one i-group per wave, LPI lanes per i-particle (swh_tile5.h).
+// The density instance asks for 3 waves per SIMD (VGPR cap 168): measured
+// 1.65 ms vs 1.92 ms at 128^3; the force instance is left alone (it spills).
+template <int LOOP>
+struct Tile5Waves {
+  static constexpr int value = (SWH_TILE_WPE > 0) ? SWH_TILE_WPE : (LOOP == LOOP_DENSITY ? 3 : 1);
+};
+
 template <int LOOP, typename T, int LPI>
-__global__ __launch_bounds__(64) void tile5_kernel(GridDev g, SoA a,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Tile5Waves<LOOP>::value)))
+void tile5_kernel(GridDev g, SoA a,
                                                    const int2* __restrict__ groups, int ngroups,
                                                    int max_active_bin, T a2H,
                                                    const unsigned int* __restrict__ hmax_bits,
@@ -385,16 +418,23 @@ static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int
                          int max_active_bin, T a2H, unsigned long long* ctr, int* ncount) {
   // the tile loop needs the rebuild's compact i-groups: subsets (ghost reruns)
   // take the per-particle direct gather
-  const int v = s->tuning.loop_variant == 0 ? 3 : s->tuning.loop_variant;
+  // default (0): the fastest measured per loop at 128^3:
+  // density variant 5, gradient and force variant 4
+  const int v = s->tuning.loop_variant != 0 ? s->tuning.loop_variant
+                                             : (LOOP == LOOP_DENSITY ? 5 : 4);
   if (v >= 3 && !subset) {
     const int sg = s->tuning.group_size > 0 ? s->tuning.group_size : 16;
     // variants 3/4 pack 64/sg groups into a wave, variant 5 gives each group a wave
-    const int nw = v == 5 ? s->ngroups : (s->ngroups + 64 / sg - 1) / (64 / sg);
+    const int nw = v == 5 ? s->ngroups
+                 : v == 6 ? (s->ngroups + 3) / 4
+                          : (s->ngroups + 64 / sg - 1) / (64 / sg);
     const int2* grp = s->groups.as<const int2>();
 #define SWH_TILE_LAUNCH(K)                                                                   \
   hipLaunchKernelGGL((K), dim3(nw), dim3(64), 0, s->stream, gd, soa_of(s), grp, s->ngroups, \
                      max_active_bin, a2H, hmax_slot(s), ctr, ncount, s->tuning.diag_mode)
-    if (v == 5) {
+    if (v == 6) {  // 16-lane rows only
+      SWH_TILE_LAUNCH((tile6_kernel<LOOP, T, 16>));
+    } else if (v == 5) {
       if (sg == 16) SWH_TILE_LAUNCH((tile5_kernel<LOOP, T, 4>));
       else if (sg == 32) SWH_TILE_LAUNCH((tile5_kernel<LOOP, T, 2>));
       else SWH_TILE_LAUNCH((tile5_kernel<LOOP, T, 1>));

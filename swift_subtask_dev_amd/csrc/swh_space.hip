@@ -493,7 +493,7 @@ swh_status swh_space_set_stream(swh_space* s, void* stream) {
 
 swh_status swh_space_set_tuning(swh_space* s, const swh_tuning* t) {
   if (!s || !t || t->cell_factor < 1 || t->cell_factor > 4 || t->loop_variant < 0 ||
-      t->loop_variant > 5 || t->group_mode < 0 || t->group_mode > 1 ||
+      t->loop_variant > 6 || t->group_mode < 0 || t->group_mode > 1 ||
       (t->group_size != 0 && t->group_size != 16 && t->group_size != 32 && t->group_size != 64) ||
       t->cell_scale < 0.f || t->cell_scale > 4.f || t->diag_mode < 0 || t->diag_mode > 2)
     return SWH_ERR_ARG;

@@ -27,7 +27,10 @@
 
 namespace swh {
 
-constexpr int kTileCap = 32;  // per-lane hit list (checked every 8 candidates)
+#ifndef SWH_TILE_CAP
+#define SWH_TILE_CAP 32
+#endif
+constexpr int kTileCap = SWH_TILE_CAP;  // per-lane hit list (checked every 8 candidates)
 
 // Staged candidate slots per wave and candidates fetched per lane per pass.
 template <int LOOP>

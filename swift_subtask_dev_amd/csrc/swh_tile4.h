@@ -26,6 +26,10 @@ namespace swh {
 constexpr double kUnitRound = 5.9604644775390625e-8;   // u = 2^-24
 constexpr float kThrSlack = 1.f + 8.f * 5.9604645e-8f;  // (1 + 8u)
 
+// Per-lane hit-list capacity of variants 4 and 6: 64 (measured at 128^3:
+// force 2.46 ms at 64, 2.75 ms at 48, 2.97 ms at 32; density 1.72 / 1.65 / 1.74).
+constexpr int kTile4Cap = 64;
+
 template <int SG, int TS>
 struct Tile4Lds {
   static constexpr int kSlots = TS + 4 * (64 / SG);  // rows padded by 4 slots
@@ -34,7 +38,7 @@ struct Tile4Lds {
   int cell_j0[256];  // per row: 4*SG cells of the current batch
   int cell_pre[256];
   unsigned char cell_code[256];
-  int hits[kTileCap * 64];  // [k][lane] global j
+  int hits[kTile4Cap * 64];  // [k][lane] global j
 };
 
 // Work counters of a counted launch (swh_space_info.loop_stats): candidates
@@ -82,22 +86,38 @@ __device__ __forceinline__ void tile4_drain(const GridDev& g, const SoA& a, cons
   nh = 0;
 }
 
+// Balanced drain of variant 6 (swh_tile6.h).
+template <bool PWRAP, typename T, class S, class LDS>
+__device__ void tile6_drain(const GridDev& g, const SoA& a, LDS& L, int& nh, int lane, S& st,
+                            TileStats& ts, T a2H, const unsigned int* hmax_bits);
+
+template <bool BAL, bool PWRAP, typename T, class S, class LDS>
+__device__ __forceinline__ void tile4_drain_any(const GridDev& g, const SoA& a,
+                                                const double4& pi, LDS& L, int& nh, int lane,
+                                                S& st, TileStats& ts, T a2H,
+                                                const unsigned int* hmax_bits) {
+  if constexpr (BAL) tile6_drain<PWRAP, T>(g, a, L, nh, lane, st, ts, a2H, hmax_bits);
+  else tile4_drain<PWRAP, T>(g, a, pi, L, nh, lane, st, ts);
+}
+
 // Phase A over the staged region of each row, 8 candidates per block. A
-// lane's list holds <= kTileCap - 8 entries at the start of a block; every
+// lane's list holds <= kTile4Cap - 8 entries at the start of a block; every
 // candidate's j is written at the list end and kept only on a hit, so the
 // appends need no branch.
-template <int LOOP, int SG, bool WRAP, bool PWRAP, typename T, class S, class LDS>
+template <int LOOP, int SG, bool WRAP, bool PWRAP, bool BAL, typename T, class S, class LDS>
 __device__ __forceinline__ void tile4_consume(const GridDev& g, const SoA& a,
                                               const CellRange& c, const double4& pi, float xi,
                                               float yi, float zi, float thr_i, bool act,
                                               int rbase, int nst, LDS& L, int& nh, int lane,
-                                              S& st, TileStats& ts) {
+                                              S& st, TileStats& ts, T a2H,
+                                              const unsigned int* hmax_bits) {
   int kmax = nst;
   for (int o = 32; o >= SG; o >>= 1) kmax = max(kmax, __shfl_xor(kmax, o));
   ts.asteps += (unsigned int)kmax;
   const float bx = (float)g.dim[0], by = (float)g.dim[1], bz = (float)g.dim[2];
   for (int k0 = 0; k0 < kmax; k0 += 8) {
-    if (__any(nh > kTileCap - 8)) tile4_drain<PWRAP, T>(g, a, pi, L, nh, lane, st, ts);
+    if (__any(nh > kTile4Cap - 8))
+      tile4_drain_any<BAL, PWRAP, T>(g, a, pi, L, nh, lane, st, ts, a2H, hmax_bits);
     float4 cv[8];
 #pragma unroll
     for (int kk = 0; kk < 8; kk++) cv[kk] = L.cand[rbase + k0 + kk];
@@ -128,7 +148,7 @@ __device__ __forceinline__ void tile4_consume(const GridDev& g, const SoA& a,
   }
 }
 
-template <int LOOP, typename T, int SG, class LDS>
+template <int LOOP, typename T, int SG, bool BAL, class LDS>
 __device__ __forceinline__ void tile4_loop(const GridDev& g, SoA& a,
                                            const int2* __restrict__ groups, int ngroups,
                                            int max_active_bin, T a2H,
@@ -162,6 +182,7 @@ __device__ __forceinline__ void tile4_loop(const GridDev& g, SoA& a,
     st.load_i(a, i, a2H, hmax_bits);
     pi = a.pos[i];
   }
+  if constexpr (BAL) L.own_i[lane] = act ? i : -1;
   const double Hi = act ? pi.w * (double)kGamma : 0.;
   const double Hg = row_max<SG>(Hi);
   double lo[3], hi[3];
@@ -342,14 +363,14 @@ __device__ __forceinline__ void tile4_loop(const GridDev& g, SoA& a,
       }
       if (diag == 2) nh = 0;
       if (wrap)
-        tile4_consume<LOOP, SG, true, true, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst,
-                                               L, nh, lane, st, ts);
+        tile4_consume<LOOP, SG, true, true, BAL, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst,
+                                               L, nh, lane, st, ts, a2H, hmax_bits);
       else if (pwrap)
-        tile4_consume<LOOP, SG, false, true, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst,
-                                                L, nh, lane, st, ts);
+        tile4_consume<LOOP, SG, false, true, BAL, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst,
+                                                L, nh, lane, st, ts, a2H, hmax_bits);
       else
-        tile4_consume<LOOP, SG, false, false, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase,
-                                                 nst, L, nh, lane, st, ts);
+        tile4_consume<LOOP, SG, false, false, BAL, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase,
+                                                 nst, L, nh, lane, st, ts, a2H, hmax_bits);
       nst = 0;
     }
     wave_sync();
@@ -358,17 +379,17 @@ __device__ __forceinline__ void tile4_loop(const GridDev& g, SoA& a,
   if (diag == 1) nst = 0;
   if (diag == 2) nh = 0;
   if (wrap) {
-    tile4_consume<LOOP, SG, true, true, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst, L,
-                                           nh, lane, st, ts);
-    tile4_drain<true, T>(g, a, pi, L, nh, lane, st, ts);
+    tile4_consume<LOOP, SG, true, true, BAL, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst, L,
+                                           nh, lane, st, ts, a2H, hmax_bits);
+    tile4_drain_any<BAL, true, T>(g, a, pi, L, nh, lane, st, ts, a2H, hmax_bits);
   } else if (pwrap) {
-    tile4_consume<LOOP, SG, false, true, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst, L,
-                                            nh, lane, st, ts);
-    tile4_drain<true, T>(g, a, pi, L, nh, lane, st, ts);
+    tile4_consume<LOOP, SG, false, true, BAL, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst, L,
+                                            nh, lane, st, ts, a2H, hmax_bits);
+    tile4_drain_any<BAL, true, T>(g, a, pi, L, nh, lane, st, ts, a2H, hmax_bits);
   } else {
-    tile4_consume<LOOP, SG, false, false, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst,
-                                             L, nh, lane, st, ts);
-    tile4_drain<false, T>(g, a, pi, L, nh, lane, st, ts);
+    tile4_consume<LOOP, SG, false, false, BAL, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst,
+                                             L, nh, lane, st, ts, a2H, hmax_bits);
+    tile4_drain_any<BAL, false, T>(g, a, pi, L, nh, lane, st, ts, a2H, hmax_bits);
   }
   if (act) {
     st.store(a, i);

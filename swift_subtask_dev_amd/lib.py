@@ -7,6 +7,7 @@ module raises immediately — there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
 import numpy as np
@@ -14,7 +15,8 @@ import numpy as np
 from . import abi
 
 PKG = Path(__file__).resolve().parent
-LIB_PATH = PKG / "libswifthip.so"
+# SWH_LIB_PATH: developer override (occupancy experiments, tools/build_variant.sh)
+LIB_PATH = Path(os.environ.get("SWH_LIB_PATH", str(PKG / "libswifthip.so")))
 ADAPTER_PATH = PKG / "libswifthip_swift.so"
 
 STATUS = {

@@ -247,8 +247,8 @@ def test_125cells_chain_vs_f64(gpu_ctx):
 
 # loop_variant 1 = per-particle direct gather, 2 = per-particle two-phase,
 # 3 = tile (64/group_size i-groups per wave), 4 = tile with fp32 candidate tests,
-# 5 = one i-group per wave
-VARIANTS = [1, 2, 3, 4, 5]
+# 5 = one i-group per wave, 6 = as 4 with the balanced phase B
+VARIANTS = [1, 2, 3, 4, 5, 6]
 
 
 def box_chain_gpu(ctx, parts, P, cell_factor=1, variant=0, group_size=0, group_mode=0):
@@ -284,7 +284,8 @@ def box_chain_oracle(parts, P, prec="f64"):
 @pytest.mark.parametrize("variant,group_size,group_mode",
                          [(1, 0, 0), (2, 0, 0), (3, 16, 0), (3, 32, 0), (3, 64, 0), (4, 16, 0),
                           (4, 32, 0), (4, 64, 0), (3, 16, 1), (4, 16, 1), (4, 32, 1),
-                          (5, 16, 0), (5, 32, 0), (5, 64, 0), (5, 16, 1)])
+                          (5, 16, 0), (5, 32, 0), (5, 64, 0), (5, 16, 1), (6, 16, 0),
+                          (6, 16, 1)])
 @pytest.mark.parametrize("cell_factor", [1, 2, 3])
 def test_box_density_vs_f64(gpu_ctx, cell_factor, variant, group_size, group_mode):
     """Batch density loop on a periodic Sedov-like box vs the fp64 oracle;
@@ -310,7 +311,8 @@ def test_box_density_vs_f64(gpu_ctx, cell_factor, variant, group_size, group_mod
 @pytest.mark.gpu
 @pytest.mark.parametrize("variant,group_size,group_mode",
                          [(1, 0, 0), (2, 0, 0), (3, 16, 0), (3, 64, 0), (4, 16, 0), (4, 64, 0),
-                          (4, 16, 1), (5, 16, 0), (5, 32, 0), (5, 64, 0)])
+                          (4, 16, 1), (5, 16, 0), (5, 32, 0), (5, 64, 0), (6, 16, 0),
+                          (6, 16, 1)])
 def test_box_chain_vs_f64(gpu_ctx, variant, group_size, group_mode):
     """Full SPHENIX chain (density, ghost with h iteration, gradient, extra
     ghost, force, end force) on a perturbed box with h off-target so the

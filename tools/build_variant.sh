@@ -1,0 +1,18 @@
+#!/bin/bash
+# Experimental build: libswifthip with swh_hydro.hip compiled under extra
+# defines (e.g. -DSWH_TILE_WPE=4), written to swift_subtask_dev_amd/_exp/<name>.so.
+# Load it with SWH_LIB_PATH=swift_subtask_dev_amd/_exp/<name>.so.
+# usage: tools/build_variant.sh <name> <defines...>
+set -e
+name="$1"; shift
+cd "$(dirname "$0")/.."
+python -c "from swift_subtask_dev_amd import build as b; b.build()" > /dev/null
+pkg=swift_subtask_dev_amd; obj=$pkg/_obj; out=$pkg/_exp
+mkdir -p "$out"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function \
+  -Wno-unused-variable -Iinclude -I$pkg/csrc -fvisibility=hidden -DSWH_BUILD "$@" \
+  -c $pkg/csrc/swh_hydro.hip -o "$out/$name.hydro.o"
+others=$(ls $obj/*.o | grep -v swh_hydro)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/$name.so" "$out/$name.hydro.o" $others
+rm -f "$out/$name.hydro.o"
+echo "built $out/$name.so"

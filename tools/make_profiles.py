@@ -44,7 +44,9 @@ for k, v in per.items():
 out = {"source": f"profiles/{tag} PMC passes (rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE, "
                  "kernel-trace only; FETCH_SIZE x2 gfx950 correction; median over dispatches)",
        "kernels": traffic}
-dens = [k for k in traffic if "tile_kernel<0, double" in k]
+# the default density kernel first (variant 5), then any density instance
+dens = [k for k in traffic if "tile5_kernel<0, double" in k] or \
+       [k for k in traffic if "_kernel<0, double" in k]
 if dens:
     out["bytes_per_launch"] = traffic[dens[0]]["bytes_per_launch"]
 (dst / f"{tag}_traffic.json").write_text(json.dumps(out, indent=1) + "\n")
@@ -55,3 +57,18 @@ print("bench:", bench["value"], bench["kernels"])
 for r in rows[:6]:
     print(f'{r["Name"][:60]:60s} calls {r["Calls"]:>4} avg {float(r["AverageNs"]) / 1e6:.4f} ms')
 print(json.dumps(out, indent=1))
+
+# per-dispatch durations of the density kernel from the kernel trace: the
+# first dispatches belong to bench.py's untimed setup (full chain + counted
+# launch, which also pays the first scratch/page set-up); the last `steps`
+# are the timed region, whose mean is what bench.py's HIP events measure
+kt = src / f"{tag}_trace" / "run_kernel_trace.csv"
+if kt.exists() and dens:
+    name = dens[0]
+    d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+         for r in csv.DictReader(open(kt)) if r["Kernel_Name"].split("(")[0] == name]
+    steps = json.loads(trace_bench[-1])["steps"] if trace_bench else 10
+    timed = d[-steps:]
+    (dst / f"{tag}_density_dispatches.json").write_text(json.dumps({
+        "kernel": name, "dispatch_ms": d, "timed_dispatches": len(timed),
+        "timed_mean_ms": sum(timed) / len(timed), "all_mean_ms": sum(d) / len(d)}, indent=1) + "\n")

@@ -28,6 +28,13 @@
 namespace swh {
 
 constexpr int kT5Region = 256;  // staged candidates per region
+#ifndef SWH_T5_KB
+#define SWH_T5_KB 8
+#endif
+constexpr int kT5Blk = SWH_T5_KB;  // phase-A candidates per lane per block
+#ifndef SWH_T5_U
+#define SWH_T5_U 1
+#endif
 
 template <int LPI>
 struct Tile5Lds {
@@ -163,20 +170,20 @@ __device__ __forceinline__ void tile5_consume(const GridDev& g, const SoA& a,
                                               TileStats& ts) {
   constexpr int GS = 64 / LPI;
   const int dummy = GS * LDS::kStride + il * LPI + s;
-  const int nblk = (nst + 8 * LPI - 1) / (8 * LPI);
-  ts.asteps += (unsigned int)(nblk * 8);
+  const int nblk = (nst + kT5Blk * LPI - 1) / (kT5Blk * LPI);
+  ts.asteps += (unsigned int)(nblk * kT5Blk);
   const float bx = (float)g.dim[0], by = (float)g.dim[1], bz = (float)g.dim[2];
   for (int b = 0; b < nblk; b++) {
-    if (__any(nq > LDS::kICap - 8 * LPI))
+    if (__any(nq > LDS::kICap - kT5Blk * LPI))
       tile5_drain<LPI, PWRAP, T>(g, a, pi, L, nq, il, s, st, ts);
-    const int c0 = b * 8 * LPI + s;
-    float4 cv[8];
+    const int c0 = b * kT5Blk * LPI + s;
+    float4 cv[kT5Blk];
 #pragma unroll
-    for (int kk = 0; kk < 8; kk++) cv[kk] = L.cand[min(c0 + kk * LPI, kT5Region - 1)];
-    bool hit[8];
+    for (int kk = 0; kk < kT5Blk; kk++) cv[kk] = L.cand[min(c0 + kk * LPI, kT5Region - 1)];
+    bool hit[kT5Blk];
     int cnt = 0;
 #pragma unroll
-    for (int kk = 0; kk < 8; kk++) {
+    for (int kk = 0; kk < kT5Blk; kk++) {
       float dx = xi - cv[kk].x, dy = yi - cv[kk].y, dz = zi - cv[kk].z;
       if (WRAP) {
         if (c.full[0]) dx = wrap_nearest_f(dx, bx);
@@ -199,7 +206,7 @@ __device__ __forceinline__ void tile5_consume(const GridDev& g, const SoA& a,
     const int tot = __shfl(inc, LPI - 1, LPI);
     int pos = il * LDS::kStride + nq + inc - cnt;
 #pragma unroll
-    for (int kk = 0; kk < 8; kk++) {
+    for (int kk = 0; kk < kT5Blk; kk++) {
       L.hits[hit[kk] ? pos : dummy] = (unsigned short)(c0 + kk * LPI);
       pos += hit[kk] ? 1 : 0;
     }
@@ -216,7 +223,7 @@ __device__ __forceinline__ void tile5_loop(const GridDev& g, SoA& a,
                                            unsigned long long* counter, int* __restrict__ ncount,
                                            int diag, LDS& L) {
   using S = LoopState<LOOP, T>;
-  constexpr int U = 2;  // candidates per lane per staging pass
+  constexpr int U = SWH_T5_U;  // candidates per lane per staging pass
   const int lane = threadIdx.x & 63;
   const int il = lane / LPI, s = lane % LPI;
   // XCD-aware order (swh_tile.h): each XCD takes a contiguous stretch of the

@@ -37,9 +37,12 @@ template <int LOOP>
 struct TileSlots {
   static constexpr int value = 256;
 };
+#ifndef SWH_TILE_FETCH
+#define SWH_TILE_FETCH 2
+#endif
 template <int LOOP>
 struct TileFetch {
-  static constexpr int value = 2;
+  static constexpr int value = SWH_TILE_FETCH;
 };
 
 template <int SG, int TS, int NPAY>

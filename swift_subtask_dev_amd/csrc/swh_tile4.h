@@ -28,7 +28,10 @@ constexpr float kThrSlack = 1.f + 8.f * 5.9604645e-8f;  // (1 + 8u)
 
 // Per-lane hit-list capacity of variants 4 and 6: 64 (measured at 128^3:
 // force 2.46 ms at 64, 2.75 ms at 48, 2.97 ms at 32; density 1.72 / 1.65 / 1.74).
-constexpr int kTile4Cap = 64;
+#ifndef SWH_TILE4_CAP
+#define SWH_TILE4_CAP 64
+#endif
+constexpr int kTile4Cap = SWH_TILE4_CAP;
 
 template <int SG, int TS>
 struct Tile4Lds {

@@ -105,16 +105,17 @@ def main():
     ap.add_argument("--n", type=int, default=128, help="particles per dimension per GPU")
     ap.add_argument("--cell-factor", type=int, default=int(os.environ.get("SWH_CELL_FACTOR", "1")))
     ap.add_argument("--loop-variant", type=int, default=int(os.environ.get("SWH_LOOP_VARIANT", "0")),
-                    help="0 default, 1 direct gather, 2 two-phase gather, 3 tile, 4 tile + fp32 tests, "
-                         "5 one group per wave, 6 tile + fp32 tests + balanced phase B")
+                    help="0 default (7), 7 pair lists, 5 tile loop (group per wave), "
+                         "4 tile loop (4 groups per wave), 1 direct gather")
     ap.add_argument("--cell-scale", type=float, default=float(os.environ.get("SWH_CELL_SCALE", "0")),
                     help="grid cells per H_max as a real number (overrides --cell-factor)")
     ap.add_argument("--diag-mode", type=int, default=0,
                     help="profiling only, results invalid: 1 tile staging only, 2 + candidate tests")
     ap.add_argument("--group-size", type=int, default=int(os.environ.get("SWH_GROUP_SIZE", "0")),
                     help="tile i-group size / row width: 0 (default 16), 16, 32, 64")
-    ap.add_argument("--group-mode", type=int, default=int(os.environ.get("SWH_GROUP_MODE", "0")),
-                    help="tile i-groups: 0 octree leaves, 1 consecutive runs of group-size parts")
+    ap.add_argument("--list-skin", type=float, default=float(os.environ.get("SWH_LIST_SKIN", "0.1")),
+                    help="pair-list reach slack over gamma*h (variant 7)")
+    ap.add_argument("--list-capacity", type=int, default=0, help="pair-list entries per particle")
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-runs", type=int, default=3)
@@ -157,7 +158,7 @@ def main():
     del parts
     sp = lib.HydroSpace(ctx)
     sp.set_tuning(args.cell_factor, args.loop_variant, args.group_size, args.cell_scale,
-                  args.diag_mode, args.group_mode)
+                  args.diag_mode, args.list_capacity, args.list_skin)
     # a dedicated (non-NULL) stream: the library's kernels and the timing
     # events share it, so the events bracket exactly the loop kernels
     stream = torch.cuda.Stream()
@@ -226,7 +227,7 @@ def main():
         b_force = n_owned * (27 * S_IN_FORCE + S_OUT_FORCE)
         achieved = b_dens / td
         # PMC traffic was measured on the default configuration only
-        default_cfg = (args.loop_variant == 0 and args.group_size == 0 and args.group_mode == 0
+        default_cfg = (args.loop_variant == 0 and args.group_size == 0 and args.list_skin == 0.1
                        and args.cell_factor == 1 and args.cell_scale == 0 and args.n == 128)
         traffic = load_traffic() if default_cfg else None
         out = {
@@ -252,18 +253,19 @@ def main():
                 "cell_factor": args.cell_scale or args.cell_factor,
                 "loop_variant": args.loop_variant,
                 "group_size": args.group_size or 16,
-                "group_mode": args.group_mode,
+                "list_skin": args.list_skin,
+                "list_entries": info["list_entries"],
+                "list_overflow": info["list_overflow"],
                 "grid_cdim": info["cdim"],
                 "i_groups": info["ngroups"],
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": {0: "tile5_kernel<DENSITY,double>", 3: "tile_kernel<DENSITY,double>",
-                           1: "loop_kernel<DENSITY,double,1>",
-                           2: "loop_kernel<DENSITY,double,2>",
+                "kernel": {0: "list_build_kernel + walk_kernel<DENSITY,double>",
+                           7: "list_build_kernel + walk_kernel<DENSITY,double>",
+                           1: "loop_kernel<DENSITY,double>",
                            4: "tile4_kernel<DENSITY,double>",
-                           5: "tile5_kernel<DENSITY,double>",
-                           6: "tile6_kernel<DENSITY,double>"}[args.loop_variant],
+                           5: "tile5_kernel<DENSITY,double>"}[args.loop_variant],
                 "achieved": achieved / 1e9,
                 "peak": HBM_PEAK / 1e9,
                 "unit": "GB/s",

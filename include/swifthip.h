@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SWH_ABI_VERSION 2
+#define SWH_ABI_VERSION 3
 
 #if defined(__GNUC__)
 #define SWH_API __attribute__((visibility("default")))
@@ -248,19 +248,19 @@ SWH_API swh_status swh_space_sync(swh_space *s);
 /* Kernel-tuning knobs of the batch loops (bench/diagnostics). */
 typedef struct swh_tuning {
   int32_t cell_factor;  /* neighbour-grid cells per H_max (1..4) */
-  int32_t loop_variant; /* 0 = default (3); 1 = per-particle direct gather, 2 = per-particle
-                           two-phase gather, 3 = tile (i-groups in 16/32/64-lane rows),
-                           4 = tile with fp32 candidate tests + exact fp64 re-test,
-                           5 = as 4 with one i-group per wave, 64/group_size lanes
-                               per particle,
-                           6 = as 4 (16-lane rows) with the hits of a drain dealt
-                               out evenly over the wave (balanced phase B) */
-  int32_t group_size;   /* tile i-group size = row width: 0 (default 16), 16, 32, 64 */
+  int32_t loop_variant; /* 0 = default (7);
+                           7 = pair lists: the density loop builds the step's lists
+                               (r < max(R_i, R_j), R = gamma h (1 + list_skin)), the
+                               density / gradient / force loops walk them;
+                           5 = one-launch tile loop, one i-group per wave;
+                           4 = one-launch tile loop, 64/group_size i-groups per wave;
+                           1 = per-particle direct gather */
+  int32_t group_size;   /* tile i-group size: 0 (default 16), 16, 32, 64 (variants 4, 5) */
   float cell_scale;     /* if > 0: cells per H_max as a real number (overrides cell_factor) */
-  int32_t diag_mode;    /* 0; profiling only (results invalid): 1 = tile staging only,
-                           2 = staging + candidate tests, no interactions */
-  int32_t group_mode;   /* tile i-groups: 0 = octree leaves of the Morton-ordered cells,
-                           1 = consecutive runs of group_size sorted particles (full rows) */
+  int32_t diag_mode;    /* 0; profiling only (results invalid): 1 = staging only (tile
+                           loops) / list build only (lists), 2 = staging + candidate tests */
+  int32_t list_capacity; /* list entries per particle (0 = 128); more hits: direct gather */
+  float list_skin;       /* relative slack of the list reach over gamma h (default 0.1) */
 } swh_tuning;
 SWH_API swh_status swh_space_set_tuning(swh_space *s, const swh_tuning *t);
 
@@ -272,8 +272,11 @@ typedef struct swh_space_info {
   int32_t reserved;
   double cell_width[3];
   double h_max;     /* max gamma*h at rebuild */
-  int64_t loop_stats[4]; /* last counted tile loop (variants 4, 5): candidates loaded, staged,
-                            phase-A wave steps, phase-B wave steps */
+  int64_t loop_stats[4]; /* last counted search (tile loop or list build): candidates loaded,
+                            staged, phase-A wave steps, phase-B / flush wave steps */
+  int64_t list_entries;  /* last counted list build: total entries */
+  int32_t list_overflow; /* last counted list build: particles over list_capacity */
+  int32_t list_valid;    /* the step's pair lists are current */
 } swh_space_info;
 SWH_API swh_status swh_space_get_info(const swh_space *s, swh_space_info *info);
 

@@ -160,14 +160,15 @@ class SpaceInfo(C.Structure):
     """swh_space_info (include/swifthip.h)."""
     _fields_ = [("cdim", C.c_int32 * 3), ("ncell", C.c_int32), ("ngroups", C.c_int32),
                 ("reserved", C.c_int32), ("cell_width", C.c_double * 3), ("h_max", C.c_double),
-                ("loop_stats", C.c_int64 * 4)]
+                ("loop_stats", C.c_int64 * 4), ("list_entries", C.c_int64),
+                ("list_overflow", C.c_int32), ("list_valid", C.c_int32)]
 
 
 class Tuning(C.Structure):
     """swh_tuning (include/swifthip.h)."""
     _fields_ = [("cell_factor", C.c_int32), ("loop_variant", C.c_int32),
                 ("group_size", C.c_int32), ("cell_scale", C.c_float), ("diag_mode", C.c_int32),
-                ("group_mode", C.c_int32)]
+                ("list_capacity", C.c_int32), ("list_skin", C.c_float)]
 
 
 class Leaf(C.Structure):

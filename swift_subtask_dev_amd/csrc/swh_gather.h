@@ -9,17 +9,10 @@
 //   kPay / load_j() / interact_staged(): the j-side record staged in LDS by
 //                the tile loop (kPay float4s + one int) and the iact on it
 //
-// Two traversals of the neighbour grid:
-//   variant 1 (gather_direct): each lane walks its own grid cells and
-//     evaluates every accepted j immediately (the hit branch runs with the
-//     lanes that hit, ~25% of the wave).
-//   variant 3 (tile, the default): swh_tile.h.
-//   variant 2 (gather_two_phase): phase A walks the cells and appends accepted
-//     j indices to a per-lane hit list in LDS ([k][lane] layout: every append
-//     and every read is one bank-conflict-free ds_*_b32 across the wave);
-//     phase B drains the lists with all lanes evaluating interactions. Drains
-//     happen at wave-uniform row boundaries once any lane's list passes
-//     CAP-16, and per lane (rare) when one row would overflow it.
+// gather_direct (variant 1): each lane walks the grid cells of its own i and
+// evaluates every accepted j immediately. It serves the subset loops (ghost
+// reruns of particles whose pair list no longer covers their h) and the
+// overflow particles of the pair lists (swh_list.h).
 #pragma once
 
 #include "swh_physics.h"
@@ -328,74 +321,6 @@ __device__ __forceinline__ void gather_direct(const GridDev& g, const SoA& a, co
       }
     }
   }
-}
-
-// Phase B: evaluate this lane's pending hits. Separations are recomputed in
-// fp64 with the nearest periodic image, which is the image phase A accepted
-// (every accepted j lies within the reach, and reach < box/2 unless the
-// dimension already used the nearest image).
-template <typename T, class S>
-__device__ __forceinline__ void drain_hits(const GridDev& g, const SoA& a, const double4& pi,
-                                           const int* hits, int nh, int lane, S& st) {
-  for (int k = 0; k < nh; k++) {
-    const int j = hits[k * 64 + lane];
-    const double4 pj = a.pos[j];
-    double dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
-    if (g.periodic) {
-      dx = wrap_nearest(dx, g.dim[0]);
-      dy = wrap_nearest(dy, g.dim[1]);
-      dz = wrap_nearest(dz, g.dim[2]);
-    }
-    const T tdx = (T)dx, tdy = (T)dy, tdz = (T)dz;
-    const T r2 = tdx * tdx + tdy * tdy + tdz * tdz;
-    st.interact(a, j, pj, tdx, tdy, tdz, r2);
-  }
-}
-
-template <int CAP, typename T, class S>
-__device__ __forceinline__ void gather_two_phase(const GridDev& g, const SoA& a,
-                                                 const double4& pi, bool active, S& st,
-                                                 int* hits, int lane) {
-  CellRange c;
-  int ny = 0, nrows = 0;
-  if (active) {
-    cell_range(g, pi.x, pi.y, pi.z, st.reach, c);
-    ny = c.hi[1] - c.lo[1] + 1;
-    nrows = ny * (c.hi[2] - c.lo[2] + 1);
-  }
-  int nrows_max = nrows;
-  for (int o = 32; o > 0; o >>= 1) nrows_max = max(nrows_max, __shfl_xor(nrows_max, o));
-  int nh = 0;
-  for (int row = 0; row < nrows_max; row++) {
-    if (row < nrows) {
-      double sy, sz;
-      const int wz = wrap_cell(g, c, 2, c.lo[2] + row / ny, sz);
-      const int wy = wrap_cell(g, c, 1, c.lo[1] + row % ny, sy);
-      for (int cx = c.lo[0]; cx <= c.hi[0]; cx++) {
-        double sx;
-        const int wx = wrap_cell(g, c, 0, cx, sx);
-        const int2 r = cell_range_of(g, wx, wy, wz);
-        for (int j = r.x; j < r.y; j++) {
-          const double4 pj = a.pos[j];
-          T dx, dy, dz;
-          const T r2 = separation<T>(g, c, pi, pj, sx, sy, sz, dx, dy, dz);
-          if (st.accept(j, pj, r2)) {
-            if (nh == CAP) {  // this lane's list is full mid-row: drain it alone
-              drain_hits<T>(g, a, pi, hits, nh, lane, st);
-              nh = 0;
-            }
-            hits[nh * 64 + lane] = j;
-            nh++;
-          }
-        }
-      }
-    }
-    if (__any(nh > CAP - 16)) {  // wave-uniform drain point
-      drain_hits<T>(g, a, pi, hits, nh, lane, st);
-      nh = 0;
-    }
-  }
-  drain_hits<T>(g, a, pi, hits, nh, lane, st);
 }
 
 }  // namespace swh

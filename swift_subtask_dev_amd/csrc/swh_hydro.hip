@@ -4,24 +4,20 @@
 // plus the ghost h-iteration (src/runner_ghost.c:1085-1596), the extra ghost
 // (:992-1083) and runner_do_end_hydro_force (src/runner_others.c:618).
 //
-// Gather formulation: one thread owns one active i-particle and visits the
-// grid rows overlapping [x_i - R, x_i + R] (R = H_i for density/gradient,
-// max over all H for force), each row one contiguous j range of the
-// cell-sorted SoA. Every directed pair (i <- j) is evaluated exactly once, with
-// the non-symmetric iact (hydro_iact.h:130,276,488), so the sums are
-// deterministic and need no atomics.
+// Gather formulation: every directed pair (i <- j) is evaluated exactly once,
+// by the owner of i, with the non-symmetric iact (hydro_iact.h:130,276,488),
+// so the sums are deterministic and need no atomics. The default loops walk
+// the step's pair lists (swh_list.h); the tile loops (swh_tile4.h,
+// swh_tile5.h) search and interact in one launch; gather_direct
+// (swh_gather.h) serves subsets and list overflow.
 #include "swh_gather.h"
 #include "swh_internal.h"
+#include "swh_list.h"
 #include "swh_tile.h"
 #include "swh_tile4.h"
 #include "swh_tile5.h"
-#include "swh_tile6.h"
 
 namespace swh {
-
-// Per-lane hit-list capacity of the two-phase gather (LDS: 4 waves x CAP x 64
-// x 4 B = 48 KiB per 256-thread block).
-constexpr int kHitCap = 48;
 
 __device__ __forceinline__ void count_add(int n, unsigned long long* counter) {
   unsigned long long v = (unsigned long long)n;
@@ -29,9 +25,9 @@ __device__ __forceinline__ void count_add(int n, unsigned long long* counter) {
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(counter, v);
 }
 
-// One thread per i-particle (item t of the launch, or subset[t]); inactive
-// and padding lanes still take part in the wave-level drains of variant 2.
-template <int LOOP, typename T, int VARIANT>
+// Variant 1: one thread per i-particle (item t of the launch, or subset[t]),
+// direct gather over its grid cells.
+template <int LOOP, typename T>
 __global__ __launch_bounds__(256) void loop_kernel(GridDev g, SoA a,
                                                    const int* __restrict__ subset,
                                                    int nitems, int max_active_bin, T a2H,
@@ -47,16 +43,102 @@ __global__ __launch_bounds__(256) void loop_kernel(GridDev g, SoA a,
   if (act) {
     st.load_i(a, i, a2H, hmax_bits);
     pi = a.pos[i];
-  }
-  if (VARIANT == 2) {
-    __shared__ int hits[4][kHitCap * 64];
-    gather_two_phase<kHitCap, T>(g, a, pi, act, st, hits[threadIdx.x >> 6], threadIdx.x & 63);
-  } else if (act) {
     gather_direct<T>(g, a, pi, st);
-  }
-  if (act) {
     st.store(a, i);
     if (ncount) ncount[i] = st.n;
+  }
+  if (counter) count_add(act ? st.n : 0, counter);
+}
+
+// ---------------------------------------------------------------------------
+// Variant 7 (default): the step's pair lists (swh_list.h).
+// ---------------------------------------------------------------------------
+constexpr int kWalkLpi = 4;  // lanes per i of the list walks
+
+__global__ void list_prep_kernel(const unsigned int* hmax_bits, float gs1, unsigned int* rwrap,
+                                 unsigned int* ovf_n) {
+  if (threadIdx.x == 0) {
+    const float r = __uint_as_float(*hmax_bits) * gs1;
+    *rwrap = __float_as_uint(r * (1.f + 1e-4f) + 1e-30f);
+    *ovf_n = 0u;
+  }
+}
+
+__global__ __launch_bounds__(64) void list_build_kernel(GridDev g, SoA a, ListDev ld,
+                                                       const int2* __restrict__ groups,
+                                                       int ngroups, int max_active_bin,
+                                                       const unsigned int* __restrict__ hmax_bits,
+                                                       unsigned long long* counter, int diag) {
+  __shared__ ListLds<kListLpiBuild> lds;
+  list_build<kListLpiBuild>(g, a, ld, groups, ngroups, max_active_bin, hmax_bits, counter, diag,
+                            lds);
+}
+
+template <int LOOP, typename T>
+__global__ __launch_bounds__(256) void walk_kernel(GridDev g, SoA a, ListDev ld, int n,
+                                                   int max_active_bin, T a2H,
+                                                   const unsigned int* __restrict__ hmax_bits,
+                                                   unsigned long long* counter,
+                                                   int* __restrict__ ncount) {
+  list_walk<LOOP, T, kWalkLpi>(g, a, ld, n, max_active_bin, a2H, hmax_bits, counter, ncount);
+}
+
+// The list's overflow particles (more than K hits): direct gather. The count
+// is read on the device, so the launch needs no host round trip.
+template <int LOOP, typename T>
+__global__ __launch_bounds__(256) void overflow_kernel(GridDev g, SoA a, ListDev ld,
+                                                       int max_active_bin, T a2H,
+                                                       const unsigned int* __restrict__ hmax_bits,
+                                                       unsigned long long* counter,
+                                                       int* __restrict__ ncount) {
+  const int nov = (int)*ld.ovf_n;
+  for (int t0 = blockIdx.x * blockDim.x; t0 < nov; t0 += gridDim.x * blockDim.x) {
+    const int t = t0 + (int)threadIdx.x;
+    const int i = t < nov ? ld.ovf[t] : -1;
+    const bool act = i >= 0 && a.tb[i] <= max_active_bin;
+    LoopState<LOOP, T> st;
+    st.n = 0;
+    if (act) {
+      st.load_i(a, i, a2H, hmax_bits);
+      gather_direct<T>(g, a, a.pos[i], st);
+      st.store(a, i);
+      if (ncount) ncount[i] = st.n;
+    }
+    if (counter) count_add(act ? st.n : 0, counter);
+  }
+}
+
+// Density on a subset (the ghost's reruns, runner_ghost.c:1503-1546): a
+// particle whose H still fits its list reach walks its list, any other one
+// searches.
+template <typename T>
+__global__ __launch_bounds__(256) void walk_subset_kernel(GridDev g, SoA a, ListDev ld,
+                                                          int list_ok,
+                                                          const int* __restrict__ subset,
+                                                          int nitems, int max_active_bin,
+                                                          const unsigned int* __restrict__ hmax_bits,
+                                                          unsigned long long* counter) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = t < nitems ? subset[t] : -1;
+  const bool act = i >= 0 && a.tb[i] <= max_active_bin;
+  LoopState<LOOP_DENSITY, T> st;
+  st.n = 0;
+  if (act) {
+    st.load_i(a, i, (T)0, hmax_bits);
+    const double4 pi = a.pos[i];
+    const int nl = list_ok ? ld.cnt[i] : 0;
+    const int lb = list_ok ? ld.base[i] : -1;
+    const bool listed = list_ok && lb >= 0 && nl <= ld.K &&
+                        pi.w * (double)kGamma <= (double)ld.reach[i];
+    if (listed) {
+      if (g.periodic)
+        walk_entries<1, true, T>(g, a, ld, pi, nl, lb, 0, st);
+      else
+        walk_entries<1, false, T>(g, a, ld, pi, nl, lb, 0, st);
+    } else {
+      gather_direct<T>(g, a, pi, st);
+    }
+    st.store(a, i);
   }
   if (counter) count_add(act ? st.n : 0, counter);
 }
@@ -72,19 +154,6 @@ __global__ __launch_bounds__(256) void loop_kernel(GridDev g, SoA a,
 #define SWH_TILE_BOUNDS __launch_bounds__(64)
 #endif
 
-// Variant 3: NS = 64/SG i-groups per 64-lane wave (swh_tile.h).
-template <int LOOP, typename T, int SG>
-__global__ SWH_TILE_BOUNDS void tile_kernel(GridDev g, SoA a,
-                                                  const int2* __restrict__ groups, int ngroups,
-                                                  int max_active_bin, T a2H,
-                                                  const unsigned int* __restrict__ hmax_bits,
-                                                  unsigned long long* counter,
-                                                  int* __restrict__ ncount, int diag) {
-  __shared__ TileLds<SG, TileSlots<LOOP>::value, LoopState<LOOP, T>::kPay> lds;
-  tile_loop<LOOP, T, SG>(g, a, groups, ngroups, max_active_bin, a2H, hmax_bits, counter, ncount,
-                         diag, lds);
-}
-
 // Variant 4: the tile loop with fp32 candidate tests (swh_tile4.h).
 template <int LOOP, typename T, int SG>
 __global__ SWH_TILE_BOUNDS void tile4_kernel(GridDev g, SoA a,
@@ -94,21 +163,8 @@ __global__ SWH_TILE_BOUNDS void tile4_kernel(GridDev g, SoA a,
                                                    unsigned long long* counter,
                                                    int* __restrict__ ncount, int diag) {
   __shared__ Tile4Lds<SG, TileSlots<LOOP>::value> lds;
-  tile4_loop<LOOP, T, SG, false>(g, a, groups, ngroups, max_active_bin, a2H, hmax_bits, counter,
+  tile4_loop<LOOP, T, SG>(g, a, groups, ngroups, max_active_bin, a2H, hmax_bits, counter,
                                  ncount, diag, lds);
-}
-
-// Variant 6: variant 4 with the balanced phase B of swh_tile6.h.
-template <int LOOP, typename T, int SG>
-__global__ SWH_TILE_BOUNDS void tile6_kernel(GridDev g, SoA a,
-                                             const int2* __restrict__ groups, int ngroups,
-                                             int max_active_bin, T a2H,
-                                             const unsigned int* __restrict__ hmax_bits,
-                                             unsigned long long* counter,
-                                             int* __restrict__ ncount, int diag) {
-  __shared__ Tile6Lds<SG, TileSlots<LOOP>::value, decltype(LoopState<LOOP, T>::A)> lds;
-  tile4_loop<LOOP, T, SG, true>(g, a, groups, ngroups, max_active_bin, a2H, hmax_bits, counter,
-                                ncount, diag, lds);
 }
 
 // Variant 5: one i-group per wave, LPI lanes per i-particle (swh_tile5.h).
@@ -146,7 +202,7 @@ __global__ void init_kernel(SoA a, int64_t n, int max_active_bin) {
 // time-steps). One thread per particle still iterating; particles whose h
 // moved by more than h_tolerance are re-initialised and appended to the redo
 // list (the subset reruns of runner_ghost.c:1503-1546 become one subset launch
-// of loop_kernel per iteration).
+// per iteration: list walks, or searches where h outgrew the list reach).
 // ---------------------------------------------------------------------------
 struct GhostParams {
   float h_max, h_min, eta_dim, eps;
@@ -168,7 +224,8 @@ __global__ void ghost_init_kernel(SoA a, int64_t n, int max_active_bin, float h_
 template <typename T>
 __global__ void ghost_kernel(SoA a, const int* __restrict__ list, int count,
                              int* __restrict__ redo, int* __restrict__ nredo, float* left,
-                             float* right, GhostParams gp, unsigned int* hmax_bits) {
+                             float* right, GhostParams gp, unsigned int* hmax_bits,
+                             const float* __restrict__ list_reach, unsigned int* list_stale) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= count) return;
   const int i = list[t];
@@ -273,6 +330,8 @@ __global__ void ghost_kernel(SoA a, const int* __restrict__ list, int count,
   pos.w = (double)hf;
   a.pos[i] = pos;
   atomicMax(hmax_bits, __float_as_uint(hf));
+  // the step's pair lists cover this particle's loops only while H <= its R
+  if (list_reach && (double)hf * (double)kGamma > (double)list_reach[i]) atomicOr(list_stale, 1u);
   // converged: hydro_prepare_gradient + hydro_reset_gradient (hydro.h:654-733)
   const T hh = (T)hf;
   const T curl_v = tsqrt(rot_x * rot_x + rot_y * rot_y + rot_z * rot_z);
@@ -413,51 +472,97 @@ static unsigned long long* counter_slot(swh_space* s) {
 }
 static unsigned int* hmax_slot(swh_space* s) { return s->counters.as<unsigned int>() + 2; }
 
+// Counter slots (s->counters, 128 bytes): u64[0] interactions, u32[2] max h
+// (float bits), u32[4..5] ghost list counts, u64[3] list entries, u64[4..7]
+// loop work counters, u32[16] list overflow count, u32[17] list-stale flag,
+// u32[18] list wrap radius (float bits).
+static unsigned int* ovf_slot(swh_space* s) { return s->counters.as<unsigned int>() + 16; }
+static unsigned int* stale_slot(swh_space* s) { return s->counters.as<unsigned int>() + 17; }
+static unsigned int* rwrap_slot(swh_space* s) { return s->counters.as<unsigned int>() + 18; }
+
+static int loop_variant_of(const swh_space* s) {
+  return s->tuning.loop_variant != 0 ? s->tuning.loop_variant : 7;
+}
+
+static ListDev list_dev(swh_space* s) {
+  ListDev d;
+  d.nbr = s->nbr.as<int>();
+  d.cnt = s->nbr_cnt.as<int>();
+  d.base = s->nbr_base.as<int>();
+  d.reach = s->nbr_reach.as<float>();
+  d.K = s->list_K;
+  d.skin1 = 1.f + s->tuning.list_skin;
+  d.rwrap_bits = rwrap_slot(s);
+  d.ovf = s->nbr_ovf.as<int>();
+  d.ovf_n = ovf_slot(s);
+  return d;
+}
+
+// Build the step's pair lists (variant 7) for the active particles.
+static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool count) {
+  const int K = s->tuning.list_capacity > 0 ? s->tuning.list_capacity : 128;
+  SWH_TRY(s->nbr.reserve((size_t)std::max(1, s->ngroups) * K * kListSlots * sizeof(int)));
+  SWH_TRY(s->nbr_cnt.reserve((size_t)s->n * sizeof(int)));
+  SWH_TRY(s->nbr_base.reserve((size_t)s->n * sizeof(int)));
+  SWH_TRY(s->nbr_reach.reserve((size_t)s->n * sizeof(float)));
+  SWH_TRY(s->nbr_ovf.reserve((size_t)s->n * sizeof(int)));
+  s->list_K = K;
+  const ListDev ld = list_dev(s);
+  hipLaunchKernelGGL(list_prep_kernel, dim3(1), dim3(64), 0, s->stream, hmax_slot(s),
+                     kGamma * ld.skin1, rwrap_slot(s), ovf_slot(s));
+  hipLaunchKernelGGL(list_build_kernel, dim3(s->ngroups), dim3(64), 0, s->stream, grid_dev(s),
+                     soa_of(s), ld, s->groups.as<const int2>(), s->ngroups, P->max_active_bin,
+                     hmax_slot(s), count ? counter_slot(s) : nullptr, s->tuning.diag_mode);
+  SWH_HIP(hipGetLastError());
+  s->list_valid = true;
+  s->list_mab = P->max_active_bin;
+  return SWH_OK;
+}
+
 template <int LOOP, typename T>
 static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int nitems,
                          int max_active_bin, T a2H, unsigned long long* ctr, int* ncount) {
-  // the tile loop needs the rebuild's compact i-groups: subsets (ghost reruns)
-  // take the per-particle direct gather
-  // default (0): the fastest measured per loop at 128^3:
-  // density variant 5, gradient and force variant 4
-  const int v = s->tuning.loop_variant != 0 ? s->tuning.loop_variant
-                                             : (LOOP == LOOP_DENSITY ? 5 : 4);
-  if (v >= 3 && !subset) {
+  const int v = loop_variant_of(s);
+  const int block = 256;
+  if (v == 7) {
+    const ListDev ld = list_dev(s);
+    if (subset) {  // density reruns of the ghost
+      hipLaunchKernelGGL((walk_subset_kernel<T>), dim3((nitems + block - 1) / block),
+                         dim3(block), 0, s->stream, gd, soa_of(s), ld, s->list_valid ? 1 : 0,
+                         subset, nitems, max_active_bin, hmax_slot(s), ctr);
+      return;
+    }
+    constexpr int ppb = block / kWalkLpi;
+    hipLaunchKernelGGL((walk_kernel<LOOP, T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
+                       s->stream, gd, soa_of(s), ld, nitems, max_active_bin, a2H, hmax_slot(s),
+                       ctr, ncount);
+    hipLaunchKernelGGL((overflow_kernel<LOOP, T>), dim3(64), dim3(block), 0, s->stream, gd,
+                       soa_of(s), ld, max_active_bin, a2H, hmax_slot(s), ctr, ncount);
+    return;
+  }
+  if ((v == 4 || v == 5) && !subset) {
     const int sg = s->tuning.group_size > 0 ? s->tuning.group_size : 16;
-    // variants 3/4 pack 64/sg groups into a wave, variant 5 gives each group a wave
-    const int nw = v == 5 ? s->ngroups
-                 : v == 6 ? (s->ngroups + 3) / 4
-                          : (s->ngroups + 64 / sg - 1) / (64 / sg);
+    // variant 4 packs 64/sg groups into a wave, variant 5 gives each group a wave
+    const int nw = v == 5 ? s->ngroups : (s->ngroups + 64 / sg - 1) / (64 / sg);
     const int2* grp = s->groups.as<const int2>();
 #define SWH_TILE_LAUNCH(K)                                                                   \
   hipLaunchKernelGGL((K), dim3(nw), dim3(64), 0, s->stream, gd, soa_of(s), grp, s->ngroups, \
                      max_active_bin, a2H, hmax_slot(s), ctr, ncount, s->tuning.diag_mode)
-    if (v == 6) {  // 16-lane rows only
-      SWH_TILE_LAUNCH((tile6_kernel<LOOP, T, 16>));
-    } else if (v == 5) {
+    if (v == 5) {
       if (sg == 16) SWH_TILE_LAUNCH((tile5_kernel<LOOP, T, 4>));
       else if (sg == 32) SWH_TILE_LAUNCH((tile5_kernel<LOOP, T, 2>));
       else SWH_TILE_LAUNCH((tile5_kernel<LOOP, T, 1>));
-    } else if (v == 4) {
+    } else {
       if (sg == 16) SWH_TILE_LAUNCH((tile4_kernel<LOOP, T, 16>));
       else if (sg == 32) SWH_TILE_LAUNCH((tile4_kernel<LOOP, T, 32>));
       else SWH_TILE_LAUNCH((tile4_kernel<LOOP, T, 64>));
-    } else {
-      if (sg == 16) SWH_TILE_LAUNCH((tile_kernel<LOOP, T, 16>));
-      else if (sg == 32) SWH_TILE_LAUNCH((tile_kernel<LOOP, T, 32>));
-      else SWH_TILE_LAUNCH((tile_kernel<LOOP, T, 64>));
     }
 #undef SWH_TILE_LAUNCH
     return;
   }
-  const int block = 256;
-  const int grid = (nitems + block - 1) / block;
-  if (v == 2)
-    hipLaunchKernelGGL((loop_kernel<LOOP, T, 2>), dim3(grid), dim3(block), 0, s->stream, gd,
-                       soa_of(s), subset, nitems, max_active_bin, a2H, hmax_slot(s), ctr, ncount);
-  else
-    hipLaunchKernelGGL((loop_kernel<LOOP, T, 1>), dim3(grid), dim3(block), 0, s->stream, gd,
-                       soa_of(s), subset, nitems, max_active_bin, a2H, hmax_slot(s), ctr, ncount);
+  hipLaunchKernelGGL((loop_kernel<LOOP, T>), dim3((nitems + block - 1) / block), dim3(block), 0,
+                     s->stream, gd, soa_of(s), subset, nitems, max_active_bin, a2H, hmax_slot(s),
+                     ctr, ncount);
 }
 
 template <int LOOP>
@@ -465,6 +570,13 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const int
                               int nitems, bool count) {
   if (nitems <= 0) return SWH_OK;
   if (!subset && s->ngroups <= 0) return SWH_OK;
+  if (!subset && loop_variant_of(s) == 7) {
+    // the density loop builds the step's lists; gradient and force reuse them
+    // while no particle's H has outgrown its list reach (ghost: stale flag)
+    if (LOOP == LOOP_DENSITY || !s->list_valid || s->list_mab != P->max_active_bin)
+      SWH_TRY(build_lists(s, P, count));
+    if (s->tuning.diag_mode == 1) return SWH_OK;
+  }
   const GridDev gd = grid_dev(s);
   const double a2H = P->a * P->a * P->H;
   unsigned long long* ctr = count ? counter_slot(s) : nullptr;
@@ -482,20 +594,29 @@ template <int LOOP>
 static swh_status run_loop(swh_space* s, const swh_hydro_params* P, int64_t* n_out) {
   SWH_TRY(check_built(s));
   if (!P) return SWH_ERR_ARG;
-  SWH_HIP(hipSetDevice(s->ctx->device));
-  // counted launch: slot 0 = interactions, slots 4-7 = tile work counters
-  unsigned long long* ctr = counter_slot(s);
-  if (n_out) {
-    SWH_HIP(hipMemsetAsync(ctr, 0, sizeof(unsigned long long), s->stream));
-    SWH_HIP(hipMemsetAsync(ctr + 4, 0, 4 * sizeof(unsigned long long), s->stream));
+  if (s->n == 0) {  // nothing to interact (the counters are not even reserved)
+    if (n_out) *n_out = 0;
+    return SWH_OK;
   }
+  SWH_HIP(hipSetDevice(s->ctx->device));
+  // counted launch: slot 0 = interactions, 3 = list entries, 4-7 = work counters
+  unsigned long long* ctr = counter_slot(s);
+  if (n_out) SWH_HIP(hipMemsetAsync(ctr + 3, 0, 5 * sizeof(unsigned long long), s->stream));
+  if (n_out) SWH_HIP(hipMemsetAsync(ctr, 0, sizeof(unsigned long long), s->stream));
+  const bool rebuilds = loop_variant_of(s) == 7 &&
+                        (LOOP == LOOP_DENSITY || !s->list_valid ||
+                         s->list_mab != P->max_active_bin);
   SWH_TRY(launch_loop<LOOP>(s, P, nullptr, (int)s->n, n_out != nullptr));
   if (n_out) {
-    unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long h[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     SWH_HIP(hipMemcpyAsync(h, ctr, sizeof(h), hipMemcpyDeviceToHost, s->stream));
     SWH_HIP(hipStreamSynchronize(s->stream));
     *n_out = (int64_t)h[0];
     for (int k = 0; k < 4; k++) s->loop_stats[k] = (int64_t)h[4 + k];
+    if (rebuilds) {
+      s->list_entries = (int64_t)h[3];
+      s->list_overflow = (int32_t)(h[8] & 0xffffffffull);
+    }
   }
   return SWH_OK;
 }
@@ -563,6 +684,9 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   gp.fac_B = P->a_factor_Balsara_eps;
   int* list = s->ghost_list.as<int>();
   int* list2 = s->ghost_list2.as<int>();
+  const float* lreach =
+      (loop_variant_of(s) == 7 && s->list_valid) ? s->nbr_reach.as<const float>() : nullptr;
+  SWH_HIP(hipMemsetAsync(stale_slot(s), 0, sizeof(unsigned int), st));
   int it = 0;
   for (; count > 0 && it < P->max_smoothing_iterations; it++) {
     SWH_HIP(hipMemsetAsync(cnt + 1, 0, sizeof(int), st));
@@ -570,16 +694,22 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
     if (s->ctx->precision == SWH_PRECISION_F64)
       hipLaunchKernelGGL(ghost_kernel<double>, dim3(g), dim3(block), 0, st, soa_of(s), list,
                          count, list2, cnt + 1, s->ghost_left.as<float>(),
-                         s->ghost_right.as<float>(), gp, hmax_slot(s));
+                         s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s));
     else
       hipLaunchKernelGGL(ghost_kernel<float>, dim3(g), dim3(block), 0, st, soa_of(s), list,
                          count, list2, cnt + 1, s->ghost_left.as<float>(),
-                         s->ghost_right.as<float>(), gp, hmax_slot(s));
+                         s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s));
     SWH_HIP(hipGetLastError());
     SWH_HIP(hipMemcpyAsync(&count, cnt + 1, sizeof(int), hipMemcpyDeviceToHost, st));
     SWH_HIP(hipStreamSynchronize(st));
     std::swap(list, list2);
     if (count > 0) SWH_TRY(launch_loop<LOOP_DENSITY>(s, P, list, count, false));
+  }
+  if (lreach) {
+    unsigned int stale = 0;
+    SWH_HIP(hipMemcpyAsync(&stale, stale_slot(s), sizeof(stale), hipMemcpyDeviceToHost, st));
+    SWH_HIP(hipStreamSynchronize(st));
+    if (stale) s->list_valid = false;  // gradient / force rebuild the lists
   }
   if (iterations) *iterations = it;
   if (n_unconverged) *n_unconverged = count;

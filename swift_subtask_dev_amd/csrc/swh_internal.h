@@ -148,7 +148,7 @@ struct swh_space {
   int64_t n = 0;
   bool built = false;
   SwhGrid grid;
-  swh_tuning tuning{1, 0, 0, 0.f, 0, 0};
+  swh_tuning tuning{1, 0, 0, 0.f, 0, 0, 0.1f};
 
   // AoS image of the caller's records (for write-back of untouched fields)
   swh::DevBuf aos;
@@ -179,6 +179,13 @@ struct swh_space {
   swh::DevBuf seg_groups, seg_off;
   int32_t ngroups = 0;
   int64_t loop_stats[4] = {0, 0, 0, 0};  // work counters of the last counted tile loop
+  // the step's pair lists (swh_list.h): valid from a density loop until the
+  // next upload / rebuild / tuning change, or a ghost that grows an H past its R
+  swh::DevBuf nbr, nbr_cnt, nbr_base, nbr_reach, nbr_ovf;
+  bool list_valid = false;
+  int32_t list_mab = 0, list_K = 0;
+  int64_t list_entries = 0;   // last counted build: total entries
+  int32_t list_overflow = 0;  // last counted build: particles over capacity
   // scratch
   swh::DevBuf keys, keys2, idx, idx2, sort_tmp, scan_tmp, counters;
   swh::DevBuf tmp_soa;     // staging for permutation gathers

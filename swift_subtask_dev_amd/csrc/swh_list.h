@@ -1,0 +1,407 @@
+// swh_list.h — the step's pair lists (loop variant 7, the default).
+//
+// SWIFT builds its neighbour structure once (runner_do_hydro_sort,
+// src/runner_sort.c:201-431) and every loop of the step walks it: density,
+// the ghost's subset reruns, gradient and force (runner_doiact_functions_
+// hydro.h DOPAIR1/DOPAIR2 walk the same sort lists). The batch path does the
+// same with explicit pair lists:
+//
+//   list build (list_build): one wave per i-group (an octree leaf of <= 16
+//     particles, swh_space.hip group_kernel), four lanes per i. The wave
+//     stages the candidates of the cells around its group (fp32 coordinates
+//     relative to the group centre, pruned by the exact box distance, as
+//     swh_tile5.h), tests every (i, candidate) in fp32 against
+//       r < max(R_i, R_j),  R = gamma h (1 + skin)
+//     with the threshold inflated by the worst-case rounding bound, and
+//     appends the hits to i's list. The list is a superset of every pair
+//     the three loops accept (density/gradient: r < H_i, DOPAIR1/DOSELF1;
+//     force: r < max(H_i, H_j), DOPAIR2/DOSELF2), and stays one while no
+//     particle's H grows past its R (the ghost checks that: skin = SWIFT's
+//     space_maxreldx-style slack for h changes between loops).
+//   list walk (list_walk): LPI lanes per active i over consecutive sorted
+//     particles (every lane of the wave busy), each lane walking every
+//     LPI-th entry of i's list: fp64 separation (nearest periodic image),
+//     the loop's exact fp64 criterion and the fp64 non-symmetric iact
+//     (hydro_iact.h:130, 276, 488), index loads two entries ahead and
+//     particle loads one entry ahead. The LPI partial sums are combined at
+//     the end. The accepted pair set is exactly the f64 oracle's.
+//
+// Layout: entry k of particle i (slot `sl` of group `gr`) lives at
+// nbr[(gr * K + k) * kListSlots + sl]: the lists of one group are
+// interleaved, so the lanes of a group read one 64-byte segment per entry
+// index. Particles with more than K hits (cnt > K) are walked by the
+// per-particle search (gather_direct) instead.
+#pragma once
+
+#include "swh_tile5.h"
+
+namespace swh {
+
+constexpr int kListSlots = 16;   // list columns per i-group (max group size)
+constexpr int kListLpiBuild = 4;  // lanes per i in the list build
+
+struct ListDev {
+  int* nbr;      // entries: sorted j indices
+  int* cnt;      // per particle: entries found (> K: overflow, searched instead)
+  int* base;     // per particle: (group * K) * kListSlots + slot
+  float* reach;  // per particle: R = gamma h (1 + skin) at build (0: not listed)
+  int K;
+  float skin1;   // 1 + skin
+  const unsigned int* rwrap_bits;  // max R at build (float bits): particles farther than
+                                   // this from every face need no periodic wrap
+  int* ovf;      // overflow particles, count in *ovf_n
+  unsigned int* ovf_n;
+};
+
+template <int LPI>
+struct ListLds {
+  static constexpr int GS = 64 / LPI;
+  static constexpr int kICap = 128;          // LDS hits per i before a flush
+  static constexpr int kStride = kICap + 2;  // odd dword stride: lists start on different banks
+  float4 cand[kT5Region];  // x, y, z relative to the box centre; w = inflated R_j^2
+  int candj[kT5Region];
+  int cell_j0[64];
+  int cell_pre[64];
+  unsigned char cell_code[64];
+  unsigned short hits[GS * kStride + 64];  // [i slot][entry] region slots; + per-lane dummies
+};
+
+// Copy i's pending LDS hits to its global list (the LPI lanes of i split them).
+template <int LPI, class LDS>
+__device__ __forceinline__ void list_flush(const ListDev& ld, LDS& L, int& nq, int& wr, int il,
+                                           int s, int gbase, TileStats& ts) {
+  wave_sync();  // list entries were written by the other lanes of i
+  const int nmax = uni_i(wave_max_i(nq));
+  ts.bsteps += (unsigned int)((nmax + LPI - 1) / LPI);
+  const unsigned short* list = &L.hits[il * LDS::kStride];
+  for (int t = s; t < nq; t += LPI) {
+    const int k = wr + t;
+    if (k < ld.K) ld.nbr[(size_t)(gbase + k) * kListSlots + il] = L.candj[list[t]];
+  }
+  wr += nq;
+  nq = 0;
+  wave_sync();
+}
+
+// Phase A over the staged region [0, nst) for the list criterion, then flush.
+template <int LPI, bool WRAP, class LDS>
+__device__ __forceinline__ void list_consume(const GridDev& g, const ListDev& ld,
+                                             const CellRange& c, float xi, float yi, float zi,
+                                             float thr_i, bool act, int nst, LDS& L, int& nq,
+                                             int& wr, int il, int s, int gbase, TileStats& ts) {
+  constexpr int GS = 64 / LPI;
+  const int dummy = GS * LDS::kStride + il * LPI + s;
+  const int nblk = (nst + kT5Blk * LPI - 1) / (kT5Blk * LPI);
+  ts.asteps += (unsigned int)(nblk * kT5Blk);
+  const float bx = (float)g.dim[0], by = (float)g.dim[1], bz = (float)g.dim[2];
+  for (int b = 0; b < nblk; b++) {
+    if (__any(nq > LDS::kICap - kT5Blk * LPI)) list_flush<LPI>(ld, L, nq, wr, il, s, gbase, ts);
+    const int c0 = b * kT5Blk * LPI + s;
+    float4 cv[kT5Blk];
+#pragma unroll
+    for (int kk = 0; kk < kT5Blk; kk++) cv[kk] = L.cand[min(c0 + kk * LPI, kT5Region - 1)];
+    bool hit[kT5Blk];
+    int cnt = 0;
+#pragma unroll
+    for (int kk = 0; kk < kT5Blk; kk++) {
+      float dx = xi - cv[kk].x, dy = yi - cv[kk].y, dz = zi - cv[kk].z;
+      if (WRAP) {
+        if (c.full[0]) dx = wrap_nearest_f(dx, bx);
+        if (c.full[1]) dy = wrap_nearest_f(dy, by);
+        if (c.full[2]) dz = wrap_nearest_f(dz, bz);
+      }
+      float r2 = dx * dx;
+      r2 = fmaf(dy, dy, r2);
+      r2 = fmaf(dz, dz, r2);
+      hit[kk] = act & (c0 + kk * LPI < nst) & (r2 < fmaxf(thr_i, cv[kk].w));
+      cnt += hit[kk] ? 1 : 0;
+    }
+    // this lane's first position in i's list: i's count + earlier sub-lanes' hits
+    int inc = cnt;
+    for (int o = 1; o < LPI; o <<= 1) {
+      const int tt = __shfl_up(inc, o, LPI);
+      if (s >= o) inc += tt;
+    }
+    const int tot = __shfl(inc, LPI - 1, LPI);
+    int pos = il * LDS::kStride + nq + inc - cnt;
+#pragma unroll
+    for (int kk = 0; kk < kT5Blk; kk++) {
+      L.hits[hit[kk] ? pos : dummy] = (unsigned short)(c0 + kk * LPI);
+      pos += hit[kk] ? 1 : 0;
+    }
+    nq += tot;
+  }
+  list_flush<LPI>(ld, L, nq, wr, il, s, gbase, ts);
+}
+
+// Build the pair lists of one i-group (one wave).
+template <int LPI, class LDS>
+__device__ __forceinline__ void list_build(const GridDev& g, const SoA& a, const ListDev ld,
+                                           const int2* __restrict__ groups, int ngroups,
+                                           int max_active_bin,
+                                           const unsigned int* __restrict__ hmax_bits,
+                                           unsigned long long* counter, int diag, LDS& L) {
+  const int lane = threadIdx.x & 63;
+  const int il = lane / LPI, s = lane % LPI;
+  const int gid = xcd_block_id();
+  const int2 gr = gid < ngroups ? groups[gid] : make_int2(0, 0);
+  const int i = il < gr.y ? gr.x + il : -1;
+  const bool act = i >= 0 && a.tb[i] <= max_active_bin;
+  const double skin1 = (double)ld.skin1;
+  double4 pi = make_double4(0., 0., 0., 0.);
+  if (act) pi = a.pos[i];
+  const double Ri = act ? pi.w * (double)kGamma * skin1 : 0.;
+  // group box and reach (wave-uniform)
+  const double Rg = uni_d(wave_max_d(Ri));
+  double lo[3], hi[3];
+  lo[0] = uni_d(wave_min_d(act ? pi.x : 1e300));
+  lo[1] = uni_d(wave_min_d(act ? pi.y : 1e300));
+  lo[2] = uni_d(wave_min_d(act ? pi.z : 1e300));
+  hi[0] = uni_d(wave_max_d(act ? pi.x : -1e300));
+  hi[1] = uni_d(wave_max_d(act ? pi.y : -1e300));
+  hi[2] = uni_d(wave_max_d(act ? pi.z : -1e300));
+  TileStats ts;
+  const int gbase = gid * ld.K;
+  int nq = 0, wr = 0;
+  if (Rg > 0.) {
+    const double Rmax = (double)__uint_as_float(*hmax_bits) * (double)kGamma * skin1;
+    const double reach = fmax(Rg, Rmax);  // r < max(R_i, R_j)
+    CellRange c;
+    double ctr[3], half[3];
+    double D2 = 0.;
+    for (int k = 0; k < 3; k++) {
+      c.lo[k] = uni_i((int)floor((lo[k] - g.origin[k] - reach) * g.inv_w[k]));
+      c.hi[k] = uni_i((int)floor((hi[k] - g.origin[k] + reach) * g.inv_w[k]));
+      c.full[k] = false;
+      if (g.periodic) {
+        c.full[k] = (c.hi[k] - c.lo[k] + 1 >= g.cdim[k]);
+        if (c.full[k]) {
+          c.lo[k] = 0;
+          c.hi[k] = g.cdim[k] - 1;
+        }
+      } else {
+        c.lo[k] = max(c.lo[k], 0);
+        c.hi[k] = min(c.hi[k], g.cdim[k] - 1);
+      }
+      ctr[k] = uni_d(0.5 * (lo[k] + hi[k]));
+      half[k] = 0.5 * (hi[k] - lo[k]);
+      const double ext = c.full[k] ? g.dim[k] : half[k] + reach;
+      D2 += ext * ext;
+    }
+    const int nx = c.hi[0] - c.lo[0] + 1;
+    const int ny = c.hi[1] - c.lo[1] + 1;
+    const int ncells = nx * ny * (c.hi[2] - c.lo[2] + 1);
+    // rounding bound of the fp32 relative coordinates (swh_tile4.h)
+    const double delta = 16. * kUnitRound * sqrt(D2);
+    const float deltaf = uni_f((float)delta);
+    const float xi = (float)(pi.x - ctr[0]);
+    const float yi = (float)(pi.y - ctr[1]);
+    const float zi = (float)(pi.z - ctr[2]);
+    const float thr_i = act ? (float)((Ri + delta) * (Ri + delta)) * kThrSlack : -1.f;
+    const float hxf = uni_f((float)(half[0] + delta)), hyf = uni_f((float)(half[1] + delta)),
+                hzf = uni_f((float)(half[2] + delta));
+    const float Rgf = uni_f((float)(Rg + delta));
+    const float gs1 = (float)((double)kGamma * skin1);
+    const bool wrap = c.full[0] || c.full[1] || c.full[2];
+    int nst = 0;
+    for (int cb = 0; cb < ncells; cb += 64) {
+      // batch of 64 cells, one per lane
+      int cnt = 0, j0 = 0, code = 0;
+      const int cl = cb + lane;
+      if (cl < ncells) {
+        double sx, sy, sz;
+        const int wx = wrap_cell(g, c, 0, c.lo[0] + cl % nx, sx);
+        const int wy = wrap_cell(g, c, 1, c.lo[1] + (cl / nx) % ny, sy);
+        const int wz = wrap_cell(g, c, 2, c.lo[2] + cl / (nx * ny), sz);
+        code = (sx < 0. ? 1 : (sx > 0. ? 2 : 0)) | ((sy < 0. ? 1 : (sy > 0. ? 2 : 0)) << 2) |
+               ((sz < 0. ? 1 : (sz > 0. ? 2 : 0)) << 4);
+        const int2 sp = cell_range_of(g, wx, wy, wz);
+        j0 = sp.x;
+        cnt = sp.y - sp.x;
+      }
+      int inc = cnt;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int tt = __shfl_up(inc, o);
+        if (lane >= o) inc += tt;
+      }
+      const int total = uni_i(__shfl(inc, 63));
+      wave_sync();
+      L.cell_j0[lane] = j0;
+      L.cell_pre[lane] = inc - cnt;
+      L.cell_code[lane] = (unsigned char)code;
+      wave_sync();
+      int k = 0;
+      for (int base = 0; base < total; base += 64) {
+        const int q = base + lane;
+        const bool val = q < total;
+        int jj = 0, sc = 0;
+        if (val) {
+          while (k + 1 < 64 && L.cell_pre[k + 1] <= q) k++;
+          jj = L.cell_j0[k] + (q - L.cell_pre[k]);
+          sc = L.cell_code[k];
+        }
+        bool keep = false;
+        float4 cf = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (val) {
+          const double4 p = a.pos[jj];
+          double rx = p.x + shift_of(sc & 3, g.dim[0]) - ctr[0];
+          double ry = p.y + shift_of((sc >> 2) & 3, g.dim[1]) - ctr[1];
+          double rz = p.z + shift_of((sc >> 4) & 3, g.dim[2]) - ctr[2];
+          if (c.full[0]) rx = wrap_nearest(rx, g.dim[0]);
+          if (c.full[1]) ry = wrap_nearest(ry, g.dim[1]);
+          if (c.full[2]) rz = wrap_nearest(rz, g.dim[2]);
+          cf.x = (float)rx;
+          cf.y = (float)ry;
+          cf.z = (float)rz;
+          const float ex = c.full[0] ? 0.f : fmaxf(fabsf(cf.x) - hxf, 0.f);
+          const float ey = c.full[1] ? 0.f : fmaxf(fabsf(cf.y) - hyf, 0.f);
+          const float ez = c.full[2] ? 0.f : fmaxf(fabsf(cf.z) - hzf, 0.f);
+          const float Rj = (float)p.w * gs1 + deltaf;
+          cf.w = Rj * Rj * kThrSlack;
+          const float rj = fmaxf(Rgf, Rj);
+          keep = ex * ex + ey * ey + ez * ez <= rj * rj * kThrSlack;
+        }
+        const unsigned long long m = __ballot(keep);
+        if (keep) {
+          const int slot = nst + __popcll(m & ((1ull << lane) - 1ull));
+          L.cand[slot] = cf;
+          L.candj[slot] = jj;
+        }
+        nst += __popcll(m);
+        ts.loaded += val ? 1u : 0u;
+        ts.staged += keep ? 1u : 0u;
+        if (nst > kT5Region - 64) {  // region full: consume it
+          wave_sync();
+          if (diag != 1) {
+            if (wrap)
+              list_consume<LPI, true>(g, ld, c, xi, yi, zi, thr_i, act, nst, L, nq, wr, il, s,
+                                      gbase, ts);
+            else
+              list_consume<LPI, false>(g, ld, c, xi, yi, zi, thr_i, act, nst, L, nq, wr, il, s,
+                                       gbase, ts);
+          }
+          nst = 0;
+          wave_sync();
+        }
+      }
+    }
+    wave_sync();
+    if (diag != 1 && nst > 0) {
+      if (wrap)
+        list_consume<LPI, true>(g, ld, c, xi, yi, zi, thr_i, act, nst, L, nq, wr, il, s, gbase,
+                                ts);
+      else
+        list_consume<LPI, false>(g, ld, c, xi, yi, zi, thr_i, act, nst, L, nq, wr, il, s, gbase,
+                                 ts);
+    }
+  }
+  if (i >= 0 && s == 0) {
+    ld.cnt[i] = act ? wr : 0;
+    ld.base[i] = act ? gbase * kListSlots + il : -1;
+    ld.reach[i] = act ? (float)Ri : 0.f;
+    if (act && wr > ld.K) ld.ovf[atomicAdd(ld.ovf_n, 1u)] = i;
+  }
+  if (counter) {
+    unsigned long long v = (unsigned long long)((act && s == 0) ? wr : 0);
+    unsigned long long ld_ = ts.loaded, sg = ts.staged;
+    for (int o = 32; o > 0; o >>= 1) {
+      v += __shfl_xor(v, o);
+      ld_ += __shfl_xor(ld_, o);
+      sg += __shfl_xor(sg, o);
+    }
+    if (lane == 0) {
+      atomicAdd(counter + 3, v);  // list entries
+      atomicAdd(counter + 4, ld_);
+      atomicAdd(counter + 5, sg);
+      atomicAdd(counter + 6, (unsigned long long)ts.asteps);
+      atomicAdd(counter + 7, (unsigned long long)ts.bsteps);
+    }
+  }
+}
+
+// Does particle x need the nearest-image wrap (within R of a periodic face)?
+__device__ __forceinline__ bool near_face(const GridDev& g, const double4& p, double R) {
+  return (p.x < R) | (p.x > g.dim[0] - R) | (p.y < R) | (p.y > g.dim[1] - R) | (p.z < R) |
+         (p.z > g.dim[2] - R);
+}
+
+// Walk entries s, s+LPI, ... of i's list (nl entries from column lb).
+template <int LPI, bool WRAP, typename T, class S>
+__device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, const ListDev& ld,
+                                             const double4& pi, int nl, int lb, int s, S& st) {
+  const int* __restrict__ col = ld.nbr + lb;
+  int k = s;
+  int jn = k < nl ? col[(size_t)k * kListSlots] : -1;
+  int jn2 = k + LPI < nl ? col[(size_t)(k + LPI) * kListSlots] : -1;
+  double4 pn = make_double4(0., 0., 0., 0.);
+  JRec<S::kPay> rn{};
+  if (jn >= 0) {
+    pn = a.pos[jn];
+    rn = S::load_j(a, jn);
+  }
+  for (; k < nl; k += LPI) {
+    const int j = jn;
+    const double4 pj = pn;
+    const JRec<S::kPay> rj = rn;
+    jn = jn2;  // issue the next entries' loads before this entry's math
+    jn2 = k + 2 * LPI < nl ? col[(size_t)(k + 2 * LPI) * kListSlots] : -1;
+    if (jn >= 0) {
+      pn = a.pos[jn];
+      rn = S::load_j(a, jn);
+    }
+    double dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+    if (WRAP) {
+      dx = wrap_nearest(dx, g.dim[0]);
+      dy = wrap_nearest(dy, g.dim[1]);
+      dz = wrap_nearest(dz, g.dim[2]);
+    }
+    const T tdx = (T)dx, tdy = (T)dy, tdz = (T)dz;
+    const T r2 = tdx * tdx + tdy * tdy + tdz * tdz;
+    if (st.accept(j, pj, r2)) st.interact_staged(rj.p, rj.meta, pj, tdx, tdy, tdz, r2);
+  }
+}
+
+// One loop over every active, listed particle: LPI lanes per i, 256/LPI
+// consecutive sorted particles per workgroup.
+template <int LOOP, typename T, int LPI>
+__device__ __forceinline__ void list_walk(const GridDev& g, SoA& a, const ListDev ld, int n,
+                                          int max_active_bin, T a2H,
+                                          const unsigned int* __restrict__ hmax_bits,
+                                          unsigned long long* counter, int* __restrict__ ncount) {
+  using S = LoopState<LOOP, T>;
+  constexpr int PPB = 256 / LPI;
+  const int i = xcd_block_id() * PPB + (int)threadIdx.x / LPI;
+  const int s = (int)threadIdx.x % LPI;
+  bool act = i < n && a.tb[i] <= max_active_bin;
+  int nl = 0, lb = 0;
+  if (act) {
+    nl = ld.cnt[i];
+    lb = ld.base[i];
+    if (nl > ld.K || lb < 0) act = false;  // overflow: the search walks it
+  }
+  S st;
+  st.n = 0;
+  double4 pi = make_double4(0., 0., 0., 0.);
+  if (act) {
+    st.load_i(a, i, a2H, hmax_bits);
+    pi = a.pos[i];
+  }
+  if (!act) nl = 0;
+  const double rwrap = (double)__uint_as_float(*ld.rwrap_bits);
+  if (__any(act && g.periodic && near_face(g, pi, rwrap)))
+    walk_entries<LPI, true, T>(g, a, ld, pi, nl, lb, s, st);
+  else
+    walk_entries<LPI, false, T>(g, a, ld, pi, nl, lb, s, st);
+  reduce_lanes<LPI, T>(st);
+  if (act && s == 0) {
+    st.store(a, i);
+    if (ncount) ncount[i] = st.n;
+  }
+  if (counter) {
+    unsigned long long v = (unsigned long long)((act && s == 0) ? st.n : 0);
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(counter, v);
+  }
+}
+
+}  // namespace swh

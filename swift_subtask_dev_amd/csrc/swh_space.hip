@@ -294,15 +294,6 @@ __global__ void group_kernel(const uint32_t* __restrict__ code, const int* __res
   if (!WRITE) ngroup[r] = ng;
 }
 
-// i-groups as consecutive runs of kGroupMax sorted particles (tuning
-// group_mode 1): every row is full; a run may straddle a Morton jump.
-__global__ void chunk_group_kernel(int64_t n, int kGroupMax, int ng, int2* __restrict__ out) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= ng) return;
-  const int64_t s = (int64_t)k * kGroupMax;
-  out[k] = make_int2((int)s, (int)min((int64_t)kGroupMax, n - s));
-}
-
 // Gather every SoA array through the sort permutation (src -> dst).
 __global__ void permute_kernel(SoA src, SoA dst, const int* __restrict__ idx, int64_t n) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -433,7 +424,7 @@ static swh_status reserve_soa(swh_space* s, int64_t n) {
 }
 
 swh_status space_hmax_to_device(swh_space* s) {
-  SWH_TRY(s->counters.reserve(64));
+  SWH_TRY(s->counters.reserve(128));
   unsigned int* hb = s->counters.as<unsigned int>() + 2;  // slot 2: hmax bits
   SWH_HIP(hipMemsetAsync(hb, 0, sizeof(unsigned int), s->stream));
   hipLaunchKernelGGL(hmax_kernel, dim3(1024), dim3(256), 0, s->stream, s->pos.as<double4>(),
@@ -470,7 +461,8 @@ swh_status swh_space_destroy(swh_space* s) {
                     &s->cell_start, &s->cell_rank, &s->cell_code, &s->cell_span, &s->groups, &s->seg_groups,
                     &s->seg_off, &s->keys, &s->keys2, &s->idx, &s->idx2, &s->sort_tmp,
                     &s->scan_tmp, &s->counters, &s->tmp_soa, &s->ghost_left,
-                    &s->ghost_right, &s->ghost_list, &s->ghost_list2, &s->ghost_flag};
+                    &s->ghost_right, &s->ghost_list, &s->ghost_list2, &s->ghost_flag,
+                    &s->nbr, &s->nbr_cnt, &s->nbr_base, &s->nbr_reach, &s->nbr_ovf};
   for (DevBuf* b : bufs) b->release();
   s->hstage.release();
   if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
@@ -492,13 +484,19 @@ swh_status swh_space_set_stream(swh_space* s, void* stream) {
 }
 
 swh_status swh_space_set_tuning(swh_space* s, const swh_tuning* t) {
-  if (!s || !t || t->cell_factor < 1 || t->cell_factor > 4 || t->loop_variant < 0 ||
-      t->loop_variant > 6 || t->group_mode < 0 || t->group_mode > 1 ||
+  const bool variant_ok = t && (t->loop_variant == 0 || t->loop_variant == 1 ||
+                                t->loop_variant == 4 || t->loop_variant == 5 ||
+                                t->loop_variant == 7);
+  const bool lists = t && (t->loop_variant == 0 || t->loop_variant == 7);
+  if (!s || !t || t->cell_factor < 1 || t->cell_factor > 4 || !variant_ok ||
       (t->group_size != 0 && t->group_size != 16 && t->group_size != 32 && t->group_size != 64) ||
-      t->cell_scale < 0.f || t->cell_scale > 4.f || t->diag_mode < 0 || t->diag_mode > 2)
+      (lists && t->group_size > 16) || t->cell_scale < 0.f || t->cell_scale > 4.f ||
+      t->diag_mode < 0 || t->diag_mode > 2 || t->list_capacity < 0 ||
+      t->list_capacity > 4096 || !(t->list_skin >= 0.f) || t->list_skin > 1.f)
     return SWH_ERR_ARG;
   s->tuning = *t;
   s->built = false;
+  s->list_valid = false;
   return SWH_OK;
 }
 
@@ -515,6 +513,9 @@ swh_status swh_space_get_info(const swh_space* s, swh_space_info* info) {
   info->ngroups = s->ngroups;
   info->h_max = s->grid.hmax;
   for (int k = 0; k < 4; k++) info->loop_stats[k] = s->loop_stats[k];
+  info->list_entries = s->list_entries;
+  info->list_overflow = s->list_overflow;
+  info->list_valid = s->list_valid ? 1 : 0;
   return SWH_OK;
 }
 
@@ -534,6 +535,7 @@ swh_status swh_space_upload_parts(swh_space* s, const void* parts, int64_t count
   s->layout = L;
   s->n = count;
   s->built = false;
+  s->list_valid = false;
   if (count == 0) return SWH_OK;
   const size_t bytes = (size_t)count * L.stride;
   SWH_TRY(s->aos.reserve(bytes));
@@ -582,6 +584,7 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
   }
   SWH_HIP(hipSetDevice(s->ctx->device));
   hipStream_t st = s->stream;
+  s->list_valid = false;
   // 1. bounding box + max h
   const int nb = 512;
   SWH_TRY(s->scan_tmp.reserve(nb * 7 * sizeof(double)));
@@ -701,17 +704,6 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
   // 5. i-groups of the tile loops
   const int nc = g.ncell;
   const int gmax = s->tuning.group_size > 0 ? s->tuning.group_size : 16;
-  if (s->tuning.group_mode == 1) {
-    const int ng = (int)((n + gmax - 1) / gmax);
-    s->ngroups = ng;
-    SWH_TRY(s->groups.reserve(((size_t)ng + 1) * sizeof(int2)));
-    hipLaunchKernelGGL(chunk_group_kernel, dim3((ng + block - 1) / block), dim3(block), 0, st,
-                       n, gmax, ng, s->groups.as<int2>());
-    SWH_HIP(hipGetLastError());
-    SWH_TRY(space_hmax_to_device(s));
-    s->built = true;
-    return SWH_OK;
-  }
   SWH_TRY(s->seg_groups.reserve(((size_t)nc + 1) * sizeof(int)));
   SWH_TRY(s->seg_off.reserve(((size_t)nc + 1) * sizeof(int)));
   const int cgrid = (nc + block - 1) / block;

@@ -26,7 +26,7 @@ namespace swh {
 constexpr double kUnitRound = 5.9604644775390625e-8;   // u = 2^-24
 constexpr float kThrSlack = 1.f + 8.f * 5.9604645e-8f;  // (1 + 8u)
 
-// Per-lane hit-list capacity of variants 4 and 6: 64 (measured at 128^3:
+// Per-lane hit-list capacity of variant 4: 64 (measured at 128^3:
 // force 2.46 ms at 64, 2.75 ms at 48, 2.97 ms at 32; density 1.72 / 1.65 / 1.74).
 #ifndef SWH_TILE4_CAP
 #define SWH_TILE4_CAP 64
@@ -89,25 +89,11 @@ __device__ __forceinline__ void tile4_drain(const GridDev& g, const SoA& a, cons
   nh = 0;
 }
 
-// Balanced drain of variant 6 (swh_tile6.h).
-template <bool PWRAP, typename T, class S, class LDS>
-__device__ void tile6_drain(const GridDev& g, const SoA& a, LDS& L, int& nh, int lane, S& st,
-                            TileStats& ts, T a2H, const unsigned int* hmax_bits);
-
-template <bool BAL, bool PWRAP, typename T, class S, class LDS>
-__device__ __forceinline__ void tile4_drain_any(const GridDev& g, const SoA& a,
-                                                const double4& pi, LDS& L, int& nh, int lane,
-                                                S& st, TileStats& ts, T a2H,
-                                                const unsigned int* hmax_bits) {
-  if constexpr (BAL) tile6_drain<PWRAP, T>(g, a, L, nh, lane, st, ts, a2H, hmax_bits);
-  else tile4_drain<PWRAP, T>(g, a, pi, L, nh, lane, st, ts);
-}
-
 // Phase A over the staged region of each row, 8 candidates per block. A
 // lane's list holds <= kTile4Cap - 8 entries at the start of a block; every
 // candidate's j is written at the list end and kept only on a hit, so the
 // appends need no branch.
-template <int LOOP, int SG, bool WRAP, bool PWRAP, bool BAL, typename T, class S, class LDS>
+template <int LOOP, int SG, bool WRAP, bool PWRAP, typename T, class S, class LDS>
 __device__ __forceinline__ void tile4_consume(const GridDev& g, const SoA& a,
                                               const CellRange& c, const double4& pi, float xi,
                                               float yi, float zi, float thr_i, bool act,
@@ -120,7 +106,7 @@ __device__ __forceinline__ void tile4_consume(const GridDev& g, const SoA& a,
   const float bx = (float)g.dim[0], by = (float)g.dim[1], bz = (float)g.dim[2];
   for (int k0 = 0; k0 < kmax; k0 += 8) {
     if (__any(nh > kTile4Cap - 8))
-      tile4_drain_any<BAL, PWRAP, T>(g, a, pi, L, nh, lane, st, ts, a2H, hmax_bits);
+      tile4_drain<PWRAP, T>(g, a, pi, L, nh, lane, st, ts);
     float4 cv[8];
 #pragma unroll
     for (int kk = 0; kk < 8; kk++) cv[kk] = L.cand[rbase + k0 + kk];
@@ -151,7 +137,7 @@ __device__ __forceinline__ void tile4_consume(const GridDev& g, const SoA& a,
   }
 }
 
-template <int LOOP, typename T, int SG, bool BAL, class LDS>
+template <int LOOP, typename T, int SG, class LDS>
 __device__ __forceinline__ void tile4_loop(const GridDev& g, SoA& a,
                                            const int2* __restrict__ groups, int ngroups,
                                            int max_active_bin, T a2H,
@@ -167,13 +153,7 @@ __device__ __forceinline__ void tile4_loop(const GridDev& g, SoA& a,
   const int row = lane / SG, r = lane % SG;
   // XCD-aware order (swh_tile.h): each XCD takes a contiguous stretch of the
   // Morton-ordered groups so neighbouring groups share its L2.
-  const int nwg = gridDim.x;
-  const int per_xcd = (nwg + 7) / 8;
-  const int xcd = blockIdx.x % 8, slot_in_xcd = blockIdx.x / 8;
-  const int full_xcds = nwg - (per_xcd - 1) * 8;
-  const int wg = xcd < full_xcds ? xcd * per_xcd + slot_in_xcd
-                                 : full_xcds * per_xcd + (xcd - full_xcds) * (per_xcd - 1) +
-                                       slot_in_xcd;
+  const int wg = xcd_block_id();
   const int gid = wg * NS + row;
   const int2 gr = gid < ngroups ? groups[gid] : make_int2(0, 0);
   const int i = r < gr.y ? gr.x + r : -1;
@@ -185,7 +165,6 @@ __device__ __forceinline__ void tile4_loop(const GridDev& g, SoA& a,
     st.load_i(a, i, a2H, hmax_bits);
     pi = a.pos[i];
   }
-  if constexpr (BAL) L.own_i[lane] = act ? i : -1;
   const double Hi = act ? pi.w * (double)kGamma : 0.;
   const double Hg = row_max<SG>(Hi);
   double lo[3], hi[3];
@@ -366,13 +345,13 @@ __device__ __forceinline__ void tile4_loop(const GridDev& g, SoA& a,
       }
       if (diag == 2) nh = 0;
       if (wrap)
-        tile4_consume<LOOP, SG, true, true, BAL, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst,
+        tile4_consume<LOOP, SG, true, true, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst,
                                                L, nh, lane, st, ts, a2H, hmax_bits);
       else if (pwrap)
-        tile4_consume<LOOP, SG, false, true, BAL, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst,
+        tile4_consume<LOOP, SG, false, true, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst,
                                                 L, nh, lane, st, ts, a2H, hmax_bits);
       else
-        tile4_consume<LOOP, SG, false, false, BAL, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase,
+        tile4_consume<LOOP, SG, false, false, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase,
                                                  nst, L, nh, lane, st, ts, a2H, hmax_bits);
       nst = 0;
     }
@@ -382,17 +361,17 @@ __device__ __forceinline__ void tile4_loop(const GridDev& g, SoA& a,
   if (diag == 1) nst = 0;
   if (diag == 2) nh = 0;
   if (wrap) {
-    tile4_consume<LOOP, SG, true, true, BAL, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst, L,
+    tile4_consume<LOOP, SG, true, true, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst, L,
                                            nh, lane, st, ts, a2H, hmax_bits);
-    tile4_drain_any<BAL, true, T>(g, a, pi, L, nh, lane, st, ts, a2H, hmax_bits);
+    tile4_drain<true, T>(g, a, pi, L, nh, lane, st, ts);
   } else if (pwrap) {
-    tile4_consume<LOOP, SG, false, true, BAL, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst, L,
+    tile4_consume<LOOP, SG, false, true, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst, L,
                                             nh, lane, st, ts, a2H, hmax_bits);
-    tile4_drain_any<BAL, true, T>(g, a, pi, L, nh, lane, st, ts, a2H, hmax_bits);
+    tile4_drain<true, T>(g, a, pi, L, nh, lane, st, ts);
   } else {
-    tile4_consume<LOOP, SG, false, false, BAL, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst,
+    tile4_consume<LOOP, SG, false, false, T>(g, a, c, pi, xi, yi, zi, thr_i, act, rbase, nst,
                                              L, nh, lane, st, ts, a2H, hmax_bits);
-    tile4_drain_any<BAL, false, T>(g, a, pi, L, nh, lane, st, ts, a2H, hmax_bits);
+    tile4_drain<false, T>(g, a, pi, L, nh, lane, st, ts);
   }
   if (act) {
     st.store(a, i);

@@ -228,13 +228,7 @@ __device__ __forceinline__ void tile5_loop(const GridDev& g, SoA& a,
   const int il = lane / LPI, s = lane % LPI;
   // XCD-aware order (swh_tile.h): each XCD takes a contiguous stretch of the
   // Morton-ordered groups so neighbouring groups share its L2.
-  const int nwg = gridDim.x;
-  const int per_xcd = (nwg + 7) / 8;
-  const int xcd = blockIdx.x % 8, slot_in_xcd = blockIdx.x / 8;
-  const int full_xcds = nwg - (per_xcd - 1) * 8;
-  const int gid = xcd < full_xcds ? xcd * per_xcd + slot_in_xcd
-                                  : full_xcds * per_xcd + (xcd - full_xcds) * (per_xcd - 1) +
-                                        slot_in_xcd;
+  const int gid = xcd_block_id();
   const int2 gr = gid < ngroups ? groups[gid] : make_int2(0, 0);
   const int i = il < gr.y ? gr.x + il : -1;
   const bool act = i >= 0 && a.tb[i] <= max_active_bin;

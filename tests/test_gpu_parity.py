@@ -245,17 +245,17 @@ def test_125cells_chain_vs_f64(gpu_ctx):
     assert_close(gr["main"]["a_hydro"], orc["main"]["a_hydro"], 1e-5, 1e-3, "a_hydro")
 
 
-# loop_variant 1 = per-particle direct gather, 2 = per-particle two-phase,
-# 3 = tile (64/group_size i-groups per wave), 4 = tile with fp32 candidate tests,
-# 5 = one i-group per wave, 6 = as 4 with the balanced phase B
-VARIANTS = [1, 2, 3, 4, 5, 6]
+# loop_variant 1 = per-particle direct gather, 4 = tile loop (64/group_size
+# i-groups per wave), 5 = tile loop (one i-group per wave), 7 = pair lists
+# (the default: density builds the step's lists, every loop walks them)
+VARIANTS = [1, 4, 5, 7]
 
 
-def box_chain_gpu(ctx, parts, P, cell_factor=1, variant=0, group_size=0, group_mode=0):
+def box_chain_gpu(ctx, parts, P, cell_factor=1, variant=0, group_size=0, **tuning):
     from swift_subtask_dev_amd import lib
     g = abi.copy_parts(parts)
     sp = lib.HydroSpace(ctx)
-    sp.set_tuning(cell_factor, variant, group_size, group_mode=group_mode)
+    sp.set_tuning(cell_factor, variant, group_size, **tuning)
     sp.upload(g)
     sp.rebuild(P)
     res = sp.hydro_step(P)
@@ -281,13 +281,11 @@ def box_chain_oracle(parts, P, prec="f64"):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant,group_size,group_mode",
-                         [(1, 0, 0), (2, 0, 0), (3, 16, 0), (3, 32, 0), (3, 64, 0), (4, 16, 0),
-                          (4, 32, 0), (4, 64, 0), (3, 16, 1), (4, 16, 1), (4, 32, 1),
-                          (5, 16, 0), (5, 32, 0), (5, 64, 0), (5, 16, 1), (6, 16, 0),
-                          (6, 16, 1)])
+@pytest.mark.parametrize("variant,group_size,skin",
+                         [(1, 0, 0.1), (4, 16, 0.1), (4, 32, 0.1), (4, 64, 0.1), (5, 16, 0.1),
+                          (5, 32, 0.1), (5, 64, 0.1), (7, 16, 0.1), (7, 16, 0.0), (7, 16, 0.5)])
 @pytest.mark.parametrize("cell_factor", [1, 2, 3])
-def test_box_density_vs_f64(gpu_ctx, cell_factor, variant, group_size, group_mode):
+def test_box_density_vs_f64(gpu_ctx, cell_factor, variant, group_size, skin):
     """Batch density loop on a periodic Sedov-like box vs the fp64 oracle;
     identical interaction count; every grid refinement gives the same sums."""
     from swift_subtask_dev_amd import lib
@@ -295,7 +293,7 @@ def test_box_density_vs_f64(gpu_ctx, cell_factor, variant, group_size, group_mod
     parts = ics.sedov_box(20, velocity="divergent", seed=11)
     g = abi.copy_parts(parts)
     sp = lib.HydroSpace(gpu_ctx)
-    sp.set_tuning(cell_factor, variant, group_size, group_mode=group_mode)
+    sp.set_tuning(cell_factor, variant, group_size, list_skin=skin)
     sp.upload(g)
     sp.rebuild(P)
     sp.init_parts(P)
@@ -309,19 +307,18 @@ def test_box_density_vs_f64(gpu_ctx, cell_factor, variant, group_size, group_mod
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant,group_size,group_mode",
-                         [(1, 0, 0), (2, 0, 0), (3, 16, 0), (3, 64, 0), (4, 16, 0), (4, 64, 0),
-                          (4, 16, 1), (5, 16, 0), (5, 32, 0), (5, 64, 0), (6, 16, 0),
-                          (6, 16, 1)])
-def test_box_chain_vs_f64(gpu_ctx, variant, group_size, group_mode):
+@pytest.mark.parametrize("variant,group_size,tuning",
+                         [(1, 0, {}), (4, 16, {}), (4, 64, {}), (5, 16, {}), (5, 32, {}),
+                          (5, 64, {}), (7, 16, {}), (7, 16, {"list_skin": 0.0}),
+                          (7, 16, {"list_capacity": 24})])
+def test_box_chain_vs_f64(gpu_ctx, variant, group_size, tuning):
     """Full SPHENIX chain (density, ghost with h iteration, gradient, extra
     ghost, force, end force) on a perturbed box with h off-target so the
     ghost iterates."""
     P = abi.default_hydro_params()
     parts = ics.sedov_box(16, velocity="divergent", pert=0.3, seed=5)
     parts["h"] *= np.random.Generator(np.random.PCG64(1)).uniform(0.8, 1.25, len(parts))
-    g, rg = box_chain_gpu(gpu_ctx, parts, P, variant=variant, group_size=group_size,
-                          group_mode=group_mode)
+    g, rg = box_chain_gpu(gpu_ctx, parts, P, variant=variant, group_size=group_size, **tuning)
     o, ro = box_chain_oracle(parts, P)
     assert rg["ghost_iterations"] >= 2
     # Chain tolerance: the GPU keeps struct-part (float) storage between the

@@ -146,7 +146,7 @@ def main():
 
     # ---- untimed setup: the full SPHENIX chain on the whole box ----------
     sp = lib.HydroSpace(ctx)
-    sp.set_tuning(args.cell_factor)
+    sp.set_tuning(args.cell_factor, list_capacity=args.list_capacity, list_skin=args.list_skin)
     sp.upload(parts)
     sp.rebuild(P)
     chain = sp.hydro_step(P)

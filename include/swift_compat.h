@@ -198,7 +198,7 @@ struct cell {
     struct sort_entry *sort[13]; /* one list per sid, count+1 entries */
     int count;
     float h_max, h_max_old, h_max_active;
-    float dx_max_part, dx_max_sort, dx_max_sort_old;
+    float dx_max_part, dx_max_sort, dx_max_sort_old, dx_max_part_old;
     uint16_t sorted;
     integertime_t ti_end_min;
     integertime_t ti_old_part;

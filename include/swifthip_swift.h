@@ -12,6 +12,8 @@
  *   runner_dopair2_branch_force        -> DOPAIR2_BRANCH (runner_doiact_functions_hydro.h:1972)
  *   runner_doself_subset_branch_density src/runner_doiact_hydro.h:182   -> DOSELF_SUBSET_BRANCH
  *   runner_dopair_subset_branch_density src/runner_doiact_hydro.h:185   -> DOPAIR_SUBSET_BRANCH
+ *   runner_dosub_{self1,pair1}_{density,gradient}, runner_dosub_{self2,pair2}_force,
+ *   runner_dosub_subset_density         src/runner_doiact_hydro.h:172-191 -> DOSUB_*
  *   runner_doself_grav_pp               src/runner_doiact_grav.h:41     (runner_doiact_grav.c:1788)
  *   runner_dopair_grav_pp               src/runner_doiact_grav.h:44-50  (runner_doiact_grav.c:1202)
  *
@@ -47,6 +49,15 @@ SWHS_API int swifthip_swift_set_precision(int precision);
 /* Last adapter error ("Interacting unsorted cells." ...) or "" . */
 SWHS_API const char *swifthip_swift_last_error(void);
 SWHS_API void swifthip_swift_clear_error(void);
+/* The struct part / struct gpart layouts this adapter was compiled against
+ * (sizeof / offsetof; what it hands to libswifthip). */
+struct swh_part_layout;
+struct swh_gpart_layout;
+SWHS_API void swifthip_swift_part_layout(struct swh_part_layout *out);
+SWHS_API void swifthip_swift_gpart_layout(struct swh_gpart_layout *out);
+/* cell_split_pairs[sid] (src/cell.c:62) as generated at init: writes 2*n ints
+ * (pid, pjd), returns n (-1 for a bad sid). */
+SWHS_API int swifthip_swift_split_pairs(int sid, int *pairs);
 
 SWHS_API void runner_doself1_branch_density(struct runner *r, struct cell *c);
 SWHS_API void runner_dopair1_branch_density(struct runner *r, struct cell *ci, struct cell *cj);
@@ -59,6 +70,22 @@ SWHS_API void runner_doself_subset_branch_density(struct runner *r, struct cell 
 SWHS_API void runner_dopair_subset_branch_density(struct runner *r, struct cell *ci,
                                                   struct part *parts_i, int *ind, int count,
                                                   struct cell *cj);
+/* Sub-cell recursion (DOSUB_*, src/runner_doiact_hydro.h:172-191 ->
+ * runner_doiact_functions_hydro.h:2524-2805): same descent as the CPU runner
+ * (cell_split_pairs, cell_can_recurse_in_{pair,self}_hydro_task), leaf tasks
+ * on the GPU. */
+SWHS_API void runner_dosub_self1_density(struct runner *r, struct cell *ci, int gettimer);
+SWHS_API void runner_dosub_pair1_density(struct runner *r, struct cell *ci, struct cell *cj,
+                                         int gettimer);
+SWHS_API void runner_dosub_self1_gradient(struct runner *r, struct cell *ci, int gettimer);
+SWHS_API void runner_dosub_pair1_gradient(struct runner *r, struct cell *ci, struct cell *cj,
+                                          int gettimer);
+SWHS_API void runner_dosub_self2_force(struct runner *r, struct cell *ci, int gettimer);
+SWHS_API void runner_dosub_pair2_force(struct runner *r, struct cell *ci, struct cell *cj,
+                                       int gettimer);
+SWHS_API void runner_dosub_subset_density(struct runner *r, struct cell *ci,
+                                          struct part *parts, int *ind, int count,
+                                          struct cell *cj, int gettimer);
 SWHS_API void runner_doself_grav_pp(struct runner *r, struct cell *c);
 SWHS_API void runner_dopair_grav_pp(struct runner *r, struct cell *ci, struct cell *cj,
                                     const int symmetric, const int allow_mpole);

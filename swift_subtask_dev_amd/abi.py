@@ -263,6 +263,7 @@ class CellHydro(C.Structure):
                 ("count", C.c_int), ("h_max", C.c_float), ("h_max_old", C.c_float),
                 ("h_max_active", C.c_float), ("dx_max_part", C.c_float),
                 ("dx_max_sort", C.c_float), ("dx_max_sort_old", C.c_float),
+                ("dx_max_part_old", C.c_float),
                 ("sorted", C.c_uint16), ("ti_end_min", C.c_longlong),
                 ("ti_old_part", C.c_longlong)]
 

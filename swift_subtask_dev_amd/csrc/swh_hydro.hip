@@ -64,6 +64,12 @@ __global__ void list_prep_kernel(const unsigned int* hmax_bits, float gs1, unsig
   }
 }
 
+__global__ void posf_kernel(GridDev g, const double4* __restrict__ pos, int64_t n,
+                            float4* __restrict__ posf) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) posf[i] = cell_local(g, pos[i]);
+}
+
 __global__ __launch_bounds__(64) void list_build_kernel(GridDev g, SoA a, ListDev ld,
                                                        const int2* __restrict__ groups,
                                                        int ngroups, int max_active_bin,
@@ -494,6 +500,8 @@ static ListDev list_dev(swh_space* s) {
   d.skin1 = 1.f + s->tuning.list_skin;
   d.rwrap_bits = rwrap_slot(s);
   d.ovf = s->nbr_ovf.as<int>();
+  d.posf = s->posf.as<const float4>();
+  d.diag = s->tuning.diag_mode;
   d.ovf_n = ovf_slot(s);
   return d;
 }
@@ -502,12 +510,19 @@ static ListDev list_dev(swh_space* s) {
 static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool count) {
   const int K = s->tuning.list_capacity > 0 ? s->tuning.list_capacity : 128;
   SWH_TRY(s->nbr.reserve((size_t)std::max(1, s->ngroups) * K * kListSlots * sizeof(int)));
+  if (K % 4 != 0) {
+    set_error("list_capacity must be a multiple of 4");
+    return SWH_ERR_ARG;
+  }
   SWH_TRY(s->nbr_cnt.reserve((size_t)s->n * sizeof(int)));
   SWH_TRY(s->nbr_base.reserve((size_t)s->n * sizeof(int)));
   SWH_TRY(s->nbr_reach.reserve((size_t)s->n * sizeof(float)));
   SWH_TRY(s->nbr_ovf.reserve((size_t)s->n * sizeof(int)));
+  SWH_TRY(s->posf.reserve((size_t)s->n * sizeof(float4)));
   s->list_K = K;
   const ListDev ld = list_dev(s);
+  hipLaunchKernelGGL(posf_kernel, dim3((int)((s->n + 255) / 256)), dim3(256), 0, s->stream,
+                     grid_dev(s), s->pos.as<const double4>(), s->n, s->posf.as<float4>());
   hipLaunchKernelGGL(list_prep_kernel, dim3(1), dim3(64), 0, s->stream, hmax_slot(s),
                      kGamma * ld.skin1, rwrap_slot(s), ovf_slot(s));
   hipLaunchKernelGGL(list_build_kernel, dim3(s->ngroups), dim3(64), 0, s->stream, grid_dev(s),
@@ -575,7 +590,7 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const int
     // while no particle's H has outgrown its list reach (ghost: stale flag)
     if (LOOP == LOOP_DENSITY || !s->list_valid || s->list_mab != P->max_active_bin)
       SWH_TRY(build_lists(s, P, count));
-    if (s->tuning.diag_mode == 1) return SWH_OK;
+    if (s->tuning.diag_mode != 0) return SWH_OK;
   }
   const GridDev gd = grid_dev(s);
   const double a2H = P->a * P->a * P->H;

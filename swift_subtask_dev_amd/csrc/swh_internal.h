@@ -182,6 +182,7 @@ struct swh_space {
   // the step's pair lists (swh_list.h): valid from a density loop until the
   // next upload / rebuild / tuning change, or a ghost that grows an H past its R
   swh::DevBuf nbr, nbr_cnt, nbr_base, nbr_reach, nbr_ovf;
+  swh::DevBuf posf;  // float4: position relative to its grid cell's corner, h
   bool list_valid = false;
   int32_t list_mab = 0, list_K = 0;
   int64_t list_entries = 0;   // last counted build: total entries

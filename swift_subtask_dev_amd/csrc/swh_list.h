@@ -8,9 +8,10 @@
 //
 //   list build (list_build): one wave per i-group (an octree leaf of <= 16
 //     particles, swh_space.hip group_kernel), four lanes per i. The wave
-//     stages the candidates of the cells around its group (fp32 coordinates
-//     relative to the group centre, pruned by the exact box distance, as
-//     swh_tile5.h), tests every (i, candidate) in fp32 against
+//     stages the candidates of the cells around its group (four cells per
+//     pass, 16 lanes per cell; fp32 coordinates relative to the group centre
+//     from the cell-local fp32 copy of the positions, pruned by the exact box
+//     distance), tests every (i, candidate) in fp32 against
 //       r < max(R_i, R_j),  R = gamma h (1 + skin)
 //     with the threshold inflated by the worst-case rounding bound, and
 //     appends the hits to i's list. The list is a superset of every pair
@@ -26,11 +27,11 @@
 //     particle loads one entry ahead. The LPI partial sums are combined at
 //     the end. The accepted pair set is exactly the f64 oracle's.
 //
-// Layout: entry k of particle i (slot `sl` of group `gr`) lives at
-// nbr[(gr * K + k) * kListSlots + sl]: the lists of one group are
-// interleaved, so the lanes of a group read one 64-byte segment per entry
-// index. Particles with more than K hits (cnt > K) are walked by the
-// per-particle search (gather_direct) instead.
+// Layout: the lists of one i-group (16 slots) form a block of 16 K entries;
+// entry k of slot sl sits at row k/4, column 4 sl + k%4 of the block's
+// 64-entry rows. The four lanes of an i read one 16-byte segment per row and
+// a wave reads whole 256-byte rows. Particles with more than K hits
+// (cnt > K) are walked by the per-particle search (gather_direct) instead.
 #pragma once
 
 #include "swh_tile5.h"
@@ -40,31 +41,59 @@ namespace swh {
 constexpr int kListSlots = 16;   // list columns per i-group (max group size)
 constexpr int kListLpiBuild = 4;  // lanes per i in the list build
 
+// First entry of a listed particle (`base` = group * kListSlots + slot) and
+// the offset of its entry k (module layout comment).
+__device__ __forceinline__ size_t list_col(int base, int K) {
+  return (size_t)(base >> 4) * (size_t)(kListSlots * K) + (size_t)((base & 15) * 4);
+}
+__device__ __forceinline__ size_t list_off(int k) { return (size_t)((k >> 2) * 64 + (k & 3)); }
+
 struct ListDev {
   int* nbr;      // entries: sorted j indices
   int* cnt;      // per particle: entries found (> K: overflow, searched instead)
-  int* base;     // per particle: (group * K) * kListSlots + slot
+  int* base;     // per particle: group * kListSlots + slot (-1: not listed)
   float* reach;  // per particle: R = gamma h (1 + skin) at build (0: not listed)
+  const float4* posf;  // per particle: x, y, z relative to its grid cell's corner, h
   int K;
   float skin1;   // 1 + skin
   const unsigned int* rwrap_bits;  // max R at build (float bits): particles farther than
                                    // this from every face need no periodic wrap
   int* ovf;      // overflow particles, count in *ovf_n
   unsigned int* ovf_n;
+  int diag;      // profiling only: 2 = the build writes no entries
 };
 
 template <int LPI>
 struct ListLds {
   static constexpr int GS = 64 / LPI;
-  static constexpr int kICap = 128;          // LDS hits per i before a flush
+  static constexpr int kICap = 96;           // LDS hits per i before a flush
   static constexpr int kStride = kICap + 2;  // odd dword stride: lists start on different banks
   float4 cand[kT5Region];  // x, y, z relative to the box centre; w = inflated R_j^2
   int candj[kT5Region];
-  int cell_j0[64];
-  int cell_pre[64];
-  unsigned char cell_code[64];
   unsigned short hits[GS * kStride + 64];  // [i slot][entry] region slots; + per-lane dummies
+  int cell_pre[64];     // staging batch: prefix sum of the cells' counts
+  int cell_j0[64];      // first sorted index of the cell minus its prefix
+  float4 cell_off[64];  // cell corner relative to the group centre (fp32)
 };
+
+#ifndef SWH_STAGE_U
+#define SWH_STAGE_U 4
+#endif
+constexpr int kStageU = SWH_STAGE_U;  // candidates per lane per staging pass
+
+// Positions relative to the lower corner of each particle's grid cell, in
+// fp32, with h: the list build's staging loads 16 B per candidate and turns
+// it into group-relative coordinates with three fp32 adds.
+__device__ __forceinline__ float4 cell_local(const GridDev& g, const double4& p) {
+  const double xs[3] = {p.x, p.y, p.z};
+  float l[3];
+  for (int k = 0; k < 3; k++) {
+    int ck = (int)floor((xs[k] - g.origin[k]) * g.inv_w[k]);  // key_kernel's binning
+    ck = ck < 0 ? 0 : (ck >= g.cdim[k] ? g.cdim[k] - 1 : ck);
+    l[k] = (float)(xs[k] - (g.origin[k] + ck * g.w[k]));
+  }
+  return make_float4(l[0], l[1], l[2], (float)p.w);
+}
 
 // Copy i's pending LDS hits to its global list (the LPI lanes of i split them).
 template <int LPI, class LDS>
@@ -74,9 +103,12 @@ __device__ __forceinline__ void list_flush(const ListDev& ld, LDS& L, int& nq, i
   const int nmax = uni_i(wave_max_i(nq));
   ts.bsteps += (unsigned int)((nmax + LPI - 1) / LPI);
   const unsigned short* list = &L.hits[il * LDS::kStride];
-  for (int t = s; t < nq; t += LPI) {
-    const int k = wr + t;
-    if (k < ld.K) ld.nbr[(size_t)(gbase + k) * kListSlots + il] = L.candj[list[t]];
+  int* col = ld.nbr + list_col(gbase + il, ld.K);
+  if (ld.diag != 2) {
+    for (int t = s; t < nq; t += LPI) {
+      const int k = wr + t;
+      if (k < ld.K) col[list_off(k)] = L.candj[list[t]];
+    }
   }
   wr += nq;
   nq = 0;
@@ -161,7 +193,7 @@ __device__ __forceinline__ void list_build(const GridDev& g, const SoA& a, const
   hi[1] = uni_d(wave_max_d(act ? pi.y : -1e300));
   hi[2] = uni_d(wave_max_d(act ? pi.z : -1e300));
   TileStats ts;
-  const int gbase = gid * ld.K;
+  const int gbase = gid * kListSlots;
   int nq = 0, wr = 0;
   if (Rg > 0.) {
     const double Rmax = (double)__uint_as_float(*hmax_bits) * (double)kGamma * skin1;
@@ -190,9 +222,13 @@ __device__ __forceinline__ void list_build(const GridDev& g, const SoA& a, const
     }
     const int nx = c.hi[0] - c.lo[0] + 1;
     const int ny = c.hi[1] - c.lo[1] + 1;
-    const int ncells = nx * ny * (c.hi[2] - c.lo[2] + 1);
-    // rounding bound of the fp32 relative coordinates (swh_tile4.h)
-    const double delta = 16. * kUnitRound * sqrt(D2);
+    const int nxy = nx * ny;
+    const int ncells = nxy * (c.hi[2] - c.lo[2] + 1);
+    // Rounding bound of the fp32 relative coordinates: a candidate is staged
+    // as fl(local) + fl(cell offset) with |local| <= w, |offset| <= D + w and
+    // |sum| <= D (swh_tile4.h's argument with 2(D + w) in place of D).
+    const double wmax = fmax(g.w[0], fmax(g.w[1], g.w[2]));
+    const double delta = 16. * kUnitRound * (sqrt(D2) + wmax);
     const float deltaf = uni_f((float)delta);
     const float xi = (float)(pi.x - ctr[0]);
     const float yi = (float)(pi.y - ctr[1]);
@@ -203,21 +239,36 @@ __device__ __forceinline__ void list_build(const GridDev& g, const SoA& a, const
     const float Rgf = uni_f((float)(Rg + delta));
     const float gs1 = (float)((double)kGamma * skin1);
     const bool wrap = c.full[0] || c.full[1] || c.full[2];
+    const float bx = (float)g.dim[0], by = (float)g.dim[1], bz = (float)g.dim[2];
+    const float inv_nx = 1.f / (float)nx, inv_nxy = 1.f / (float)nxy;
+    // Staging, in batches of up to 64 cells (one lane per cell: its sorted
+    // range and the offset of its lower corner from the group centre go to
+    // LDS with a prefix sum of the counts). Candidates are then streamed
+    // kStageU per lane per pass: each lane finds the cell of its candidate by
+    // a binary search over the prefix sums and issues its 16-byte cell-local
+    // position load; the kStageU searches and loads are independent, so a
+    // lane keeps kStageU loads in flight.
     int nst = 0;
     for (int cb = 0; cb < ncells; cb += 64) {
-      // batch of 64 cells, one per lane
-      int cnt = 0, j0 = 0, code = 0;
+      int cnt = 0, j0 = 0;
+      float ox = 0.f, oy = 0.f, oz = 0.f;
       const int cl = cb + lane;
       if (cl < ncells) {
+        const int iz = (int)(((float)cl + 0.5f) * inv_nxy);
+        const int rxy = cl - iz * nxy;
+        const int iy = (int)(((float)rxy + 0.5f) * inv_nx);
+        const int ix = rxy - iy * nx;
         double sx, sy, sz;
-        const int wx = wrap_cell(g, c, 0, c.lo[0] + cl % nx, sx);
-        const int wy = wrap_cell(g, c, 1, c.lo[1] + (cl / nx) % ny, sy);
-        const int wz = wrap_cell(g, c, 2, c.lo[2] + cl / (nx * ny), sz);
-        code = (sx < 0. ? 1 : (sx > 0. ? 2 : 0)) | ((sy < 0. ? 1 : (sy > 0. ? 2 : 0)) << 2) |
-               ((sz < 0. ? 1 : (sz > 0. ? 2 : 0)) << 4);
+        const int wx = wrap_cell(g, c, 0, c.lo[0] + ix, sx);
+        const int wy = wrap_cell(g, c, 1, c.lo[1] + iy, sy);
+        const int wz = wrap_cell(g, c, 2, c.lo[2] + iz, sz);
         const int2 sp = cell_range_of(g, wx, wy, wz);
         j0 = sp.x;
         cnt = sp.y - sp.x;
+        // lower corner of this image of the cell, relative to the group centre
+        ox = (float)(g.origin[0] + wx * g.w[0] + sx - ctr[0]);
+        oy = (float)(g.origin[1] + wy * g.w[1] + sy - ctr[1]);
+        oz = (float)(g.origin[2] + wz * g.w[2] + sz - ctr[2]);
       }
       int inc = cnt;
       for (int o = 1; o < 64; o <<= 1) {
@@ -226,51 +277,12 @@ __device__ __forceinline__ void list_build(const GridDev& g, const SoA& a, const
       }
       const int total = uni_i(__shfl(inc, 63));
       wave_sync();
-      L.cell_j0[lane] = j0;
-      L.cell_pre[lane] = inc - cnt;
-      L.cell_code[lane] = (unsigned char)code;
+      L.cell_pre[lane] = inc - cnt;  // cells past ncells: pre = total (never found)
+      L.cell_j0[lane] = j0 - (inc - cnt);
+      L.cell_off[lane] = make_float4(ox, oy, oz, 0.f);
       wave_sync();
-      int k = 0;
-      for (int base = 0; base < total; base += 64) {
-        const int q = base + lane;
-        const bool val = q < total;
-        int jj = 0, sc = 0;
-        if (val) {
-          while (k + 1 < 64 && L.cell_pre[k + 1] <= q) k++;
-          jj = L.cell_j0[k] + (q - L.cell_pre[k]);
-          sc = L.cell_code[k];
-        }
-        bool keep = false;
-        float4 cf = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (val) {
-          const double4 p = a.pos[jj];
-          double rx = p.x + shift_of(sc & 3, g.dim[0]) - ctr[0];
-          double ry = p.y + shift_of((sc >> 2) & 3, g.dim[1]) - ctr[1];
-          double rz = p.z + shift_of((sc >> 4) & 3, g.dim[2]) - ctr[2];
-          if (c.full[0]) rx = wrap_nearest(rx, g.dim[0]);
-          if (c.full[1]) ry = wrap_nearest(ry, g.dim[1]);
-          if (c.full[2]) rz = wrap_nearest(rz, g.dim[2]);
-          cf.x = (float)rx;
-          cf.y = (float)ry;
-          cf.z = (float)rz;
-          const float ex = c.full[0] ? 0.f : fmaxf(fabsf(cf.x) - hxf, 0.f);
-          const float ey = c.full[1] ? 0.f : fmaxf(fabsf(cf.y) - hyf, 0.f);
-          const float ez = c.full[2] ? 0.f : fmaxf(fabsf(cf.z) - hzf, 0.f);
-          const float Rj = (float)p.w * gs1 + deltaf;
-          cf.w = Rj * Rj * kThrSlack;
-          const float rj = fmaxf(Rgf, Rj);
-          keep = ex * ex + ey * ey + ez * ez <= rj * rj * kThrSlack;
-        }
-        const unsigned long long m = __ballot(keep);
-        if (keep) {
-          const int slot = nst + __popcll(m & ((1ull << lane) - 1ull));
-          L.cand[slot] = cf;
-          L.candj[slot] = jj;
-        }
-        nst += __popcll(m);
-        ts.loaded += val ? 1u : 0u;
-        ts.staged += keep ? 1u : 0u;
-        if (nst > kT5Region - 64) {  // region full: consume it
+      for (int base = 0; base < total; base += 64 * kStageU) {
+        if (nst > kT5Region - 64 * kStageU) {  // no room for this pass: consume the region
           wave_sync();
           if (diag != 1) {
             if (wrap)
@@ -283,7 +295,56 @@ __device__ __forceinline__ void list_build(const GridDev& g, const SoA& a, const
           nst = 0;
           wave_sync();
         }
+        int jj[kStageU];
+        float4 q[kStageU];
+        float4 off[kStageU];
+        bool val[kStageU];
+#pragma unroll
+        for (int u = 0; u < kStageU; u++) {
+          const int qq = base + 64 * u + lane;
+          val[u] = qq < total;
+          // largest cell k with pre[k] <= qq (pre is non-decreasing, pre[0] = 0)
+          int k = 0;
+#pragma unroll
+          for (int st = 32; st > 0; st >>= 1)
+            if (L.cell_pre[k + st] <= qq) k += st;
+          jj[u] = val[u] ? L.cell_j0[k] + qq : 0;
+          off[u] = L.cell_off[k];
+        }
+#pragma unroll
+        for (int u = 0; u < kStageU; u++)
+          q[u] = val[u] ? ld.posf[jj[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < kStageU; u++) {
+          bool keep = false;
+          float4 cf = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (val[u]) {
+            cf.x = q[u].x + off[u].x;  // x, y, z relative to its cell's corner; h
+            cf.y = q[u].y + off[u].y;
+            cf.z = q[u].z + off[u].z;
+            if (c.full[0]) cf.x = wrap_nearest_f(cf.x, bx);
+            if (c.full[1]) cf.y = wrap_nearest_f(cf.y, by);
+            if (c.full[2]) cf.z = wrap_nearest_f(cf.z, bz);
+            const float ex = c.full[0] ? 0.f : fmaxf(fabsf(cf.x) - hxf, 0.f);
+            const float ey = c.full[1] ? 0.f : fmaxf(fabsf(cf.y) - hyf, 0.f);
+            const float ez = c.full[2] ? 0.f : fmaxf(fabsf(cf.z) - hzf, 0.f);
+            const float Rj = q[u].w * gs1 + deltaf;
+            cf.w = Rj * Rj * kThrSlack;
+            const float rj = fmaxf(Rgf, Rj);
+            keep = ex * ex + ey * ey + ez * ez <= rj * rj * kThrSlack;
+          }
+          const unsigned long long m = __ballot(keep);
+          if (keep) {
+            const int slot = nst + __popcll(m & ((1ull << lane) - 1ull));
+            L.cand[slot] = cf;
+            L.candj[slot] = jj[u];
+          }
+          nst += __popcll(m);
+          ts.loaded += val[u] ? 1u : 0u;
+          ts.staged += keep ? 1u : 0u;
+        }
       }
+      wave_sync();  // the next batch rewrites the cell table
     }
     wave_sync();
     if (diag != 1 && nst > 0) {
@@ -297,7 +358,7 @@ __device__ __forceinline__ void list_build(const GridDev& g, const SoA& a, const
   }
   if (i >= 0 && s == 0) {
     ld.cnt[i] = act ? wr : 0;
-    ld.base[i] = act ? gbase * kListSlots + il : -1;
+    ld.base[i] = act ? gbase + il : -1;
     ld.reach[i] = act ? (float)Ri : 0.f;
     if (act && wr > ld.K) ld.ovf[atomicAdd(ld.ovf_n, 1u)] = i;
   }
@@ -325,30 +386,50 @@ __device__ __forceinline__ bool near_face(const GridDev& g, const double4& p, do
          (p.z > g.dim[2] - R);
 }
 
-// Walk entries s, s+LPI, ... of i's list (nl entries from column lb).
+// Walk entries s, s+LPI, ... of i's list (nl entries from list base lb):
+// indices are loaded four entries ahead, the particle data of the next entry
+// before this entry's math, so each lane keeps several independent loads in
+// flight (the list itself streams from HBM).
 template <int LPI, bool WRAP, typename T, class S>
 __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, const ListDev& ld,
                                              const double4& pi, int nl, int lb, int s, S& st) {
-  const int* __restrict__ col = ld.nbr + lb;
-  int k = s;
-  int jn = k < nl ? col[(size_t)k * kListSlots] : -1;
-  int jn2 = k + LPI < nl ? col[(size_t)(k + LPI) * kListSlots] : -1;
-  double4 pn = make_double4(0., 0., 0., 0.);
-  JRec<S::kPay> rn{};
-  if (jn >= 0) {
-    pn = a.pos[jn];
-    rn = S::load_j(a, jn);
-  }
-  for (; k < nl; k += LPI) {
-    const int j = jn;
-    const double4 pj = pn;
-    const JRec<S::kPay> rj = rn;
-    jn = jn2;  // issue the next entries' loads before this entry's math
-    jn2 = k + 2 * LPI < nl ? col[(size_t)(k + 2 * LPI) * kListSlots] : -1;
+  const int* __restrict__ col = ld.nbr + (nl > 0 ? list_col(lb, ld.K) : 0);
+  const int nme = nl > s ? (nl - s + LPI - 1) / LPI : 0;  // this lane's entries
+  auto idx = [&](int m) { return m < nme ? col[list_off(s + m * LPI)] : -1; };
+  if constexpr (S::kPay > 1) {
+    // heavy j records (gradient, force): index two entries ahead, data one
+    // ahead; the register budget of the wide records allows no more
+    int k = 0;
+    int jn = idx(0), jn2 = idx(1);
+    double4 pn = make_double4(0., 0., 0., 0.);
+    JRec<S::kPay> rn{};
     if (jn >= 0) {
       pn = a.pos[jn];
       rn = S::load_j(a, jn);
     }
+    for (; k < nme; k++) {
+      const int j = jn;
+      const double4 pj = pn;
+      const JRec<S::kPay> rj = rn;
+      jn = jn2;
+      jn2 = idx(k + 2);
+      if (jn >= 0) {
+        pn = a.pos[jn];
+        rn = S::load_j(a, jn);
+      }
+      double dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
+      if (WRAP) {
+        dx = wrap_nearest(dx, g.dim[0]);
+        dy = wrap_nearest(dy, g.dim[1]);
+        dz = wrap_nearest(dz, g.dim[2]);
+      }
+      const T tdx = (T)dx, tdy = (T)dy, tdz = (T)dz;
+      const T r2 = tdx * tdx + tdy * tdy + tdz * tdz;
+      if (st.accept(j, pj, r2)) st.interact_staged(rj.p, rj.meta, pj, tdx, tdy, tdz, r2);
+    }
+    return;
+  }
+  auto step = [&](int j, const double4& pj, const JRec<S::kPay>& rj) {
     double dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
     if (WRAP) {
       dx = wrap_nearest(dx, g.dim[0]);
@@ -358,7 +439,40 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
     const T tdx = (T)dx, tdy = (T)dy, tdz = (T)dz;
     const T r2 = tdx * tdx + tdy * tdy + tdz * tdz;
     if (st.accept(j, pj, r2)) st.interact_staged(rj.p, rj.meta, pj, tdx, tdy, tdz, r2);
+  };
+  int j0 = idx(0), j1 = idx(1), j2 = idx(2), j3 = idx(3);
+  double4 pc = make_double4(0., 0., 0., 0.);
+  JRec<S::kPay> rc{};
+  if (j0 >= 0) {
+    pc = a.pos[j0];
+    rc = S::load_j(a, j0);
   }
+  // one entry: compute j (data pc/rc) after issuing the loads of jn and the
+  // index four entries ahead
+#define SWH_WALK_STEP(J, JN, M)                   \
+  {                                              \
+    double4 pn = make_double4(0., 0., 0., 0.);   \
+    JRec<S::kPay> rn{};                          \
+    if (JN >= 0) {                               \
+      pn = a.pos[JN];                            \
+      rn = S::load_j(a, JN);                     \
+    }                                            \
+    const int jc = J;                            \
+    J = idx(M + 4);                              \
+    step(jc, pc, rc);                            \
+    pc = pn;                                     \
+    rc = rn;                                     \
+  }
+  for (int m = 0; m < nme; m += 4) {
+    SWH_WALK_STEP(j0, j1, m)
+    if (m + 1 >= nme) break;
+    SWH_WALK_STEP(j1, j2, m + 1)
+    if (m + 2 >= nme) break;
+    SWH_WALK_STEP(j2, j3, m + 2)
+    if (m + 3 >= nme) break;
+    SWH_WALK_STEP(j3, j0, m + 3)
+  }
+#undef SWH_WALK_STEP
 }
 
 // One loop over every active, listed particle: LPI lanes per i, 256/LPI

@@ -462,7 +462,7 @@ swh_status swh_space_destroy(swh_space* s) {
                     &s->seg_off, &s->keys, &s->keys2, &s->idx, &s->idx2, &s->sort_tmp,
                     &s->scan_tmp, &s->counters, &s->tmp_soa, &s->ghost_left,
                     &s->ghost_right, &s->ghost_list, &s->ghost_list2, &s->ghost_flag,
-                    &s->nbr, &s->nbr_cnt, &s->nbr_base, &s->nbr_reach, &s->nbr_ovf};
+                    &s->nbr, &s->nbr_cnt, &s->nbr_base, &s->nbr_reach, &s->nbr_ovf, &s->posf};
   for (DevBuf* b : bufs) b->release();
   s->hstage.release();
   if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
@@ -492,7 +492,8 @@ swh_status swh_space_set_tuning(swh_space* s, const swh_tuning* t) {
       (t->group_size != 0 && t->group_size != 16 && t->group_size != 32 && t->group_size != 64) ||
       (lists && t->group_size > 16) || t->cell_scale < 0.f || t->cell_scale > 4.f ||
       t->diag_mode < 0 || t->diag_mode > 2 || t->list_capacity < 0 ||
-      t->list_capacity > 4096 || !(t->list_skin >= 0.f) || t->list_skin > 1.f)
+      t->list_capacity > 4096 || (t->list_capacity % 4) != 0 || !(t->list_skin >= 0.f) ||
+      t->list_skin > 1.f)
     return SWH_ERR_ARG;
   s->tuning = *t;
   s->built = false;

@@ -10,6 +10,7 @@
  */
 #include <float.h>
 #include <math.h>
+#include <stddef.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -38,12 +39,61 @@ static const int swhs_runner_flip[27] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 
 static const int swhs_sortlistID[27] = {0, 1, 2, 3, 4,  5,  6,  7,  8,  9,  10, 11, 12, 0,
                                         12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0};
 
+/* The record layouts as THIS translation unit sees them: compiled against
+ * SWIFT's headers inside SWIFT, the offsets follow whatever configure built
+ * struct part / struct gpart (debug checks, subgrid fields, ...); the library
+ * never assumes a layout of its own. */
+void swifthip_swift_part_layout(swh_part_layout *o) {
+  o->stride = (int32_t)sizeof(struct part);
+  o->off_id = (int32_t)offsetof(struct part, id);
+  o->off_x = (int32_t)offsetof(struct part, x);
+  o->off_v = (int32_t)offsetof(struct part, v);
+  o->off_a_hydro = (int32_t)offsetof(struct part, a_hydro);
+  o->off_mass = (int32_t)offsetof(struct part, mass);
+  o->off_h = (int32_t)offsetof(struct part, h);
+  o->off_u = (int32_t)offsetof(struct part, u);
+  o->off_u_dt = (int32_t)offsetof(struct part, u_dt);
+  o->off_rho = (int32_t)offsetof(struct part, rho);
+  o->off_div_v = (int32_t)offsetof(struct part, viscosity.div_v);
+  o->off_div_v_dt = (int32_t)offsetof(struct part, viscosity.div_v_dt);
+  o->off_div_v_previous_step = (int32_t)offsetof(struct part, viscosity.div_v_previous_step);
+  o->off_visc_alpha = (int32_t)offsetof(struct part, viscosity.alpha);
+  o->off_v_sig = (int32_t)offsetof(struct part, viscosity.v_sig);
+  o->off_laplace_u = (int32_t)offsetof(struct part, diffusion.laplace_u);
+  o->off_diff_alpha = (int32_t)offsetof(struct part, diffusion.alpha);
+  o->off_wcount = (int32_t)offsetof(struct part, density.wcount);
+  o->off_wcount_dh = (int32_t)offsetof(struct part, density.wcount_dh);
+  o->off_rho_dh = (int32_t)offsetof(struct part, density.rho_dh);
+  o->off_rot_v = (int32_t)offsetof(struct part, density.rot_v);
+  o->off_f = (int32_t)offsetof(struct part, force.f);
+  o->off_pressure = (int32_t)offsetof(struct part, force.pressure);
+  o->off_soundspeed = (int32_t)offsetof(struct part, force.soundspeed);
+  o->off_h_dt = (int32_t)offsetof(struct part, force.h_dt);
+  o->off_balsara = (int32_t)offsetof(struct part, force.balsara);
+  o->off_alpha_visc_max_ngb = (int32_t)offsetof(struct part, force.alpha_visc_max_ngb);
+  o->off_time_bin = (int32_t)offsetof(struct part, time_bin);
+  o->off_min_ngb_time_bin = (int32_t)offsetof(struct part, limiter_data.min_ngb_time_bin);
+}
+
+void swifthip_swift_gpart_layout(swh_gpart_layout *o) {
+  o->stride = (int32_t)sizeof(struct gpart);
+  o->off_x = (int32_t)offsetof(struct gpart, x);
+  o->off_a_grav = (int32_t)offsetof(struct gpart, a_grav);
+  o->off_potential = (int32_t)offsetof(struct gpart, potential);
+  o->off_mass = (int32_t)offsetof(struct gpart, mass);
+  o->off_epsilon = (int32_t)offsetof(struct gpart, epsilon);
+  o->off_time_bin = (int32_t)offsetof(struct gpart, time_bin);
+}
+
+static void split_pairs_init(void);
+
 int swifthip_swift_init(int device, int precision) {
   if (swhs_ctx) return 0;
   if (swh_init(&swhs_ctx, device) != SWH_OK) return -1;
   swh_set_precision(swhs_ctx, precision ? SWH_PRECISION_F32 : SWH_PRECISION_F64);
-  swh_part_layout_sphenix(&swhs_layout);
-  swh_gpart_layout_multisoftening(&swhs_glayout);
+  swifthip_swift_part_layout(&swhs_layout);
+  swifthip_swift_gpart_layout(&swhs_glayout);
+  split_pairs_init();
   return 0;
 }
 
@@ -250,6 +300,196 @@ void runner_dopair_subset_branch_density(struct runner *r, struct cell *ci,
   view_of(cj, e, &vj);
   report(swh_dopair_subset_density(swhs_ctx, &vi, parts_i, ind, count, &vj, shift,
                                    &swhs_layout, &P));
+}
+
+/* ------------------------------------------------------------------------ */
+/* Sub-cell recursion (DOSUB_SELF1/PAIR1/SELF2/PAIR2/SUBSET,                 */
+/* src/runner_doiact_functions_hydro.h:2524-2805): the same descent as the   */
+/* CPU runner, down to the leaf self/pair tasks above.                       */
+/* ------------------------------------------------------------------------ */
+
+/* cell_split_pairs (src/cell.c:62): for the 13 pair directions of
+ * sortlistID (cj relative to ci after space_getsid's flip), the progeny
+ * pairs (pid of ci, pjd of cj) that touch. Progeny k sits at offset
+ * ((k >> 2) & 1, (k >> 1) & 1, k & 1) half-widths (space_split.c:233);
+ * two progeny touch when every component of 2 d + off_j - off_i is in
+ * [-1, 1]. Built at init instead of tabulated. */
+static const int swhs_sid_dir[13][3] = {{1, 1, 1},  {1, 1, 0},  {1, 1, -1}, {1, 0, 1},
+                                        {1, 0, 0},  {1, 0, -1}, {1, -1, 1}, {1, -1, 0},
+                                        {1, -1, -1}, {0, 1, 1}, {0, 1, 0},  {0, 1, -1},
+                                        {0, 0, 1}};
+static int swhs_split_count[13];
+static int swhs_split_pairs[13][16][2];
+
+static void split_pairs_init(void) {
+  for (int sid = 0; sid < 13; sid++) {
+    int n = 0;
+    for (int a = 0; a < 8; a++)
+      for (int b = 0; b < 8; b++) {
+        int ok = 1;
+        for (int k = 0; k < 3; k++) {
+          const int oa = (a >> (2 - k)) & 1, ob = (b >> (2 - k)) & 1;
+          const int d = 2 * swhs_sid_dir[sid][k] + ob - oa;
+          if (d < -1 || d > 1) ok = 0;
+        }
+        if (ok && n < 16) {
+          swhs_split_pairs[sid][n][0] = a;
+          swhs_split_pairs[sid][n][1] = b;
+          n++;
+        }
+      }
+    swhs_split_count[sid] = n;
+  }
+}
+
+/* Number of progeny pairs of sid (tests compare with src/cell.c:62). */
+int swifthip_swift_split_pairs(int sid, int *pairs) {
+  if (sid < 0 || sid > 12) return -1;
+  if (!swhs_split_count[12]) split_pairs_init();
+  for (int k = 0; k < swhs_split_count[sid]; k++) {
+    pairs[2 * k] = swhs_split_pairs[sid][k][0];
+    pairs[2 * k + 1] = swhs_split_pairs[sid][k][1];
+  }
+  return swhs_split_count[sid];
+}
+
+/* src/cell.h:761-782 */
+static int cell_can_recurse_in_pair_hydro_task(const struct cell *c) {
+  return c->split &&
+         ((kernel_gamma * c->hydro.h_max_old + c->hydro.dx_max_part_old) < 0.5f * c->dmin);
+}
+static int cell_can_recurse_in_self_hydro_task(const struct cell *c) {
+  return c->split && (kernel_gamma * c->hydro.h_max_old < 0.5f * c->dmin);
+}
+
+/* DOSUB_PAIR1 (loop 0, 1) / DOSUB_PAIR2 (loop 2) */
+static void dosub_pair(struct runner *r, struct cell *ci, struct cell *cj, int loop) {
+  const struct engine *e = r->e;
+  if (!cell_is_active_hydro(ci, e) && !cell_is_active_hydro(cj, e)) return;
+  if (ci->hydro.count == 0 || cj->hydro.count == 0) return;
+  double shift[3];
+  const int sid = space_getsid(e->s, &ci, &cj, shift);
+  if (cell_can_recurse_in_pair_hydro_task(ci) && cell_can_recurse_in_pair_hydro_task(cj)) {
+    for (int k = 0; k < swhs_split_count[sid]; k++) {
+      struct cell *pi = ci->progeny[swhs_split_pairs[sid][k][0]];
+      struct cell *pj = cj->progeny[swhs_split_pairs[sid][k][1]];
+      if (pi != NULL && pj != NULL) {
+        dosub_pair(r, pi, pj, loop);
+        if (swhs_err[0]) return;
+      }
+    }
+  } else if (cell_is_active_hydro(ci, e) || cell_is_active_hydro(cj, e)) {
+    /* the branch re-derives sid/shift and checks drift + sort state */
+    pair_branch(r, ci, cj, loop);
+  }
+}
+
+/* DOSUB_SELF1 / DOSUB_SELF2 */
+static void dosub_self(struct runner *r, struct cell *ci, int loop) {
+  if (ci->hydro.count == 0 || !cell_is_active_hydro(ci, r->e)) return;
+  if (cell_can_recurse_in_self_hydro_task(ci)) {
+    for (int k = 0; k < 8; k++)
+      if (ci->progeny[k] != NULL) {
+        dosub_self(r, ci->progeny[k], loop);
+        if (swhs_err[0]) return;
+        for (int j = k + 1; j < 8; j++)
+          if (ci->progeny[j] != NULL) {
+            dosub_pair(r, ci->progeny[k], ci->progeny[j], loop);
+            if (swhs_err[0]) return;
+          }
+      }
+  } else {
+    if (loop != 2 && !cell_are_part_drifted(ci, r->e))
+      SWH_ADAPTER_ERROR("Interacting undrifted cell.");
+    self_branch(r, ci, loop);
+  }
+}
+
+void runner_dosub_self1_density(struct runner *r, struct cell *ci, int gettimer) {
+  (void)gettimer;
+  if (!swhs_ctx) SWH_ADAPTER_ERROR("swifthip_swift_init() was not called");
+  dosub_self(r, ci, 0);
+}
+void runner_dosub_pair1_density(struct runner *r, struct cell *ci, struct cell *cj,
+                                int gettimer) {
+  (void)gettimer;
+  if (!swhs_ctx) SWH_ADAPTER_ERROR("swifthip_swift_init() was not called");
+  dosub_pair(r, ci, cj, 0);
+}
+void runner_dosub_self1_gradient(struct runner *r, struct cell *ci, int gettimer) {
+  (void)gettimer;
+  if (!swhs_ctx) SWH_ADAPTER_ERROR("swifthip_swift_init() was not called");
+  dosub_self(r, ci, 1);
+}
+void runner_dosub_pair1_gradient(struct runner *r, struct cell *ci, struct cell *cj,
+                                 int gettimer) {
+  (void)gettimer;
+  if (!swhs_ctx) SWH_ADAPTER_ERROR("swifthip_swift_init() was not called");
+  dosub_pair(r, ci, cj, 1);
+}
+void runner_dosub_self2_force(struct runner *r, struct cell *ci, int gettimer) {
+  (void)gettimer;
+  if (!swhs_ctx) SWH_ADAPTER_ERROR("swifthip_swift_init() was not called");
+  dosub_self(r, ci, 2);
+}
+void runner_dosub_pair2_force(struct runner *r, struct cell *ci, struct cell *cj,
+                              int gettimer) {
+  (void)gettimer;
+  if (!swhs_ctx) SWH_ADAPTER_ERROR("swifthip_swift_init() was not called");
+  dosub_pair(r, ci, cj, 2);
+}
+
+/* DOSUB_SUBSET (runner_doiact_functions_hydro.h:2721-2805): density of the
+ * particles parts[ind[0..count)] (all inside one progeny `sub` of ci) against
+ * ci itself (cj == NULL) or cj, descending while the cells can recurse. */
+void runner_dosub_subset_density(struct runner *r, struct cell *ci, struct part *parts,
+                                 int *ind, int count, struct cell *cj, int gettimer) {
+  const struct engine *e = r->e;
+  (void)gettimer;
+  if (!swhs_ctx) SWH_ADAPTER_ERROR("swifthip_swift_init() was not called");
+  if (!cell_is_active_hydro(ci, e) && (cj == NULL || !cell_is_active_hydro(cj, e))) return;
+  if (ci->hydro.count == 0 || (cj != NULL && cj->hydro.count == 0)) return;
+  /* the progeny of ci holding the subset */
+  struct cell *sub = NULL;
+  if (ci->split) {
+    for (int k = 0; k < 8; k++) {
+      struct cell *p = ci->progeny[k];
+      if (p != NULL && &parts[ind[0]] >= &p->hydro.parts[0] &&
+          &parts[ind[0]] < &p->hydro.parts[p->hydro.count]) {
+        sub = p;
+        break;
+      }
+    }
+  }
+  if (cj == NULL) {
+    if (cell_can_recurse_in_self_hydro_task(ci)) {
+      runner_dosub_subset_density(r, sub, parts, ind, count, NULL, 0);
+      for (int j = 0; j < 8; j++)
+        if (ci->progeny[j] != sub && ci->progeny[j] != NULL) {
+          if (swhs_err[0]) return;
+          runner_dosub_subset_density(r, sub, parts, ind, count, ci->progeny[j], 0);
+        }
+    } else {
+      runner_doself_subset_branch_density(r, ci, parts, ind, count);
+    }
+  } else {
+    if (cell_can_recurse_in_pair_hydro_task(ci) && cell_can_recurse_in_pair_hydro_task(cj)) {
+      double shift[3] = {0.0, 0.0, 0.0};
+      const int sid = space_getsid(e->s, &ci, &cj, shift);
+      for (int k = 0; k < swhs_split_count[sid]; k++) {
+        struct cell *pi = ci->progeny[swhs_split_pairs[sid][k][0]];
+        struct cell *pj = cj->progeny[swhs_split_pairs[sid][k][1]];
+        if (swhs_err[0]) return;
+        if (pi == sub && pj != NULL)
+          runner_dosub_subset_density(r, pi, parts, ind, count, pj, 0);
+        if (pi != NULL && pj == sub)
+          runner_dosub_subset_density(r, pj, parts, ind, count, pi, 0);
+      }
+    } else if (cell_is_active_hydro(ci, e) || cell_is_active_hydro(cj, e)) {
+      if (!cell_are_part_drifted(cj, e)) SWH_ADAPTER_ERROR("Cell should be drifted!");
+      runner_dopair_subset_branch_density(r, ci, parts, ind, count, cj);
+    }
+  }
 }
 
 static void grav_params_of(const struct engine *e, swh_grav_params *G) {

@@ -49,6 +49,10 @@ ADAPTER_SYMBOLS = [
     "runner_dopair1_branch_gradient", "runner_doself2_branch_force",
     "runner_dopair2_branch_force", "runner_doself_subset_branch_density",
     "runner_dopair_subset_branch_density", "runner_doself_grav_pp", "runner_dopair_grav_pp",
+    "runner_dosub_self1_density", "runner_dosub_pair1_density", "runner_dosub_self1_gradient",
+    "runner_dosub_pair1_gradient", "runner_dosub_self2_force", "runner_dosub_pair2_force",
+    "runner_dosub_subset_density", "swifthip_swift_part_layout", "swifthip_swift_gpart_layout",
+    "swifthip_swift_split_pairs",
 ]
 
 

@@ -101,3 +101,21 @@ def test_aligned_parts():
     q = abi.copy_parts(p)
     assert q.tobytes() == p.tobytes()
     assert np.all(q["time_bin"] == 0)
+
+
+def test_adapter_layout_is_its_own_offsetof():
+    """The adapter hands libswifthip the struct part / gpart layout it was
+    compiled against (sizeof / offsetof in swh_swift_adapter.c), not the
+    library's built-in default: here both see include/swift_compat.h, so they
+    must agree field by field."""
+    ad = lib.load_adapter()
+    ad.swifthip_swift_part_layout.argtypes = [C.POINTER(abi.PartLayout)]
+    ad.swifthip_swift_gpart_layout.argtypes = [C.POINTER(abi.GPartLayout)]
+    mine, theirs = abi.PartLayout(), lib.part_layout()
+    ad.swifthip_swift_part_layout(C.byref(mine))
+    for name, _ in abi.PartLayout._fields_:
+        assert getattr(mine, name) == getattr(theirs, name), name
+    gm, gt = abi.GPartLayout(), lib.gpart_layout()
+    ad.swifthip_swift_gpart_layout(C.byref(gm))
+    for name, _ in abi.GPartLayout._fields_:
+        assert getattr(gm, name) == getattr(gt, name), name

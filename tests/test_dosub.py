@@ -1,0 +1,322 @@
+"""Sub-cell recursion entry points (DOSUB_*) through the SWIFT-signature
+adapter, on a split cell tree (src/runner_doiact_functions_hydro.h:2524-2805,
+src/cell.c:62 cell_split_pairs, src/cell.h:761-782 recursion predicates).
+
+The tree: 27 top-level cells of width 1 (8^3 particles each), every one split
+into its 8 progeny (space_split's octant order, src/space_split.c:233), all
+sorted. gamma*h ~ 0.28 < dmin/2, so every top-level pair and self recurses
+once and the leaves do the work; the results must equal the brute-force
+oracle on the top-level cells (test27cells' structure and tolerance files).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import scenarios as S
+from compare import compare_columns, load_tolerance
+from swift_subtask_dev_amd import abi
+
+MAIN = 13
+
+
+class TreeCells:
+    """Top-level cells + their 8 progeny over one particle array (each top
+    cell's particles reordered by octant so every progeny is contiguous)."""
+
+    def __init__(self, parts, bounds, locs, width=1.0, ti=8):
+        half = 0.5 * width
+        for (s, e), loc in zip(bounds, locs):
+            x = parts["x"][s:e]
+            octant = ((x[:, 0] >= loc[0] + half).astype(int) * 4 +
+                      (x[:, 1] >= loc[1] + half).astype(int) * 2 +
+                      (x[:, 2] >= loc[2] + half).astype(int))
+            order = np.argsort(octant, kind="stable")
+            raw = parts.view(np.uint8).reshape(len(parts), parts.itemsize)
+            raw[s:e] = raw[s:e][order]
+        self.parts = parts
+        n = len(bounds)
+        self.top = (abi.Cell * n)()
+        self.prog = (abi.Cell * (8 * n))()
+        isz = parts.itemsize
+        for c, ((s, e), loc) in enumerate(zip(bounds, locs)):
+            x = parts["x"][s:e]
+            octant = ((x[:, 0] >= loc[0] + half).astype(int) * 4 +
+                      (x[:, 1] >= loc[1] + half).astype(int) * 2 +
+                      (x[:, 2] >= loc[2] + half).astype(int))
+            self._fill(self.top[c], parts, s, e, loc, width, ti)
+            self.top[c].split = 1
+            start = s
+            for k in range(8):
+                cnt = int((octant == k).sum())
+                ploc = (loc[0] + half * ((k >> 2) & 1), loc[1] + half * ((k >> 1) & 1),
+                        loc[2] + half * (k & 1))
+                pc = self.prog[8 * c + k]
+                self._fill(pc, parts, start, start + cnt, ploc, half, ti)
+                pc.parent = C.addressof(self.top[c])
+                self.top[c].progeny[k] = C.addressof(pc) if cnt else None
+                start += cnt
+        self.bounds = list(bounds)
+        self._isz = isz
+
+    @staticmethod
+    def _fill(cell, parts, s, e, loc, width, ti):
+        for k in range(3):
+            cell.loc[k] = loc[k]
+            cell.width[k] = width
+        cell.dmin = width
+        cell.hydro.parts = parts.ctypes.data + s * parts.itemsize
+        cell.hydro.count = e - s
+        hmax = float(parts["h"][s:e].max()) if e > s else 0.0
+        cell.hydro.h_max = cell.hydro.h_max_old = cell.hydro.h_max_active = hmax
+        cell.hydro.ti_end_min = ti
+        cell.hydro.ti_old_part = ti
+        cell.grav.ti_end_min = ti
+
+    def all_cells(self):
+        return list(self.top) + list(self.prog)
+
+    def sort_all(self):
+        f = O.fn("f32", "cell_sort")
+        for c in self.all_cells():
+            if c.hydro.count:
+                f(C.addressof(c), 0x1FFF)
+
+    def free_sorts(self):
+        f = O.fn("f32", "cell_free_sorts")
+        for c in self.all_cells():
+            f(C.addressof(c))
+
+
+def brute(parts, bounds, locs, P, loop):
+    b = abi.copy_parts(parts)
+    eb = abi.EngineBundle(dim=(3.0, 3.0, 3.0), periodic=True, params=P,
+                          max_active_bin=P.max_active_bin)
+    cs = O.CellSet(b, bounds, locs, 1.0)
+    pair = O.fn("f32", f"pairs_all_{loop}")
+    slf = O.fn("f32", f"self_all_{loop}")
+    for j in range(len(bounds)):
+        if j != MAIN:
+            pair(C.addressof(eb.runner), cs.ptr(MAIN), cs.ptr(j))
+    slf(C.addressof(eb.runner), cs.ptr(MAIN))
+    return b
+
+
+@pytest.fixture(scope="module")
+def adapter():
+    from swift_subtask_dev_amd import lib
+    ad = lib.load_adapter()
+    assert ad.swifthip_swift_init(0, 0) == 0
+    for n in ("runner_dosub_self1_density", "runner_dosub_self1_gradient",
+              "runner_dosub_self2_force"):
+        getattr(ad, n).argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        getattr(ad, n).restype = None
+    for n in ("runner_dosub_pair1_density", "runner_dosub_pair1_gradient",
+              "runner_dosub_pair2_force"):
+        getattr(ad, n).argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        getattr(ad, n).restype = None
+    ad.runner_dosub_subset_density.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p,
+                                               C.POINTER(C.c_int), C.c_int, C.c_void_p, C.c_int]
+    ad.runner_dosub_subset_density.restype = None
+    yield ad
+
+
+def tree27(seed, vel="random", h_pert=0.0, pert=0.1):
+    parts, bounds, locs = S.cells_grid(3, 8, vel=vel, h_pert=h_pert, pert=pert, seed=seed)
+    return parts, bounds, locs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("vel,h_pert", [("random", 0.0), ("divergent", 1.1), ("rotating", 0.0)])
+def test_dosub_density(adapter, vel, h_pert):
+    """runner_dosub_self1_density + 26 runner_dosub_pair1_density on a split
+    tree == brute force on the top-level cells (tolerance_27_*)."""
+    P = abi.default_hydro_params((3.0, 3.0, 3.0), True)
+    parts, bounds, locs = tree27(5, vel, h_pert)
+    S.zero_density_fields(parts)
+    tree = TreeCells(parts, bounds, locs)
+    tree.sort_all()
+    ref = brute(parts, bounds, locs, P, "density")
+    eb = abi.EngineBundle(dim=(3.0, 3.0, 3.0), periodic=True, params=P)
+    r = C.addressof(eb.runner)
+    adapter.swifthip_swift_clear_error()
+    adapter.runner_dosub_self1_density(r, C.addressof(tree.top[MAIN]), 1)
+    for j in range(27):
+        if j != MAIN:
+            adapter.runner_dosub_pair1_density(r, C.addressof(tree.top[MAIN]),
+                                               C.addressof(tree.top[j]), 1)
+    assert not adapter.swifthip_swift_last_error(), adapter.swifthip_swift_last_error()
+    tree.free_sorts()
+    s, e = bounds[MAIN]
+    mg, mb = abi.copy_parts(parts[s:e]), abi.copy_parts(ref[s:e])
+    S.end_calculation(mg, P)
+    S.end_calculation(mb, P)
+    tol = "tolerance_27_perturbed_h.dat" if h_pert else "tolerance_27_perturbed.dat"
+    names, at, rt, lt = load_tolerance(tol)
+    errs = compare_columns(S.density_columns(mb), S.density_columns(mg), at, rt * 1.5, lt, names)
+    assert not errs, "\n".join(errs)
+
+
+@pytest.mark.gpu
+def test_dosub_force(adapter):
+    """runner_dosub_self2_force + runner_dosub_pair2_force (DOSUB_SELF2 /
+    DOSUB_PAIR2) == brute-force pairs_all_force / self_all_force."""
+    P = abi.default_hydro_params((3.0, 3.0, 3.0), True)
+    parts, bounds, locs = tree27(7, "divergent", 1.2)
+    rng = np.random.Generator(np.random.PCG64(7))
+    n = len(parts)
+    parts["rho"] = rng.uniform(0.8, 1.2, n)
+    parts["u"] = rng.uniform(0.5, 1.5, n)
+    parts["pressure"] = (2.0 / 3.0) * parts["u"] * parts["rho"]
+    parts["soundspeed"] = np.sqrt(5.0 / 3.0 * parts["pressure"] / parts["rho"])
+    parts["f"] = rng.uniform(-0.05, 0.05, n) * parts["mass"]
+    parts["balsara"] = rng.uniform(0, 1, n)
+    parts["visc_alpha"] = rng.uniform(0, 1, n)
+    parts["diff_alpha"] = rng.uniform(0, 0.5, n)
+    parts["a_hydro"] = 0
+    parts["u_dt"] = 0
+    parts["h_dt"] = 0
+    parts["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
+    tree = TreeCells(parts, bounds, locs)
+    tree.sort_all()
+    ref = brute(parts, bounds, locs, P, "force")
+    eb = abi.EngineBundle(dim=(3.0, 3.0, 3.0), periodic=True, params=P)
+    r = C.addressof(eb.runner)
+    adapter.swifthip_swift_clear_error()
+    adapter.runner_dosub_self2_force(r, C.addressof(tree.top[MAIN]), 1)
+    for j in range(27):
+        if j != MAIN:
+            adapter.runner_dosub_pair2_force(r, C.addressof(tree.top[MAIN]),
+                                             C.addressof(tree.top[j]), 1)
+    assert not adapter.swifthip_swift_last_error(), adapter.swifthip_swift_last_error()
+    tree.free_sorts()
+    s, e = bounds[MAIN]
+    cols = lambda p: np.column_stack([p["a_hydro"], p["u_dt"], p["h_dt"]])  # noqa: E731
+    # The leaves write ~60 float partial sums per particle back into struct
+    # part (one per leaf task, as SWIFT's runners do), and these random
+    # (non-smooth) force inputs cancel hard: the float brute force itself is
+    # off by up to ~6e-4 relative here. Hold the GPU to the fp64 oracle on
+    # the same box (rel 1e-4 with a floor of 1e-4 of the column maximum: one
+    # particle's a_z cancels to ~1e-6 of the largest), and to the float brute
+    # force at 2x its tolerance.
+    o = abi.copy_parts(tree.parts)
+    o["a_hydro"] = 0
+    o["u_dt"] = 0
+    o["h_dt"] = 0
+    o["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
+    O.fn("f64", "box_force")(o.ctypes.data, len(o), C.byref(P), None)
+    a, b = cols(parts[s:e]).astype(np.float64), cols(o[s:e]).astype(np.float64)
+    for j in range(a.shape[1]):
+        fl = 1e-4 * np.abs(b[:, j]).max()
+        err = np.abs(a[:, j] - b[:, j]) / np.maximum(np.abs(b[:, j]), fl)
+        assert err.max() < 1e-4, (j, err.max())
+    names = ["a_x", "a_y", "a_z", "du/dt", "h_dt"]
+    errs = compare_columns(cols(ref[s:e]), cols(parts[s:e]), np.full(5, 1e-4), np.full(5, 6e-4),
+                           np.full(5, 1e-4), names)
+    assert not errs, "\n".join(errs)
+    assert np.array_equal(parts["min_ngb_time_bin"][s:e], ref["min_ngb_time_bin"][s:e])
+    assert np.array_equal(parts["min_ngb_time_bin"][s:e], o["min_ngb_time_bin"][s:e])
+
+
+@pytest.mark.gpu
+def test_dosub_gradient_runs_leaf_pairs(adapter):
+    """runner_dosub_{self1,pair1}_gradient recurse to the same leaves as the
+    density variants and update the gradient fields of the main cell only
+    through its active leaves (compared with the per-task leaf calls)."""
+    P = abi.default_hydro_params((3.0, 3.0, 3.0), True)
+    parts, bounds, locs = tree27(9, "divergent", 0.0)
+    rng = np.random.Generator(np.random.PCG64(9))
+    parts["rho"] = rng.uniform(0.8, 1.2, len(parts))
+    parts["u"] = rng.uniform(0.5, 1.5, len(parts))
+    parts["soundspeed"] = rng.uniform(0.5, 1.0, len(parts))
+    parts["visc_alpha"] = rng.uniform(0, 1, len(parts))
+    parts["v_sig"] = 0
+    parts["laplace_u"] = 0
+    parts["alpha_visc_max_ngb"] = 0
+    g = abi.copy_parts(parts)
+    tree = TreeCells(g, bounds, locs)
+    tree.sort_all()
+    eb = abi.EngineBundle(dim=(3.0, 3.0, 3.0), periodic=True, params=P)
+    r = C.addressof(eb.runner)
+    adapter.swifthip_swift_clear_error()
+    adapter.runner_dosub_self1_gradient(r, C.addressof(tree.top[MAIN]), 1)
+    for j in range(27):
+        if j != MAIN:
+            adapter.runner_dosub_pair1_gradient(r, C.addressof(tree.top[MAIN]),
+                                                C.addressof(tree.top[j]), 1)
+    assert not adapter.swifthip_swift_last_error()
+    tree.free_sorts()
+    # the same interactions as the f64 oracle's gradient loop on the whole box
+    o = abi.copy_parts(tree.parts)
+    o["v_sig"] = 0
+    o["laplace_u"] = 0
+    o["alpha_visc_max_ngb"] = 0
+    O.fn("f64", "box_gradient")(o.ctypes.data, len(o), C.byref(P), None)
+    s, e = bounds[MAIN]
+    for f in ("v_sig", "laplace_u", "alpha_visc_max_ngb"):
+        a, b = g[f][s:e].astype(np.float64), o[f][s:e].astype(np.float64)
+        fl = 1e-6 * max(np.abs(b).max(), 1e-30)
+        err = np.abs(a - b) / np.maximum(np.abs(b), fl)
+        assert err.max() < 1e-4, (f, err.max())
+
+
+@pytest.mark.gpu
+def test_dosub_subset(adapter):
+    """runner_dosub_subset_density (DOSUB_SUBSET, the ghost's rerun entry):
+    a subset inside one progeny of the main cell against the main cell itself
+    (cj = NULL) and its 26 neighbours == brute force for those particles,
+    everything else untouched."""
+    P = abi.default_hydro_params((3.0, 3.0, 3.0), True)
+    parts, bounds, locs = tree27(11, "random", 0.0)
+    S.zero_density_fields(parts)
+    tree = TreeCells(parts, bounds, locs)
+    tree.sort_all()
+    ref = brute(parts, bounds, locs, P, "density")
+    s, e = bounds[MAIN]
+    top = tree.top[MAIN]
+    sub = C.cast(C.c_void_p(top.progeny[0]), C.POINTER(abi.Cell)).contents
+    nsub = sub.hydro.count
+    off = (sub.hydro.parts - top.hydro.parts) // parts.itemsize
+    pick = list(range(off, off + nsub, 3))  # every third particle of the progeny
+    ind = (C.c_int * len(pick))(*pick)
+    before = abi.copy_parts(parts)
+    eb = abi.EngineBundle(dim=(3.0, 3.0, 3.0), periodic=True, params=P)
+    r = C.addressof(eb.runner)
+    adapter.swifthip_swift_clear_error()
+    adapter.runner_dosub_subset_density(r, C.addressof(top), C.c_void_p(top.hydro.parts), ind,
+                                        len(pick), None, 1)
+    for j in range(27):
+        if j != MAIN:
+            adapter.runner_dosub_subset_density(r, C.addressof(top), C.c_void_p(top.hydro.parts),
+                                                ind, len(pick), C.addressof(tree.top[j]), 1)
+    assert not adapter.swifthip_swift_last_error(), adapter.swifthip_swift_last_error()
+    tree.free_sorts()
+    sel = np.array(pick) + s
+    mg, mb = abi.copy_parts(parts[sel]), abi.copy_parts(ref[sel])
+    S.end_calculation(mg, P)
+    S.end_calculation(mb, P)
+    names, at, rt, lt = load_tolerance("tolerance_27_perturbed.dat")
+    errs = compare_columns(S.density_columns(mb), S.density_columns(mg), at, rt * 1.5, lt, names)
+    assert not errs, "\n".join(errs)
+    rest = np.setdiff1d(np.arange(len(parts)), sel)
+    assert np.array_equal(parts["rho"][rest], before["rho"][rest])
+
+
+def test_split_pairs_table():
+    """The generated cell_split_pairs match the counts of src/cell.c:62
+    (1 corner, 4 edge, 16 face progeny pairs) and the corner entries (CPU:
+    the table needs no device)."""
+    from swift_subtask_dev_amd import lib
+    adapter = lib.load_adapter()
+    adapter.swifthip_swift_split_pairs.restype = C.c_int
+    adapter.swifthip_swift_split_pairs.argtypes = [C.c_int, C.POINTER(C.c_int)]
+    buf = (C.c_int * 32)()
+    counts = [adapter.swifthip_swift_split_pairs(sid, buf) for sid in range(13)]
+    assert counts == [1, 4, 1, 4, 16, 4, 1, 4, 1, 4, 16, 4, 16]
+    assert adapter.swifthip_swift_split_pairs(0, buf) == 1 and (buf[0], buf[1]) == (7, 0)
+    assert adapter.swifthip_swift_split_pairs(2, buf) == 1 and (buf[0], buf[1]) == (6, 1)
+    assert adapter.swifthip_swift_split_pairs(6, buf) == 1 and (buf[0], buf[1]) == (5, 2)
+    assert adapter.swifthip_swift_split_pairs(8, buf) == 1 and (buf[0], buf[1]) == (4, 3)

@@ -547,3 +547,81 @@ def test_grav_batch_vs_oracle(gpu_ctx, periodic, truncated):
     # largest component
     assert_close(g["a_grav"], o["a_grav"], 1e-6, 1e-6, "a_grav")
     assert_close(g["potential"], o["potential"], 1e-6, 1e-6, "potential")
+
+
+# ---------------------------------------------------------------------------
+# The headline configuration itself (bench.py's 128^3 input, default tuning)
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def headline_state(gpu_ctx):
+    """bench.py's exact input: ics.sedov_slabs(128, 1) taken through the full
+    SPHENIX chain on the GPU (density, ghost, gradient, extra ghost, force),
+    i.e. the converged state the bench's timed step starts from."""
+    from swift_subtask_dev_amd import lib
+    parts = ics.sedov_slabs(128, 1)
+    P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
+    P.max_active_bin = 1
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.upload(parts)
+    sp.rebuild(P)
+    sp.hydro_step(P)
+    sp.download(parts, abi.FIELDS_ALL)
+    sp.close()
+    return parts, P
+
+
+def _by_id(p):
+    return p[np.argsort(p["id"], kind="stable")]
+
+
+@pytest.mark.gpu
+def test_headline_128_density_vs_f64(gpu_ctx, headline_state):
+    """The bench's timed density loop (hydro_init_part + density) at 128^3 on
+    the bench's own input vs the fp64 oracle, every particle: rho, wcount,
+    wcount_dh, rho_dh, div_v, rot_v to 2e-6 and the exact interaction count
+    (98,518,377 directed density interactions)."""
+    from swift_subtask_dev_amd import lib
+    parts, P = headline_state
+    g = abi.copy_parts(parts)
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.upload(g)
+    sp.rebuild(P)
+    sp.init_parts(P)
+    n = sp.density(P)
+    sp.download(g, abi.FIELDS_DENSITY)
+    sp.close()
+    o = abi.copy_parts(parts)
+    O.fn("f32", "init_parts")(o.ctypes.data, len(o), C.byref(P))
+    no = O.fn("f64", "box_density")(o.ctypes.data, len(o), C.byref(P), None)
+    assert n == no == 98518377
+    assert_hydro_close(_by_id(g), _by_id(o), TIGHT, "128^3 density")
+
+
+@pytest.mark.gpu
+def test_headline_128_force_vs_f64(gpu_ctx, headline_state):
+    """The bench's timed force loop (hydro_reset_acceleration + force) at
+    128^3 on the converged inputs vs the fp64 oracle: a_hydro, u_dt, h_dt to
+    5e-5 (floor 1e-4 of the column maximum), min_ngb_time_bin exact, and the
+    exact count (101,420,958 directed force interactions)."""
+    from swift_subtask_dev_amd import lib
+    parts, P = headline_state
+    g = abi.copy_parts(parts)
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.upload(g)
+    sp.rebuild(P)
+    sp.reset_acceleration(P)
+    n = sp.force(P)
+    sp.download(g, abi.FIELDS_FORCE)
+    sp.close()
+    o = abi.copy_parts(parts)
+    o["a_hydro"] = 0
+    o["u_dt"] = 0
+    o["h_dt"] = 0
+    o["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
+    no = O.fn("f64", "box_force")(o.ctypes.data, len(o), C.byref(P), None)
+    assert n == no == 101420958
+    g, o = _by_id(g), _by_id(o)
+    assert_close(g["a_hydro"], o["a_hydro"], 5e-5, 1e-4, "a_hydro")
+    assert_close(g["u_dt"], o["u_dt"], 5e-5, 1e-4, "u_dt")
+    assert_close(g["h_dt"], o["h_dt"], 5e-5, 1e-4, "h_dt")
+    assert np.array_equal(g["min_ngb_time_bin"], o["min_ngb_time_bin"])

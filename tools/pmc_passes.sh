@@ -1,13 +1,14 @@
 #!/bin/bash
 # PMC passes over a short bench run (one counter group per pass, kernel-trace
 # only; no runtime/sys trace domains are combined with --pmc).
-# usage: tools/pmc_passes.sh <outdir> [bench args...]
+# usage: KREGEX=<kernel regex> BENCH_ARGS="..." tools/pmc_passes.sh <outdir>
 out="$1"; shift
 mkdir -p "$out"
-rocprofv3 -L > "$out/counters_list.txt" 2>&1 || true
+export TMPDIR=/tmp
+KREGEX="${KREGEX:-list_build|walk_kernel|tile|loop_kernel|p2p_kernel}"
 run() {
   local name="$1"; shift
-  timeout -k 10 240 rocprofv3 --pmc "$@" --kernel-include-regex "tile_kernel|loop_kernel|p2p_kernel" \
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "$KREGEX" \
     -d "$out/$name" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline $BENCH_ARGS \
     > "$out/$name.log" 2>&1
   local rc=$?
@@ -19,3 +20,4 @@ run sq2 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INS
 run tcc1 FETCH_SIZE || exit $?
 run tcc2 WRITE_SIZE || exit $?
 run tcc3 TCC_HIT_sum TCC_MISS_sum || exit $?
+python3 tools/pmc_summary.py "$out"

@@ -75,16 +75,121 @@ def cpu_baseline(parts, P, n_density, n_force, runs=3, threads=None):
         free(gd)
         free(gf)
     t = statistics.median(times)
+    calib = None
+    cpath = ROOT / "profiles" / "cpu_calibration.json"
+    if cpath.exists():
+        calib = json.loads(cpath.read_text())
     return {
         "value": (n_density + n_force) / t,
         "unit": "interactions/s",
         "cores": threads,
         "kind": "port",
+        "host": host_cpu_info(),
+        "calibration": calib,
         "sample": f"full 128^3 box, density+force loops (float restatement of DOSELF1/DOPAIR1/"
                   f"DOSELF2/DOPAIR2, cdim=20 cells), median of {runs} runs after 1 warm-up, "
                   f"{t:.3f} s per step",
         "seconds_per_step": t,
     }
+
+
+def host_cpu_info():
+    """CPU model, logical CPUs visible, physical cores and SMT state of this host."""
+    info = {"model": None, "logical_cpus": os.cpu_count(), "physical_cores": None, "smt": None}
+    try:
+        cores = set()
+        phys = core = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name" and info["model"] is None:
+                info["model"] = v
+            elif k == "physical id":
+                phys = v
+            elif k == "core id":
+                core = v
+            elif not k and phys is not None:
+                cores.add((phys, core))
+                phys = core = None
+        if phys is not None:
+            cores.add((phys, core))
+        info["physical_cores"] = len(cores) or None
+    except OSError:
+        pass
+    try:
+        info["smt"] = open("/sys/devices/system/cpu/smt/active").read().strip() == "1"
+    except OSError:
+        pass
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        pass
+    return info
+
+
+def _grid_parts(O, g, n):
+    """numpy copy of an oracle cell grid's (cell-ordered) struct part array."""
+    from swift_subtask_dev_amd import abi
+
+    ptr = O.fn("f32", "cellgrid_parts")(g)
+    raw = (C.c_uint8 * (n * abi.PART_DTYPE.itemsize)).from_address(ptr)
+    return abi.copy_parts(np.frombuffer(raw, dtype=np.uint8).view(abi.PART_DTYPE))
+
+
+def parity_vs_cpu(ctx, parts, P, tuning, threads):
+    """Outside the timed region: one density loop (after hydro_init_part) and
+    one force loop (after hydro_reset_acceleration) on the bench's own input,
+    on the GPU and in the CPU baseline's float port; max relative differences
+    per output field, matched by particle id."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib as O
+    from swift_subtask_dev_amd import abi, lib
+
+    n = len(parts)
+    eb = abi.EngineBundle(dim=tuple(P.dim), periodic=True, params=P, max_active_bin=P.max_active_bin)
+    # GPU
+    gd, gf = abi.copy_parts(parts), abi.copy_parts(parts)
+    sp = lib.HydroSpace(ctx)
+    sp.set_tuning(*tuning)
+    sp.upload(gd)
+    sp.rebuild(P)
+    sp.init_parts(P)
+    sp.density(P)
+    sp.download(gd, abi.FIELDS_DENSITY)
+    sp.upload(gf)
+    sp.rebuild(P)
+    sp.reset_acceleration(P)
+    sp.force(P)
+    sp.download(gf, abi.FIELDS_FORCE)
+    sp.close()
+    # CPU float port
+    cd, cf = abi.copy_parts(parts), abi.copy_parts(parts)
+    O.fn("f32", "init_parts")(cd.ctypes.data, n, C.byref(P))
+    cf["a_hydro"] = 0
+    cf["u_dt"] = 0
+    cf["h_dt"] = 0
+    cf["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
+    out = {}
+    for arr, loop, fields in ((cd, 0, ("rho", "wcount", "wcount_dh", "rho_dh", "div_v")),
+                              (cf, 2, ("a_hydro", "u_dt", "h_dt"))):
+        g = O.fn("f32", "cellgrid_new")(arr.ctypes.data, n, float(P.dim[0]), 20)
+        O.fn("f32", "cellgrid_run")(g, C.addressof(eb.runner), loop, threads)
+        cpu = _grid_parts(O, g, n)
+        O.fn("f32", "cellgrid_free")(g)
+        gpu = gd if loop == 0 else gf
+        cpu = cpu[np.argsort(cpu["id"], kind="stable")]
+        gpu = gpu[np.argsort(gpu["id"], kind="stable")]
+        for f in fields:
+            a = gpu[f].astype(np.float64).reshape(n, -1)
+            b = cpu[f].astype(np.float64).reshape(n, -1)
+            floor = (1e-6 if loop == 0 else 1e-4) * max(np.abs(b).max(), 1e-300)
+            out[f] = float((np.abs(a - b) / np.maximum(np.abs(b), floor)).max())
+        if loop == 2:
+            out["min_ngb_time_bin_equal"] = bool(np.array_equal(gpu["min_ngb_time_bin"],
+                                                                cpu["min_ngb_time_bin"]))
+    return {"vs": "cpu_baseline float port (same input, one density + one force loop)",
+            "max_rel": out,
+            "floor": "1e-6 (density fields) / 1e-4 (force fields) x the column maximum"}
 
 
 def load_traffic():
@@ -95,6 +200,82 @@ def load_traffic():
         except Exception:
             return None
     return None
+
+
+def run_grav(args, ctx, rank, world, dist, torch):
+    """BASELINE config 4: GravityTests uniform DM box, P2P leaf interactions
+    (runner_doself_grav_pp + runner_dopair_grav_pp over each leaf and its 26
+    neighbours, the near field a tree walk leaves to P2P), fp64. n^3 uniform
+    gparts (Gravity_glass/makeIC.py: L = 1, rho = 1), softening 0.001
+    (uniform_DM_box.yml), leaves of <= 400 gparts (space_splitsize). With
+    N ranks the i-leaves are split into N contiguous ranges (strong split of
+    the one box; gparts replicated read-only)."""
+    from swift_subtask_dev_amd import abi, ics, lib
+
+    n = args.n
+    t0 = time.time()
+    gp = ics.uniform_gravity_box(n, epsilon=0.001, seed=256)
+    cdim = int(np.ceil((n ** 3 / 400.0) ** (1.0 / 3.0)))
+    gs, leaves = ics.leaf_cells(gp, cdim)
+    del gp
+    offs, pairs = ics.neighbour_pairs(cdim, periodic=False, truncated=0)
+    nl = len(leaves)
+    lo, hi = rank * nl // world, (rank + 1) * nl // world
+    if world > 1:  # this rank's i-leaves keep their source lists, the others none
+        own = np.zeros(nl + 1, dtype=np.int64)
+        own[lo + 1:hi + 1] = np.diff(offs)[lo:hi]
+        sel = np.concatenate([np.arange(offs[k], offs[k + 1]) for k in range(lo, hi)])
+        pairs = pairs[sel]
+        offs = np.cumsum(own).astype(np.int32)
+    G = abi.GravParams(0, (C.c_float * 3)(1, 1, 1), 0.0, 1e30, abi.NUM_TIME_BINS)
+    sp = lib.GravSpace(ctx)
+    stream = torch.cuda.Stream()
+    sp.upload(gs)
+    sp.set_leaves(leaves, offs, pairs)
+    n_int = sp.pp(G)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] grav setup {time.time() - t0:.1f}s: {len(gs)} gparts, {nl} leaves "
+        f"(cdim {cdim}, max {int(leaves['count'].max())}), {n_int} P2P interactions/step")
+    for _ in range(args.warmup):
+        sp.pp(G, count=False)
+    sp.sync()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        sp.pp(G, count=False)
+    sp.sync()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    tot = torch.tensor([float(n_int) * args.steps], dtype=torch.float64, device="cuda")
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    total, el = tot.item(), tmax.item()
+    if rank == 0:
+        flops = total * 28.0 / el  # SURVEY 8d: P2P Newtonian 28 flops per interaction
+        out = {
+            "metric": "P2P gravity interactions/s (runner_doself/dopair_grav_pp near field), "
+                      f"uniform DM box {n}^3",
+            "value": total / el, "unit": "interactions/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (uniform random gparts, seed 256; Gravity_glass ICs unavailable offline)",
+            "config": {"workload": f"GravityTests uniform DM box {n}^3: leaf self + 26 neighbour "
+                                   "leaf pairs, P2P, softening 0.001, non-periodic",
+                       "gparts": int(len(gs)), "leaves": nl, "leaf_cdim": cdim,
+                       "interactions_per_step": int(total / args.steps)},
+            "roofline": {"bound": "fp64-vector", "achieved": flops / 1e12,
+                         "peak": FP64_PEAK / 1e12, "unit": "TFLOP/s", "frac": flops / FP64_PEAK,
+                         "traffic": None, "flops_model": "28 flops per directed P2P interaction"},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(out), flush=True)
+    sp.close()
 
 
 def main():
@@ -113,12 +294,16 @@ def main():
                     help="profiling only, results invalid: 1 tile staging only, 2 + candidate tests")
     ap.add_argument("--group-size", type=int, default=int(os.environ.get("SWH_GROUP_SIZE", "0")),
                     help="tile i-group size / row width: 0 (default 16), 16, 32, 64")
-    ap.add_argument("--list-skin", type=float, default=float(os.environ.get("SWH_LIST_SKIN", "0.1")),
+    ap.add_argument("--list-skin", type=float, default=float(os.environ.get("SWH_LIST_SKIN", "0")),
                     help="pair-list reach slack over gamma*h (variant 7)")
     ap.add_argument("--list-capacity", type=int, default=0, help="pair-list entries per particle")
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-runs", type=int, default=3)
+    ap.add_argument("--workload", default="sedov", choices=["sedov", "grav", "eagle"],
+                    help="sedov: the headline metric (SedovBlast_3D 128^3 density + force); "
+                         "grav: BASELINE config 4 (uniform DM box P2P, --n 256); "
+                         "eagle: BASELINE config 3 stand-in (clustered box)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -135,6 +320,14 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     from swift_subtask_dev_amd import abi, decomp, ics, lib
+
+    if args.workload == "grav":
+        ctx = lib.Context(local_rank, args.precision)
+        run_grav(args, ctx, rank, world, dist, torch)
+        ctx.close()
+        if dist:
+            dist.destroy_process_group()
+        return
 
     n = args.n
     t_setup = time.time()
@@ -227,7 +420,7 @@ def main():
         b_force = n_owned * (27 * S_IN_FORCE + S_OUT_FORCE)
         achieved = b_dens / td
         # PMC traffic was measured on the default configuration only
-        default_cfg = (args.loop_variant == 0 and args.group_size == 0 and args.list_skin == 0.1
+        default_cfg = (args.loop_variant == 0 and args.group_size == 0 and args.list_skin == 0.0
                        and args.cell_factor == 1 and args.cell_scale == 0 and args.n == 128)
         traffic = load_traffic() if default_cfg else None
         out = {
@@ -288,13 +481,21 @@ def main():
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
-            # the CPU path times the same loops on the same (prepared) inputs
-            sp.download(local, abi.FIELDS_ALL)
+            # the CPU path times the same loops on the same (prepared) inputs:
+            # `local` still holds the converged chain state the GPU started from
             try:
                 out["cpu_baseline"] = cpu_baseline(local, P, n_density, n_force, args.cpu_runs)
                 out["gpu_over_cpu"] = out["value"] / out["cpu_baseline"]["value"]
             except Exception as e:  # report, never fake
                 log(f"cpu baseline failed: {e}")
+            try:
+                tuning = (args.cell_factor, args.loop_variant, args.group_size, args.cell_scale,
+                          0, args.list_capacity, args.list_skin)
+                out["parity"] = parity_vs_cpu(ctx, local, P, tuning,
+                                              out["cpu_baseline"]["cores"]
+                                              if out["cpu_baseline"] else 16)
+            except Exception as e:  # report, never fake
+                log(f"parity check failed: {e}")
         print(json.dumps(out), flush=True)
     sp.close()
     ctx.close()

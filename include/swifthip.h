@@ -260,7 +260,9 @@ typedef struct swh_tuning {
   int32_t diag_mode;    /* 0; profiling only (results invalid): 1 = staging only (tile
                            loops) / list build only (lists), 2 = staging + candidate tests */
   int32_t list_capacity; /* list entries per particle (0 = 128); more hits: direct gather */
-  float list_skin;       /* relative slack of the list reach over gamma h (default 0.1) */
+  float list_skin;       /* relative slack of the list reach over gamma h (default 0: exact
+                            lists; a ghost that grows any H past its reach makes gradient /
+                            force rebuild them) */
 } swh_tuning;
 SWH_API swh_status swh_space_set_tuning(swh_space *s, const swh_tuning *t);
 

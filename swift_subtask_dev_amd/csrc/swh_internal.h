@@ -148,7 +148,7 @@ struct swh_space {
   int64_t n = 0;
   bool built = false;
   SwhGrid grid;
-  swh_tuning tuning{1, 0, 0, 0.f, 0, 0, 0.1f};
+  swh_tuning tuning{1, 0, 0, 0.f, 0, 0, 0.f};
 
   // AoS image of the caller's records (for write-back of untouched fields)
   swh::DevBuf aos;

@@ -242,6 +242,27 @@ SWH_API swh_status swh_gradient_loop(swh_space *s, const swh_hydro_params *P, in
 SWH_API swh_status swh_extra_ghost(swh_space *s, const swh_hydro_params *P);
 SWH_API swh_status swh_force_loop(swh_space *s, const swh_hydro_params *P, int64_t *n_interactions);
 SWH_API swh_status swh_end_force(swh_space *s, const swh_hydro_params *P);
+/* Multi-GPU (one process per GPU). Caller indices >= n_owned are
+ * foreign: read-only halo copies of particles another rank owns (SWIFT's
+ * foreign cells). They are neighbours of every loop and are never updated.
+ * Default after an upload: every particle owned. */
+SWH_API swh_status swh_space_set_owned(swh_space *s, int64_t n_owned);
+/* Halo refresh between loop phases. A halo record is 8 floats: h, rho,
+ * pressure, soundspeed, f (grad-h term), balsara, alpha_visc, alpha_diff.
+ * pack writes the records of the particles with caller indices idx[0..n)
+ * (DEVICE arrays) to out (device, n * 8 floats); unpack writes the `fields`
+ * groups of the records in `in` to the particles idx[0..n). Both are ordered
+ * on the space's stream. */
+#define SWH_HALO_RECORD_FLOATS 8
+#define SWH_HALO_H 1
+#define SWH_HALO_RHO 2
+#define SWH_HALO_PC 4         /* pressure, soundspeed */
+#define SWH_HALO_F_BALSARA 8  /* f, balsara */
+#define SWH_HALO_ALPHAS 16    /* alpha_visc, alpha_diff */
+#define SWH_HALO_ALL 31
+SWH_API swh_status swh_space_pack_halo(swh_space *s, const int32_t *idx, int32_t n, float *out);
+SWH_API swh_status swh_space_unpack_halo(swh_space *s, const int32_t *idx, int32_t n,
+                                         const float *in, int fields);
 /* Wait for all queued work on the space's stream. */
 SWH_API swh_status swh_space_sync(swh_space *s);
 

@@ -179,6 +179,9 @@ LEAF_DTYPE = np.dtype([("start", "<i4"), ("count", "<i4")])
 LEAF_PAIR_DTYPE = np.dtype([("j", "<i4"), ("truncated", "<i4")])
 
 FIELDS_DENSITY, FIELDS_GRADIENT, FIELDS_FORCE, FIELDS_ALL = 1, 2, 4, 7
+# halo record fields (swh_space_unpack_halo): h, rho, P + c, f + balsara, alphas
+HALO_H, HALO_RHO, HALO_PC, HALO_F_BALSARA, HALO_ALPHAS, HALO_ALL = 1, 2, 4, 8, 16, 31
+HALO_RECORD_FLOATS = 8
 
 
 def default_hydro_params(dim=(1.0, 1.0, 1.0), periodic=True, **kw) -> HydroParams:

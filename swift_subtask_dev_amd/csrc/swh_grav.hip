@@ -2,14 +2,20 @@
 // runner_dopair_grav_pp, src/runner_doiact_grav.c:1500-1871 and 584-760) on a
 // device-resident gpart set.
 //
-// One 256-thread workgroup per i-leaf; each thread keeps up to kIPer i-particle
-// accumulators in registers (fp64). Source leaves of the i-leaf's CSR list
-// are streamed through LDS in 256-particle tiles (x,y,z fp64 + eps, mass);
-// every lane reads the same tile entry (LDS broadcast), so the inner loop is
-// pure FMA work: the compute-bound P2P roofline (fp64 vector, no MFMA — this
-// is a gather/FMA path, not a dense contraction).
+// One 256-thread workgroup per i-leaf (leaves in XCD-contiguous order, so the
+// leaves one XCD works on are neighbours and share its L2); each thread keeps
+// up to kIPer i-particle accumulators in registers (fp64). Source leaves of
+// the i-leaf's CSR list are streamed through LDS in 256-particle tiles
+// (x, y, z, softening and its reciprocal in fp64, mass); every lane reads
+// the same tile entry (LDS broadcast), so the inner loop is pure fp64 FMA
+// work: the compute-bound P2P roofline (fp64 vector, no MFMA: a gather/FMA
+// path, not a dense contraction). Per pair: 1/sqrt(r^2) by the hardware
+// reciprocal square root refined by Newton steps, 1/max(eps_i, eps_j) as
+// min(1/eps_i, 1/eps_j) from per-particle reciprocals (no division), and the
+// i == j term of a self tile removed by a zero mass instead of a branch.
 #include "swh_internal.h"
 #include "swh_physics.h"
+#include "swh_tile.h"
 
 namespace swh {
 
@@ -18,6 +24,7 @@ constexpr int kIPer = 2;  // i-particles per thread per pass (leaves up to 512 i
 
 struct GSoA {
   double4* pos;  // x, y, z, epsilon
+  double* hinv;  // 1 / epsilon
   float* mass;   // 0 for inhibited
   int8_t* active;
   double4* acc;  // a_x, a_y, a_z, potential
@@ -31,6 +38,7 @@ __global__ void gunpack_kernel(GLayout L, const char* __restrict__ aos, int64_t 
   const double* x = reinterpret_cast<const double*>(r + L.x);
   const float eps = *reinterpret_cast<const float*>(r + L.epsilon);
   g.pos[i] = make_double4(x[0], x[1], x[2], (double)eps);
+  g.hinv[i] = 1.0 / (double)eps;
   const int tb = *reinterpret_cast<const int8_t*>(r + L.time_bin);
   const bool inhibited = tb == kTimeBinInhibited;
   g.mass[i] = inhibited ? 0.f : *reinterpret_cast<const float*>(r + L.mass);
@@ -51,14 +59,180 @@ __global__ void gpack_kernel(GLayout L, char* __restrict__ aos, int64_t n, GSoA 
   g.acc[i] = make_double4(0., 0., 0., 0.);  // a second download adds nothing
 }
 
-template <typename T>
+// fp64 1/sqrt(x): the hardware approximation refined by one Newton step
+// (~1e-14 relative; the results are stored as float).
+__device__ __forceinline__ double rsqrt1_f64(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  return fma(y * fma(-0.5 * x * y, y, 0.5), 1., y);
+}
+
+// runner_iact_grav_pp_full / _truncated (gravity_iact.h:47-135) for one
+// pair, fp64: h2 = max(eps_i^2, eps_j^2), h_inv = min(1/eps_i, 1/eps_j).
+template <bool TRUNC>
+__device__ __forceinline__ void p2p_pair(double dx, double dy, double dz, double h2,
+                                         double h_inv, double mass, double r_s_inv,
+                                         double& ax, double& ay, double& az, double& pot) {
+  const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
+  const double r_inv = rsqrt1_f64(r2 + (double)FLT_MIN);
+  double f_ij, pot_ij;
+  if (r2 >= h2) {
+    const double mr = mass * r_inv;
+    f_ij = mr * (r_inv * r_inv);
+    pot_ij = -mr;
+  } else {
+    const double ui = r2 * r_inv * h_inv;
+    const double mh = mass * h_inv;
+    f_ij = mh * (h_inv * h_inv) * grav_force_eval(ui);
+    pot_ij = mh * grav_pot_eval(ui);
+  }
+  if (TRUNC) {
+    const double x = 2. * (r2 * r_inv * r_s_inv);
+    const double exp_x = exp(x);
+    const double alpha = rcp_f64(1. + exp_x);
+    const double corr_pot = 2. * (1. - alpha * exp_x);
+    const double corr_f = 2. * fma(fma(1. - alpha, x, -exp_x), alpha, 1.);
+    f_ij *= corr_f;
+    pot_ij *= corr_pot;
+  }
+  ax = fma(f_ij, dx, ax);
+  ay = fma(f_ij, dy, ay);
+  az = fma(f_ij, dz, az);
+  pot += pot_ij;
+}
+
+// One LDS tile against this thread's kIPer i-particles: every j entry is read
+// once and used kIPer times. SELF: the tile may hold an i itself (the
+// i-leaf's own leaf), whose term is removed by a zero mass.
+template <bool TRUNC, bool PERIODIC, bool SELF>
+__device__ __forceinline__ void p2p_tile(const double* sx, const double* sy, const double* sz,
+                                         const double* se2, const double* sh, const float* sm,
+                                         int nt, const int* self_local, const double* xi,
+                                         const double* yi, const double* zi, const double* hi2,
+                                         const double* hv, const bool* act, double dimx,
+                                         double dimy, double dimz, double r_s_inv, double* ax,
+                                         double* ay, double* az, double* pot) {
+  for (int t = 0; t < nt; t++) {
+    const double xj = sx[t], yj = sy[t], zj = sz[t], e2j = se2[t], hvj = sh[t];
+    const double mj = (double)sm[t];
+#pragma unroll
+    for (int k = 0; k < kIPer; k++) {
+      double dx = xj - xi[k], dy = yj - yi[k], dz = zj - zi[k];
+      if (PERIODIC) {
+        dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
+        dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
+        dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
+      }
+      double mass = act[k] ? mj : 0.;
+      if (SELF) mass = t == self_local[k] ? 0. : mass;  // j == i: no term
+      p2p_pair<TRUNC>(dx, dy, dz, fmax(hi2[k], e2j), fmin(hv[k], hvj), mass, r_s_inv, ax[k],
+                      ay[k], az[k], pot[k]);
+    }
+  }
+}
+
 __global__ __launch_bounds__(kGravBlock) void p2p_kernel(
     GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
     const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
-    double dimz, T r_s_inv, unsigned long long* counter) {
+    double dimz, double r_s_inv, unsigned long long* counter) {
+  __shared__ double sx[kGravBlock], sy[kGravBlock], sz[kGravBlock], se2[kGravBlock],
+      sh[kGravBlock];
+  __shared__ float sm[kGravBlock];
+  const int li = xcd_block_id();
+  const swh_leaf L = leaves[li];
+  const int p0 = pair_off[li], p1 = pair_off[li + 1];
+  unsigned long long nint = 0;
+  for (int ibase = 0; ibase < L.count; ibase += kGravBlock * kIPer) {
+    int gi[kIPer], self_local[kIPer];
+    double xi[kIPer], yi[kIPer], zi[kIPer], hi2[kIPer], hv[kIPer];
+    double ax[kIPer], ay[kIPer], az[kIPer], pot[kIPer];
+    bool act[kIPer];
+#pragma unroll
+    for (int k = 0; k < kIPer; k++) {
+      const int local = ibase + k * kGravBlock + (int)threadIdx.x;
+      gi[k] = L.start + local;
+      act[k] = local < L.count && g.active[gi[k]];
+      const double4 p = act[k] ? g.pos[gi[k]] : make_double4(0., 0., 0., 1.);
+      xi[k] = p.x; yi[k] = p.y; zi[k] = p.z;
+      hi2[k] = p.w * p.w;
+      hv[k] = act[k] ? g.hinv[gi[k]] : 1.;
+      ax[k] = ay[k] = az[k] = pot[k] = 0.;
+    }
+    for (int q = p0; q < p1; q++) {
+      const swh_leaf_pair pr = pairs[q];
+      const swh_leaf J = leaves[pr.j];
+      for (int jbase = 0; jbase < J.count; jbase += kGravBlock) {
+        const int nt = min(kGravBlock, J.count - jbase);
+        __syncthreads();
+        if ((int)threadIdx.x < nt) {
+          const int gj = J.start + jbase + (int)threadIdx.x;
+          const double4 p = g.pos[gj];
+          sx[threadIdx.x] = p.x;
+          sy[threadIdx.x] = p.y;
+          sz[threadIdx.x] = p.z;
+          se2[threadIdx.x] = p.w * p.w;
+          sh[threadIdx.x] = g.hinv[gj];
+          sm[threadIdx.x] = g.mass[gj];
+        }
+        __syncthreads();
+        // the i-leaf's own particles can only sit in a tile of a leaf range
+        // overlapping it (block-uniform test)
+        const bool self = J.start + jbase < L.start + L.count && L.start < J.start + jbase + nt;
+#pragma unroll
+        for (int k = 0; k < kIPer; k++) {
+          self_local[k] = gi[k] - (J.start + jbase);
+          if (act[k])
+            nint += (unsigned long long)(nt - ((self_local[k] >= 0 && self_local[k] < nt) ? 1 : 0));
+        }
+#define SWH_P2P_TILE(TR, PE, SE)                                                             \
+  p2p_tile<TR, PE, SE>(sx, sy, sz, se2, sh, sm, nt, self_local, xi, yi, zi, hi2, hv, act, dimx, \
+                       dimy, dimz, r_s_inv, ax, ay, az, pot)
+        if (self) {
+          if (pr.truncated) {
+            if (periodic) SWH_P2P_TILE(true, true, true);
+            else SWH_P2P_TILE(true, false, true);
+          } else {
+            if (periodic) SWH_P2P_TILE(false, true, true);
+            else SWH_P2P_TILE(false, false, true);
+          }
+        } else {
+          if (pr.truncated) {
+            if (periodic) SWH_P2P_TILE(true, true, false);
+            else SWH_P2P_TILE(true, false, false);
+          } else {
+            if (periodic) SWH_P2P_TILE(false, true, false);
+            else SWH_P2P_TILE(false, false, false);
+          }
+        }
+#undef SWH_P2P_TILE
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kIPer; k++) {
+      if (!act[k]) continue;
+      double4 a = g.acc[gi[k]];
+      a.x += ax[k];
+      a.y += ay[k];
+      a.z += az[k];
+      a.w += pot[k];
+      g.acc[gi[k]] = a;
+    }
+  }
+  if (counter) {
+    for (int o = 32; o > 0; o >>= 1) nint += __shfl_xor(nint, o);
+    if ((threadIdx.x & 63) == 0 && nint) atomicAdd(counter, nint);
+  }
+}
+
+// fp32 mode (SWH_PRECISION_F32): the reference's own float arithmetic,
+// operation by operation (gravity_iact.h), for parity with the float runner.
+__global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
+    GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
+    const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
+    double dimz, float r_s_inv, unsigned long long* counter) {
+  using T = float;
   __shared__ double sx[kGravBlock], sy[kGravBlock], sz[kGravBlock];
   __shared__ float se[kGravBlock], sm[kGravBlock];
-  const int li = blockIdx.x;
+  const int li = xcd_block_id();
   const swh_leaf L = leaves[li];
   const int p0 = pair_off[li], p1 = pair_off[li + 1];
   unsigned long long nint = 0;
@@ -96,43 +270,27 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel(
 #pragma unroll
         for (int k = 0; k < kIPer; k++) {
           if (!act[k]) continue;
-          const int self_local = gi[k] - (J.start + jbase);  // skip j == i
-          if (pr.truncated) {
-            for (int t = 0; t < nt; t++) {
-              if (t == self_local) continue;
-              double dxd = sx[t] - xi[k], dyd = sy[t] - yi[k], dzd = sz[t] - zi[k];
-              if (periodic) {
-                dxd = dxd > 0.5 * dimx ? dxd - dimx : (dxd < -0.5 * dimx ? dxd + dimx : dxd);
-                dyd = dyd > 0.5 * dimy ? dyd - dimy : (dyd < -0.5 * dimy ? dyd + dimy : dyd);
-                dzd = dzd > 0.5 * dimz ? dzd - dimz : (dzd < -0.5 * dimz ? dzd + dimz : dzd);
-              }
-              const T dx = (T)dxd, dy = (T)dyd, dz = (T)dzd;
-              const T r2 = dx * dx + dy * dy + dz * dz;
-              const T h = tmax(hi[k], (T)se[t]);
-              const T h_inv = (T)1 / h;
-              T f, pt;
+          const int self_local = gi[k] - (J.start + jbase);
+          for (int t = 0; t < nt; t++) {
+            if (t == self_local) continue;
+            double dxd = sx[t] - xi[k], dyd = sy[t] - yi[k], dzd = sz[t] - zi[k];
+            if (periodic) {
+              dxd = dxd > 0.5 * dimx ? dxd - dimx : (dxd < -0.5 * dimx ? dxd + dimx : dxd);
+              dyd = dyd > 0.5 * dimy ? dyd - dimy : (dyd < -0.5 * dimy ? dyd + dimy : dyd);
+              dzd = dzd > 0.5 * dimz ? dzd - dimz : (dzd < -0.5 * dimz ? dzd + dimz : dzd);
+            }
+            const T dx = (T)dxd, dy = (T)dyd, dz = (T)dzd;
+            const T r2 = dx * dx + dy * dy + dz * dz;
+            const T h = tmax(hi[k], se[t]);
+            const T h_inv = (T)1 / h;
+            T f, pt;
+            if (pr.truncated)
               iact_grav_pp<T, true>(r2, h * h, h_inv, h_inv * h_inv * h_inv, (T)sm[t], r_s_inv,
                                     f, pt);
-              ax[k] += f * dx; ay[k] += f * dy; az[k] += f * dz; pot[k] += pt;
-            }
-          } else {
-            for (int t = 0; t < nt; t++) {
-              if (t == self_local) continue;
-              double dxd = sx[t] - xi[k], dyd = sy[t] - yi[k], dzd = sz[t] - zi[k];
-              if (periodic) {
-                dxd = dxd > 0.5 * dimx ? dxd - dimx : (dxd < -0.5 * dimx ? dxd + dimx : dxd);
-                dyd = dyd > 0.5 * dimy ? dyd - dimy : (dyd < -0.5 * dimy ? dyd + dimy : dyd);
-                dzd = dzd > 0.5 * dimz ? dzd - dimz : (dzd < -0.5 * dimz ? dzd + dimz : dzd);
-              }
-              const T dx = (T)dxd, dy = (T)dyd, dz = (T)dzd;
-              const T r2 = dx * dx + dy * dy + dz * dz;
-              const T h = tmax(hi[k], (T)se[t]);
-              const T h_inv = (T)1 / h;
-              T f, pt;
+            else
               iact_grav_pp<T, false>(r2, h * h, h_inv, h_inv * h_inv * h_inv, (T)sm[t],
                                      r_s_inv, f, pt);
-              ax[k] += f * dx; ay[k] += f * dy; az[k] += f * dz; pot[k] += pt;
-            }
+            ax[k] += f * dx; ay[k] += f * dy; az[k] += f * dz; pot[k] += pt;
           }
           nint += (unsigned long long)(nt - ((self_local >= 0 && self_local < nt) ? 1 : 0));
         }
@@ -158,6 +316,7 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel(
 static GSoA gsoa_of(swh_gspace* g) {
   GSoA s;
   s.pos = g->pos.as<double4>();
+  s.hinv = g->hinv.as<double>();
   s.mass = g->mass.as<float>();
   s.active = g->active.as<int8_t>();
   s.acc = g->accel.as<double4>();
@@ -187,7 +346,7 @@ swh_status swh_gspace_destroy(swh_gspace* g) {
   if (!g) return SWH_OK;
   (void)hipSetDevice(g->ctx->device);
   (void)hipStreamSynchronize(g->stream);
-  DevBuf* bufs[] = {&g->aos, &g->pos, &g->mass, &g->active, &g->accel,
+  DevBuf* bufs[] = {&g->aos, &g->pos, &g->hinv, &g->mass, &g->active, &g->accel,
                     &g->leaves, &g->pair_off, &g->pairs, &g->counter};
   for (DevBuf* b : bufs) b->release();
   (void)hipStreamDestroy(g->stream);
@@ -209,6 +368,7 @@ swh_status swh_gspace_upload(swh_gspace* g, const void* gparts, int64_t count,
   if (count == 0) return SWH_OK;
   SWH_TRY(g->aos.reserve((size_t)count * L.stride));
   SWH_TRY(g->pos.reserve((size_t)count * sizeof(double4)));
+  SWH_TRY(g->hinv.reserve((size_t)count * sizeof(double)));
   SWH_TRY(g->mass.reserve((size_t)count * sizeof(float)));
   SWH_TRY(g->active.reserve((size_t)count));
   SWH_TRY(g->accel.reserve((size_t)count * sizeof(double4)));
@@ -279,12 +439,12 @@ swh_status swh_grav_pp_batch(swh_gspace* g, const swh_grav_params* G, int64_t* n
   unsigned long long* ctr = n_int ? g->counter.as<unsigned long long>() : nullptr;
   if (ctr) SWH_HIP(hipMemsetAsync(ctr, 0, sizeof(unsigned long long), g->stream));
   if (g->ctx->precision == SWH_PRECISION_F64)
-    hipLaunchKernelGGL(p2p_kernel<double>, dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
+    hipLaunchKernelGGL(p2p_kernel, dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
                        gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
                        g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
                        (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, ctr);
   else
-    hipLaunchKernelGGL(p2p_kernel<float>, dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
+    hipLaunchKernelGGL(p2p_kernel_f32, dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
                        gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
                        g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
                        (double)G->dim[1], (double)G->dim[2], (float)G->r_s_inv, ctr);

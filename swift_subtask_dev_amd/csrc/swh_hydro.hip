@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) void loop_kernel(GridDev g, SoA a,
                                                    int* __restrict__ ncount) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int i = (t < nitems) ? (subset ? subset[t] : t) : -1;
-  const bool act = i >= 0 && a.tb[i] <= max_active_bin;
+  const bool act = i >= 0 && active_part(a, i, max_active_bin);
   LoopState<LOOP, T> st;
   st.n = 0;
   double4 pi = make_double4(0., 0., 0., 0.);
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void overflow_kernel(GridDev g, SoA a, ListDev
   for (int t0 = blockIdx.x * blockDim.x; t0 < nov; t0 += gridDim.x * blockDim.x) {
     const int t = t0 + (int)threadIdx.x;
     const int i = t < nov ? ld.ovf[t] : -1;
-    const bool act = i >= 0 && a.tb[i] <= max_active_bin;
+    const bool act = i >= 0 && active_part(a, i, max_active_bin);
     LoopState<LOOP, T> st;
     st.n = 0;
     if (act) {
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void walk_subset_kernel(GridDev g, SoA a, List
                                                           unsigned long long* counter) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int i = t < nitems ? subset[t] : -1;
-  const bool act = i >= 0 && a.tb[i] <= max_active_bin;
+  const bool act = i >= 0 && active_part(a, i, max_active_bin);
   LoopState<LOOP_DENSITY, T> st;
   st.n = 0;
   if (act) {
@@ -197,7 +197,7 @@ void tile5_kernel(GridDev g, SoA a,
 // hydro_init_part (src/hydro/SPHENIX/hydro.h:553-566) on active particles.
 __global__ void init_kernel(SoA a, int64_t n, int max_active_bin) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || a.tb[i] > max_active_bin) return;
+  if (i >= n || !active_part(a, i, max_active_bin)) return;
   a.th[i].y = 0.f;
   a.dens[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   a.rot[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -220,7 +220,7 @@ template <typename T>
 __global__ void ghost_init_kernel(SoA a, int64_t n, int max_active_bin, float h_max,
                                   float* left, float* right, int* list, int* count) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || a.tb[i] > max_active_bin) return;
+  if (i >= n || !active_part(a, i, max_active_bin)) return;
   left[i] = 0.f;
   right[i] = h_max;
   const int slot = atomicAdd(count, 1);
@@ -387,7 +387,7 @@ __global__ void extra_ghost_kernel(SoA a, int64_t n, int max_active_bin, ForcePr
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int tb = a.tb[i];
-  if (tb > max_active_bin) return;
+  if (!active_part(a, i, max_active_bin)) return;
   const T h = (T)(float)a.pos[i].w;
   const T h_inv = (T)1 / h;
   const T h_inv_dim = h_inv * h_inv * h_inv;
@@ -449,7 +449,7 @@ __global__ void extra_ghost_kernel(SoA a, int64_t n, int max_active_bin, ForcePr
 // hydro_reset_acceleration (hydro.h:944-955) + timestep_limiter_prepare_force.
 __global__ void reset_acc_kernel(SoA a, int64_t n, int max_active_bin) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || a.tb[i] > max_active_bin) return;
+  if (i >= n || !active_part(a, i, max_active_bin)) return;
   a.acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   a.hdt[i] = 0.f;
   a.mintb[i] = (int8_t)(kNumTimeBins + 1);
@@ -457,7 +457,7 @@ __global__ void reset_acc_kernel(SoA a, int64_t n, int max_active_bin) {
 
 __global__ void end_force_kernel(SoA a, int64_t n, int max_active_bin) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || a.tb[i] > max_active_bin) return;
+  if (i >= n || !active_part(a, i, max_active_bin)) return;
   a.hdt[i] = a.hdt[i] * ((float)a.pos[i].w * kDimInv);  // hydro.h:1080-1084
 }
 

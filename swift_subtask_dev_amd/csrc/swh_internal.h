@@ -168,6 +168,8 @@ struct swh_space {
   swh::DevBuf hdt;   // float h_dt
   swh::DevBuf mintb; // int8 min_ngb_time_bin
   swh::DevBuf perm;  // int32 sorted index -> caller index
+  swh::DevBuf iperm; // int32 caller index -> sorted index
+  int64_t n_owned = 0;  // caller indices >= n_owned: foreign halo (swh_space_set_owned)
   swh::DevBuf ncount;  // int32 per-particle interaction count (diagnostic)
   // grid
   swh::DevBuf cell_start;  // int32[ncell+1], indexed by Morton rank
@@ -201,6 +203,7 @@ struct swh_gspace {
   swh::DevBuf aos;
   swh::GLayout layout{};
   swh::DevBuf pos;     // double4 x,y,z,eps
+  swh::DevBuf hinv;    // double 1/eps
   swh::DevBuf mass;    // float  mass (0 for inhibited)
   swh::DevBuf active;  // int8
   swh::DevBuf accel;   // double4 ax, ay, az, pot (accumulated this call)

@@ -178,7 +178,7 @@ __device__ __forceinline__ void list_build(const GridDev& g, const SoA& a, const
   const int gid = xcd_block_id();
   const int2 gr = gid < ngroups ? groups[gid] : make_int2(0, 0);
   const int i = il < gr.y ? gr.x + il : -1;
-  const bool act = i >= 0 && a.tb[i] <= max_active_bin;
+  const bool act = i >= 0 && active_part(a, i, max_active_bin);
   const double skin1 = (double)ld.skin1;
   double4 pi = make_double4(0., 0., 0., 0.);
   if (act) pi = a.pos[i];
@@ -486,7 +486,7 @@ __device__ __forceinline__ void list_walk(const GridDev& g, SoA& a, const ListDe
   constexpr int PPB = 256 / LPI;
   const int i = xcd_block_id() * PPB + (int)threadIdx.x / LPI;
   const int s = (int)threadIdx.x % LPI;
-  bool act = i < n && a.tb[i] <= max_active_bin;
+  bool act = i < n && active_part(a, i, max_active_bin);
   int nl = 0, lb = 0;
   if (act) {
     nl = ld.cnt[i];

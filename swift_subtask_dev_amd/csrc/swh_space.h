@@ -19,7 +19,16 @@ struct SoA {
   float* hdt;     // h_dt
   int8_t* mintb;  // limiter min_ngb_time_bin
   int* perm;      // sorted index -> caller index
+  int* iperm;     // caller index -> sorted index
+  int n_owned;    // caller indices >= n_owned are foreign (read-only halo)
 };
+
+// part_is_active (src/active.h:357-373) for a particle this space owns:
+// foreign halo copies (another rank's particles, SWIFT's foreign cells) are
+// neighbours of the loops but are never updated.
+__device__ __forceinline__ bool active_part(const SoA& a, int64_t i, int max_active_bin) {
+  return a.tb[i] <= max_active_bin && a.perm[i] < a.n_owned;
+}
 
 struct GridDev {
   int cdim[3];

@@ -313,6 +313,53 @@ __global__ void permute_kernel(SoA src, SoA dst, const int* __restrict__ idx, in
   dst.perm[s] = src.perm[i];
 }
 
+__global__ void iperm_kernel(const int* __restrict__ perm, int64_t n, int* __restrict__ iperm) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n) iperm[perm[s]] = (int)s;
+}
+
+// Halo records (swh_space_pack_halo): h, rho, P, c, f, balsara, alpha_visc,
+// alpha_diff of the particles with caller indices idx[0..n).
+__global__ void halo_pack_kernel(SoA a, const int* __restrict__ idx, int n,
+                                 float4* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int s = a.iperm[idx[t]];
+  const float4 th = a.th[s];
+  out[2 * t] = make_float4((float)a.pos[s].w, th.y, th.z, th.w);
+  out[2 * t + 1] = a.fc[s];
+}
+
+__global__ void halo_unpack_kernel(SoA a, const int* __restrict__ idx, int n,
+                                   const float4* __restrict__ in, int mask,
+                                   unsigned int* hmax_bits) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int s = a.iperm[idx[t]];
+  const float4 r0 = in[2 * t], r1 = in[2 * t + 1];
+  if (mask & SWH_HALO_H) {
+    a.pos[s].w = (double)r0.x;
+    atomicMax(hmax_bits, __float_as_uint(r0.x));
+  }
+  float4 th = a.th[s];
+  if (mask & SWH_HALO_RHO) th.y = r0.y;
+  if (mask & SWH_HALO_PC) {
+    th.z = r0.z;
+    th.w = r0.w;
+  }
+  a.th[s] = th;
+  float4 fc = a.fc[s];
+  if (mask & SWH_HALO_F_BALSARA) {
+    fc.x = r1.x;
+    fc.y = r1.y;
+  }
+  if (mask & SWH_HALO_ALPHAS) {
+    fc.z = r1.z;
+    fc.w = r1.w;
+  }
+  a.fc[s] = fc;
+}
+
 // cell_start[c] = first sorted index with key >= c (c in [0, ncell]).
 __global__ void cell_start_kernel(const uint32_t* __restrict__ keys, int64_t n, int ncell,
                                   int* __restrict__ start) {
@@ -357,6 +404,8 @@ SoA soa_of(swh_space* s) {
   a.hdt = s->hdt.as<float>();
   a.mintb = s->mintb.as<int8_t>();
   a.perm = s->perm.as<int>();
+  a.iperm = s->iperm.as<int>();
+  a.n_owned = (int)std::min<int64_t>(s->n_owned, INT32_MAX);
   return a;
 }
 
@@ -384,6 +433,8 @@ static SoA soa_carve(char* base, int64_t n) {
   a.acc = reinterpret_cast<float4*>(take(n * sizeof(float4)));
   a.hdt = reinterpret_cast<float*>(take(n * sizeof(float)));
   a.perm = reinterpret_cast<int*>(take(n * sizeof(int)));
+  a.iperm = nullptr;
+  a.n_owned = INT32_MAX;
   a.tb = reinterpret_cast<int8_t*>(take(n));
   a.mintb = reinterpret_cast<int8_t*>(take(n));
   return a;
@@ -419,6 +470,7 @@ static swh_status reserve_soa(swh_space* s, int64_t n) {
   SWH_TRY(s->hdt.reserve(n * sizeof(float)));
   SWH_TRY(s->mintb.reserve(n));
   SWH_TRY(s->perm.reserve(n * sizeof(int)));
+  SWH_TRY(s->iperm.reserve(n * sizeof(int)));
   SWH_TRY(s->ncount.reserve(n * sizeof(int)));
   return SWH_OK;
 }
@@ -462,7 +514,8 @@ swh_status swh_space_destroy(swh_space* s) {
                     &s->seg_off, &s->keys, &s->keys2, &s->idx, &s->idx2, &s->sort_tmp,
                     &s->scan_tmp, &s->counters, &s->tmp_soa, &s->ghost_left,
                     &s->ghost_right, &s->ghost_list, &s->ghost_list2, &s->ghost_flag,
-                    &s->nbr, &s->nbr_cnt, &s->nbr_base, &s->nbr_reach, &s->nbr_ovf, &s->posf};
+                    &s->nbr, &s->nbr_cnt, &s->nbr_base, &s->nbr_reach, &s->nbr_ovf, &s->posf,
+                    &s->iperm};
   for (DevBuf* b : bufs) b->release();
   s->hstage.release();
   if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
@@ -535,6 +588,7 @@ swh_status swh_space_upload_parts(swh_space* s, const void* parts, int64_t count
   SWH_HIP(hipSetDevice(s->ctx->device));
   s->layout = L;
   s->n = count;
+  s->n_owned = count;
   s->built = false;
   s->list_valid = false;
   if (count == 0) return SWH_OK;
@@ -573,6 +627,47 @@ swh_status swh_space_download_parts(swh_space* s, void* parts, const swh_part_la
                          on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
                          s->stream));
   SWH_HIP(hipStreamSynchronize(s->stream));
+  return SWH_OK;
+}
+
+swh_status swh_space_set_owned(swh_space* s, int64_t n_owned) {
+  if (!s || n_owned < 0 || n_owned > s->n) return SWH_ERR_ARG;
+  s->n_owned = n_owned;
+  s->list_valid = false;  // the lists hold owned (active) particles only
+  return SWH_OK;
+}
+
+static swh_status halo_check(swh_space* s, const int32_t* idx, int32_t n, const void* buf) {
+  if (!s || n < 0 || (n > 0 && (!idx || !buf))) return SWH_ERR_ARG;
+  if (n > 0 && !s->built) {
+    set_error("swh_space_rebuild must precede the halo exchange");
+    return SWH_ERR_STATE;
+  }
+  return SWH_OK;
+}
+
+swh_status swh_space_pack_halo(swh_space* s, const int32_t* idx, int32_t n, float* out) {
+  SWH_TRY(halo_check(s, idx, n, out));
+  if (n == 0) return SWH_OK;
+  SWH_HIP(hipSetDevice(s->ctx->device));
+  hipLaunchKernelGGL(halo_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, s->stream,
+                     soa_of(s), idx, n, reinterpret_cast<float4*>(out));
+  SWH_HIP(hipGetLastError());
+  return SWH_OK;
+}
+
+swh_status swh_space_unpack_halo(swh_space* s, const int32_t* idx, int32_t n, const float* in,
+                                 int fields) {
+  SWH_TRY(halo_check(s, idx, n, in));
+  if (fields & ~SWH_HALO_ALL) return SWH_ERR_ARG;
+  if (n == 0) return SWH_OK;
+  SWH_HIP(hipSetDevice(s->ctx->device));
+  hipLaunchKernelGGL(halo_unpack_kernel, dim3((n + 255) / 256), dim3(256), 0, s->stream,
+                     soa_of(s), idx, n, reinterpret_cast<const float4*>(in), fields,
+                     s->counters.as<unsigned int>() + 2);
+  SWH_HIP(hipGetLastError());
+  // a halo h that grew can bring new force pairs (r < H_j): relist
+  if (fields & SWH_HALO_H) s->list_valid = false;
   return SWH_OK;
 }
 
@@ -691,6 +786,9 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
                      s->idx2.as<const int>(), n);
   SWH_HIP(hipGetLastError());
   SWH_TRY(copy_soa(tmp, s, st));
+  hipLaunchKernelGGL(iperm_kernel, dim3(grid), dim3(block), 0, st, s->perm.as<const int>(), n,
+                     s->iperm.as<int>());
+  SWH_HIP(hipGetLastError());
   // 4. cell starts
   hipLaunchKernelGGL(cell_start_kernel, dim3((int)((n + 1 + block - 1) / block)), dim3(block),
                      0, st, s->keys2.as<const uint32_t>(), n, g.ncell,

@@ -157,7 +157,7 @@ __device__ __forceinline__ void tile4_loop(const GridDev& g, SoA& a,
   const int gid = wg * NS + row;
   const int2 gr = gid < ngroups ? groups[gid] : make_int2(0, 0);
   const int i = r < gr.y ? gr.x + r : -1;
-  const bool act = i >= 0 && a.tb[i] <= max_active_bin;
+  const bool act = i >= 0 && active_part(a, i, max_active_bin);
   S st;
   st.n = 0;
   double4 pi = make_double4(0., 0., 0., 0.);

@@ -231,7 +231,7 @@ __device__ __forceinline__ void tile5_loop(const GridDev& g, SoA& a,
   const int gid = xcd_block_id();
   const int2 gr = gid < ngroups ? groups[gid] : make_int2(0, 0);
   const int i = il < gr.y ? gr.x + il : -1;
-  const bool act = i >= 0 && a.tb[i] <= max_active_bin;
+  const bool act = i >= 0 && active_part(a, i, max_active_bin);
   S st;
   st.n = 0;
   double4 pi = make_double4(0., 0., 0., 0.);

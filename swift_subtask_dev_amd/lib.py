@@ -37,6 +37,7 @@ HIP_SYMBOLS = [
     "swh_space_reset_acceleration",
     "swh_density_loop", "swh_ghost", "swh_gradient_loop", "swh_extra_ghost", "swh_force_loop",
     "swh_end_force", "swh_space_sync", "swh_space_set_tuning", "swh_space_get_info",
+    "swh_space_set_owned", "swh_space_pack_halo", "swh_space_unpack_halo",
     "swh_gspace_create",
     "swh_gspace_destroy", "swh_gspace_upload", "swh_gspace_set_leaves", "swh_grav_pp_batch",
     "swh_gspace_download", "swh_gspace_sync",
@@ -113,6 +114,9 @@ def load() -> C.CDLL:
         "swh_force_loop": (C.c_int, [vp, P(abi.HydroParams), P(i64)]),
         "swh_end_force": (C.c_int, [vp, P(abi.HydroParams)]),
         "swh_space_sync": (C.c_int, [vp]),
+        "swh_space_set_owned": (C.c_int, [vp, i64]),
+        "swh_space_pack_halo": (C.c_int, [vp, vp, i32, vp]),
+        "swh_space_unpack_halo": (C.c_int, [vp, vp, i32, vp, C.c_int]),
         "swh_space_set_tuning": (C.c_int, [vp, P(abi.Tuning)]),
         "swh_space_get_info": (C.c_int, [vp, P(abi.SpaceInfo)]),
         "swh_gspace_create": (C.c_int, [vp, P(vp)]),
@@ -330,6 +334,19 @@ class HydroSpace:
 
     def sync(self):
         _check(self._lib.swh_space_sync(self.handle), "sync")
+
+    def set_owned(self, n_owned: int):
+        """Caller indices >= n_owned become read-only halo (foreign) particles."""
+        _check(self._lib.swh_space_set_owned(self.handle, n_owned), "set_owned")
+
+    def pack_halo(self, idx_ptr: int, n: int, out_ptr: int):
+        """Device pointers: int32 caller indices -> n * 8 float halo records."""
+        _check(self._lib.swh_space_pack_halo(self.handle, C.c_void_p(idx_ptr), n,
+                                             C.c_void_p(out_ptr)), "pack_halo")
+
+    def unpack_halo(self, idx_ptr: int, n: int, in_ptr: int, fields: int = 31):
+        _check(self._lib.swh_space_unpack_halo(self.handle, C.c_void_p(idx_ptr), n,
+                                               C.c_void_p(in_ptr), fields), "unpack_halo")
 
     def hydro_step(self, P):
         """The full SPHENIX hydro chain of one step:

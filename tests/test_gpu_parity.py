@@ -625,3 +625,33 @@ def test_headline_128_force_vs_f64(gpu_ctx, headline_state):
     assert_close(g["u_dt"], o["u_dt"], 5e-5, 1e-4, "u_dt")
     assert_close(g["h_dt"], o["h_dt"], 5e-5, 1e-4, "h_dt")
     assert np.array_equal(g["min_ngb_time_bin"], o["min_ngb_time_bin"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,cdim,periodic,truncated", [(32, 4, False, 0), (40, 5, True, 1)])
+def test_grav_bench_geometry_vs_oracle(gpu_ctx, n, cdim, periodic, truncated):
+    """P2P at the bench's geometry scaled down (BASELINE config 4: uniform DM
+    box, softening 0.001, leaves of ~400-500 gparts, every leaf with itself and
+    its 26 neighbours) vs the fp64 oracle's runner_doself/dopair_grav_pp:
+    a_grav and potential to 1e-6 (floor 1e-6 of the column maximum), exact
+    interaction count."""
+    from swift_subtask_dev_amd import lib
+    gp = ics.uniform_gravity_box(n, epsilon=0.001, seed=7)
+    gs, leaves = ics.leaf_cells(gp, cdim)
+    offs, pairs = ics.neighbour_pairs(cdim, periodic=periodic, truncated=truncated)
+    G = abi.GravParams(1 if periodic else 0, (C.c_float * 3)(1, 1, 1),
+                       1.0 / 0.3 if truncated else 0.0, 0.0 if truncated else 1e30,
+                       abi.NUM_TIME_BINS)
+    g = abi.copy_parts(gs)
+    sp = lib.GravSpace(gpu_ctx)
+    sp.upload(g)
+    sp.set_leaves(leaves, offs, pairs)
+    ng = sp.pp(G)
+    sp.download(g)
+    sp.close()
+    o = abi.copy_parts(gs)
+    no = O.fn("f64", "grav_pp_leaves")(o.ctypes.data, leaves.ctypes.data, len(leaves),
+                                       offs.ctypes.data, pairs.ctypes.data, C.byref(G))
+    assert ng == no
+    assert_close(g["a_grav"], o["a_grav"], 1e-6, 1e-6, "a_grav")
+    assert_close(g["potential"], o["potential"], 1e-6, 1e-6, "potential")

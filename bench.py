@@ -11,10 +11,13 @@ force-loop inputs in an untimed setup. Timed per step, on the library's HIP
 stream: hydro_init_part + density gather, hydro_reset_acceleration + force
 gather.
 
-Multi-GPU (weak scaling): the periodic box is N unit Sedov cubes along x,
-one x-slab per rank; each rank holds its slab + a read-only halo and runs the
-loops for its own particles — no collective in the data path
-(swift_subtask_dev_amd/decomp.py).
+Multi-GPU (default --scaling strong): the one 128^3 box is split into N
+blocks (2x1x1, 2x2x1, 2x2x2); each rank holds its block + a read-only halo
+(everything within gamma h_max), runs the loops for its own particles, and
+between density and force refreshes the halo's rho point-to-point
+(batch_isend_irecv over RCCL; swift_subtask_dev_amd/decomp.py). The timed step
+includes that exchange. --scaling weak: N unit cubes along x, one x-slab per
+rank, no exchange.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun ... bench.py --gpus N   (one process per GPU)
@@ -34,6 +37,8 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
+
+from swift_subtask_dev_amd import decomp  # noqa: E402  (numpy only)
 
 METRIC = "particle-pair interactions/s (density+force) on SedovBlast_3D 128³; 1/2/4/8 GPU"
 HBM_PEAK = 8.0e12       # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -300,6 +305,9 @@ def main():
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-runs", type=int, default=3)
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong: the 128^3 box split over the GPUs (the metric); "
+                         "weak: one 128^3 box per GPU")
     ap.add_argument("--workload", default="sedov", choices=["sedov", "grav", "eagle"],
                     help="sedov: the headline metric (SedovBlast_3D 128^3 density + force); "
                          "grav: BASELINE config 4 (uniform DM box P2P, --n 256); "
@@ -331,8 +339,10 @@ def main():
 
     n = args.n
     t_setup = time.time()
-    parts = ics.sedov_slabs(n, world)
-    box = (float(world), 1.0, 1.0)
+    strong = args.scaling == "strong"
+    nslab = 1 if strong else world
+    parts = ics.sedov_slabs(n, nslab)
+    box = (float(nslab), 1.0, 1.0)
     P = abi.default_hydro_params(box, True)
     P.max_active_bin = 1
     ctx = lib.Context(local_rank, args.precision)
@@ -347,17 +357,27 @@ def main():
     sp.close()
     hmax = float(parts["h"].max()) * 1.825742
 
-    local, n_owned = decomp.slab_local_set(parts, rank, world, box[0], 1.02 * hmax)
+    if strong:
+        # one box, world blocks (2x2x2 at 8 GPUs); halo = everything within
+        # gamma h_max of the block (decomp.py)
+        plan = decomp.HaloPlan(parts["x"], box, world, rank, 1.01 * hmax)
+        local, n_owned = plan.local_set(parts), plan.n_owned
+    else:
+        plan = None
+        local, n_owned = decomp.slab_local_set(parts, rank, world, box[0], 1.02 * hmax,
+                                               halo_time_bin=None)
     del parts
     sp = lib.HydroSpace(ctx)
     sp.set_tuning(args.cell_factor, args.loop_variant, args.group_size, args.cell_scale,
                   args.diag_mode, args.list_capacity, args.list_skin)
-    # a dedicated (non-NULL) stream: the library's kernels and the timing
-    # events share it, so the events bracket exactly the loop kernels
+    # a dedicated (non-NULL) stream: the library's kernels, the halo exchange
+    # and the timing events share it, so the events bracket exactly the loops
     stream = torch.cuda.Stream()
     sp.set_stream(stream.cuda_stream)
     sp.upload(local)
+    sp.set_owned(n_owned)
     sp.rebuild(P)
+    exchanger = decomp.DeviceHalo(plan, sp, dist, torch, stream) if plan and world > 1 else None
     # exact interaction counts of one step (same work every step: h is fixed)
     sp.init_parts(P)
     n_density = sp.density(P)
@@ -379,6 +399,8 @@ def main():
         sp.density(P, count=False)
         if ev:
             ev[1].record(stream)
+        if exchanger:  # the force loop reads the neighbours' new rho
+            exchanger.refresh(abi.HALO_RHO)
         sp.reset_acceleration(P)
         if ev:
             ev[2].record(stream)
@@ -432,15 +454,21 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64" if args.precision == "f64" else "f32",
             "data": "synthetic (SedovBlast_3D-like perturbed lattice, eta=1.2348; glass IC unavailable offline)",
             "config": {
-                "workload": f"SedovBlast_3D {n}^3 per GPU: density + force loops (SPHENIX, cubic spline)",
+                "workload": (f"SedovBlast_3D {n}^3 split over {world} GPU(s)" if strong else
+                             f"SedovBlast_3D {n}^3 per GPU") +
+                            ": density + force loops (SPHENIX, cubic spline)",
                 "particles_per_gpu": n_owned,
                 "global_particles": int(total_owned),
-                "decomposition": f"{world} x-slab(s) + read-only halo, no data-path collective",
+                "decomposition": (f"{'x'.join(map(str, decomp.block_dims(world)))} blocks + "
+                                  "read-only halo, halo rho refreshed point-to-point "
+                                  "between density and force"
+                                  if strong else
+                                  f"{world} x-slab(s) + read-only halo, no data-path collective"),
                 "density_interactions_per_step": n_density,
                 "force_interactions_per_step": n_force,
                 "cell_factor": args.cell_scale or args.cell_factor,

@@ -1,10 +1,19 @@
-"""Multi-process decomposition (bench.py's weak-scaling layout) on CPU with
-the gloo backend, world_size 2 and 3: every rank holds its x-slab + a
-read-only halo (swift_subtask_dev_amd/decomp.py) and evaluates the loops of
-its own particles; the union over ranks must equal the single-domain result
-and the interaction counts must add up, with no data-path collective (only
-the test's final gather). The oracle stands in for the GPU here (no GPU in
-CI); the GPU path runs the same decomposition in bench.py."""
+"""Multi-process decomposition on CPU with the gloo backend.
+
+* bench.py --scaling weak: every rank holds its x-slab + a read-only halo and
+  evaluates the loops of its own particles; the union over ranks must equal
+  the single-domain result and the interaction counts must add up, with no
+  data-path exchange.
+* bench.py --scaling strong (the metric): one box split into 2x1x1 / 2x2x1
+  blocks (decomp.HaloPlan); a whole SPHENIX step (density, ghost
+  h-iteration, halo refresh of h/rho/P/c/f/balsara, gradient, extra ghost,
+  halo refresh of the alphas, force) run per block with the point-to-point
+  halo exchange (decomp.exchange) must reproduce the single-domain step.
+
+The oracle stands in for the GPU here (no GPU in CI); the GPU variant of the
+strong test (two ranks sharing cuda:0, gloo host staging, the library's
+set_owned + pack_halo/unpack_halo) is marked gpu.
+"""
 from __future__ import annotations
 
 import ctypes as C
@@ -16,6 +25,8 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+GAMMA = 1.825742  # cubic spline H/h in 3D
+
 
 def _free_port():
     s = socket.socket()
@@ -25,35 +36,60 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, queue):
+def _spawn(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return out
+
+
+def _init(rank, world, port):
     import sys
     from pathlib import Path
 
     root = Path(__file__).resolve().parents[1]
     sys.path.insert(0, str(root))
     sys.path.insert(0, str(root / "tests"))
-    import oracle_lib as O
-    from swift_subtask_dev_amd import abi, decomp, ics
-
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    parts = ics.sedov_slabs(n, world, pert=0.2, seed=42)
-    box = (float(world), 1.0, 1.0)
-    P = abi.default_hydro_params(box, True)
-    P.max_active_bin = 1
-    hmax = float(parts["h"].max()) * 1.825742
-    local, n_owned = decomp.slab_local_set(parts, rank, world, box[0], 1.02 * hmax)
-    O.fn("f32", "init_parts")(local.ctypes.data, len(local), C.byref(P))
-    nd = O.fn("f64", "box_density")(local.ctypes.data, len(local), C.byref(P), None)
-    owned = local[:n_owned]
-    res = {"id": owned["id"].copy(), "rho": owned["rho"].copy(),
-           "div_v": owned["div_v"].copy(), "n": nd}
+
+
+def _gather(rank, world, res, queue):
     out = [None] * world
     dist.all_gather_object(out, res)
     if rank == 0:
         queue.put(out)
     dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------
+# weak scaling: x-slabs, no exchange
+# --------------------------------------------------------------------------
+
+def _slab_worker(rank, world, port, queue, n):
+    _init(rank, world, port)
+    import oracle_lib as O
+    from swift_subtask_dev_amd import abi, decomp, ics
+
+    parts = ics.sedov_slabs(n, world, pert=0.2, seed=42)
+    box = (float(world), 1.0, 1.0)
+    P = abi.default_hydro_params(box, True)
+    P.max_active_bin = 1
+    hmax = float(parts["h"].max()) * GAMMA
+    local, n_owned = decomp.slab_local_set(parts, rank, world, box[0], 1.02 * hmax)
+    O.fn("f32", "init_parts")(local.ctypes.data, len(local), C.byref(P))
+    nd = O.fn("f64", "box_density")(local.ctypes.data, len(local), C.byref(P), None)
+    owned = local[:n_owned]
+    _gather(rank, world, {"id": owned["id"].copy(), "rho": owned["rho"].copy(),
+                          "div_v": owned["div_v"].copy(), "n": nd}, queue)
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -62,16 +98,7 @@ def test_slab_decomposition_matches_single_domain(world):
     import oracle_lib as O
 
     n = 10
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    out = q.get(timeout=300)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    out = _spawn(_slab_worker, world, n)
     parts = ics.sedov_slabs(n, world, pert=0.2, seed=42)
     P = abi.default_hydro_params((float(world), 1.0, 1.0), True)
     P.max_active_bin = 1
@@ -85,3 +112,201 @@ def test_slab_decomposition_matches_single_domain(world):
     ref = parts[np.argsort(parts["id"])]
     assert np.array_equal(rho[order], ref["rho"])
     assert np.array_equal(np.concatenate([r["div_v"] for r in out])[order], ref["div_v"])
+
+
+# --------------------------------------------------------------------------
+# strong scaling: blocks + halo refresh
+# --------------------------------------------------------------------------
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_halo_plan_is_consistent_and_complete(world):
+    """Every rank derives the same plan: what r sends q is exactly q's halo
+    group from r, in order; owned sets partition the box; every particle
+    within `reach` of an owned particle is in the owner's local set."""
+    from scipy.spatial import cKDTree
+
+    from swift_subtask_dev_amd import decomp, ics
+
+    parts = ics.sedov_slabs(12, 1, pert=0.2, seed=7)
+    x = np.mod(parts["x"], 1.0)
+    reach = 0.17
+    plans = [decomp.HaloPlan(parts["x"], (1.0, 1.0, 1.0), world, r, reach) for r in range(world)]
+    owned = np.concatenate([p.owned for p in plans])
+    assert np.array_equal(np.sort(owned), np.arange(len(parts)))
+    tree = cKDTree(x, boxsize=1.0)
+    for r, p in enumerate(plans):
+        assert p.n_local == p.n_owned + len(p.halo)
+        for q, idx in p.send.items():
+            s, c = plans[q].recv[r]
+            assert np.array_equal(p.owned[idx], plans[q].halo[s - plans[q].n_owned:
+                                                                s - plans[q].n_owned + c])
+            assert np.array_equal(plans[q].recv_idx[r], np.arange(s, s + c))
+        assert set(p.recv) == {q for q in range(world) if r in plans[q].send}
+        local = set(p.owned.tolist()) | set(p.halo.tolist())
+        need = set()
+        for nb in tree.query_ball_point(x[p.owned], reach * 0.999):
+            need.update(nb)
+        assert need <= local
+
+
+def _exchange_host(plan, local, fields):
+    """decomp.exchange with host halo records (the oracle's side)."""
+    import torch
+
+    from swift_subtask_dev_amd import decomp
+
+    def alloc(n):
+        return torch.empty(n * len(decomp.HALO_FIELDS), dtype=torch.float32)
+
+    def pack(q, buf):
+        buf.copy_(torch.from_numpy(decomp.pack_host(local, plan.send[q] ).ravel()))
+
+    def unpack(q, buf):
+        decomp.unpack_host(local, plan.recv_idx[q], buf.numpy().reshape(-1, 8), fields)
+
+    decomp.exchange(plan, dist, pack, unpack, alloc)
+
+
+STEP_FIELDS = ("rho", "h", "pressure", "soundspeed", "f", "balsara", "laplace_u",
+               "visc_alpha", "diff_alpha", "a_hydro", "u_dt", "h_dt", "v_sig")
+
+
+def _step_oracle(parts, P, plan=None):
+    """The SPHENIX chain of one step through the f64 oracle; with a plan, the
+    halo refreshes of the decomposed step between the phases."""
+    import oracle_lib as O
+    from swift_subtask_dev_amd import decomp
+
+    f = lambda n: O.fn("f64", n)  # noqa: E731
+    N = len(parts)
+    O.fn("f32", "init_parts")(parts.ctypes.data, N, C.byref(P))
+    counts = [f("box_density")(parts.ctypes.data, N, C.byref(P), None)]
+    nfail = C.c_longlong(0)
+    f("box_ghost")(parts.ctypes.data, N, C.byref(P), C.byref(nfail))
+    if plan:
+        _exchange_host(plan, parts, decomp.HALO_AFTER_GHOST)
+    parts["laplace_u"] = 0
+    counts.append(f("box_gradient")(parts.ctypes.data, N, C.byref(P), None))
+    f("box_extra_ghost")(parts.ctypes.data, N, C.byref(P))
+    if plan:
+        _exchange_host(plan, parts, decomp.HALO_AFTER_EXTRA_GHOST)
+    counts.append(f("box_force")(parts.ctypes.data, N, C.byref(P), None))
+    f("box_end_force")(parts.ctypes.data, N, C.byref(P))
+    return counts, nfail.value
+
+
+def _strong_worker(rank, world, port, queue, n, reach):
+    _init(rank, world, port)
+    from swift_subtask_dev_amd import abi, decomp, ics
+
+    parts = ics.sedov_slabs(n, 1, pert=0.2, seed=42)
+    P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
+    P.max_active_bin = 1
+    plan = decomp.HaloPlan(parts["x"], (1.0, 1.0, 1.0), world, rank, reach)
+    # the oracle has no ownership: the halo is inactive via its time bin
+    local = plan.local_set(parts, halo_time_bin=2)
+    counts, nfail = _step_oracle(local, P, plan)
+    own = local[: plan.n_owned]
+    res = {"id": own["id"].copy(), "counts": counts, "nfail": nfail,
+           "hmax": float(own["h"].max())}
+    res.update({k: own[k].copy() for k in STEP_FIELDS})
+    _gather(rank, world, res, queue)
+
+
+def _compare_step(out, ref, rtol):
+    ids = np.concatenate([r["id"] for r in out])
+    assert len(ids) == len(ref) and len(np.unique(ids)) == len(ref)
+    order = np.argsort(ids)
+    ref = ref[np.argsort(ref["id"])]
+    for k in STEP_FIELDS:
+        got = np.concatenate([r[k] for r in out])[order].astype(np.float64)
+        want = ref[k].astype(np.float64)
+        scale = np.abs(want).max() + 1e-30
+        err = np.abs(got - want).max() / scale
+        assert err <= rtol, f"{k}: max err {err:.3e} (scale {scale:.3e})"
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_block_decomposition_full_step_matches_single_domain(world):
+    from swift_subtask_dev_amd import abi, ics
+
+    n = 16
+    parts = ics.sedov_slabs(n, 1, pert=0.2, seed=42)
+    P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
+    P.max_active_bin = 1
+    ref = parts.copy()
+    h0 = float(parts["h"].max())
+    counts, nfail = _step_oracle(ref, P)
+    # reach: gamma * the largest h the ghost iteration can try (its Newton
+    # steps are clamped to 2x; the converged h stay well below that)
+    reach = 1.5 * GAMMA * max(h0, float(ref["h"].max()))
+    out = _spawn(_strong_worker, world, n, reach)
+    assert [sum(r["counts"][k] for r in out) for k in range(3)] == counts
+    assert sum(r["nfail"] for r in out) == nfail
+    assert max(r["hmax"] for r in out) * GAMMA < reach
+    _compare_step(out, ref, 1e-5)
+
+
+def _strong_gpu_worker(rank, world, port, queue, n, reach):
+    _init(rank, world, port)
+    import torch
+
+    from swift_subtask_dev_amd import abi, decomp, ics, lib
+
+    torch.cuda.set_device(0)
+    parts = ics.sedov_slabs(n, 1, pert=0.2, seed=42)
+    P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
+    P.max_active_bin = 1
+    plan = decomp.HaloPlan(parts["x"], (1.0, 1.0, 1.0), world, rank, reach)
+    local = plan.local_set(parts)
+    ctx = lib.Context(0, "f64")
+    sp = lib.HydroSpace(ctx)
+    stream = torch.cuda.Stream()
+    halo = decomp.DeviceHalo(plan, sp, dist, torch, stream)
+    sp.upload(local)
+    sp.set_owned(plan.n_owned)
+    sp.rebuild(P)
+    sp.init_parts(P)
+    counts = [sp.density(P)]
+    it, nfail = sp.ghost(P)
+    halo.refresh(decomp.HALO_AFTER_GHOST)
+    counts.append(sp.gradient(P))
+    sp.extra_ghost(P)
+    halo.refresh(decomp.HALO_AFTER_EXTRA_GHOST)
+    counts.append(sp.force(P))
+    sp.end_force(P)
+    sp.download(local, abi.FIELDS_ALL)
+    sp.close()
+    ctx.close()
+    own = local[: plan.n_owned]
+    res = {"id": own["id"].copy(), "counts": counts, "nfail": nfail,
+           "hmax": float(own["h"].max())}
+    res.update({k: own[k].copy() for k in STEP_FIELDS})
+    _gather(rank, world, res, queue)
+
+
+@pytest.mark.gpu
+def test_block_decomposition_full_step_gpu_matches_single_domain():
+    """Two ranks on cuda:0 (gloo, host-staged halo records) vs the library's
+    own single-domain step."""
+    from swift_subtask_dev_amd import abi, ics, lib
+
+    n, world = 16, 2
+    parts = ics.sedov_slabs(n, 1, pert=0.2, seed=42)
+    P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
+    P.max_active_bin = 1
+    ctx = lib.Context(0, "f64")
+    sp = lib.HydroSpace(ctx)
+    sp.upload(parts)
+    sp.rebuild(P)
+    h0 = float(parts["h"].max())
+    chain = sp.hydro_step(P)
+    ref = parts.copy()
+    sp.download(ref, abi.FIELDS_ALL)
+    sp.close()
+    ctx.close()
+    reach = 1.5 * GAMMA * max(h0, float(ref["h"].max()))
+    out = _spawn(_strong_gpu_worker, world, n, reach)
+    assert [sum(r["counts"][k] for r in out) for k in range(3)] == \
+        [chain["density"], chain["gradient"], chain["force"]]
+    _compare_step(out, ref, 1e-5)

@@ -1,0 +1,4 @@
+#!/bin/bash
+tools/gpu_steps.sh \
+ "900:t_all:python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread" \
+ "400:bench:python -u bench.py"

@@ -10,6 +10,7 @@
 // the step's pair lists (swh_list.h); the tile loops (swh_tile4.h,
 // swh_tile5.h) search and interact in one launch; gather_direct
 // (swh_gather.h) serves subsets and list overflow.
+#include <cstring>
 #include "swh_gather.h"
 #include "swh_internal.h"
 #include "swh_list.h"
@@ -720,11 +721,24 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
     std::swap(list, list2);
     if (count > 0) SWH_TRY(launch_loop<LOOP_DENSITY>(s, P, list, count, false));
   }
-  if (lreach) {
-    unsigned int stale = 0;
-    SWH_HIP(hipMemcpyAsync(&stale, stale_slot(s), sizeof(stale), hipMemcpyDeviceToHost, st));
+  {
+    // slots 2 (max h) .. 17 (list-stale flag) in one read
+    unsigned int c[18];
+    SWH_HIP(hipMemcpyAsync(c, s->counters.ptr, sizeof(c), hipMemcpyDeviceToHost, st));
     SWH_HIP(hipStreamSynchronize(st));
-    if (stale) s->list_valid = false;  // gradient / force rebuild the lists
+    if (lreach && c[17]) s->list_valid = false;  // gradient / force rebuild the lists
+    float hmax;
+    std::memcpy(&hmax, &c[2], sizeof(hmax));
+    // a kernel reach of half the periodic box or more would need more than
+    // the nearest image (runner_doiact_functions_hydro.h:2283, "Cell smaller
+    // than smoothing length")
+    if (s->grid.periodic &&
+        (double)hmax * kGamma >= 0.5 * std::min(s->grid.dim[0], std::min(s->grid.dim[1],
+                                                                         s->grid.dim[2]))) {
+      swh::set_error("Cell smaller than smoothing length: gamma*h_max=%g, box %g", hmax * kGamma,
+                     std::min(s->grid.dim[0], std::min(s->grid.dim[1], s->grid.dim[2])));
+      return SWH_ERR_CELL_SMALL;
+    }
   }
   if (iterations) *iterations = it;
   if (n_unconverged) *n_unconverged = count;

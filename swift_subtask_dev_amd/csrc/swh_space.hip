@@ -729,6 +729,16 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
   }
   for (int k = 0; k < 3; k++) g.w[k] = g.dim[k] / g.cdim[k];
   g.ncell = (int)total;
+  if (g.periodic) {
+    // the loops take the nearest periodic image only: the kernel reach must
+    // stay below half the box (runner_doiact_functions_hydro.h:2283)
+    const double dmin = std::min(g.dim[0], std::min(g.dim[1], g.dim[2]));
+    if (g.hmax >= 0.5 * dmin) {
+      s->built = false;
+      swh::set_error("Cell smaller than smoothing length: gamma*h_max=%g, box %g", g.hmax, dmin);
+      return SWH_ERR_CELL_SMALL;
+    }
+  }
   const int block = 256;
   const int64_t nsort = std::max<int64_t>(n, g.ncell);
   SWH_TRY(s->keys.reserve(nsort * sizeof(uint32_t)));

@@ -265,6 +265,53 @@ def test_dosub_gradient_runs_leaf_pairs(adapter):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_branch_gradient_per_task(adapter, prec):
+    """The per-task gradient entries themselves (runner_doself1_branch_gradient
+    + 26 runner_dopair1_branch_gradient on unsplit, sorted top-level cells,
+    SPHENIX runner_iact_nonsym_gradient, hydro_iact.h:276-329) == the f64
+    oracle's gradient loop on the same periodic box: v_sig and
+    alpha_visc_max_ngb are maxima (exact up to the float rounding of one
+    term), laplace_u a sum."""
+    P = abi.default_hydro_params((3.0, 3.0, 3.0), True)
+    parts, bounds, locs = tree27(11, "divergent", 1.1)
+    rng = np.random.Generator(np.random.PCG64(11))
+    n = len(parts)
+    parts["rho"] = rng.uniform(0.8, 1.2, n)
+    parts["u"] = rng.uniform(0.5, 1.5, n)
+    parts["soundspeed"] = rng.uniform(0.5, 1.0, n)
+    parts["visc_alpha"] = rng.uniform(0, 1, n)
+    for f in ("v_sig", "laplace_u", "alpha_visc_max_ngb"):
+        parts[f] = 0
+    o = abi.copy_parts(parts)
+    adapter.swifthip_swift_set_precision(1 if prec == "f64" else 0)
+    cs = O.CellSet(parts, bounds, locs, 1.0)
+    cs.sort_all()
+    eb = abi.EngineBundle(dim=(3.0, 3.0, 3.0), periodic=True, params=P)
+    r = C.addressof(eb.runner)
+    adapter.swifthip_swift_clear_error()
+    adapter.runner_doself1_branch_gradient(r, cs.ptr(MAIN))
+    for j in range(27):
+        if j != MAIN:
+            adapter.runner_dopair1_branch_gradient(r, cs.ptr(MAIN), cs.ptr(j))
+    err_msg = adapter.swifthip_swift_last_error()
+    adapter.swifthip_swift_set_precision(1)
+    assert not err_msg, err_msg
+    cs.free_sorts()
+    O.fn("f64", "box_gradient")(o.ctypes.data, len(o), C.byref(P), None)
+    s, e = bounds[MAIN]
+    # each of the 27 tasks writes its partial laplace_u sum back into the
+    # float struct part field (as SWIFT's runners do): measured 1.1e-5 (f64
+    # arithmetic) at the 1e-6 floor of this cancelling sum
+    tol = 2e-5
+    for f in ("v_sig", "laplace_u", "alpha_visc_max_ngb"):
+        a, b = parts[f][s:e].astype(np.float64), o[f][s:e].astype(np.float64)
+        fl = 1e-6 * max(np.abs(b).max(), 1e-30)
+        err = np.abs(a - b) / np.maximum(np.abs(b), fl)
+        assert err.max() < tol, (f, err.max())
+
+
+@pytest.mark.gpu
 def test_dosub_subset(adapter):
     """runner_dosub_subset_density (DOSUB_SUBSET, the ghost's rerun entry):
     a subset inside one progeny of the main cell against the main cell itself

@@ -206,6 +206,30 @@ def test_27cells_adapter_vs_f64(adapter):
 
 
 @pytest.mark.gpu
+def test_periodic_reach_over_half_box_is_an_error(gpu_ctx):
+    """A kernel reach >= half the periodic box would need more than the
+    nearest image: rebuild refuses it with SWH_ERR_CELL_SMALL ("Cell smaller
+    than smoothing length", runner_doiact_functions_hydro.h:2283) instead of
+    silently dropping images. 4^3 lattice in a unit box: gamma*h = 0.56."""
+    from swift_subtask_dev_amd import ics, lib
+    parts = ics.sedov_slabs(4, 1)
+    P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.upload(parts)
+    with pytest.raises(lib.SwhError) as e:
+        sp.rebuild(P)
+    assert e.value.status == 4  # SWH_ERR_CELL_SMALL
+    with pytest.raises(lib.SwhError):  # the loops refuse an unbuilt space
+        sp.density(P)
+    sp.close()
+    parts = ics.sedov_slabs(6, 1)  # gamma*h = 0.376: fine
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.upload(parts)
+    sp.rebuild(P)
+    sp.close()
+
+
+@pytest.mark.gpu
 def test_unsorted_cells_error(adapter):
     """DOPAIR1_BRANCH's "Interacting unsorted cells." precondition."""
     P = abi.default_hydro_params((3.0, 3.0, 3.0), True)

@@ -268,13 +268,63 @@ def test_interactions_per_particle():
     assert abs(per - 47.82) < 0.25, per
 
 
-def test_125cells_chain_analytic():
+# Tightest tolerances the 6^3-per-cell lattice supports for the f32 oracle
+# chain, measured over all 12 cases (x1.2-2.5 headroom): the SPH estimates
+# of rho (and P = (gamma-1) rho u) carry the lattice's 0.4 % bias; c depends
+# on u only; v_sig = max over neighbours of c_i + c_j exceeds 2 c_i where c
+# varies; a for the divergent pressure field is singular at the centre of
+# the main cell, so it is held away from the centre (r > 0.3 / 0.5).
+def _analytic125(m, vel, press):
+    """tests/test125cells.c:148-206 get_solution for the main cell."""
+    gamma, rho = 5.0 / 3.0, 2.5
+    x = m["x"].astype(np.float64)
+    n = len(m)
+    if press == "const":
+        P, gP = np.full(n, 1.5), np.zeros((n, 3))
+    elif press == "gradient":
+        P, gP = 1.5 * x[:, 0], np.zeros((n, 3))
+        gP[:, 0] = 1.5
+    else:
+        d = x - 2.5
+        r = np.sqrt((d ** 2).sum(axis=1))
+        P = r + 1.5
+        gP = np.where(r[:, None] > 0, d / np.where(r > 0, r, 1.0)[:, None], 0.0)
+    c = np.sqrt(gamma * P / rho)
+    div_v = 3.0 if vel == "divergent" else 0.0
+    return {"rho": np.full(n, rho), "pressure": P, "soundspeed": c,
+            "div_v": np.full(n, div_v), "h_dt": m["h"] * div_v / 3.0, "a_hydro": -gP / rho,
+            "v_sig": 2.0 * c, "u_dt": -(P / rho) * div_v}
+
+
+@pytest.mark.parametrize("vel", ["zero", "const", "divergent", "rotating"])
+@pytest.mark.parametrize("press", ["const", "gradient", "divergent"])
+def test_125cells_chain_analytic(vel, press):
     """tests/test125cells.c: density -> ghost -> gradient -> extra ghost ->
-    force on 5^3 cells; the main cell vs the analytic solution (get_solution:
-    rho = 2.5, a = -grad P / rho, div_v = 3 for the divergent field)."""
+    force on 5^3 cells of 6^3 particles, every velocity x pressure field of
+    the reference script (test125cells.sh: -v 0..3 -p 0..2); the main cell
+    vs every field get_solution defines."""
     from test_gpu_parity import run125_oracle
-    res = run125_oracle(vel="divergent", press="gradient")
-    main = res["main"]
-    assert np.allclose(main["rho"], 2.5, rtol=1e-2)  # SPH lattice estimate
-    assert np.allclose(main["div_v"], 3.0, rtol=2e-2)
-    assert np.allclose(main["a_hydro"][:, 0], -1.5 / 2.5, rtol=3e-2)
+    m = run125_oracle(vel=vel, press=press)["main"]
+    sol = _analytic125(m, vel, press)
+
+    def err(field, scale):
+        got = m[field].astype(np.float64)
+        return (np.abs(got - sol[field]) / scale).max()
+
+    assert err("rho", 2.5) < 5e-3
+    assert err("pressure", sol["pressure"]) < 5e-3
+    assert err("soundspeed", sol["soundspeed"]) < 2e-7
+    div_tol = 1.5e-2 if vel == "divergent" else 1e-12  # scale 3 (the divergent field)
+    assert err("div_v", 3.0) < div_tol
+    assert err("h_dt", m["h"].astype(np.float64)) < div_tol
+    pv = sol["pressure"] / 2.5
+    assert err("u_dt", 3.0 * pv) < (1e-6 if vel == "divergent" else 1e-12)
+    v_tol = {"const": 1e-6, "gradient": 5e-2, "divergent": 6e-2}[press]
+    assert err("v_sig", sol["v_sig"]) < v_tol
+    a_err = (np.abs(m["a_hydro"].astype(np.float64) - sol["a_hydro"]) / 0.6).max(axis=1)
+    if press == "divergent":
+        r = np.sqrt(((m["x"] - 2.5) ** 2).sum(axis=1))
+        assert a_err[r > 0.3].max() < 5e-2
+        assert a_err[r > 0.5].max() < 2.5e-2
+    else:
+        assert a_err.max() < (1e-6 if press == "const" else 5e-6)

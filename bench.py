@@ -41,6 +41,7 @@ sys.path.insert(0, str(ROOT))
 from swift_subtask_dev_amd import decomp  # noqa: E402  (numpy only)
 
 METRIC = "particle-pair interactions/s (density+force) on SedovBlast_3D 128³; 1/2/4/8 GPU"
+METRIC_EAGLE = "particle-pair interactions/s (density+force) on an EAGLE_6 stand-in (clustered)"
 HBM_PEAK = 8.0e12       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK = 78.6e12     # MI355X fp64 vector
 S_IN_DENSITY, S_OUT_DENSITY = 45, 32   # SURVEY 8d algorithmic bytes per particle
@@ -341,8 +342,17 @@ def main():
     t_setup = time.time()
     strong = args.scaling == "strong"
     nslab = 1 if strong else world
-    parts = ics.sedov_slabs(n, nslab)
-    box = (float(nslab), 1.0, 1.0)
+    eagle = args.workload == "eagle"
+    if eagle:
+        # EAGLE_6 stand-in: 94^3 background + 64 Plummer clumps of
+        # 13,000 (2 x 94^3-order gas particles, h spanning ~10x after the ghost)
+        if not strong:
+            raise SystemExit("--workload eagle runs one box (--scaling strong)")
+        parts = ics.clustered_box(94, n_clumps=64, per_clump=13000, seed=6)
+        box = (1.0, 1.0, 1.0)
+    else:
+        parts = ics.sedov_slabs(n, nslab)
+        box = (float(nslab), 1.0, 1.0)
     P = abi.default_hydro_params(box, True)
     P.max_active_bin = 1
     ctx = lib.Context(local_rank, args.precision)
@@ -355,6 +365,9 @@ def main():
     chain = sp.hydro_step(P)
     sp.download(parts, abi.FIELDS_ALL)
     sp.close()
+    if eagle:  # converged h: re-bin on the final smoothing lengths
+        log(f"[rank {rank}] eagle stand-in: {len(parts)} parts, h {parts['h'].min():.3g}.."
+            f"{parts['h'].max():.3g}, chain ghost iterations {chain['ghost_iterations']}")
     hmax = float(parts["h"].max()) * 1.825742
 
     if strong:
@@ -446,7 +459,7 @@ def main():
                        and args.cell_factor == 1 and args.cell_scale == 0 and args.n == 128)
         traffic = load_traffic() if default_cfg else None
         out = {
-            "metric": METRIC,
+            "metric": METRIC_EAGLE if eagle else METRIC,
             "value": total_interactions / elapsed_max,
             "unit": "interactions/s",
             "n_gpus": world,
@@ -457,9 +470,14 @@ def main():
             "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f64" if args.precision == "f64" else "f32",
-            "data": "synthetic (SedovBlast_3D-like perturbed lattice, eta=1.2348; glass IC unavailable offline)",
+            "data": ("synthetic (EAGLE_6 stand-in: perturbed 94^3 lattice + 64 Plummer clumps of "
+                     "13,000, h from the ghost; EAGLE ICs unavailable offline)" if eagle else
+                     "synthetic (SedovBlast_3D-like perturbed lattice, eta=1.2348; glass IC "
+                     "unavailable offline)"),
             "config": {
-                "workload": (f"SedovBlast_3D {n}^3 split over {world} GPU(s)" if strong else
+                "workload": (f"EAGLE_6 stand-in ({int(total_owned)} gas parts, clustered) split "
+                             f"over {world} GPU(s)" if eagle else
+                             f"SedovBlast_3D {n}^3 split over {world} GPU(s)" if strong else
                              f"SedovBlast_3D {n}^3 per GPU") +
                             ": density + force loops (SPHENIX, cubic spline)",
                 "particles_per_gpu": n_owned,
@@ -508,7 +526,11 @@ def main():
             },
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if eagle:
+            # the port's fixed cdim=20 grid puts ~10^4 clump particles in one
+            # cell (O(n^2) per cell pair): no bounded CPU sample of this box
+            out["cpu_baseline_note"] = "not timed: the CPU port's uniform grid is O(n^2) in the clumps"
+        elif world == 1 and not args.no_cpu_baseline:
             # the CPU path times the same loops on the same (prepared) inputs:
             # `local` still holds the converged chain state the GPU started from
             try:

@@ -90,8 +90,12 @@ __global__ __launch_bounds__(256) void walk_kernel(GridDev g, SoA a, ListDev ld,
   list_walk<LOOP, T, kWalkLpi>(g, a, ld, n, max_active_bin, a2H, hmax_bits, counter, ncount);
 }
 
-// The list's overflow particles (more than K hits): direct gather. The count
-// is read on the device, so the launch needs no host round trip.
+// The list's overflow particles (more than K hits: a large H in a dense
+// region): one wave per particle searches the cells around it, the 64 lanes
+// striding over each cell's particles, cells farther than max(H_i, the
+// cell's own max H) (force) or H_i (density, gradient) skipped; the lane
+// partial sums are combined at the end. The count is read on the device, so
+// the launch needs no host round trip.
 template <int LOOP, typename T>
 __global__ __launch_bounds__(256) void overflow_kernel(GridDev g, SoA a, ListDev ld,
                                                        int max_active_bin, T a2H,
@@ -99,19 +103,59 @@ __global__ __launch_bounds__(256) void overflow_kernel(GridDev g, SoA a, ListDev
                                                        unsigned long long* counter,
                                                        int* __restrict__ ncount) {
   const int nov = (int)*ld.ovf_n;
-  for (int t0 = blockIdx.x * blockDim.x; t0 < nov; t0 += gridDim.x * blockDim.x) {
-    const int t = t0 + (int)threadIdx.x;
-    const int i = t < nov ? ld.ovf[t] : -1;
-    const bool act = i >= 0 && active_part(a, i, max_active_bin);
+  const int lane = threadIdx.x & 63;
+  const int nwaves = gridDim.x * (blockDim.x / 64);
+  for (int w = blockIdx.x * (blockDim.x / 64) + (int)(threadIdx.x / 64); w < nov; w += nwaves) {
+    const int i = ld.ovf[w];
+    if (!active_part(a, i, max_active_bin)) continue;  // wave-uniform
     LoopState<LOOP, T> st;
     st.n = 0;
-    if (act) {
-      st.load_i(a, i, a2H, hmax_bits);
-      gather_direct<T>(g, a, a.pos[i], st);
+    st.load_i(a, i, a2H, hmax_bits);
+    const double4 pi = a.pos[i];
+    const double Hi = pi.w * (double)kGamma;
+    CellRange c;
+    cell_range(g, pi.x, pi.y, pi.z, st.reach, c);
+    for (int cz = c.lo[2]; cz <= c.hi[2]; cz++) {
+      double sz;
+      const int wz = wrap_cell(g, c, 2, cz, sz);
+      for (int cy = c.lo[1]; cy <= c.hi[1]; cy++) {
+        double sy;
+        const int wy = wrap_cell(g, c, 1, cy, sy);
+        for (int cx = c.lo[0]; cx <= c.hi[0]; cx++) {
+          double sx;
+          const int wx = wrap_cell(g, c, 0, cx, sx);
+          const int2 r = cell_range_of(g, wx, wy, wz);
+          if (r.y <= r.x) continue;
+          // box gap between i and this image of the cell
+          const double cl[3] = {g.origin[0] + wx * g.w[0] + sx, g.origin[1] + wy * g.w[1] + sy,
+                                g.origin[2] + wz * g.w[2] + sz};
+          const double xs[3] = {pi.x, pi.y, pi.z};
+          double gap2 = 0.;
+          for (int k = 0; k < 3; k++) {
+            if (c.full[k]) continue;
+            const double gk = fmax(fmax(cl[k] - xs[k], xs[k] - cl[k] - g.w[k]), 0.);
+            gap2 += gk * gk;
+          }
+          const int lin = (wz * g.cdim[1] + wy) * g.cdim[0] + wx;
+          const double Rc = LOOP != LOOP_FORCE ? Hi
+                            : ld.cell_R           ? fmax(Hi, (double)ld.cell_R[lin])
+                                                  : st.reach;
+          if (gap2 > Rc * Rc * (1. + 1e-6) + 1e-300) continue;
+          for (int j = r.x + lane; j < r.y; j += 64) {
+            const double4 pj = a.pos[j];
+            T dx, dy, dz;
+            const T r2 = separation<T>(g, c, pi, pj, sx, sy, sz, dx, dy, dz);
+            if (st.accept(j, pj, r2)) st.interact(a, j, pj, dx, dy, dz, r2);
+          }
+        }
+      }
+    }
+    reduce_lanes<64, T>(st);
+    if (lane == 0) {
       st.store(a, i);
       if (ncount) ncount[i] = st.n;
+      if (counter) atomicAdd(counter, (unsigned long long)st.n);
     }
-    if (counter) count_add(act ? st.n : 0, counter);
   }
 }
 
@@ -504,6 +548,8 @@ static ListDev list_dev(swh_space* s) {
   d.posf = s->posf.as<const float4>();
   d.diag = s->tuning.diag_mode;
   d.ovf_n = ovf_slot(s);
+  // per-cell reach pruning only pays on an adaptive (clustered) grid
+  d.cell_R = s->grid.adaptive ? s->cell_hreach.as<const float>() : nullptr;
   return d;
 }
 
@@ -520,8 +566,16 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
   SWH_TRY(s->nbr_reach.reserve((size_t)s->n * sizeof(float)));
   SWH_TRY(s->nbr_ovf.reserve((size_t)s->n * sizeof(int)));
   SWH_TRY(s->posf.reserve((size_t)s->n * sizeof(float4)));
+  SWH_TRY(s->cell_hreach.reserve((size_t)std::max(1, s->grid.ncell) * sizeof(float)));
   s->list_K = K;
   const ListDev ld = list_dev(s);
+  if (ld.cell_R) {
+    SWH_HIP(hipMemsetAsync(s->cell_hreach.ptr, 0, (size_t)s->grid.ncell * sizeof(float),
+                           s->stream));
+    hipLaunchKernelGGL(cell_reach_kernel, dim3((int)((s->n + 255) / 256)), dim3(256), 0,
+                       s->stream, grid_dev(s), s->pos.as<const double4>(), s->n,
+                       (float)(kGamma * ld.skin1), s->cell_hreach.as<unsigned int>());
+  }
   hipLaunchKernelGGL(posf_kernel, dim3((int)((s->n + 255) / 256)), dim3(256), 0, s->stream,
                      grid_dev(s), s->pos.as<const double4>(), s->n, s->posf.as<float4>());
   hipLaunchKernelGGL(list_prep_kernel, dim3(1), dim3(64), 0, s->stream, hmax_slot(s),

@@ -137,6 +137,7 @@ struct SwhGrid {
   int periodic = 0;
   int ncell = 0;
   double hmax = 0;  // max H = gamma*h over all particles at rebuild
+  bool adaptive = false;  // cells sized by the typical H (h spans a wide range)
 };
 
 // Device-resident particle set, sorted by grid cell in Morton order of the
@@ -176,6 +177,7 @@ struct swh_space {
   swh::DevBuf cell_rank;   // int32[ncell]: linear cell -> Morton rank
   swh::DevBuf cell_code;   // uint32[ncell]: Morton code of each rank (ascending)
   swh::DevBuf cell_span;   // int2[ncell]: linear cell -> sorted range
+  swh::DevBuf cell_hreach; // float[ncell]: max R = gamma h (1 + skin) of the cell (list build)
   int rank_cdim[3] = {0, 0, 0};  // grid the rank table was built for
   swh::DevBuf groups;      // int2[ngroups]: i-groups (start, count) of the tile loops
   swh::DevBuf seg_groups, seg_off;

@@ -60,8 +60,29 @@ struct ListDev {
                                    // this from every face need no periodic wrap
   int* ovf;      // overflow particles, count in *ovf_n
   unsigned int* ovf_n;
+  const float* cell_R;  // per linear grid cell: max R of its particles (cell_reach_kernel);
+                        // null on a uniform grid (no per-cell pruning)
   int diag;      // profiling only: 2 = the build writes no entries
 };
+
+// Per-cell maximum R = gamma h (1 + skin): the list build skips a cell whose
+// box lies farther than max(R_group, R_cell) from the group box (SWIFT's
+// per-cell h_max pruning of DOPAIR2, runner_doiact_functions_hydro.h:1424-1530).
+__global__ void cell_reach_kernel(GridDev g, const double4* __restrict__ pos, int64_t n,
+                                  float gs1, unsigned int* __restrict__ cell_R) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const double4 p = pos[j];
+  int lin = 0;
+  const double xs[3] = {p.x, p.y, p.z};
+  for (int k = 2; k >= 0; k--) {  // key_kernel's binning, linear x-fastest index
+    int ck = (int)floor((xs[k] - g.origin[k]) * g.inv_w[k]);
+    ck = ck < 0 ? 0 : (ck >= g.cdim[k] ? g.cdim[k] - 1 : ck);
+    lin = lin * g.cdim[k] + ck;
+  }
+  // positive floats order as their bit patterns
+  atomicMax(&cell_R[lin], __float_as_uint((float)(p.w * (double)gs1) * 1.0000005f));
+}
 
 template <int LPI>
 struct ListLds {
@@ -266,9 +287,22 @@ __device__ __forceinline__ void list_build(const GridDev& g, const SoA& a, const
         j0 = sp.x;
         cnt = sp.y - sp.x;
         // lower corner of this image of the cell, relative to the group centre
-        ox = (float)(g.origin[0] + wx * g.w[0] + sx - ctr[0]);
-        oy = (float)(g.origin[1] + wy * g.w[1] + sy - ctr[1]);
-        oz = (float)(g.origin[2] + wz * g.w[2] + sz - ctr[2]);
+        const double dox = g.origin[0] + wx * g.w[0] + sx - ctr[0];
+        const double doy = g.origin[1] + wy * g.w[1] + sy - ctr[1];
+        const double doz = g.origin[2] + wz * g.w[2] + sz - ctr[2];
+        ox = (float)dox;
+        oy = (float)doy;
+        oz = (float)doz;
+        if (cnt > 0 && ld.cell_R && Rmax > Rg) {
+          // prune by the cell's own reach: box gap group <-> cell (an axis
+          // spanning the whole periodic box has no gap)
+          const double gx = c.full[0] ? 0. : fmax(fmax(dox - half[0], -half[0] - dox - g.w[0]), 0.);
+          const double gy = c.full[1] ? 0. : fmax(fmax(doy - half[1], -half[1] - doy - g.w[1]), 0.);
+          const double gz = c.full[2] ? 0. : fmax(fmax(doz - half[2], -half[2] - doz - g.w[2]), 0.);
+          const double Rc = fmax(Rg, (double)ld.cell_R[(wz * g.cdim[1] + wy) * g.cdim[0] + wx]) +
+                            delta;
+          if (gx * gx + gy * gy + gz * gz > Rc * Rc * (1. + 1e-6)) cnt = 0;
+        }
       }
       int inc = cnt;
       for (int o = 1; o < 64; o <<= 1) {

@@ -8,6 +8,7 @@
 // The tile loops' i-groups are cut from that order the way SWIFT splits its
 // cell tree into leaves (space_split, cell.c): runs of consecutive cells of
 // one aligned Morton block holding <= 64 particles.
+#include <cmath>
 #include <hipcub/hipcub.hpp>
 
 #include <cstring>
@@ -105,8 +106,9 @@ __global__ void pack_kernel(Layout L, char* __restrict__ aos, int64_t n, SoA a, 
 // Per-block partial bounding box + max h over non-inhibited particles.
 __global__ void bbox_kernel(const double4* __restrict__ pos, const int8_t* __restrict__ tb,
                             int64_t n, double* out) {
-  __shared__ double red[7][256];
-  double v[7] = {1e300, 1e300, 1e300, -1e300, -1e300, -1e300, 0.};
+  // per block: min x,y,z; max x,y,z; max h; sum of log h (the grid's typical h)
+  __shared__ double red[8][256];
+  double v[8] = {1e300, 1e300, 1e300, -1e300, -1e300, -1e300, 0., 0.};
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     if (tb[i] == kTimeBinInhibited) continue;
@@ -114,8 +116,9 @@ __global__ void bbox_kernel(const double4* __restrict__ pos, const int8_t* __res
     v[0] = fmin(v[0], p.x); v[1] = fmin(v[1], p.y); v[2] = fmin(v[2], p.z);
     v[3] = fmax(v[3], p.x); v[4] = fmax(v[4], p.y); v[5] = fmax(v[5], p.z);
     v[6] = fmax(v[6], p.w);
+    v[7] += p.w > 0. ? log(p.w) : 0.;
   }
-  for (int k = 0; k < 7; k++) red[k][threadIdx.x] = v[k];
+  for (int k = 0; k < 8; k++) red[k][threadIdx.x] = v[k];
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
     if ((int)threadIdx.x < s) {
@@ -123,11 +126,12 @@ __global__ void bbox_kernel(const double4* __restrict__ pos, const int8_t* __res
         red[k][threadIdx.x] = fmin(red[k][threadIdx.x], red[k][threadIdx.x + s]);
       for (int k = 3; k < 7; k++)
         red[k][threadIdx.x] = fmax(red[k][threadIdx.x], red[k][threadIdx.x + s]);
+      red[7][threadIdx.x] += red[7][threadIdx.x + s];
     }
     __syncthreads();
   }
   if (threadIdx.x == 0)
-    for (int k = 0; k < 7; k++) out[blockIdx.x * 7 + k] = red[k][0];
+    for (int k = 0; k < 8; k++) out[blockIdx.x * 8 + k] = red[k][0];
 }
 
 // Inhibited particles get key = ncell: they sort behind every cell and are
@@ -510,7 +514,7 @@ swh_status swh_space_destroy(swh_space* s) {
   (void)hipStreamSynchronize(s->stream);
   DevBuf* bufs[] = {&s->aos, &s->pos, &s->vm, &s->th, &s->fc, &s->tb, &s->dens, &s->rot,
                     &s->grad, &s->acc, &s->hdt, &s->mintb, &s->perm, &s->ncount,
-                    &s->cell_start, &s->cell_rank, &s->cell_code, &s->cell_span, &s->groups, &s->seg_groups,
+                    &s->cell_start, &s->cell_rank, &s->cell_code, &s->cell_span, &s->cell_hreach, &s->groups, &s->seg_groups,
                     &s->seg_off, &s->keys, &s->keys2, &s->idx, &s->idx2, &s->sort_tmp,
                     &s->scan_tmp, &s->counters, &s->tmp_soa, &s->ghost_left,
                     &s->ghost_right, &s->ghost_list, &s->ghost_list2, &s->ghost_flag,
@@ -683,26 +687,37 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
   s->list_valid = false;
   // 1. bounding box + max h
   const int nb = 512;
-  SWH_TRY(s->scan_tmp.reserve(nb * 7 * sizeof(double)));
-  SWH_TRY(s->hstage.reserve(nb * 7 * sizeof(double)));
+  SWH_TRY(s->scan_tmp.reserve(nb * 8 * sizeof(double)));
+  SWH_TRY(s->hstage.reserve(nb * 8 * sizeof(double)));
   hipLaunchKernelGGL(bbox_kernel, dim3(nb), dim3(256), 0, st, s->pos.as<double4>(),
                      s->tb.as<int8_t>(), n, s->scan_tmp.as<double>());
   SWH_HIP(hipGetLastError());
-  SWH_HIP(hipMemcpyAsync(s->hstage.ptr, s->scan_tmp.ptr, nb * 7 * sizeof(double),
+  SWH_HIP(hipMemcpyAsync(s->hstage.ptr, s->scan_tmp.ptr, nb * 8 * sizeof(double),
                          hipMemcpyDeviceToHost, st));
   SWH_HIP(hipStreamSynchronize(st));
   const double* hb = static_cast<const double*>(s->hstage.ptr);
-  double bb[7] = {1e300, 1e300, 1e300, -1e300, -1e300, -1e300, 0.};
+  double bb[8] = {1e300, 1e300, 1e300, -1e300, -1e300, -1e300, 0., 0.};
   for (int b = 0; b < nb; b++) {
-    for (int k = 0; k < 3; k++) bb[k] = std::min(bb[k], hb[b * 7 + k]);
-    for (int k = 3; k < 7; k++) bb[k] = std::max(bb[k], hb[b * 7 + k]);
+    for (int k = 0; k < 3; k++) bb[k] = std::min(bb[k], hb[b * 8 + k]);
+    for (int k = 3; k < 7; k++) bb[k] = std::max(bb[k], hb[b * 8 + k]);
+    bb[7] += hb[b * 8 + 7];
   }
   SwhGrid& g = s->grid;
   g.periodic = P->periodic;
   g.hmax = bb[6] * (double)kGamma;
   const double cells_per_h = s->tuning.cell_scale > 0.f ? (double)s->tuning.cell_scale
                                                        : (double)std::max(1, s->tuning.cell_factor);
-  double width = min_cell_width > 0 ? min_cell_width : g.hmax / cells_per_h;
+  // Cell width: the largest kernel reach H_max when h is near-uniform (a
+  // group's neighbourhood is then its 27 cells). When h spans a wide range
+  // (clustered boxes) cells sized by H_max would hold whole clumps: size them
+  // by the typical H instead (0.75 x the geometric mean, at least H_max / 8);
+  // the large-h particles then reach over more cells, and the list build
+  // prunes cells by their own maximum H (SWIFT's per-cell h_max in DOPAIR2,
+  // runner_doiact_functions_hydro.h:1424-1530).
+  const double h_geo = std::exp(bb[7] / (double)n) * (double)kGamma;
+  g.adaptive = g.hmax > 1.5 * h_geo;
+  const double h_cell = g.adaptive ? std::max(0.75 * h_geo, g.hmax / 8.) : g.hmax;
+  double width = min_cell_width > 0 ? min_cell_width : h_cell / cells_per_h;
   if (!(width > 0)) width = 1.0;
   int64_t total = 1;
   for (int k = 0; k < 3; k++) {

@@ -421,6 +421,65 @@ def test_clustered_box_chain(gpu_ctx, variant):
     assert_close(g["a_hydro"], o["a_hydro"], 1e-4, 1e-3, "a_hydro")
 
 
+@pytest.fixture(scope="module")
+def clustered_state(gpu_ctx):
+    """A clustered box (24^3 background + 6 clumps of 6,000) with h converged
+    by the GPU chain: H_max / H_typical > 1.5, so the grid is sized by the
+    typical H and the list build prunes cells by their own H_max."""
+    P = abi.default_hydro_params()
+    parts = ics.clustered_box(24, n_clumps=6, per_clump=6000, seed=9)
+    g, res = box_chain_gpu(gpu_ctx, parts, P)
+    return g, P
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("capacity", [0, 24])
+def test_clustered_adaptive_grid_loops_vs_f64(gpu_ctx, clustered_state, capacity):
+    """Density and force on the clustered box vs the fp64 oracle, every
+    particle, exact interaction counts; capacity 24 sends hundreds of
+    particles through the wave-per-particle overflow search."""
+    from swift_subtask_dev_amd import lib
+    parts, P = clustered_state
+    g = abi.copy_parts(parts)
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.set_tuning(list_capacity=capacity)
+    sp.upload(g)
+    sp.rebuild(P)
+    info = sp.info()
+    assert g["h"].max() / g["h"].min() > 10
+    sp.init_parts(P)
+    nd = sp.density(P)
+    if capacity:
+        assert sp.info()["list_overflow"] > 100
+    sp.download(g, abi.FIELDS_DENSITY)
+    sp.close()
+    o = abi.copy_parts(parts)
+    O.fn("f32", "init_parts")(o.ctypes.data, len(o), C.byref(P))
+    assert nd == O.fn("f64", "box_density")(o.ctypes.data, len(o), C.byref(P), None)
+    assert_hydro_close(_by_id(g), _by_id(o), TIGHT, "clustered density")
+    # force on the converged chain state (its force-side union fields intact)
+    gf = abi.copy_parts(parts)
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.set_tuning(list_capacity=capacity)
+    sp.upload(gf)
+    sp.rebuild(P)
+    sp.reset_acceleration(P)
+    nf = sp.force(P)
+    sp.download(gf, abi.FIELDS_FORCE)
+    sp.close()
+    of = abi.copy_parts(parts)
+    of["a_hydro"] = 0
+    of["u_dt"] = 0
+    of["h_dt"] = 0
+    of["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
+    assert nf == O.fn("f64", "box_force")(of.ctypes.data, len(of), C.byref(P), None)
+    a, b = _by_id(gf), _by_id(of)
+    assert_close(a["a_hydro"], b["a_hydro"], 5e-5, 1e-4, "a_hydro")
+    assert_close(a["u_dt"], b["u_dt"], 5e-5, 1e-4, "u_dt")
+    assert np.array_equal(a["min_ngb_time_bin"], b["min_ngb_time_bin"])
+    assert info["cdim"][0] > 1.0 / (float(parts["h"].max()) * 1.825742) * 1.3
+
+
 # ---------------------------------------------------------------------------
 # Per-task force / gradient through the adapter on prepared inputs
 # ---------------------------------------------------------------------------

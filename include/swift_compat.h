@@ -158,9 +158,51 @@ struct pm_mesh {
   double r_cut_max;
 };
 
+/* src/multipole_struct.h:36-220 at SELF_GRAVITY_MULTIPOLE_ORDER 4 (the
+ * adapter reads the fields by name; compiled against SWIFT's headers it
+ * uses SWIFT's own layout) */
+struct grav_tensor {
+  float F_000;
+  float F_100, F_010, F_001;
+  float F_200, F_020, F_002, F_110, F_101, F_011;
+  float F_300, F_030, F_003, F_210, F_201, F_120, F_021, F_102, F_012, F_111;
+  float F_400, F_040, F_004, F_310, F_301, F_130, F_031, F_103, F_013, F_220, F_202, F_022,
+      F_211, F_121, F_112;
+  int interacted;
+};
+
+struct multipole {
+  float vel[3];
+  float max_delta_vel[3];
+  float min_delta_vel[3];
+  float max_softening;
+  float min_old_a_grav_norm;
+  float power[5];
+  float M_000;
+  float M_200, M_020, M_002, M_110, M_101, M_011;
+  float M_300, M_030, M_003, M_210, M_201, M_120, M_021, M_102, M_012, M_111;
+  float M_400, M_040, M_004, M_310, M_301, M_130, M_031, M_103, M_013, M_220, M_202, M_022,
+      M_211, M_121, M_112;
+};
+
 struct gravity_tensors {
+  struct grav_tensor pot;
+  struct multipole m_pole;
   double CoM[3];
-  float r_max;
+  double CoM_rebuild[3];
+  double r_max;
+  double r_max_rebuild;
+};
+
+/* src/gravity_properties.h: the M2P acceptance fields */
+struct gravity_props {
+  int use_advanced_MAC;
+  int use_adaptive_tolerance;
+  int use_gadget_tolerance;
+  float adaptive_tolerance;
+  double theta_crit;
+  int use_tree_below_softening;
+  int consider_truncation_in_MAC;
 };
 
 struct engine {
@@ -168,6 +210,7 @@ struct engine {
   const struct cosmology *cosmology;
   const struct hydro_props *hydro_properties;
   struct pm_mesh *mesh;
+  const struct gravity_props *gravity_properties;
   timebin_t max_active_bin;
   integertime_t ti_current;
   double time_base;

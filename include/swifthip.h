@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SWH_ABI_VERSION 3
+#define SWH_ABI_VERSION 4
 
 #if defined(__GNUC__)
 #define SWH_API __attribute__((visibility("default")))
@@ -95,6 +95,7 @@ typedef struct swh_gpart_layout {
   int32_t off_mass;       /* float     */
   int32_t off_epsilon;    /* float     */
   int32_t off_time_bin;   /* int8      */
+  int32_t off_old_a_grav_norm; /* float (the adaptive MAC's acceleration estimate) */
 } swh_gpart_layout;
 
 /* Layouts of SWIFT's default configure (SPHENIX part: 160 B; multi-softening
@@ -125,7 +126,36 @@ typedef struct swh_grav_params {
   float r_s_inv;     /* e->mesh->r_s_inv   */
   double r_cut_min;  /* e->mesh->r_cut_min */
   int32_t max_active_bin;
+  /* M2P acceptance (gravity_M2P_accept, src/multipole_accept.h:290-373):
+   * e->gravity_properties fields */
+  float theta_crit;
+  float adaptive_tolerance;
+  int32_t use_advanced_MAC;
+  int32_t use_gadget_tolerance;
+  int32_t use_tree_below_softening;
+  int32_t consider_truncation_in_MAC;
 } swh_grav_params;
+
+/* A cell's multipole expansion about its centre of mass, order 4 (SWIFT's
+ * default SELF_GRAVITY_MULTIPOLE_ORDER): the fields of struct gravity_tensors
+ * / struct multipole (src/multipole_struct.h:110-220) that M2P reads.
+ * M[] holds the 35 terms M_abc, a+b+c <= 4, in struct multipole's member
+ * order with the (zero) dipole at 1..3:
+ *   0 M_000 | 1 M_100 2 M_010 3 M_001 |
+ *   4 M_200 5 M_020 6 M_002 7 M_110 8 M_101 9 M_011 |
+ *   10 M_300 11 M_030 12 M_003 13 M_210 14 M_201 15 M_120 16 M_021 17 M_102
+ *   18 M_012 19 M_111 |
+ *   20 M_400 21 M_040 22 M_004 23 M_310 24 M_301 25 M_130 26 M_031 27 M_103
+ *   28 M_013 29 M_220 30 M_202 31 M_022 32 M_211 33 M_121 34 M_112 */
+#define SWH_MPOLE_TERMS 35
+typedef struct swh_multipole {
+  double CoM[3];
+  double r_max;
+  float M[SWH_MPOLE_TERMS];
+  float power[5];           /* multipole power per order */
+  float max_softening;
+  float min_old_a_grav_norm;
+} swh_multipole;
 
 /* ------------------------------------------------------------------ */
 /* Context: one per (process, device). Thread-safe: per-task calls     */
@@ -192,12 +222,17 @@ typedef struct swh_gcell_view {
   double width[3];
   double CoM[3];   /* multipole->CoM   */
   double r_max;    /* multipole->r_max */
+  const swh_multipole *multipole; /* the cell's expansion (needed with allow_mpole) */
 } swh_gcell_view;
 
 SWH_API swh_status swh_grav_self_pp(swh_context *ctx, const swh_gcell_view *c,
                             const swh_gpart_layout *L, const swh_grav_params *G);
+/* runner_dopair_grav_pp: with allow_mpole, every active particle of one
+ * cell that passes gravity_M2P_accept against the other cell's multipole
+ * (evaluated in float exactly as gravity_cache_populate does) takes the M2P
+ * route (runner_dopair_grav_pm_full / _truncated) instead of P2P. */
 SWH_API swh_status swh_grav_pair_pp(swh_context *ctx, const swh_gcell_view *ci,
-                            const swh_gcell_view *cj, int symmetric,
+                            const swh_gcell_view *cj, int symmetric, int allow_mpole,
                             const swh_gpart_layout *L, const swh_grav_params *G);
 
 /* ================================================================== */
@@ -314,8 +349,9 @@ typedef struct swh_leaf {
   int32_t count;
 } swh_leaf;
 typedef struct swh_leaf_pair {
-  int32_t j;         /* source leaf index */
-  int32_t truncated; /* 1: long-range truncated kernel */
+  int32_t j;           /* source leaf index */
+  int32_t truncated;   /* 1: long-range truncated kernel */
+  int32_t allow_mpole; /* 1: i-particles passing the MAC take leaf j's multipole (M2P) */
 } swh_leaf_pair;
 SWH_API swh_status swh_gspace_create(swh_context *ctx, swh_gspace **g);
 SWH_API swh_status swh_gspace_destroy(swh_gspace *g);
@@ -324,7 +360,14 @@ SWH_API swh_status swh_gspace_upload(swh_gspace *g, const void *gparts, int64_t 
 SWH_API swh_status swh_gspace_set_leaves(swh_gspace *g, const swh_leaf *leaves, int32_t nleaves,
                                  const int32_t *pair_offset, const swh_leaf_pair *pairs,
                                  int32_t npairs);
-SWH_API swh_status swh_grav_pp_batch(swh_gspace *g, const swh_grav_params *G, int64_t *n_interactions);
+/* Leaf multipoles (gravity_P2M + gravity_multipole_compute_power,
+ * src/multipole.h:878-1266) of every leaf, on the device; needed before a
+ * batch with allow_mpole pairs. `out` (nullable): a host copy. */
+SWH_API swh_status swh_gspace_make_multipoles(swh_gspace *g, swh_multipole *out);
+/* P2P (+ M2P on allow_mpole pairs) of every leaf's active particles.
+ * n_interactions: P2P pair interactions; n_m2p (nullable): M2P evaluations. */
+SWH_API swh_status swh_grav_pp_batch(swh_gspace *g, const swh_grav_params *G,
+                                     int64_t *n_interactions, int64_t *n_m2p);
 SWH_API swh_status swh_gspace_download(swh_gspace *g, void *gparts, const swh_gpart_layout *L,
                                int on_device);
 SWH_API swh_status swh_gspace_sync(swh_gspace *g);

@@ -2092,7 +2092,295 @@ struct oracle_grav_params {
   float r_s_inv;       /* e->mesh->r_s_inv */
   double r_cut_min;    /* e->mesh->r_cut_min */
   int max_active_bin;
+  /* gravity_props fields of gravity_M2P_accept */
+  float theta_crit;
+  float adaptive_tolerance;
+  int use_advanced_MAC;
+  int use_gadget_tolerance;
+  int use_tree_below_softening;
+  int consider_truncation_in_MAC;
 };
+
+/* ------------------------------------------------------------------------ */
+/* Multipoles, order 4 (SELF_GRAVITY_MULTIPOLE_ORDER of the default build): */
+/* struct multipole / gravity_tensors (src/multipole_struct.h:110-220) with */
+/* the 35 terms in member order (dipole zero at 1..3), P2M                  */
+/* (src/multipole.h:983-1266), the multipole power (878-972), the M2P       */
+/* acceptance (src/multipole_accept.h:290-373) and M2P                      */
+/* (src/multipole.h:2257-2480, src/gravity_derivatives.h:516-760).          */
+/* ------------------------------------------------------------------------ */
+struct oracle_multipole {
+  double CoM[3];
+  double r_max;
+  float M[35];
+  float power[5];
+  float max_softening;
+  float min_old_a_grav_norm;
+};
+
+static const int mp_a[35] = {0, 1, 0, 0, 2, 0, 0, 1, 1, 0, 3, 0, 0, 2, 2, 1, 0, 1,
+                             0, 1, 4, 0, 0, 3, 3, 1, 0, 1, 0, 2, 2, 0, 2, 1, 1};
+static const int mp_b[35] = {0, 0, 1, 0, 0, 2, 0, 1, 0, 1, 0, 3, 0, 1, 0, 2, 2, 0,
+                             1, 1, 0, 4, 0, 1, 0, 3, 3, 0, 1, 2, 0, 2, 1, 2, 1};
+static const int mp_c[35] = {0, 0, 0, 1, 0, 0, 2, 0, 1, 1, 0, 0, 3, 0, 1, 0, 1, 2,
+                             2, 1, 0, 0, 4, 0, 1, 0, 1, 3, 3, 0, 2, 2, 1, 1, 2};
+
+static double fact_d(int n) { return n <= 1 ? 1. : n * fact_d(n - 1); }
+
+/* gravity_P2M: mass, CoM, then M_n = (-1)^|n| sum m X_n(dx) with X_n =
+ * dx^n / n! (vector_power.h) about the CoM, accumulated in double and stored
+ * as float; r_max; then gravity_multipole_compute_power (float squares for
+ * unit weights, double products for the fractional ones, as written). */
+API void PFX(grav_p2m)(const struct gpart *g, int n, struct oracle_multipole *out) {
+  float eps_max = 0.f, oag_min = FLT_MAX;
+  double mass = 0., com[3] = {0., 0., 0.};
+  for (int k = 0; k < n; k++) {
+    const double m = g[k].mass;
+    eps_max = eps_max > g[k].epsilon ? eps_max : g[k].epsilon;
+    oag_min = oag_min < g[k].old_a_grav_norm ? oag_min : g[k].old_a_grav_norm;
+    mass += m;
+    for (int d = 0; d < 3; d++) com[d] += g[k].x[d] * m;
+  }
+  const double imass = 1.0 / mass;
+  for (int d = 0; d < 3; d++) com[d] *= imass;
+  double Md[35] = {0.};
+  double r_max2 = 0.;
+  for (int k = 0; k < n; k++) {
+    const double dx[3] = {g[k].x[0] - com[0], g[k].x[1] - com[1], g[k].x[2] - com[2]};
+    r_max2 = fmax(r_max2, dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2]);
+    const double m = g[k].mass;
+    for (int t = 4; t < 35; t++) {
+      const int a = mp_a[t], b = mp_b[t], c = mp_c[t];
+      const double X = pow(dx[0], a) * pow(dx[1], b) * pow(dx[2], c) /
+                       (fact_d(a) * fact_d(b) * fact_d(c));
+      Md[t] += ((a + b + c) & 1) ? -m * X : m * X;
+    }
+  }
+  for (int d = 0; d < 3; d++) out->CoM[d] = com[d];
+  out->r_max = sqrt(r_max2);
+  out->M[0] = (float)mass;
+  out->M[1] = out->M[2] = out->M[3] = 0.f;
+  for (int t = 4; t < 35; t++) out->M[t] = (float)Md[t];
+  out->max_softening = eps_max;
+  out->min_old_a_grav_norm = oag_min;
+  double pw[5] = {0., 0., 0., 0., 0.};
+  for (int t = 4; t < 35; t++) {
+    const int a = mp_a[t], b = mp_b[t], c = mp_c[t], o = a + b + c;
+    const double w = fact_d(a) * fact_d(b) * fact_d(c) / fact_d(o);
+    const float M = out->M[t];
+    if (w == 1.)
+      pw[o] += (double)(M * M);
+    else
+      pw[o] += w * (double)M * (double)M;
+  }
+  out->power[0] = out->M[0];
+  out->power[1] = 0.f;
+  for (int o = 2; o <= 4; o++) out->power[o] = (float)sqrt(pw[o]);
+}
+
+/* gravity_M2P_accept for a gpart at float cache position x (the float
+ * arithmetic of the reference in both builds: the choice is discrete). */
+static int m2p_accept(const struct oracle_grav_params *G, const struct gpart *pa,
+                      const struct oracle_multipole *B, const float x[3], int periodic) {
+  float dx[3];
+  for (int k = 0; k < 3; k++) {
+    dx[k] = x[k] - (float)B->CoM[k];
+    if (periodic) {
+      const float L = G->dim[k];
+      dx[k] = (dx[k] > 0.5f * L) ? dx[k] - L : ((dx[k] < -0.5f * L) ? dx[k] + L : dx[k]);
+    }
+  }
+  const float r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+  const float rho_B = (float)B->r_max;
+  const float max_softening = B->max_softening > pa->epsilon ? B->max_softening : pa->epsilon;
+  const float E_BA_term = 8.f * B->power[2];
+  const float r_to_p = r2;
+  float f_MAC_inv;
+  if (periodic && G->consider_truncation_in_MAC) {
+    const float H = max_softening;
+    if (r2 < (25.f / 81.f) * H * H)
+      f_MAC_inv = (25.f / 81.f) * H * H;
+    else if (G->r_s_inv * G->r_s_inv * r2 > (25.f / 9.f))
+      f_MAC_inv = (9.f / 25.f) * G->r_s_inv * G->r_s_inv * r2 * r2;
+    else
+      f_MAC_inv = r2;
+  } else {
+    f_MAC_inv = r2;
+  }
+  const float old_a_grav = pa->old_a_grav_norm;
+  const float eps = G->adaptive_tolerance;
+  const float theta_crit = G->theta_crit;
+  const float theta_crit2 = theta_crit * theta_crit;
+  const int cond_2 = G->use_tree_below_softening || max_softening * max_softening < r2;
+  if (G->use_advanced_MAC && G->use_gadget_tolerance) {
+    const float q = rho_B / sqrtf(r2);
+    const float q2 = q * q;
+    const float ratio = q2 * q2;
+    return (B->M[0] * ratio < eps * old_a_grav * f_MAC_inv) && cond_2;
+  } else if (G->use_advanced_MAC) {
+    const int cond_1 = rho_B * rho_B < r2;
+    const int cond_3 = E_BA_term < eps * old_a_grav * r_to_p * f_MAC_inv;
+    return cond_1 && cond_2 && cond_3;
+  }
+  return (rho_B * rho_B < theta_crit2 * r2) && cond_2;
+}
+
+/* kernel_gravity.h:169-275: D_soft_1..6 */
+static void d_soft_all(real u, real d[7]) {
+  real p = (real)-3.f * u + (real)15.f;
+  p = p * u - (real)28.f; p = p * u + (real)21.f; p = p * u; p = p * u - (real)7.f;
+  p = p * u; p = p * u + (real)3.f;
+  d[1] = p;
+  p = (real)-21.f * u + (real)90.f;
+  p = p * u - (real)140.f; p = p * u + (real)84.f; p = p * u; p = p * u - (real)14.f;
+  p = p * u;
+  d[2] = p;
+  p = (real)-105.f * u + (real)360.f;
+  p = p * u - (real)420.f; p = p * u + (real)168.f; p = p * u; p = p * u;
+  d[3] = p;
+  p = (real)-315.f * u + (real)720.f;
+  p = p * u - (real)420.f; p = p * u; p = p * u;
+  d[4] = p;
+  p = (real)-315.f * u; p = p * u + (real)420.f; p = p * u;
+  d[5] = p;
+  p = (real)315.f * u; p = p * u - (real)1260.f;
+  d[6] = p;
+}
+
+/* potential_derivatives_compute_M2P: the radial factors Dt_1..Dt_6, then
+ * D_abc for a+b+c <= 5 in the reference's closed forms (by the shape of the
+ * sorted exponents; the Dt are rescaled by r^-1 between orders exactly as
+ * the reference does). */
+struct m2p_derivs {
+  real rr[3];     /* r_x / r, r_y / r, r_z / r */
+  real Dt[6][7];  /* Dt[o][k]: Dt_k as scaled when order o is formed */
+};
+
+static void m2p_radial(real r_x, real r_y, real r_z, real r2, real r_inv, real eps,
+                       int periodic, real r_s_inv, struct m2p_derivs *d) {
+  real Dt[7];
+  if (r2 < eps * eps) {
+    const real eps_inv = (real)1.f / eps;
+    const real r = r2 * r_inv;
+    const real u = r * eps_inv;
+    real ds[7];
+    d_soft_all(u, ds);
+    real e = eps_inv;
+    for (int k = 1; k <= 6; k++) {
+      Dt[k] = e * ds[k];
+      e = e * eps_inv;
+    }
+  } else if (!periodic) {
+    Dt[1] = r_inv;
+    Dt[2] = (real)-1.f * Dt[1] * r_inv;
+    Dt[3] = (real)-3.f * Dt[2] * r_inv;
+    Dt[4] = (real)-5.f * Dt[3] * r_inv;
+    Dt[5] = (real)-7.f * Dt[4] * r_inv;
+    Dt[6] = (real)-9.f * Dt[5] * r_inv;
+  } else {
+    /* kernel_long_grav_derivatives, default branch (kernel_long_gravity.h:151-183) */
+    const real r = r2 * r_inv;
+    const real c1 = (real)2.f * r_s_inv;
+    const real c2 = c1 * c1, c3 = c2 * c1, c4 = c3 * c1, c5 = c4 * c1;
+    const real x = c1 * r;
+    const real exp_x = EXP(x);
+    const real a_inv = (real)1.f + exp_x;
+    const real a1 = (real)1.f / a_inv;
+    const real a2 = a1 * a1, a3 = a2 * a1, a4 = a3 * a1, a5 = a4 * a1, a6 = a5 * a1;
+    const real chi0 = (real)-2.f * exp_x * a1 + (real)2.f;
+    const real chi1 = (real)-2.f * exp_x * c1 * a2;
+    const real chi2 = (real)-2.f * exp_x * c2 * ((real)2.f * a3 - a2);
+    const real chi3 = (real)-2.f * exp_x * c3 * ((real)6.f * a4 - (real)6.f * a3 + a2);
+    const real chi4 =
+        (real)-2.f * exp_x * c4 * ((real)24.f * a5 - (real)36.f * a4 + (real)14.f * a3 - a2);
+    const real chi5 = (real)-2.f * exp_x * c5 *
+                      ((real)120.f * a6 - (real)240.f * a5 + (real)150.f * a4 -
+                       (real)30.f * a3 + a2);
+    Dt[1] = chi0 * r_inv;
+    Dt[2] = (chi1 - chi0 * r_inv) * r_inv;
+    Dt[3] = ((chi0 * r_inv - chi1) * (real)3.f * r_inv + chi2) * r_inv;
+    Dt[4] = (((-chi0 * r_inv + chi1) * (real)15.f * r_inv - (real)6.f * chi2) * r_inv + chi3) *
+            r_inv;
+    Dt[5] = ((((chi0 * r_inv - chi1) * (real)105.f * r_inv + (real)45.f * chi2) * r_inv -
+              (real)10.f * chi3) * r_inv + chi4) * r_inv;
+    Dt[6] = (((((-chi0 * r_inv + chi1) * (real)945.f * r_inv - (real)420.f * chi2) * r_inv +
+               (real)105.f * chi3) * r_inv - (real)15.f * chi4) * r_inv + chi5) * r_inv;
+  }
+  d->rr[0] = r_x * r_inv;
+  d->rr[1] = r_y * r_inv;
+  d->rr[2] = r_z * r_inv;
+  /* the reference's in-place rescaling: before order 2 Dt_2 *= r^-1, before
+   * order 3 Dt_3 *= r^-1, before 4 Dt_3, Dt_4 *= r^-1, before 5 Dt_4, Dt_5 */
+  for (int o = 0; o < 6; o++) {
+    if (o == 2) Dt[2] = Dt[2] * r_inv;
+    if (o == 3) Dt[3] = Dt[3] * r_inv;
+    if (o == 4) { Dt[3] = Dt[3] * r_inv; Dt[4] = Dt[4] * r_inv; }
+    if (o == 5) { Dt[4] = Dt[4] * r_inv; Dt[5] = Dt[5] * r_inv; }
+    for (int k = 0; k < 7; k++) d->Dt[o][k] = Dt[k];
+  }
+}
+
+static real ipow(real x, int n) {
+  real y = (real)1.f;
+  for (int k = 0; k < n; k++) y = y * x;
+  return y;
+}
+
+/* D_abc from the closed form of its shape: e = exponents, sorted so that
+ * e[p[0]] >= e[p[1]] >= e[p[2]] */
+static real m2p_D(const struct m2p_derivs *d, int a, int b, int c) {
+  const int e[3] = {a, b, c};
+  int p[3] = {0, 1, 2};
+  for (int i = 0; i < 3; i++)
+    for (int j = i + 1; j < 3; j++)
+      if (e[p[j]] > e[p[i]]) { const int t = p[i]; p[i] = p[j]; p[j] = t; }
+  const int n1 = e[p[0]], n2 = e[p[1]], n3 = e[p[2]], o = a + b + c;
+  const real u = d->rr[p[0]], v = d->rr[p[1]], w = d->rr[p[2]];
+  const real *Dt = d->Dt[o];
+  switch (o) {
+    case 0: return Dt[1];
+    case 1: return u * Dt[2];
+    case 2: return n1 == 2 ? u * u * Dt[3] + Dt[2] : u * v * Dt[3];
+    case 3:
+      if (n1 == 3) return ipow(u, 3) * Dt[4] + (real)3.f * u * Dt[3];
+      if (n1 == 2) return u * u * v * Dt[4] + v * Dt[3];
+      return u * v * w * Dt[4];
+    case 4:
+      if (n1 == 4) return ipow(u, 4) * Dt[5] + (real)6.f * u * u * Dt[4] + (real)3.f * Dt[3];
+      if (n1 == 3) return ipow(u, 3) * v * Dt[5] + (real)3.f * u * v * Dt[4];
+      if (n2 == 2) return u * u * v * v * Dt[5] + u * u * Dt[4] + v * v * Dt[4] + Dt[3];
+      return u * u * v * w * Dt[5] + v * w * Dt[4];
+    default:
+      if (n1 == 5) return ipow(u, 5) * Dt[6] + (real)10.f * ipow(u, 3) * Dt[5] + (real)15.f * u * Dt[4];
+      if (n1 == 4) return ipow(u, 4) * v * Dt[6] + (real)6.f * u * u * v * Dt[5] + (real)3.f * v * Dt[4];
+      if (n1 == 3 && n2 == 2)
+        return ipow(u, 3) * v * v * Dt[6] + ipow(u, 3) * Dt[5] + (real)3.f * u * v * v * Dt[5] +
+               (real)3.f * u * Dt[4];
+      if (n1 == 3) return ipow(u, 3) * v * w * Dt[6] + (real)3.f * u * v * w * Dt[5];
+      (void)n3;
+      return w * u * u * v * v * Dt[6] + w * u * u * Dt[5] + w * v * v * Dt[5] + w * Dt[4];
+  }
+}
+
+/* gravity_M2P: F_000 -= M_000 D_000, ... with the sign of each order as the
+ * reference writes it (orders 0, 2, 4 subtract; order 3 adds), i.e.
+ * F = -sum_n (-1)^|n| M_n D_n and F_e = -sum_n (-1)^|n| M_n D_(n+e). */
+static void grav_m2p(const struct oracle_multipole *m, real r_x, real r_y, real r_z, real r2,
+                     real eps, int periodic, real r_s_inv, real F[4]) {
+  const real r_inv = (real)1.f / SQRT(r2);
+  struct m2p_derivs d;
+  m2p_radial(r_x, r_y, r_z, r2, r_inv, eps, periodic, r_s_inv, &d);
+  F[0] = F[1] = F[2] = F[3] = (real)0.f;
+  for (int t = 0; t < 35; t++) {
+    if (t >= 1 && t <= 3) continue;
+    const int a = mp_a[t], b = mp_b[t], c = mp_c[t];
+    const real M = ((a + b + c) & 1) ? -(real)m->M[t] : (real)m->M[t];
+    F[0] -= M * m2p_D(&d, a, b, c);
+    F[1] -= M * m2p_D(&d, a + 1, b, c);
+    F[2] -= M * m2p_D(&d, a, b + 1, c);
+    F[3] -= M * m2p_D(&d, a, b, c + 1);
+  }
+}
 
 /* P2P of the (active) particles of gi against all of gj (no multipoles):
  * runner_dopair_grav_pp_full / _truncated (runner_doiact_grav.c:584-760),
@@ -2102,7 +2390,8 @@ struct oracle_grav_params {
  * (runner_doself_grav_pp_full, runner_doiact_grav.c:1500-1622). */
 static long long grav_pp(struct gpart *gi, int ni, const struct gpart *gj, int nj,
                          int self, int truncated, const double shift_i[3],
-                         const double shift_j[3], const struct oracle_grav_params *G) {
+                         const double shift_j[3], const struct oracle_grav_params *G,
+                         const struct oracle_multipole *mj, long long *n_m2p) {
   long long n = 0;
   const real dim[3] = {(real)G->dim[0], (real)G->dim[1], (real)G->dim[2]};
   for (int pid = 0; pid < ni; pid++) {
@@ -2114,6 +2403,30 @@ static long long grav_pp(struct gpart *gi, int ni, const struct gpart *gj, int n
     const real z_i = (real)(gp->x[2] - shift_i[2]);
     const real h_i = gp->epsilon;
     real a_x = 0, a_y = 0, a_z = 0, pot = 0;
+    if (mj) {
+      /* gravity_cache_populate's use_mpole, then runner_dopair_grav_pm_*
+       * (runner_doiact_grav.c:911-1200): dx = CoM_j - x_i, softening
+       * max(eps_i, multipole max softening), truncated as the pair */
+      const float xf[3] = {(float)(gp->x[0] - shift_i[0]), (float)(gp->x[1] - shift_i[1]),
+                           (float)(gp->x[2] - shift_i[2])};
+      if (m2p_accept(G, gp, mj, xf, G->periodic)) {
+        real dx[3];
+        for (int k = 0; k < 3; k++) {
+          dx[k] = (real)(mj->CoM[k] - shift_j[k]) - (real)(gp->x[k] - shift_i[k]);
+          if (G->periodic) dx[k] = nearest_r(dx[k], dim[k]);
+        }
+        const real r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+        const real eps = rmax(h_i, (real)mj->max_softening);
+        real F[4];
+        grav_m2p(mj, dx[0], dx[1], dx[2], r2, eps, truncated, (real)G->r_s_inv, F);
+        gp->a_grav[0] += (float)F[1];
+        gp->a_grav[1] += (float)F[2];
+        gp->a_grav[2] += (float)F[3];
+        gp->potential += (float)F[0];
+        if (n_m2p) (*n_m2p)++;
+        continue;
+      }
+    }
     for (int pjd = 0; pjd < nj; pjd++) {
       if (self && pid == pjd) continue;
       const struct gpart *gq = &gj[pjd];
@@ -2160,10 +2473,11 @@ static long long grav_pp(struct gpart *gi, int ni, const struct gpart *gj, int n
  * Positions: direct differences, nearest image when periodic. */
 API long long PFX(grav_pp_leaves)(struct gpart *g, const int *leaves, int nleaves,
                                   const int *off, const int *pairs,
-                                  const struct oracle_grav_params *G) {
-  long long total = 0;
+                                  const struct oracle_grav_params *G,
+                                  const struct oracle_multipole *mp, long long *n_m2p) {
+  long long total = 0, total_m2p = 0;
   const real dim[3] = {(real)G->dim[0], (real)G->dim[1], (real)G->dim[2]};
-#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total)
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total, total_m2p)
   for (int l = 0; l < nleaves; l++) {
     const int s = leaves[2 * l], c = leaves[2 * l + 1];
     for (int pid = s; pid < s + c; pid++) {
@@ -2172,8 +2486,30 @@ API long long PFX(grav_pp_leaves)(struct gpart *g, const int *leaves, int nleave
       real a_x = 0, a_y = 0, a_z = 0, pot = 0;
       const real h_i = gp->epsilon;
       for (int q = off[l]; q < off[l + 1]; q++) {
-        const int jl = pairs[2 * q], trunc = pairs[2 * q + 1];
+        /* pairs: {j, truncated, allow_mpole} (swh_leaf_pair) */
+        const int jl = pairs[3 * q], trunc = pairs[3 * q + 1], allow = pairs[3 * q + 2];
         const int sj = leaves[2 * jl], cj = leaves[2 * jl + 1];
+        if (allow && mp && cj > 1) {
+          const struct oracle_multipole *B = &mp[jl];
+          const float xf[3] = {(float)gp->x[0], (float)gp->x[1], (float)gp->x[2]};
+          if (m2p_accept(G, gp, B, xf, G->periodic)) {
+            real dx[3];
+            for (int k = 0; k < 3; k++) {
+              dx[k] = (real)(B->CoM[k] - gp->x[k]);
+              if (G->periodic) dx[k] = nearest_r(dx[k], dim[k]);
+            }
+            const real r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+            real F[4];
+            grav_m2p(B, dx[0], dx[1], dx[2], r2, rmax(h_i, (real)B->max_softening), trunc,
+                     (real)G->r_s_inv, F);
+            a_x += F[1];
+            a_y += F[2];
+            a_z += F[3];
+            pot += F[0];
+            total_m2p++;
+            continue;
+          }
+        }
         for (int pjd = sj; pjd < sj + cj; pjd++) {
           if (pjd == pid) continue;
           const struct gpart *gq = &g[pjd];
@@ -2209,6 +2545,7 @@ API long long PFX(grav_pp_leaves)(struct gpart *g, const int *leaves, int nleave
       gp->potential += (float)pot;
     }
   }
+  if (n_m2p) *n_m2p = total_m2p;
   return total;
 }
 
@@ -2220,13 +2557,37 @@ API long long PFX(grav_self_pp)(struct gpart *g, int n, const double loc[3],
   const double c[3] = {loc[0] + 0.5 * width[0], loc[1] + 0.5 * width[1],
                        loc[2] + 0.5 * width[2]};
   const int truncated = G->periodic && (2. * r_max > G->r_cut_min);
-  return grav_pp(g, n, g, n, 1, truncated, c, c, G);
+  return grav_pp(g, n, g, n, 1, truncated, c, c, G, NULL, NULL);
 }
 
-/* runner_dopair_grav_pp with allow_mpole = 0 (runner_doiact_grav.c:1202-1425):
- * absolute float positions, nearest-image dx when periodic; truncated iff
- * periodic && |CoM_i - CoM_j| + rmax_i + rmax_j > r_cut_min. Updates gi (and
- * gj when symmetric). */
+/* runner_dopair_grav_pp (runner_doiact_grav.c:1202-1425): absolute float
+ * positions, nearest-image dx when periodic; truncated iff periodic &&
+ * |CoM_i - CoM_j| + rmax_i + rmax_j > r_cut_min. Updates gi (and gj when
+ * symmetric). With allow_mpole (mi, mj non-NULL) a cell of more than one
+ * particle offers its multipole to the other cell's particles (1273-1274). */
+API long long PFX(grav_pair_pp_mpole)(struct gpart *gi, int ni, struct gpart *gj, int nj,
+                                      const struct oracle_multipole *mi,
+                                      const struct oracle_multipole *mj, int symmetric,
+                                      int allow_mpole, const struct oracle_grav_params *G,
+                                      long long *n_m2p) {
+  const double zero[3] = {0., 0., 0.};
+  int truncated = 0;
+  if (G->periodic) {
+    double dx[3];
+    for (int k = 0; k < 3; k++) {
+      dx[k] = (float)mj->CoM[k] - (float)mi->CoM[k];
+      dx[k] = nearest_r((real)dx[k], (real)G->dim[k]);
+    }
+    const double r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+    truncated = (sqrt(r2) + (float)mi->r_max + (float)mj->r_max) > G->r_cut_min;
+  }
+  const struct oracle_multipole *use_j = (allow_mpole && nj > 1) ? mj : NULL;
+  const struct oracle_multipole *use_i = (allow_mpole && ni > 1) ? mi : NULL;
+  long long n = grav_pp(gi, ni, gj, nj, 0, truncated, zero, zero, G, use_j, n_m2p);
+  if (symmetric) n += grav_pp(gj, nj, gi, ni, 0, truncated, zero, zero, G, use_i, n_m2p);
+  return n;
+}
+
 API long long PFX(grav_pair_pp)(struct gpart *gi, int ni, struct gpart *gj, int nj,
                                 const double CoM_i[3], const double CoM_j[3],
                                 double rmax_i, double rmax_j, int symmetric,
@@ -2242,7 +2603,7 @@ API long long PFX(grav_pair_pp)(struct gpart *gi, int ni, struct gpart *gj, int 
     const double r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
     truncated = (sqrt(r2) + rmax_i + rmax_j) > G->r_cut_min;
   }
-  long long n = grav_pp(gi, ni, gj, nj, 0, truncated, zero, zero, G);
-  if (symmetric) n += grav_pp(gj, nj, gi, ni, 0, truncated, zero, zero, G);
+  long long n = grav_pp(gi, ni, gj, nj, 0, truncated, zero, zero, G, NULL, NULL);
+  if (symmetric) n += grav_pp(gj, nj, gi, ni, 0, truncated, zero, zero, G, NULL, NULL);
   return n;
 }

@@ -119,7 +119,7 @@ class PartLayout(C.Structure):
 class GPartLayout(C.Structure):
     _fields_ = [(n, C.c_int32) for n in (
         "stride", "off_x", "off_a_grav", "off_potential", "off_mass", "off_epsilon",
-        "off_time_bin")]
+        "off_time_bin", "off_old_a_grav_norm")]
 
 
 class HydroParams(C.Structure):
@@ -141,8 +141,34 @@ class HydroParams(C.Structure):
 
 
 class GravParams(C.Structure):
+    """swh_grav_params (identical layout to the oracle's oracle_grav_params):
+    mesh scalars, then the M2P acceptance (gravity_props) fields."""
+
     _fields_ = [("periodic", C.c_int32), ("dim", C.c_float * 3), ("r_s_inv", C.c_float),
-                ("r_cut_min", C.c_double), ("max_active_bin", C.c_int32)]
+                ("r_cut_min", C.c_double), ("max_active_bin", C.c_int32),
+                ("theta_crit", C.c_float), ("adaptive_tolerance", C.c_float),
+                ("use_advanced_MAC", C.c_int32), ("use_gadget_tolerance", C.c_int32),
+                ("use_tree_below_softening", C.c_int32),
+                ("consider_truncation_in_MAC", C.c_int32)]
+
+
+MPOLE_TERMS = 35
+# swh_multipole::M order (include/swifthip.h): struct multipole's member order
+MPOLE_INDEX = [(0, 0, 0), (1, 0, 0), (0, 1, 0), (0, 0, 1),
+               (2, 0, 0), (0, 2, 0), (0, 0, 2), (1, 1, 0), (1, 0, 1), (0, 1, 1),
+               (3, 0, 0), (0, 3, 0), (0, 0, 3), (2, 1, 0), (2, 0, 1), (1, 2, 0), (0, 2, 1),
+               (1, 0, 2), (0, 1, 2), (1, 1, 1),
+               (4, 0, 0), (0, 4, 0), (0, 0, 4), (3, 1, 0), (3, 0, 1), (1, 3, 0), (0, 3, 1),
+               (1, 0, 3), (0, 1, 3), (2, 2, 0), (2, 0, 2), (0, 2, 2), (2, 1, 1), (1, 2, 1),
+               (1, 1, 2)]
+
+
+class Multipole(C.Structure):
+    """swh_multipole (== the oracle's oracle_multipole)."""
+
+    _fields_ = [("CoM", C.c_double * 3), ("r_max", C.c_double), ("M", C.c_float * MPOLE_TERMS),
+                ("power", C.c_float * 5), ("max_softening", C.c_float),
+                ("min_old_a_grav_norm", C.c_float)]
 
 
 class CellView(C.Structure):
@@ -153,7 +179,7 @@ class CellView(C.Structure):
 class GCellView(C.Structure):
     _fields_ = [("gparts", C.c_void_p), ("count", C.c_int32), ("active", C.c_int32),
                 ("loc", C.c_double * 3), ("width", C.c_double * 3), ("CoM", C.c_double * 3),
-                ("r_max", C.c_double)]
+                ("r_max", C.c_double), ("multipole", C.POINTER(Multipole))]
 
 
 class SpaceInfo(C.Structure):
@@ -176,7 +202,7 @@ class Leaf(C.Structure):
 
 
 LEAF_DTYPE = np.dtype([("start", "<i4"), ("count", "<i4")])
-LEAF_PAIR_DTYPE = np.dtype([("j", "<i4"), ("truncated", "<i4")])
+LEAF_PAIR_DTYPE = np.dtype([("j", "<i4"), ("truncated", "<i4"), ("allow_mpole", "<i4")])
 
 FIELDS_DENSITY, FIELDS_GRADIENT, FIELDS_FORCE, FIELDS_ALL = 1, 2, 4, 7
 # halo record fields (swh_space_unpack_halo): h, rho, P + c, f + balsara, alphas
@@ -246,13 +272,58 @@ class PmMesh(C.Structure):
                 ("r_cut_min", C.c_double), ("r_cut_max", C.c_double)]
 
 
+_TENSOR_NAMES = ["%d%d%d" % t for t in MPOLE_INDEX]
+
+
+class GravTensor(C.Structure):
+    """include/swift_compat.h struct grav_tensor (SWIFT multipole_struct.h:36)."""
+
+    _fields_ = [("F_" + n, C.c_float) for n in _TENSOR_NAMES] + [("interacted", C.c_int)]
+
+
+class MultipoleStruct(C.Structure):
+    """include/swift_compat.h struct multipole (SWIFT multipole_struct.h:110):
+    the dipole terms are not stored."""
+
+    _fields_ = ([("vel", C.c_float * 3), ("max_delta_vel", C.c_float * 3),
+                 ("min_delta_vel", C.c_float * 3), ("max_softening", C.c_float),
+                 ("min_old_a_grav_norm", C.c_float), ("power", C.c_float * 5)] +
+                [("M_" + n, C.c_float) for n in _TENSOR_NAMES if n not in ("100", "010", "001")])
+
+
 class GravityTensors(C.Structure):
-    _fields_ = [("CoM", C.c_double * 3), ("r_max", C.c_float)]
+    _fields_ = [("pot", GravTensor), ("m_pole", MultipoleStruct), ("CoM", C.c_double * 3),
+                ("CoM_rebuild", C.c_double * 3), ("r_max", C.c_double),
+                ("r_max_rebuild", C.c_double)]
+
+    def set_from(self, m: Multipole) -> None:
+        """Fill from a swh_multipole (the adapter's inverse map)."""
+        for k in range(3):
+            self.CoM[k] = m.CoM[k]
+        self.r_max = m.r_max
+        mp = self.m_pole
+        mp.max_softening = m.max_softening
+        mp.min_old_a_grav_norm = m.min_old_a_grav_norm
+        for k in range(5):
+            mp.power[k] = m.power[k]
+        for t, n in enumerate(_TENSOR_NAMES):
+            if n not in ("100", "010", "001"):
+                setattr(mp, "M_" + n, m.M[t])
+
+
+class GravityProps(C.Structure):
+    """include/swift_compat.h struct gravity_props (the MAC fields)."""
+
+    _fields_ = [("use_advanced_MAC", C.c_int), ("use_adaptive_tolerance", C.c_int),
+                ("use_gadget_tolerance", C.c_int), ("adaptive_tolerance", C.c_float),
+                ("theta_crit", C.c_double), ("use_tree_below_softening", C.c_int),
+                ("consider_truncation_in_MAC", C.c_int)]
 
 
 class Engine(C.Structure):
     _fields_ = [("s", C.POINTER(Space)), ("cosmology", C.POINTER(Cosmology)),
                 ("hydro_properties", C.POINTER(HydroProps)), ("mesh", C.POINTER(PmMesh)),
+                ("gravity_properties", C.POINTER(GravityProps)),
                 ("max_active_bin", C.c_int8), ("ti_current", C.c_longlong),
                 ("time_base", C.c_double), ("policy", C.c_int), ("nodeID", C.c_int)]
 
@@ -287,7 +358,7 @@ class EngineBundle:
     """Owns a compat engine + the structs it points to (keeps them alive)."""
 
     def __init__(self, dim=(1.0, 1.0, 1.0), periodic=True, ti_current=8, params=None,
-                 max_active_bin=NUM_TIME_BINS, mesh=None):
+                 max_active_bin=NUM_TIME_BINS, mesh=None, gravity_props=None):
         P = params or default_hydro_params(dim, periodic)
         self.params = P
         self.space = Space(1 if periodic else 0, (C.c_double * 3)(*dim))
@@ -300,8 +371,10 @@ class EngineBundle:
                              DiffusionGlobal(P.diff_alpha, P.diff_beta, P.diff_alpha_max,
                                              P.diff_alpha_min))
         self.mesh = mesh or PmMesh(0, (C.c_double * 3)(*dim), 0.0, 0.0, 0.0)
+        self.gprops = gravity_props or GravityProps(0, 0, 0, 0.0, 0.5, 0, 0)
         self.engine = Engine(C.pointer(self.space), C.pointer(self.cosmo), C.pointer(self.hp),
-                             C.pointer(self.mesh), max_active_bin, ti_current, P.time_base, 0, 0)
+                             C.pointer(self.mesh), C.pointer(self.gprops), max_active_bin,
+                             ti_current, P.time_base, 0, 0)
         self.runner = Runner(C.pointer(self.engine), 0)
 
     @property

@@ -87,6 +87,7 @@ swh_status make_glayout(const swh_gpart_layout* L, GLayout* o) {
   o->mass = L->off_mass;
   o->epsilon = L->off_epsilon;
   o->time_bin = L->off_time_bin;
+  o->old_a_grav_norm = L->off_old_a_grav_norm;
   return SWH_OK;
 }
 
@@ -170,6 +171,7 @@ void swh_gpart_layout_multisoftening(swh_gpart_layout* o) {
   o->off_mass = offsetof(struct gpart, mass);
   o->off_epsilon = offsetof(struct gpart, epsilon);
   o->off_time_bin = offsetof(struct gpart, time_bin);
+  o->off_old_a_grav_norm = offsetof(struct gpart, old_a_grav_norm);
 }
 
 swh_status swh_init(swh_context** out, int device) {

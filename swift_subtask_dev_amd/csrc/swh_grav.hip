@@ -13,7 +13,14 @@
 // reciprocal square root refined by Newton steps, 1/max(eps_i, eps_j) as
 // min(1/eps_i, 1/eps_j) from per-particle reciprocals (no division), and the
 // i == j term of a self tile removed by a zero mass instead of a branch.
+//
+// Pairs flagged allow_mpole (runner_dopair_grav_pp's allow_mpole, the
+// recursive pair task's M2P branch, runner_doiact_grav.c:1273-1400): an
+// i-particle that passes gravity_M2P_accept against the source leaf's
+// multipole (float test, swh_mpole.h) skips that leaf's P2P tiles (zero mass)
+// and takes M2P instead, in m2p_kernel; leaf multipoles come from p2m_kernel.
 #include "swh_internal.h"
+#include "swh_mpole.h"
 #include "swh_physics.h"
 #include "swh_tile.h"
 
@@ -28,6 +35,8 @@ struct GSoA {
   float* mass;   // 0 for inhibited
   int8_t* active;
   double4* acc;  // a_x, a_y, a_z, potential
+  float* oagn;   // old_a_grav_norm (adaptive MAC)
+  const swh_multipole* mp;  // per leaf (p2m_kernel)
 };
 
 __global__ void gunpack_kernel(GLayout L, const char* __restrict__ aos, int64_t n, GSoA g,
@@ -44,6 +53,106 @@ __global__ void gunpack_kernel(GLayout L, const char* __restrict__ aos, int64_t 
   g.mass[i] = inhibited ? 0.f : *reinterpret_cast<const float*>(r + L.mass);
   g.active[i] = (!inhibited && tb <= max_active_bin) ? 1 : 0;
   g.acc[i] = make_double4(0., 0., 0., 0.);
+  g.oagn[i] = L.old_a_grav_norm >= 0 ? *reinterpret_cast<const float*>(r + L.old_a_grav_norm)
+                                     : 0.f;
+}
+
+// gravity_P2M + gravity_multipole_compute_power (multipole.h:878-1266) of one
+// leaf per workgroup: mass, CoM and bulk sums in double, then the moments
+// M_n = (-1)^|n| sum m dx^n / n! about the CoM, r_max, max softening and the
+// minimum old |a|; stored as the reference stores them (float terms).
+__global__ __launch_bounds__(256) void p2m_kernel(GLayout L, const char* __restrict__ aos,
+                                                  const swh_leaf* __restrict__ leaves,
+                                                  swh_multipole* __restrict__ out) {
+  __shared__ double red[4][SWH_MPOLE_TERMS + 1];
+  __shared__ double com_s[4];
+  const swh_leaf lf = leaves[blockIdx.x];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  auto rec = [&](int k) { return aos + (size_t)(lf.start + k) * L.stride; };
+  auto block_sum = [&](double* v, int n) {  // sums v[0..n) over the block into red[0]
+    for (int t = 0; t < n; t++) {
+      double x = v[t];
+      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+      if (lane == 0) red[wv][t] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int t = 0; t < n; t++) red[0][t] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+    __syncthreads();
+  };
+  double v[SWH_MPOLE_TERMS + 1];
+  // pass 1: mass and mass-weighted position
+  v[0] = v[1] = v[2] = v[3] = 0.;
+  float eps_max = 0.f, oag_min = FLT_MAX;
+  for (int k = threadIdx.x; k < lf.count; k += blockDim.x) {
+    const char* r = rec(k);
+    const double* x = reinterpret_cast<const double*>(r + L.x);
+    const double m = *reinterpret_cast<const float*>(r + L.mass);
+    v[0] += m;
+    v[1] += x[0] * m;
+    v[2] += x[1] * m;
+    v[3] += x[2] * m;
+    eps_max = fmaxf(eps_max, *reinterpret_cast<const float*>(r + L.epsilon));
+    if (L.old_a_grav_norm >= 0)
+      oag_min = fminf(oag_min, *reinterpret_cast<const float*>(r + L.old_a_grav_norm));
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    eps_max = fmaxf(eps_max, __shfl_xor(eps_max, o));
+    oag_min = fminf(oag_min, __shfl_xor(oag_min, o));
+  }
+  __shared__ float em_s[4], om_s[4];
+  if (lane == 0) {
+    em_s[wv] = eps_max;
+    om_s[wv] = oag_min;
+  }
+  block_sum(v, 4);
+  if (threadIdx.x == 0) {
+    const double imass = 1.0 / red[0][0];
+    for (int k = 0; k < 3; k++) com_s[k] = red[0][k + 1] * imass;
+    com_s[3] = red[0][0];
+  }
+  __syncthreads();
+  const double com[3] = {com_s[0], com_s[1], com_s[2]};
+  const double mass = com_s[3];
+  // pass 2: moments about the CoM and r_max^2
+  for (int t = 0; t <= SWH_MPOLE_TERMS; t++) v[t] = 0.;
+  double rmax2 = 0.;
+  for (int k = threadIdx.x; k < lf.count; k += blockDim.x) {
+    const char* r = rec(k);
+    const double* x = reinterpret_cast<const double*>(r + L.x);
+    const double m = *reinterpret_cast<const float*>(r + L.mass);
+    const double d[3] = {x[0] - com[0], x[1] - com[1], x[2] - com[2]};
+    rmax2 = fmax(rmax2, d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    double px[5], py[5], pz[5];
+    px[0] = py[0] = pz[0] = 1.;
+    for (int q = 1; q < 5; q++) {
+      px[q] = px[q - 1] * d[0];
+      py[q] = py[q - 1] * d[1];
+      pz[q] = pz[q - 1] * d[2];
+    }
+#pragma unroll
+    for (int t = 4; t < SWH_MPOLE_TERMS; t++) {
+      const int a = kMpA[t], b = kMpB[t], c = kMpC[t];
+      const double X = px[a] * py[b] * pz[c] / (fact(a) * fact(b) * fact(c));
+      v[t] += ((a + b + c) & 1) ? -m * X : m * X;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) rmax2 = fmax(rmax2, __shfl_xor(rmax2, o));
+  __shared__ double rm_s[4];
+  if (lane == 0) rm_s[wv] = rmax2;
+  block_sum(v, SWH_MPOLE_TERMS);
+  if (threadIdx.x == 0) {
+    swh_multipole M;
+    for (int k = 0; k < 3; k++) M.CoM[k] = com[k];
+    M.r_max = sqrt(fmax(fmax(rm_s[0], rm_s[1]), fmax(rm_s[2], rm_s[3])));
+    M.M[0] = (float)mass;
+    M.M[1] = M.M[2] = M.M[3] = 0.f;
+    for (int t = 4; t < SWH_MPOLE_TERMS; t++) M.M[t] = (float)red[0][t];
+    M.max_softening = fmaxf(fmaxf(em_s[0], em_s[1]), fmaxf(em_s[2], em_s[3]));
+    M.min_old_a_grav_norm = fminf(fminf(om_s[0], om_s[1]), fminf(om_s[2], om_s[3]));
+    mpole_power(M);
+    out[blockIdx.x] = M;
+  }
 }
 
 __global__ void gpack_kernel(GLayout L, char* __restrict__ aos, int64_t n, GSoA g) {
@@ -130,10 +239,33 @@ __device__ __forceinline__ void p2p_tile(const double* sx, const double* sy, con
   }
 }
 
+// Per pair: which of this thread's i-particles take the source leaf's
+// multipole instead (allow_mpole pairs only; block-uniform branch).
+__device__ __forceinline__ void mpole_mask(const GSoA& g, const MacParams& P,
+                                           const swh_leaf_pair& pr, const swh_leaf& J,
+                                           const bool* act, const int* gi, bool* actp) {
+  const bool mp = pr.allow_mpole && J.count > 1;
+  if (!mp) {
+#pragma unroll
+    for (int k = 0; k < kIPer; k++) actp[k] = act[k];
+    return;
+  }
+  const MacSource B = mac_source(g.mp[pr.j]);
+#pragma unroll
+  for (int k = 0; k < kIPer; k++) {
+    bool use = false;
+    if (act[k]) {
+      const double4 p = g.pos[gi[k]];
+      use = m2p_accept(P, B, (float)p.x, (float)p.y, (float)p.z, (float)p.w, g.oagn[gi[k]]);
+    }
+    actp[k] = act[k] && !use;
+  }
+}
+
 __global__ __launch_bounds__(kGravBlock) void p2p_kernel(
     GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
     const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
-    double dimz, double r_s_inv, unsigned long long* counter) {
+    double dimz, double r_s_inv, MacParams mac, unsigned long long* counter) {
   __shared__ double sx[kGravBlock], sy[kGravBlock], sz[kGravBlock], se2[kGravBlock],
       sh[kGravBlock];
   __shared__ float sm[kGravBlock];
@@ -160,6 +292,8 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel(
     for (int q = p0; q < p1; q++) {
       const swh_leaf_pair pr = pairs[q];
       const swh_leaf J = leaves[pr.j];
+      bool actp[kIPer];  // act minus the particles taking this leaf's multipole
+      mpole_mask(g, mac, pr, J, act, gi, actp);
       for (int jbase = 0; jbase < J.count; jbase += kGravBlock) {
         const int nt = min(kGravBlock, J.count - jbase);
         __syncthreads();
@@ -180,11 +314,11 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel(
 #pragma unroll
         for (int k = 0; k < kIPer; k++) {
           self_local[k] = gi[k] - (J.start + jbase);
-          if (act[k])
+          if (actp[k])
             nint += (unsigned long long)(nt - ((self_local[k] >= 0 && self_local[k] < nt) ? 1 : 0));
         }
 #define SWH_P2P_TILE(TR, PE, SE)                                                             \
-  p2p_tile<TR, PE, SE>(sx, sy, sz, se2, sh, sm, nt, self_local, xi, yi, zi, hi2, hv, act, dimx, \
+  p2p_tile<TR, PE, SE>(sx, sy, sz, se2, sh, sm, nt, self_local, xi, yi, zi, hi2, hv, actp, dimx, \
                        dimy, dimz, r_s_inv, ax, ay, az, pot)
         if (self) {
           if (pr.truncated) {
@@ -228,7 +362,7 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel(
 __global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
     GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
     const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
-    double dimz, float r_s_inv, unsigned long long* counter) {
+    double dimz, float r_s_inv, MacParams mac, unsigned long long* counter) {
   using T = float;
   __shared__ double sx[kGravBlock], sy[kGravBlock], sz[kGravBlock];
   __shared__ float se[kGravBlock], sm[kGravBlock];
@@ -254,6 +388,8 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
     for (int q = p0; q < p1; q++) {
       const swh_leaf_pair pr = pairs[q];
       const swh_leaf J = leaves[pr.j];
+      bool actp[kIPer];
+      mpole_mask(g, mac, pr, J, act, gi, actp);
       for (int jbase = 0; jbase < J.count; jbase += kGravBlock) {
         const int nt = min(kGravBlock, J.count - jbase);
         __syncthreads();
@@ -269,7 +405,7 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < kIPer; k++) {
-          if (!act[k]) continue;
+          if (!actp[k]) continue;
           const int self_local = gi[k] - (J.start + jbase);
           for (int t = 0; t < nt; t++) {
             if (t == self_local) continue;
@@ -313,6 +449,58 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
   }
 }
 
+// M2P of the allow_mpole pairs (runner_dopair_grav_pm_full / _truncated,
+// runner_doiact_grav.c:911-1200): every active i of the i-leaf that passes
+// the MAC against source leaf j's multipole. Runs after p2p_kernel on the
+// same stream (both add into acc).
+template <typename T>
+__global__ __launch_bounds__(kGravBlock) void m2p_kernel(
+    GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
+    const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
+    double dimz, double r_s_inv, MacParams mac, unsigned long long* counter) {
+  const int li = xcd_block_id();
+  const swh_leaf L = leaves[li];
+  const int p0 = pair_off[li], p1 = pair_off[li + 1];
+  unsigned long long nm = 0;
+  for (int local = threadIdx.x; local < L.count; local += kGravBlock) {
+    const int i = L.start + local;
+    if (!g.active[i]) continue;
+    const double4 p = g.pos[i];
+    const float oag = g.oagn[i];
+    T F[4] = {(T)0, (T)0, (T)0, (T)0};
+    for (int q = p0; q < p1; q++) {
+      const swh_leaf_pair pr = pairs[q];
+      if (!pr.allow_mpole || leaves[pr.j].count <= 1) continue;
+      const swh_multipole& M = g.mp[pr.j];
+      if (!m2p_accept(mac, mac_source(M), (float)p.x, (float)p.y, (float)p.z, (float)p.w, oag))
+        continue;
+      double dx = M.CoM[0] - p.x, dy = M.CoM[1] - p.y, dz = M.CoM[2] - p.z;
+      if (periodic) {
+        dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
+        dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
+        dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
+      }
+      const T eps = (T)fmaxf((float)p.w, M.max_softening);
+      T f[4];
+      m2p<T>(M.M, (T)dx, (T)dy, (T)dz, eps, pr.truncated != 0, (T)r_s_inv, f);
+      for (int k = 0; k < 4; k++) F[k] += f[k];
+      nm++;
+    }
+    if (F[0] != (T)0 || F[1] != (T)0 || F[2] != (T)0 || F[3] != (T)0) {
+      double4 a = g.acc[i];
+      a.x += (double)F[1];
+      a.y += (double)F[2];
+      a.z += (double)F[3];
+      a.w += (double)F[0];
+      g.acc[i] = a;
+    }
+  }
+  if (counter) {
+    for (int o = 32; o > 0; o >>= 1) nm += __shfl_xor(nm, o);
+    if ((threadIdx.x & 63) == 0 && nm) atomicAdd(counter + 1, nm);
+  }
+}
+
 static GSoA gsoa_of(swh_gspace* g) {
   GSoA s;
   s.pos = g->pos.as<double4>();
@@ -320,6 +508,8 @@ static GSoA gsoa_of(swh_gspace* g) {
   s.mass = g->mass.as<float>();
   s.active = g->active.as<int8_t>();
   s.acc = g->accel.as<double4>();
+  s.oagn = g->oagn.as<float>();
+  s.mp = g->mpoles.as<const swh_multipole>();
   return s;
 }
 
@@ -347,7 +537,7 @@ swh_status swh_gspace_destroy(swh_gspace* g) {
   (void)hipSetDevice(g->ctx->device);
   (void)hipStreamSynchronize(g->stream);
   DevBuf* bufs[] = {&g->aos, &g->pos, &g->hinv, &g->mass, &g->active, &g->accel,
-                    &g->leaves, &g->pair_off, &g->pairs, &g->counter};
+                    &g->oagn, &g->mpoles, &g->leaves, &g->pair_off, &g->pairs, &g->counter};
   for (DevBuf* b : bufs) b->release();
   (void)hipStreamDestroy(g->stream);
   delete g;
@@ -372,6 +562,8 @@ swh_status swh_gspace_upload(swh_gspace* g, const void* gparts, int64_t count,
   SWH_TRY(g->mass.reserve((size_t)count * sizeof(float)));
   SWH_TRY(g->active.reserve((size_t)count));
   SWH_TRY(g->accel.reserve((size_t)count * sizeof(double4)));
+  SWH_TRY(g->oagn.reserve((size_t)count * sizeof(float)));
+  g->mpoles_valid = false;
   SWH_HIP(hipMemcpyAsync(g->aos.ptr, gparts, (size_t)count * L.stride,
                          on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
                          g->stream));
@@ -420,40 +612,84 @@ swh_status swh_gspace_set_leaves(swh_gspace* g, const swh_leaf* leaves, int32_t 
   g->nleaves = nleaves;
   g->npairs = npairs;
   g->max_leaf = maxc;
+  g->mpoles_valid = false;
+  g->any_mpole = false;
+  for (int q = 0; q < npairs; q++) g->any_mpole = g->any_mpole || pairs[q].allow_mpole;
   return SWH_OK;
 }
 
-swh_status swh_grav_pp_batch(swh_gspace* g, const swh_grav_params* G, int64_t* n_int) {
+swh_status swh_gspace_make_multipoles(swh_gspace* g, swh_multipole* out) {
+  if (!g) return SWH_ERR_ARG;
+  if (g->nleaves == 0) return SWH_OK;
+  SWH_HIP(hipSetDevice(g->ctx->device));
+  SWH_TRY(g->mpoles.reserve((size_t)g->nleaves * sizeof(swh_multipole)));
+  hipLaunchKernelGGL(p2m_kernel, dim3(g->nleaves), dim3(256), 0, g->stream, g->layout,
+                     g->aos.as<const char>(), g->leaves.as<const swh_leaf>(),
+                     g->mpoles.as<swh_multipole>());
+  SWH_HIP(hipGetLastError());
+  g->mpoles_valid = true;
+  if (out) {
+    SWH_HIP(hipMemcpyAsync(out, g->mpoles.ptr, (size_t)g->nleaves * sizeof(swh_multipole),
+                           hipMemcpyDeviceToHost, g->stream));
+    SWH_HIP(hipStreamSynchronize(g->stream));
+  }
+  return SWH_OK;
+}
+
+swh_status swh_grav_pp_batch(swh_gspace* g, const swh_grav_params* G, int64_t* n_int,
+                             int64_t* n_m2p) {
   if (!g || !G) return SWH_ERR_ARG;
+  if (n_m2p) *n_m2p = 0;
   if (g->n == 0 || g->nleaves == 0) {
     if (n_int) *n_int = 0;
     return SWH_OK;
   }
+  if (g->any_mpole && !g->mpoles_valid) {
+    set_error("allow_mpole pairs need swh_gspace_make_multipoles first");
+    return SWH_ERR_STATE;
+  }
+  const MacParams mac = mac_params(G);
+  const bool want = n_int || n_m2p;
   SWH_HIP(hipSetDevice(g->ctx->device));
   const int block = 256;
   hipLaunchKernelGGL(gunpack_kernel, dim3((int)((g->n + block - 1) / block)), dim3(block), 0,
                      g->stream, g->layout, g->aos.as<const char>(), g->n, gsoa_of(g),
                      G->max_active_bin);
   SWH_HIP(hipGetLastError());
-  SWH_TRY(g->counter.reserve(sizeof(unsigned long long)));
-  unsigned long long* ctr = n_int ? g->counter.as<unsigned long long>() : nullptr;
-  if (ctr) SWH_HIP(hipMemsetAsync(ctr, 0, sizeof(unsigned long long), g->stream));
-  if (g->ctx->precision == SWH_PRECISION_F64)
+  SWH_TRY(g->counter.reserve(2 * sizeof(unsigned long long)));
+  unsigned long long* ctr = want ? g->counter.as<unsigned long long>() : nullptr;
+  if (ctr) SWH_HIP(hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned long long), g->stream));
+  const bool f64 = g->ctx->precision == SWH_PRECISION_F64;
+  if (f64)
     hipLaunchKernelGGL(p2p_kernel, dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
                        gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
                        g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
-                       (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, ctr);
+                       (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, mac, ctr);
   else
     hipLaunchKernelGGL(p2p_kernel_f32, dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
                        gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
                        g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
-                       (double)G->dim[1], (double)G->dim[2], (float)G->r_s_inv, ctr);
+                       (double)G->dim[1], (double)G->dim[2], (float)G->r_s_inv, mac, ctr);
   SWH_HIP(hipGetLastError());
-  if (n_int) {
-    unsigned long long h = 0;
-    SWH_HIP(hipMemcpyAsync(&h, ctr, sizeof(h), hipMemcpyDeviceToHost, g->stream));
+  if (g->any_mpole) {
+    if (f64)
+      hipLaunchKernelGGL((m2p_kernel<double>), dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
+                         gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
+                         g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
+                         (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, mac, ctr);
+    else
+      hipLaunchKernelGGL((m2p_kernel<float>), dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
+                         gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
+                         g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
+                         (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, mac, ctr);
+    SWH_HIP(hipGetLastError());
+  }
+  if (want) {
+    unsigned long long h[2] = {0, 0};
+    SWH_HIP(hipMemcpyAsync(h, ctr, sizeof(h), hipMemcpyDeviceToHost, g->stream));
     SWH_HIP(hipStreamSynchronize(g->stream));
-    *n_int = (int64_t)h;
+    if (n_int) *n_int = (int64_t)h[0];
+    if (n_m2p) *n_m2p = (int64_t)h[1];
   }
   return SWH_OK;
 }

@@ -105,6 +105,7 @@ swh_status make_layout(const swh_part_layout* L, Layout* out);
 
 struct GLayout {
   int stride, x, a_grav, potential, mass, epsilon, time_bin;
+  int old_a_grav_norm;  // -1: not in the record (the adaptive MAC then sees 0)
 };
 swh_status make_glayout(const swh_gpart_layout* L, GLayout* out);
 
@@ -209,6 +210,10 @@ struct swh_gspace {
   swh::DevBuf mass;    // float  mass (0 for inhibited)
   swh::DevBuf active;  // int8
   swh::DevBuf accel;   // double4 ax, ay, az, pot (accumulated this call)
+  swh::DevBuf oagn;    // float old_a_grav_norm (the adaptive MAC's estimate)
+  swh::DevBuf mpoles;  // swh_multipole[nleaves] (swh_gspace_make_multipoles)
+  bool mpoles_valid = false;
+  bool any_mpole = false;  // some pair has allow_mpole
   swh::DevBuf leaves, pair_off, pairs;
   int32_t nleaves = 0, npairs = 0;
   int32_t max_leaf = 0;

@@ -1,0 +1,269 @@
+// swh_mpole.h — multipole side of the gravity path: the M2P acceptance test
+// (gravity_M2P_accept, src/multipole_accept.h:290-373, as evaluated by
+// gravity_cache_populate, src/gravity_cache.h:200-290), the M2P kernel
+// (gravity_M2P + potential_derivatives_compute_M2P, src/multipole.h:2257-2480,
+// src/gravity_derivatives.h:516-760) and leaf P2M (gravity_P2M +
+// gravity_multipole_compute_power, src/multipole.h:878-1266), order 4.
+//
+// The acceptance test is a discrete choice between two approximations, so it
+// is evaluated in float, operation by operation as the reference does
+// (contraction off): the GPU takes the M2P route for exactly the particles
+// SWIFT does. The M2P itself is written differently from the reference's
+// term-by-term listing: with g_m = (r^-1 d/dr)^m phi the derivative tensor of
+// a radial potential is
+//   D_abc = sum_{i,j,k} C(a,i) C(b,j) C(c,k) x^(a-2i) y^(b-2j) z^(c-2k) g_(a+b+c-i-j-k),
+//   C(a,i) = a! / (2^i i! (a-2i)!),
+// and the field is F_000 = -sum_n (-1)^|n| M_n D_n, F_e = -sum_n (-1)^|n| M_n
+// D_(n+e) over the 35 terms n of the order-4 expansion; the loops are
+// compile-time, so the compiler emits straight-line FMA code.
+#pragma once
+
+#include "swh_physics.h"
+#include "swifthip.h"
+
+namespace swh {
+
+// Multi-indices of swh_multipole::M (include/swifthip.h), struct multipole's
+// member order.
+constexpr int kMpA[SWH_MPOLE_TERMS] = {0, 1, 0, 0, 2, 0, 0, 1, 1, 0, 3, 0, 0, 2, 2, 1, 0, 1,
+                                       0, 1, 4, 0, 0, 3, 3, 1, 0, 1, 0, 2, 2, 0, 2, 1, 1};
+constexpr int kMpB[SWH_MPOLE_TERMS] = {0, 0, 1, 0, 0, 2, 0, 1, 0, 1, 0, 3, 0, 1, 0, 2, 2, 0,
+                                       1, 1, 0, 4, 0, 1, 0, 3, 3, 0, 1, 2, 0, 2, 1, 2, 1};
+constexpr int kMpC[SWH_MPOLE_TERMS] = {0, 0, 0, 1, 0, 0, 2, 0, 1, 1, 0, 0, 3, 0, 1, 0, 1, 2,
+                                       2, 1, 0, 0, 4, 0, 1, 0, 1, 3, 3, 0, 2, 2, 1, 1, 2};
+
+// C(a, i) = a! / (2^i i! (a - 2i)!), a <= 5.
+__host__ __device__ constexpr double herm_coef(int a, int i) {
+  return a == 2 ? 1.
+       : a == 3 ? (i == 0 ? 1. : 3.)
+       : a == 4 ? (i == 0 ? 1. : (i == 1 ? 6. : 3.))
+       : a == 5 ? (i == 0 ? 1. : (i == 1 ? 10. : 15.))
+                : 1.;
+}
+
+// n! for n <= 4
+__host__ __device__ constexpr double fact(int n) { return n <= 1 ? 1. : n * fact(n - 1); }
+
+// MAC parameters (swh_grav_params) in the float form the reference uses.
+struct MacParams {
+  float theta_crit2, eps, r_s_inv;
+  int advanced, gadget, below_soft, trunc_mac, periodic;
+  float dim[3];
+};
+
+inline MacParams mac_params(const swh_grav_params* G) {
+  MacParams m;
+  const float th = G->theta_crit;
+  m.theta_crit2 = th * th;
+  m.eps = G->adaptive_tolerance;
+  m.r_s_inv = G->r_s_inv;
+  m.advanced = G->use_advanced_MAC;
+  m.gadget = G->use_gadget_tolerance;
+  m.below_soft = G->use_tree_below_softening;
+  m.trunc_mac = G->consider_truncation_in_MAC;
+  m.periodic = G->periodic;
+  for (int k = 0; k < 3; k++) m.dim[k] = G->dim[k];
+  return m;
+}
+
+// The multipole fields the acceptance test reads, as floats.
+struct MacSource {
+  float CoM[3];
+  float rho;        // r_max
+  float max_soft;   // m_pole.max_softening
+  float power2;     // m_pole.power[2]
+  float M000;
+};
+
+__host__ __device__ inline MacSource mac_source(const swh_multipole& m) {
+  MacSource s;
+  for (int k = 0; k < 3; k++) s.CoM[k] = (float)m.CoM[k];
+  s.rho = (float)m.r_max;
+  s.max_soft = m.max_softening;
+  s.power2 = m.power[2];
+  s.M000 = m.M[0];
+  return s;
+}
+
+// gravity_cache_populate's use_mpole for one particle at float position
+// (x, y, z) with softening eps_i and old_a_grav_norm old_a.
+__device__ inline bool m2p_accept(const MacParams& P, const MacSource& B, float x, float y,
+                                  float z, float eps_i, float old_a) {
+#pragma clang fp contract(off)
+  float dx = x - B.CoM[0];
+  float dy = y - B.CoM[1];
+  float dz = z - B.CoM[2];
+  if (P.periodic) {
+    dx = dx > 0.5f * P.dim[0] ? dx - P.dim[0] : (dx < -0.5f * P.dim[0] ? dx + P.dim[0] : dx);
+    dy = dy > 0.5f * P.dim[1] ? dy - P.dim[1] : (dy < -0.5f * P.dim[1] ? dy + P.dim[1] : dy);
+    dz = dz > 0.5f * P.dim[2] ? dz - P.dim[2] : (dz < -0.5f * P.dim[2] ? dz + P.dim[2] : dz);
+  }
+  const float r2 = dx * dx + dy * dy + dz * dz;
+  const float max_soft = fmaxf(B.max_soft, eps_i);
+  const float E_BA_term = 8.f * B.power2;
+  float f_MAC_inv = r2;
+  if (P.periodic && P.trunc_mac) {  // gravity_f_MAC_inverse
+    const float H = max_soft;
+    if (r2 < (25.f / 81.f) * H * H)
+      f_MAC_inv = (25.f / 81.f) * H * H;
+    else if (P.r_s_inv * P.r_s_inv * r2 > (25.f / 9.f))
+      f_MAC_inv = (9.f / 25.f) * P.r_s_inv * P.r_s_inv * r2 * r2;
+  }
+  const bool cond_2 = P.below_soft || max_soft * max_soft < r2;
+  if (P.advanced && P.gadget) {
+    const float q = B.rho / sqrtf(r2);
+    const float q2 = q * q;
+    const float ratio = q2 * q2;  // integer_powf(q, 4)
+    return (B.M000 * ratio < P.eps * old_a * f_MAC_inv) && cond_2;
+  }
+  if (P.advanced) {
+    const bool cond_1 = B.rho * B.rho < r2;
+    const bool cond_3 = E_BA_term < P.eps * old_a * r2 * f_MAC_inv;
+    return cond_1 && cond_2 && cond_3;
+  }
+  return (B.rho * B.rho < P.theta_crit2 * r2) && cond_2;
+}
+
+// D_soft_k(u) of the Wendland-C2 softening (kernel_gravity.h:169-275).
+template <typename T>
+__device__ __forceinline__ void d_soft(T u, T* d) {
+  const T u2 = u * u;
+  d[1] = ((((-(T)3 * u + (T)15) * u - (T)28) * u + (T)21) * u2 - (T)7) * u2 + (T)3;
+  d[2] = (((-(T)21 * u + (T)90) * u - (T)140) * u + (T)84) * u2 * u - (T)14 * u;
+  d[3] = (((-(T)105 * u + (T)360) * u - (T)420) * u + (T)168) * u2;
+  d[4] = ((-(T)315 * u + (T)720) * u - (T)420) * u2;
+  d[5] = (-(T)315 * u2 + (T)420) * u;
+  d[6] = (T)315 * u2 - (T)1260;
+}
+
+// g_m = Dt_(m+1) r^-m, m = 0..5 (Dt of potential_derivatives_compute_M2P):
+// softened below eps, Newtonian, or truncated by the long-range kernel
+// (kernel_long_grav_derivatives, default branch, kernel_long_gravity.h:151-183).
+template <typename T>
+__device__ __forceinline__ void radial_chain(T r2, T r_inv, T eps, bool periodic, T r_s_inv,
+                                             T* g) {
+  T Dt[7];
+  if (r2 < eps * eps) {
+    const T eps_inv = (T)1 / eps;
+    const T u = r2 * r_inv * eps_inv;
+    T d[7];
+    d_soft<T>(u, d);
+    T e = eps_inv;
+    for (int k = 1; k <= 6; k++) {
+      Dt[k] = e * d[k];
+      e *= eps_inv;
+    }
+  } else if (!periodic) {
+    Dt[1] = r_inv;
+    for (int k = 2; k <= 6; k++) Dt[k] = -(T)(2 * k - 3) * Dt[k - 1] * r_inv;
+  } else {
+    const T r = r2 * r_inv;
+    const T c1 = (T)2 * r_s_inv;
+    const T x = c1 * r;
+    const T exp_x = exp(x);
+    const T a1 = (T)1 / ((T)1 + exp_x);
+    const T a2 = a1 * a1, a3 = a2 * a1, a4 = a3 * a1, a5 = a4 * a1, a6 = a5 * a1;
+    const T c2 = c1 * c1, c3 = c2 * c1, c4 = c3 * c1, c5 = c4 * c1;
+    const T m2e = -(T)2 * exp_x;
+    T chi[6];
+    chi[0] = m2e * a1 + (T)2;
+    chi[1] = m2e * c1 * a2;
+    chi[2] = m2e * c2 * ((T)2 * a3 - a2);
+    chi[3] = m2e * c3 * ((T)6 * a4 - (T)6 * a3 + a2);
+    chi[4] = m2e * c4 * ((T)24 * a5 - (T)36 * a4 + (T)14 * a3 - a2);
+    chi[5] = m2e * c5 * ((T)120 * a6 - (T)240 * a5 + (T)150 * a4 - (T)30 * a3 + a2);
+    // Dt_k from chi_0..chi_(k-1), nested in r^-1 as the reference does
+    const T ri = r_inv;
+    Dt[1] = chi[0] * ri;
+    Dt[2] = (chi[1] - chi[0] * ri) * ri;
+    Dt[3] = ((chi[0] * ri - chi[1]) * (T)3 * ri + chi[2]) * ri;
+    Dt[4] = (((-chi[0] * ri + chi[1]) * (T)15 * ri - (T)6 * chi[2]) * ri + chi[3]) * ri;
+    Dt[5] = ((((chi[0] * ri - chi[1]) * (T)105 * ri + (T)45 * chi[2]) * ri - (T)10 * chi[3]) *
+                 ri + chi[4]) * ri;
+    Dt[6] = (((((-chi[0] * ri + chi[1]) * (T)945 * ri - (T)420 * chi[2]) * ri +
+               (T)105 * chi[3]) * ri - (T)15 * chi[4]) * ri + chi[5]) * ri;
+  }
+  T rp = (T)1;
+  for (int m = 0; m <= 5; m++) {
+    g[m] = Dt[m + 1] * rp;
+    rp *= r_inv;
+  }
+}
+
+// D_abc from the powers of the separation and the radial chain.
+template <typename T, int A, int B, int C>
+__device__ __forceinline__ T dtensor(const T* xp, const T* yp, const T* zp, const T* g) {
+  T d = (T)0;
+#pragma unroll
+  for (int i = 0; 2 * i <= A; i++)
+#pragma unroll
+    for (int j = 0; 2 * j <= B; j++)
+#pragma unroll
+      for (int k = 0; 2 * k <= C; k++)
+        d += (T)(herm_coef(A, i) * herm_coef(B, j) * herm_coef(C, k)) * xp[A - 2 * i] *
+             yp[B - 2 * j] * zp[C - 2 * k] * g[A + B + C - i - j - k];
+  return d;
+}
+
+template <typename T, int t>
+__device__ __forceinline__ void m2p_term(const float* M, const T* xp, const T* yp, const T* zp,
+                                         const T* g, T* F) {
+  constexpr int a = kMpA[t], b = kMpB[t], c = kMpC[t];
+  const T m = ((a + b + c) & 1) ? -(T)M[t] : (T)M[t];  // (-1)^|n| M_n
+  F[0] -= m * dtensor<T, a, b, c>(xp, yp, zp, g);
+  F[1] -= m * dtensor<T, a + 1, b, c>(xp, yp, zp, g);
+  F[2] -= m * dtensor<T, a, b + 1, c>(xp, yp, zp, g);
+  F[3] -= m * dtensor<T, a, b, c + 1>(xp, yp, zp, g);
+}
+
+template <typename T, int t>
+__device__ __forceinline__ void m2p_terms(const float* M, const T* xp, const T* yp,
+                                          const T* zp, const T* g, T* F) {
+  if constexpr (t < SWH_MPOLE_TERMS) {
+    if constexpr (t == 0 || t > 3) m2p_term<T, t>(M, xp, yp, zp, g, F);  // dipole is zero
+    m2p_terms<T, t + 1>(M, xp, yp, zp, g, F);
+  }
+}
+
+// runner_iact_grav_pm_full / _truncated (MultiSoftening/gravity_iact.h:142-
+// 210): (r_x, r_y, r_z) = CoM - x_i, softening eps = max(eps_i, multipole's
+// max softening). F = {potential, a_x, a_y, a_z}.
+template <typename T>
+__device__ __forceinline__ void m2p(const float* M, T rx, T ry, T rz, T eps, bool truncated,
+                                    T r_s_inv, T* F) {
+  const T r2 = rx * rx + ry * ry + rz * rz;
+  const T r_inv = (T)1 / sqrt(r2);
+  T g[6];
+  radial_chain<T>(r2, r_inv, eps, truncated, r_s_inv, g);
+  T xp[6], yp[6], zp[6];
+  xp[0] = yp[0] = zp[0] = (T)1;
+#pragma unroll
+  for (int k = 1; k < 6; k++) {
+    xp[k] = xp[k - 1] * rx;
+    yp[k] = yp[k - 1] * ry;
+    zp[k] = zp[k - 1] * rz;
+  }
+  F[0] = F[1] = F[2] = F[3] = (T)0;
+  m2p_terms<T, 0>(M, xp, yp, zp, g, F);
+}
+
+// gravity_multipole_compute_power (multipole.h:878-972) on the stored
+// float terms, with the reference's mixed float/double arithmetic: unit
+// weights square in float, fractional weights multiply in double.
+__host__ __device__ inline void mpole_power(swh_multipole& m) {
+  double p[5] = {0., 0., 0., 0., 0.};
+  for (int t = 4; t < SWH_MPOLE_TERMS; t++) {
+    const int a = kMpA[t], b = kMpB[t], c = kMpC[t], o = a + b + c;
+    const double w = fact(a) * fact(b) * fact(c) / fact(o);
+    const float M = m.M[t];
+    if (w == 1.)
+      p[o] += (double)(M * M);
+    else
+      p[o] += w * (double)M * (double)M;
+  }
+  m.power[0] = m.M[0];
+  m.power[1] = 0.f;
+  for (int o = 2; o <= 4; o++) m.power[o] = (float)sqrt(p[o]);
+}
+
+}  // namespace swh

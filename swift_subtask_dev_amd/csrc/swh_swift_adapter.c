@@ -83,6 +83,7 @@ void swifthip_swift_gpart_layout(swh_gpart_layout *o) {
   o->off_mass = (int32_t)offsetof(struct gpart, mass);
   o->off_epsilon = (int32_t)offsetof(struct gpart, epsilon);
   o->off_time_bin = (int32_t)offsetof(struct gpart, time_bin);
+  o->off_old_a_grav_norm = (int32_t)offsetof(struct gpart, old_a_grav_norm);
 }
 
 static void split_pairs_init(void);
@@ -499,6 +500,31 @@ static void grav_params_of(const struct engine *e, swh_grav_params *G) {
   G->r_s_inv = e->mesh->r_s_inv;
   G->r_cut_min = e->mesh->r_cut_min;
   G->max_active_bin = e->max_active_bin;
+  const struct gravity_props *gp = e->gravity_properties;
+  if (gp) {  /* gravity_M2P_accept's inputs (multipole_accept.h:290-373) */
+    G->theta_crit = (float)gp->theta_crit;
+    G->adaptive_tolerance = gp->adaptive_tolerance;
+    G->use_advanced_MAC = gp->use_advanced_MAC;
+    G->use_gadget_tolerance = gp->use_gadget_tolerance;
+    G->use_tree_below_softening = gp->use_tree_below_softening;
+    G->consider_truncation_in_MAC = gp->consider_truncation_in_MAC;
+  }
+}
+
+/* struct gravity_tensors -> swh_multipole (include/swifthip.h's M order) */
+static void multipole_of(const struct gravity_tensors *t, swh_multipole *o) {
+  const struct multipole *m = &t->m_pole;
+  for (int k = 0; k < 3; k++) o->CoM[k] = t->CoM[k];
+  o->r_max = t->r_max;
+  const float M[SWH_MPOLE_TERMS] = {
+      m->M_000, 0.f,      0.f,      0.f,      m->M_200, m->M_020, m->M_002, m->M_110, m->M_101,
+      m->M_011, m->M_300, m->M_030, m->M_003, m->M_210, m->M_201, m->M_120, m->M_021, m->M_102,
+      m->M_012, m->M_111, m->M_400, m->M_040, m->M_004, m->M_310, m->M_301, m->M_130, m->M_031,
+      m->M_103, m->M_013, m->M_220, m->M_202, m->M_022, m->M_211, m->M_121, m->M_112};
+  memcpy(o->M, M, sizeof(M));
+  for (int k = 0; k < 5; k++) o->power[k] = m->power[k];
+  o->max_softening = m->max_softening;
+  o->min_old_a_grav_norm = m->min_old_a_grav_norm;
 }
 
 static void gview_of(const struct cell *c, int active, swh_gcell_view *v) {
@@ -511,6 +537,7 @@ static void gview_of(const struct cell *c, int active, swh_gcell_view *v) {
     v->CoM[k] = c->grav.multipole ? c->grav.multipole->CoM[k] : 0.;
   }
   v->r_max = c->grav.multipole ? c->grav.multipole->r_max : 0.;
+  v->multipole = NULL;
 }
 
 /* runner_doself_grav_pp (runner_doiact_grav.c:1788-1871) */
@@ -526,23 +553,35 @@ void runner_doself_grav_pp(struct runner *r, struct cell *c) {
   report(swh_grav_self_pp(swhs_ctx, &v, &swhs_glayout, &G));
 }
 
-/* runner_dopair_grav_pp (runner_doiact_grav.c:1202-1425). The M2P branch
- * (allow_mpole) is outside this path: every particle takes the P2P route,
- * i.e. the result equals the reference with no particle passing
- * gravity_M2P_accept. */
+/* runner_dopair_grav_pp (runner_doiact_grav.c:1202-1425), including the M2P
+ * branch: with allow_mpole (the recursive pair task always passes 1,
+ * runner_doiact_grav.c:2315) the particles that pass gravity_M2P_accept
+ * against the other cell's multipole take runner_dopair_grav_pm_* instead of
+ * P2P; the library evaluates the acceptance in float exactly as
+ * gravity_cache_populate does. */
 void runner_dopair_grav_pp(struct runner *r, struct cell *ci, struct cell *cj,
                            const int symmetric, const int allow_mpole) {
   const struct engine *e = r->e;
-  (void)allow_mpole;
   if (!swhs_ctx) SWH_ADAPTER_ERROR("swifthip_swift_init() was not called");
   const int ci_active = cell_is_active_gravity(ci, e) && (ci->nodeID == e->nodeID);
   const int cj_active = cell_is_active_gravity(cj, e) && (cj->nodeID == e->nodeID);
   if (!ci_active && !cj_active) return;
   if (!ci_active && !symmetric) return;
+  if (allow_mpole && (!ci->grav.multipole || !cj->grav.multipole))
+    SWH_ADAPTER_ERROR("allow_mpole without cell multipoles");
+  if (allow_mpole && !e->gravity_properties)
+    SWH_ADAPTER_ERROR("allow_mpole without e->gravity_properties");
   swh_grav_params G;
   grav_params_of(e, &G);
   swh_gcell_view vi, vj;
   gview_of(ci, ci_active, &vi);
   gview_of(cj, cj_active, &vj);
-  report(swh_grav_pair_pp(swhs_ctx, &vi, &vj, symmetric, &swhs_glayout, &G));
+  swh_multipole mi, mj;
+  if (allow_mpole) {
+    multipole_of(ci->grav.multipole, &mi);
+    multipole_of(cj->grav.multipole, &mj);
+    vi.multipole = &mi;
+    vj.multipole = &mj;
+  }
+  report(swh_grav_pair_pp(swhs_ctx, &vi, &vj, symmetric, allow_mpole, &swhs_glayout, &G));
 }

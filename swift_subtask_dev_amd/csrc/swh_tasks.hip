@@ -14,6 +14,7 @@
 //   swh_do{self,pair}_subset_density          DOSELF_SUBSET / DOPAIR_SUBSET
 //   swh_grav_self_pp / swh_grav_pair_pp       runner_doself/dopair_grav_pp (P2P)
 #include "swh_internal.h"
+#include "swh_mpole.h"
 #include "swh_physics.h"
 
 namespace swh {
@@ -287,7 +288,8 @@ static swh_status run_subset(swh_context* ctx, const swh_cell_view* ci, void* pa
 template <typename T, bool TRUNC>
 __global__ void grav_task_kernel(GLayout L, char* gi, int ni, const char* gj, int nj,
                                  int self, double fx, double fy, double fz, int periodic,
-                                 T dimx, T dimy, T dimz, T r_s_inv, int max_active_bin) {
+                                 T dimx, T dimy, T dimz, T r_s_inv, int max_active_bin,
+                                 const swh_multipole* __restrict__ mpj, MacParams mac) {
   const int pid = blockIdx.x * blockDim.x + threadIdx.x;
   if (pid >= ni) return;
   char* ri = gi + (size_t)pid * L.stride;
@@ -298,6 +300,28 @@ __global__ void grav_task_kernel(GLayout L, char* gi, int ni, const char* gj, in
           z_i = (T)(ldd(ri, L.x + 16) - fz);
   const T h_i = ldf(ri, L.epsilon);
   T ax = 0, ay = 0, az = 0, pot = 0;
+  if (mpj) {
+    // gravity_cache_populate's use_mpole (float, frame = the pair's zero
+    // shift), then runner_dopair_grav_pm_full / _truncated in T
+    const double xd = ldd(ri, L.x), yd = ldd(ri, L.x + 8), zd = ldd(ri, L.x + 16);
+    const float oag = L.old_a_grav_norm >= 0 ? ldf(ri, L.old_a_grav_norm) : 0.f;
+    const float eps_i = ldf(ri, L.epsilon);
+    if (m2p_accept(mac, mac_source(*mpj), (float)xd, (float)yd, (float)zd, eps_i, oag)) {
+      T dx = (T)(mpj->CoM[0] - xd), dy = (T)(mpj->CoM[1] - yd), dz = (T)(mpj->CoM[2] - zd);
+      if (periodic) {
+        dx = dx > (T)0.5 * dimx ? dx - dimx : (dx < (T)-0.5 * dimx ? dx + dimx : dx);
+        dy = dy > (T)0.5 * dimy ? dy - dimy : (dy < (T)-0.5 * dimy ? dy + dimy : dy);
+        dz = dz > (T)0.5 * dimz ? dz - dimz : (dz < (T)-0.5 * dimz ? dz + dimz : dz);
+      }
+      T F[4];
+      m2p<T>(mpj->M, dx, dy, dz, (T)fmaxf(eps_i, mpj->max_softening), TRUNC, r_s_inv, F);
+      stf(ri, L.a_grav, ldf(ri, L.a_grav) + (float)F[1]);
+      stf(ri, L.a_grav + 4, ldf(ri, L.a_grav + 4) + (float)F[2]);
+      stf(ri, L.a_grav + 8, ldf(ri, L.a_grav + 8) + (float)F[3]);
+      stf(ri, L.potential, ldf(ri, L.potential) + (float)F[0]);
+      return;
+    }
+  }
   for (int pjd = 0; pjd < nj; pjd++) {
     if (self && pjd == pid) continue;
     const char* rj = gj + (size_t)pjd * L.stride;
@@ -331,16 +355,18 @@ __global__ void grav_task_kernel(GLayout L, char* gi, int ni, const char* gj, in
 template <typename T>
 static void launch_grav_task(hipStream_t s, const GLayout& L, char* gi, int ni,
                              const char* gj, int nj, int self, const double f[3],
-                             int periodic, const swh_grav_params* G, bool trunc) {
+                             int periodic, const swh_grav_params* G, bool trunc,
+                             const swh_multipole* mpj = nullptr) {
   const int block = 64, grid = (ni + block - 1) / block;
+  const MacParams mac = mac_params(G);
   if (trunc)
     hipLaunchKernelGGL((grav_task_kernel<T, true>), dim3(grid), dim3(block), 0, s, L, gi,
                        ni, gj, nj, self, f[0], f[1], f[2], periodic, (T)G->dim[0],
-                       (T)G->dim[1], (T)G->dim[2], (T)G->r_s_inv, G->max_active_bin);
+                       (T)G->dim[1], (T)G->dim[2], (T)G->r_s_inv, G->max_active_bin, mpj, mac);
   else
     hipLaunchKernelGGL((grav_task_kernel<T, false>), dim3(grid), dim3(block), 0, s, L, gi,
                        ni, gj, nj, self, f[0], f[1], f[2], periodic, (T)G->dim[0],
-                       (T)G->dim[1], (T)G->dim[2], (T)G->r_s_inv, G->max_active_bin);
+                       (T)G->dim[1], (T)G->dim[2], (T)G->r_s_inv, G->max_active_bin, mpj, mac);
 }
 
 }  // namespace swh
@@ -428,14 +454,23 @@ swh_status swh_grav_self_pp(swh_context* ctx, const swh_gcell_view* c,
   return SWH_OK;
 }
 
-// runner_dopair_grav_pp with allow_mpole = 0 (src/runner_doiact_grav.c:1202-1425)
+// runner_dopair_grav_pp (src/runner_doiact_grav.c:1202-1425): P2P, and with
+// allow_mpole the M2P route for the particles passing the MAC against the
+// other cell's multipole (allow_multipole_i/j need more than one particle,
+// runner_doiact_grav.c:1273-1274).
 swh_status swh_grav_pair_pp(swh_context* ctx, const swh_gcell_view* ci,
-                            const swh_gcell_view* cj, int symmetric,
+                            const swh_gcell_view* cj, int symmetric, int allow_mpole,
                             const swh_gpart_layout* GL, const swh_grav_params* G) {
   if (!ctx || !ci || !cj || !GL || !G) return SWH_ERR_ARG;
   const bool do_i = ci->active, do_j = cj->active && symmetric;
   if (!do_i && !do_j) return SWH_OK;
   if (ci->count <= 0 || cj->count <= 0) return SWH_OK;
+  const bool mp_j = allow_mpole && cj->count > 1;  // multipole of cj used by ci's particles
+  const bool mp_i = allow_mpole && ci->count > 1;
+  if ((mp_j && do_i && !cj->multipole) || (mp_i && do_j && !ci->multipole)) {
+    set_error("allow_mpole needs the cells' multipoles (swh_gcell_view.multipole)");
+    return SWH_ERR_ARG;
+  }
   GLayout L;
   SWH_TRY(make_glayout(GL, &L));
   TaskWorker* w = ctx->lease();
@@ -447,16 +482,21 @@ swh_status swh_grav_pair_pp(swh_context* ctx, const swh_gcell_view* ci,
   } unl{ctx, w};
   SWH_HIP(hipSetDevice(ctx->device));
   const size_t bi = (size_t)ci->count * L.stride, bj = (size_t)cj->count * L.stride;
-  SWH_TRY(w->dparts.reserve(bi + bj));
-  SWH_TRY(w->dparts2.reserve(bi + bj));
-  SWH_TRY(w->hstage.reserve(bi + bj));
+  const size_t bm = 2 * sizeof(swh_multipole);  // multipoles of ci, cj after the records
+  SWH_TRY(w->dparts.reserve(bi + bj + bm));
+  SWH_TRY(w->dparts2.reserve(bi + bj + bm));
+  SWH_TRY(w->hstage.reserve(bi + bj + bm));
   char* hs = static_cast<char*>(w->hstage.ptr);
   std::memcpy(hs, ci->gparts, bi);
   std::memcpy(hs + bi, cj->gparts, bj);
-  SWH_HIP(hipMemcpyAsync(w->dparts.ptr, hs, bi + bj, hipMemcpyHostToDevice, w->stream));
+  swh_multipole* hm = reinterpret_cast<swh_multipole*>(hs + bi + bj);
+  if (ci->multipole) hm[0] = *ci->multipole;
+  if (cj->multipole) hm[1] = *cj->multipole;
+  SWH_HIP(hipMemcpyAsync(w->dparts.ptr, hs, bi + bj + bm, hipMemcpyHostToDevice, w->stream));
   // read-only source copy so both directions see the pre-task accelerations
-  SWH_HIP(hipMemcpyAsync(w->dparts2.ptr, w->dparts.ptr, bi + bj, hipMemcpyDeviceToDevice,
+  SWH_HIP(hipMemcpyAsync(w->dparts2.ptr, w->dparts.ptr, bi + bj + bm, hipMemcpyDeviceToDevice,
                          w->stream));
+  const swh_multipole* dm = reinterpret_cast<const swh_multipole*>(w->dparts2.as<char>() + bi + bj);
   bool trunc = false;
   if (G->periodic) {
     double d2 = 0;
@@ -473,13 +513,15 @@ swh_status swh_grav_pair_pp(swh_context* ctx, const swh_gcell_view* ci,
   const char* si = w->dparts2.as<char>();
   const char* sj = si + bi;
   const bool f64 = ctx->precision == SWH_PRECISION_F64;
+  const swh_multipole* use_j = mp_j ? dm + 1 : nullptr;
+  const swh_multipole* use_i = mp_i ? dm : nullptr;
   if (do_i) {
-    if (f64) launch_grav_task<double>(w->stream, L, di, ci->count, sj, cj->count, 0, zero, G->periodic, G, trunc);
-    else launch_grav_task<float>(w->stream, L, di, ci->count, sj, cj->count, 0, zero, G->periodic, G, trunc);
+    if (f64) launch_grav_task<double>(w->stream, L, di, ci->count, sj, cj->count, 0, zero, G->periodic, G, trunc, use_j);
+    else launch_grav_task<float>(w->stream, L, di, ci->count, sj, cj->count, 0, zero, G->periodic, G, trunc, use_j);
   }
   if (do_j) {
-    if (f64) launch_grav_task<double>(w->stream, L, dj, cj->count, si, ci->count, 0, zero, G->periodic, G, trunc);
-    else launch_grav_task<float>(w->stream, L, dj, cj->count, si, ci->count, 0, zero, G->periodic, G, trunc);
+    if (f64) launch_grav_task<double>(w->stream, L, dj, cj->count, si, ci->count, 0, zero, G->periodic, G, trunc, use_i);
+    else launch_grav_task<float>(w->stream, L, dj, cj->count, si, ci->count, 0, zero, G->periodic, G, trunc, use_i);
   }
   SWH_HIP(hipGetLastError());
   SWH_HIP(hipMemcpyAsync(hs, w->dparts.ptr, bi + bj, hipMemcpyDeviceToHost, w->stream));

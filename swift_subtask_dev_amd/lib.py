@@ -40,6 +40,7 @@ HIP_SYMBOLS = [
     "swh_space_set_owned", "swh_space_pack_halo", "swh_space_unpack_halo",
     "swh_gspace_create",
     "swh_gspace_destroy", "swh_gspace_upload", "swh_gspace_set_leaves", "swh_grav_pp_batch",
+    "swh_gspace_make_multipoles",
     "swh_gspace_download", "swh_gspace_sync",
 ]
 ADAPTER_SYMBOLS = [
@@ -97,7 +98,7 @@ def load() -> C.CDLL:
         "swh_doself_subset_density": (C.c_int, [vp, P(abi.CellView), vp, P(i32), i32, P(abi.PartLayout), P(abi.HydroParams)]),
         "swh_dopair_subset_density": (C.c_int, [vp, P(abi.CellView), vp, P(i32), i32, P(abi.CellView), P(dp), P(abi.PartLayout), P(abi.HydroParams)]),
         "swh_grav_self_pp": (C.c_int, [vp, P(abi.GCellView), P(abi.GPartLayout), P(abi.GravParams)]),
-        "swh_grav_pair_pp": (C.c_int, [vp, P(abi.GCellView), P(abi.GCellView), C.c_int, P(abi.GPartLayout), P(abi.GravParams)]),
+        "swh_grav_pair_pp": (C.c_int, [vp, P(abi.GCellView), P(abi.GCellView), C.c_int, C.c_int, P(abi.GPartLayout), P(abi.GravParams)]),
         "swh_space_create": (C.c_int, [vp, P(vp)]),
         "swh_space_destroy": (C.c_int, [vp]),
         "swh_space_set_stream": (C.c_int, [vp, vp]),
@@ -123,7 +124,8 @@ def load() -> C.CDLL:
         "swh_gspace_destroy": (C.c_int, [vp]),
         "swh_gspace_upload": (C.c_int, [vp, vp, i64, P(abi.GPartLayout), C.c_int]),
         "swh_gspace_set_leaves": (C.c_int, [vp, vp, i32, P(i32), vp, i32]),
-        "swh_grav_pp_batch": (C.c_int, [vp, P(abi.GravParams), P(i64)]),
+        "swh_grav_pp_batch": (C.c_int, [vp, P(abi.GravParams), P(i64), P(i64)]),
+        "swh_gspace_make_multipoles": (C.c_int, [vp, vp]),
         "swh_gspace_download": (C.c_int, [vp, vp, P(abi.GPartLayout), C.c_int]),
         "swh_gspace_sync": (C.c_int, [vp]),
     }
@@ -396,10 +398,21 @@ class GravSpace:
             pair_offset.ctypes.data_as(C.POINTER(C.c_int32)), _ptr(pairs), len(pairs)),
             "set_leaves")
 
-    def pp(self, G: abi.GravParams, count=True):
-        n = C.c_int64(0)
-        _check(self._lib.swh_grav_pp_batch(self.handle, C.byref(G), C.byref(n) if count else None),
-               "grav_pp_batch")
+    def make_multipoles(self, want=False):
+        """Leaf multipoles on the device (P2M); want=True returns a host copy
+        (ctypes array of abi.Multipole)."""
+        out = (abi.Multipole * max(1, len(self._keep[0])))() if want else None
+        _check(self._lib.swh_gspace_make_multipoles(self.handle, out), "make_multipoles")
+        return out
+
+    def pp(self, G: abi.GravParams, count=True, m2p=False):
+        """P2P (+ M2P on allow_mpole pairs). count: P2P interactions; with
+        m2p=True returns (P2P interactions, M2P evaluations)."""
+        n, m = C.c_int64(0), C.c_int64(0)
+        _check(self._lib.swh_grav_pp_batch(self.handle, C.byref(G), C.byref(n) if count else None,
+                                           C.byref(m) if m2p else None), "grav_pp_batch")
+        if m2p:
+            return n.value, m.value
         return n.value if count else None
 
     def download(self, gparts: np.ndarray):

@@ -66,7 +66,11 @@ def load(prec: str = "f32") -> C.CDLL:
                               P(abi.GravParams)])
     sig("grav_pair_pp", i64, [vp, C.c_int, vp, C.c_int, P(C.c_double), P(C.c_double),
                               C.c_double, C.c_double, C.c_int, P(abi.GravParams)])
-    sig("grav_pp_leaves", i64, [vp, vp, C.c_int, vp, vp, P(abi.GravParams)])
+    sig("grav_pp_leaves", i64, [vp, vp, C.c_int, vp, vp, P(abi.GravParams), vp, P(i64)])
+    sig("grav_pair_pp_mpole", i64, [vp, C.c_int, vp, C.c_int, P(abi.Multipole),
+                                    P(abi.Multipole), C.c_int, C.c_int, P(abi.GravParams),
+                                    P(i64)])
+    sig("grav_p2m", None, [vp, C.c_int, P(abi.Multipole)])
     if prec == "f32":
         for n in ("iact_density", "iact_force", "iact_gradient"):
             sig(n, None, [real, P(real), real, real, vp, vp, real, real])

@@ -284,7 +284,7 @@ def test_branch_gradient_per_task(adapter, prec):
     for f in ("v_sig", "laplace_u", "alpha_visc_max_ngb"):
         parts[f] = 0
     o = abi.copy_parts(parts)
-    adapter.swifthip_swift_set_precision(1 if prec == "f64" else 0)
+    adapter.swifthip_swift_set_precision(0 if prec == "f64" else 1)  # SWH_PRECISION_F64 = 0
     cs = O.CellSet(parts, bounds, locs, 1.0)
     cs.sort_all()
     eb = abi.EngineBundle(dim=(3.0, 3.0, 3.0), periodic=True, params=P)
@@ -295,7 +295,7 @@ def test_branch_gradient_per_task(adapter, prec):
         if j != MAIN:
             adapter.runner_dopair1_branch_gradient(r, cs.ptr(MAIN), cs.ptr(j))
     err_msg = adapter.swifthip_swift_last_error()
-    adapter.swifthip_swift_set_precision(1)
+    adapter.swifthip_swift_set_precision(0)
     assert not err_msg, err_msg
     cs.free_sorts()
     O.fn("f64", "box_gradient")(o.ctypes.data, len(o), C.byref(P), None)

@@ -565,7 +565,7 @@ def test_potential_self_kat_gpu(adapter):
     cell.width[:] = (1.0, 1.0, 1.0)
     cell.grav.parts = g.ctypes.data
     cell.grav.count = len(g)
-    mp = abi.GravityTensors((C.c_double * 3)(0, 0.5, 0.5), 0.0)
+    mp = abi.GravityTensors(CoM=(C.c_double * 3)(0, 0.5, 0.5), r_max=0.0)
     cell.grav.multipole = C.pointer(mp)
     cell.grav.ti_end_min = 8
     eb = abi.EngineBundle(dim=(10.0, 10.0, 10.0), periodic=False)
@@ -583,8 +583,8 @@ def test_potential_pair_kat_gpu(adapter):
     from test_oracle import _acceleration, _check_kat, _potential, potential_pair_gparts
     gi, gj = potential_pair_gparts()
     cells = (abi.Cell * 2)()
-    mps = [abi.GravityTensors((C.c_double * 3)(0, 0.5, 0.5), 0.1),
-           abi.GravityTensors((C.c_double * 3)(1.5, 0.5, 0.5), 0.1)]
+    mps = [abi.GravityTensors(CoM=(C.c_double * 3)(0, 0.5, 0.5), r_max=0.1),
+           abi.GravityTensors(CoM=(C.c_double * 3)(1.5, 0.5, 0.5), r_max=0.1)]
     for c, g, mp, loc in ((cells[0], gi, mps[0], 0.0), (cells[1], gj, mps[1], 1.0)):
         c.loc[0] = loc
         c.width[:] = (1.0, 1.0, 1.0)
@@ -624,7 +624,7 @@ def test_grav_batch_vs_oracle(gpu_ctx, periodic, truncated):
     sp.download(g)
     o = abi.copy_parts(gs)
     no = O.fn("f64", "grav_pp_leaves")(o.ctypes.data, leaves.ctypes.data, len(leaves),
-                                       offs.ctypes.data, pairs.ctypes.data, C.byref(G))
+                                       offs.ctypes.data, pairs.ctypes.data, C.byref(G), None, None)
     assert n == no
     # net accelerations cancel strongly in a uniform box: floor at 1e-6 of the
     # largest component
@@ -734,7 +734,7 @@ def test_grav_bench_geometry_vs_oracle(gpu_ctx, n, cdim, periodic, truncated):
     sp.close()
     o = abi.copy_parts(gs)
     no = O.fn("f64", "grav_pp_leaves")(o.ctypes.data, leaves.ctypes.data, len(leaves),
-                                       offs.ctypes.data, pairs.ctypes.data, C.byref(G))
+                                       offs.ctypes.data, pairs.ctypes.data, C.byref(G), None, None)
     assert ng == no
     assert_close(g["a_grav"], o["a_grav"], 1e-6, 1e-6, "a_grav")
     assert_close(g["potential"], o["potential"], 1e-6, 1e-6, "potential")

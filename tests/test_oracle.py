@@ -328,3 +328,148 @@ def test_125cells_chain_analytic(vel, press):
         assert a_err[r > 0.5].max() < 2.5e-2
     else:
         assert a_err.max() < (1e-6 if press == "const" else 5e-6)
+
+
+# ---------------------------------------------------------------------------
+# Multipoles: P2M, MAC and M2P (order 4)
+# ---------------------------------------------------------------------------
+def _cube_leaf():
+    """testPotentialPair.c:357-398: 8 particles of mass 1/8 on a cube of side
+    0.2 around (0, 0.5, 0.5) (the reference moves y and z together)."""
+    g = abi.new_gparts(8)
+    for n in range(8):
+        g["x"][n, 0] = -0.1 if n & 1 else 0.1
+        g["x"][n, 1] = 0.4 if n & 2 else 0.6
+        g["x"][n, 2] = 0.4 if n & 2 else 0.6
+    g["mass"] = 1.0 / 8.0
+    g["epsilon"] = 0.1
+    g["time_bin"] = 1
+    return g
+
+
+def _p2m(prec, g):
+    m = abi.Multipole()
+    O.fn(prec, "grav_p2m")(g.ctypes.data, len(g), C.byref(m))
+    return m
+
+
+def _direct_p2m(g):
+    """P2M in numpy: M_n = (-1)^|n| sum m dx^n / n! about the CoM."""
+    from math import factorial
+    m = g["mass"].astype(np.float64)
+    x = g["x"].astype(np.float64)
+    com = (m[:, None] * x).sum(0) / m.sum()
+    d = x - com
+    M = []
+    for a, b, c in abi.MPOLE_INDEX:
+        v = (m * d[:, 0] ** a * d[:, 1] ** b * d[:, 2] ** c).sum() / (
+            factorial(a) * factorial(b) * factorial(c))
+        M.append(-v if (a + b + c) % 2 else v)
+    return com, np.array(M), np.sqrt((d ** 2).sum(1)).max()
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_p2m_matches_definition(prec):
+    """gravity_P2M + compute_power vs the moment definition on a random leaf:
+    mass, CoM, r_max, every M_n (float storage), power[p] = sqrt(sum n!/p!
+    M_n^2), max softening, min old |a|."""
+    rng = np.random.Generator(np.random.PCG64(5))
+    g = abi.new_gparts(300)
+    g["x"] = rng.uniform(0.2, 0.4, (300, 3))
+    g["mass"] = rng.uniform(0.5, 1.5, 300)
+    g["epsilon"] = rng.uniform(0.01, 0.02, 300)
+    g["old_a_grav_norm"] = rng.uniform(1.0, 2.0, 300)
+    m = _p2m(prec, g)
+    com, M, rmax = _direct_p2m(g)
+    assert np.allclose(np.array(m.CoM), com, rtol=0, atol=1e-14)
+    assert abs(m.r_max - rmax) < 1e-14
+    got = np.array(m.M[:], dtype=np.float64)
+    assert np.all(got[1:4] == 0)
+    scale = np.abs(M).max()
+    assert np.abs(got - M).max() <= 1e-6 * scale
+    assert m.max_softening == np.float32(g["epsilon"].max())
+    assert m.min_old_a_grav_norm == np.float32(g["old_a_grav_norm"].min())
+    from math import factorial
+    for p in (2, 3, 4):
+        s = sum(factorial(a) * factorial(b) * factorial(c) / factorial(p) * float(got[t]) ** 2
+                for t, (a, b, c) in enumerate(abi.MPOLE_INDEX) if a + b + c == p)
+        assert abs(m.power[p] - np.sqrt(s)) <= 1e-6 * np.sqrt(s)
+    assert m.power[0] == m.M[0] and m.power[1] == 0
+
+
+def _grav_params(periodic=0, dim=10.0, r_s_inv=0.0, theta=1.0, **mac):
+    G = abi.GravParams(periodic, (C.c_float * 3)(dim, dim, dim), r_s_inv, 0.0,
+                       abi.NUM_TIME_BINS)
+    G.theta_crit = theta
+    for k, v in mac.items():
+        setattr(G, k, v)
+    return G
+
+
+def test_high_order_pm_kat(oracle32):
+    """testPotentialPair.c:348-443 "high-order P-M": the cube leaf's multipole
+    acting on 100 test particles at x in (1, 2], theta_crit = 1, against the
+    analytic sum over the 8 particles: the reference's 1e-2 check, and the
+    order-4 truncation error (< 2e-4 relative at these distances)."""
+    gi = _cube_leaf()
+    gi["epsilon"][0] = 0.1
+    _, gj = potential_pair_gparts(eps=0.1)
+    G = _grav_params(theta=1.0)
+    mi = _p2m("f32", gi)
+    mj = _p2m("f32", gj) if False else abi.Multipole()
+    mj.r_max = 0.1
+    nm = C.c_longlong(0)
+    O.fn("f32", "grav_pair_pp_mpole")(gi.ctypes.data, 8, gj.ctypes.data, 100, C.byref(mi),
+                                      C.byref(mj), 1, 1, C.byref(G), C.byref(nm))
+    # every test particle took ci's multipole; ci's 8 took cj's (empty) one
+    assert nm.value == 108
+    for n in range(100):
+        x = gj["x"][n].astype(np.float64)
+        pot, acc = 0.0, 0.0
+        for k in range(8):
+            d = gi["x"][k].astype(np.float64) - x
+            r = np.sqrt((d ** 2).sum())
+            pot += _potential(0.125, r, 0.1, np.finfo(np.float32).max)
+            acc -= _acceleration(0.125, r, 0.1, np.finfo(np.float32).max) * d[0] / r
+        assert _check_kat(gj["potential"][n], pot, 1e-2, 1e-6)
+        assert _check_kat(gj["a_grav"][n, 0], acc, 1e-2, 1e-6)
+        assert abs(gj["a_grav"][n, 0] - acc) <= 2e-4 * abs(acc)
+        assert abs(gj["potential"][n] - pot) <= 2e-4 * abs(pot)
+
+
+@pytest.mark.parametrize("periodic,r_s_inv", [(0, 0.0), (1, 0.5)])
+def test_m2p_converges_to_p2p(periodic, r_s_inv):
+    """M2P of a random 200-particle leaf vs the direct P2P sum (f64 oracle,
+    theta_crit large enough to accept everything): the error falls like
+    (r_max / r)^5 for the order-4 expansion, Newtonian and truncated."""
+    rng = np.random.Generator(np.random.PCG64(8))
+    gi = abi.new_gparts(200)
+    gi["x"] = 0.5 + rng.uniform(-0.05, 0.05, (200, 3))
+    gi["mass"] = rng.uniform(0.5, 1.5, 200)
+    gi["epsilon"] = 0.001
+    gi["time_bin"] = 1
+    mi = _p2m("f64", gi)
+    errs = []
+    for dist in (0.4, 0.8, 1.6):
+        gj = abi.new_gparts(8)
+        gj["x"] = 0.5 + dist * rng.normal(size=(8, 3)) / np.sqrt(3)
+        gj["x"] = 0.5 + (gj["x"] - 0.5) / np.linalg.norm(gj["x"] - 0.5, axis=1)[:, None] * dist
+        gj["epsilon"] = 0.001
+        gj["time_bin"] = 1
+        ref = abi.copy_gparts(gj) if hasattr(abi, "copy_gparts") else gj.copy()
+        G = _grav_params(periodic, 10.0, r_s_inv, theta=10.0)
+        mj = abi.Multipole()
+        mj.r_max = 1.0
+        nm = C.c_longlong(0)
+        O.fn("f64", "grav_pair_pp_mpole")(gj.ctypes.data, 8, gi.ctypes.data, 200, C.byref(mj),
+                                          C.byref(mi), 0, 1, C.byref(G), C.byref(nm))
+        assert nm.value == 8
+        G0 = _grav_params(periodic, 10.0, r_s_inv, theta=0.0)
+        O.fn("f64", "grav_pair_pp_mpole")(ref.ctypes.data, 8, gi.ctypes.data, 200, C.byref(mj),
+                                          C.byref(mi), 0, 1, C.byref(G0), None)
+        a = gj["a_grav"].astype(np.float64)
+        b = ref["a_grav"].astype(np.float64)
+        errs.append(np.abs(a - b).max() / np.abs(b).max())
+    # (r_max / r)^5: x32 per doubling, down to the float storage of a_grav
+    assert errs[0] < 1e-4
+    assert errs[1] < errs[0] / 20 and errs[2] < max(errs[1] / 20, 1e-7), errs

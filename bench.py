@@ -510,6 +510,10 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK,
                 "traffic": traffic.get("bytes_per_launch") if traffic else None,
+                # PMC-measured HBM bytes of one density loop's kernels, from the
+                # committed profile named here (not re-measured by this run)
+                "traffic_source": (traffic.get("source", "profiles/traffic_density.json")
+                                   if traffic else None),
                 "bytes_model": f"N*(27*{S_IN_DENSITY}+{S_OUT_DENSITY}) = {b_dens} B per launch",
                 "launch_ms": td * 1e3,
             },

@@ -81,8 +81,18 @@ __global__ __launch_bounds__(64) void list_build_kernel(GridDev g, SoA a, ListDe
                             lds);
 }
 
+#ifndef SWH_WALK_WPE
+#define SWH_WALK_WPE 0
+#endif
+#ifndef SWH_WALK_WPE_DENS
+#define SWH_WALK_WPE_DENS SWH_WALK_WPE
+#endif
 template <int LOOP, typename T>
-__global__ __launch_bounds__(256) void walk_kernel(GridDev g, SoA a, ListDev ld, int n,
+__global__ __launch_bounds__(256)
+#if SWH_WALK_WPE > 0
+__attribute__((amdgpu_waves_per_eu(SWH_WALK_WPE)))
+#endif
+void walk_kernel(GridDev g, SoA a, ListDev ld, int n,
                                                    int max_active_bin, T a2H,
                                                    const unsigned int* __restrict__ hmax_bits,
                                                    unsigned long long* counter,

@@ -44,13 +44,17 @@ for k, v in per.items():
 out = {"source": f"profiles/{tag} PMC passes (rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE, "
                  "kernel-trace only; FETCH_SIZE x2 gfx950 correction; median over dispatches)",
        "kernels": traffic}
-# the default density kernel first (variant 5), then any density instance
-dens = [k for k in traffic if "tile5_kernel<0, double" in k] or \
-       [k for k in traffic if "_kernel<0, double" in k]
-if dens:
-    out["bytes_per_launch"] = traffic[dens[0]]["bytes_per_launch"]
+# one density loop of the list path = the kernels it launches: positions
+# staging, list prep + build, the walk and the overflow search
+DENSITY_LIST = ("posf_kernel", "list_prep_kernel", "cell_reach_kernel", "list_build_kernel",
+                "walk_kernel<0, double>", "overflow_kernel<0, double>")
+parts = {k: v for k, v in traffic.items() if any(k.endswith(d) or d in k for d in DENSITY_LIST)}
+if parts:
+    out["density_kernels"] = sorted(parts)
+    out["bytes_per_launch"] = sum(v["bytes_per_launch"] for v in parts.values())
 (dst / f"{tag}_traffic.json").write_text(json.dumps(out, indent=1) + "\n")
 (dst / "traffic_density.json").write_text(json.dumps(out, indent=1) + "\n")
+dens = [k for k in traffic if "list_build_kernel" in k]
 
 rows = list(csv.DictReader(open(stats)))
 print("bench:", bench["value"], bench["kernels"])

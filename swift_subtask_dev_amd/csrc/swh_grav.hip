@@ -27,7 +27,10 @@
 namespace swh {
 
 constexpr int kGravBlock = 256;
-constexpr int kIPer = 2;  // i-particles per thread per pass (leaves up to 512 in one pass)
+#ifndef SWH_GRAV_IPER
+#define SWH_GRAV_IPER 2
+#endif
+constexpr int kIPer = SWH_GRAV_IPER;  // i-particles per thread per pass
 
 struct GSoA {
   double4* pos;  // x, y, z, epsilon
@@ -262,6 +265,7 @@ __device__ __forceinline__ void mpole_mask(const GSoA& g, const MacParams& P,
   }
 }
 
+template <bool MPOLE>
 __global__ __launch_bounds__(kGravBlock) void p2p_kernel(
     GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
     const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
@@ -293,7 +297,12 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel(
       const swh_leaf_pair pr = pairs[q];
       const swh_leaf J = leaves[pr.j];
       bool actp[kIPer];  // act minus the particles taking this leaf's multipole
-      mpole_mask(g, mac, pr, J, act, gi, actp);
+      if (MPOLE) {
+        mpole_mask(g, mac, pr, J, act, gi, actp);
+      } else {
+#pragma unroll
+        for (int k = 0; k < kIPer; k++) actp[k] = act[k];
+      }
       for (int jbase = 0; jbase < J.count; jbase += kGravBlock) {
         const int nt = min(kGravBlock, J.count - jbase);
         __syncthreads();
@@ -660,11 +669,14 @@ swh_status swh_grav_pp_batch(swh_gspace* g, const swh_grav_params* G, int64_t* n
   unsigned long long* ctr = want ? g->counter.as<unsigned long long>() : nullptr;
   if (ctr) SWH_HIP(hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned long long), g->stream));
   const bool f64 = g->ctx->precision == SWH_PRECISION_F64;
-  if (f64)
-    hipLaunchKernelGGL(p2p_kernel, dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
+  if (f64) {
+    // the multipole-free instance keeps the P2P kernel's register budget
+    auto k = g->any_mpole ? p2p_kernel<true> : p2p_kernel<false>;
+    hipLaunchKernelGGL(k, dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
                        gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
                        g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
                        (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, mac, ctr);
+  }
   else
     hipLaunchKernelGGL(p2p_kernel_f32, dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
                        gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),

@@ -473,3 +473,42 @@ def test_m2p_converges_to_p2p(periodic, r_s_inv):
     # (r_max / r)^5: x32 per doubling, down to the float storage of a_grav
     assert errs[0] < 1e-4
     assert errs[1] < errs[0] / 20 and errs[2] < max(errs[1] / 20, 1e-7), errs
+
+
+def test_reference_tolerances_are_draw_specific():
+    """tests/tolerance_27_*.dat were tuned on the reference's own srand(0)
+    draws. On other draws the reference's own float algorithm (the oracle's
+    sorted DOPAIR1/DOSELF1 restatement) exceeds them against brute force:
+    measured up to 3.6x (random velocities, seed 3), 2.8x (perturbed h, seed
+    1), 3.0x (perturbed lattice, seed 6). This is why the GPU-vs-brute test
+    scales the relative columns by 1.5 on its draw; the tight pin is the fp64
+    adapter vs the fp64 oracle at 2e-6 on seed 3 itself
+    (test_gpu_parity.py::test_27cells_adapter_vs_f64)."""
+    from compare import load_tolerance
+    P = abi.default_hydro_params((3.0, 3.0, 3.0), True)
+
+    def worst(vel, h_pert, pert, tol, seed):
+        parts, bounds, locs = S.cells_grid(3, 6, vel=vel, h_pert=h_pert, pert=pert, seed=seed)
+        g, b = abi.copy_parts(parts), abi.copy_parts(parts)
+        S.zero_density_fields(g)
+        S.zero_density_fields(b)
+        S.run27(g, bounds, locs, "sorted", P)
+        S.run27(b, bounds, locs, "brute", P)
+        s, e = bounds[13]
+        mg, mb = abi.copy_parts(g[s:e]), abi.copy_parts(b[s:e])
+        S.end_calculation(mg, P)
+        S.end_calculation(mb, P)
+        names, at, rt, lt = load_tolerance(tol)
+        x, y = S.density_columns(mb), S.density_columns(mg)
+        d = np.abs(x - y)
+        ssum = np.abs(x + y)
+        rel = np.where(ssum > 0, d / np.where(ssum > 0, ssum, 1), 0.0)
+        r = 0.0
+        for j in range(x.shape[1]):
+            chk = (np.abs(x[:, j]) + np.abs(y[:, j])) >= lt[j]
+            if rt[j] > 0 and chk.any():
+                r = max(r, float((rel[chk, j] / (1.1 * rt[j])).max()))
+        return r
+
+    assert worst("random", 0.0, 0.0, "tolerance_27_normal.dat", 3) > 3.0
+    assert worst("random", 0.0, 0.0, "tolerance_27_normal.dat", 1) < 1.0

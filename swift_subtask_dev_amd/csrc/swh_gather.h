@@ -178,6 +178,7 @@ struct LoopState<LOOP_FORCE, T> {
     I.h = hi;
     I.u = th.x; I.rho = th.y; I.P = th.z; I.c = th.w;
     I.f = fc.x; I.balsara = fc.y; I.alpha_visc = fc.z; I.alpha_diff = fc.w;
+    force_prep_i(I);
     A.ax = A.ay = A.az = A.u_dt = A.h_dt = (T)0;
     A.min_ngb_time_bin = a.mintb[i];
     const double hmax = (double)__uint_as_float(*hmax_bits) * (double)kGamma;

@@ -171,12 +171,6 @@ __global__ void gpack_kernel(GLayout L, char* __restrict__ aos, int64_t n, GSoA 
   g.acc[i] = make_double4(0., 0., 0., 0.);  // a second download adds nothing
 }
 
-// fp64 1/sqrt(x): the hardware approximation refined by one Newton step
-// (~1e-14 relative; the results are stored as float).
-__device__ __forceinline__ double rsqrt1_f64(double x) {
-  const double y = __builtin_amdgcn_rsq(x);
-  return fma(y * fma(-0.5 * x * y, y, 0.5), 1., y);
-}
 
 // runner_iact_grav_pp_full / _truncated (gravity_iact.h:47-135) for one
 // pair, fp64: h2 = max(eps_i^2, eps_j^2), h_inv = min(1/eps_i, 1/eps_j).

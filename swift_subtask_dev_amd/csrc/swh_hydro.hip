@@ -655,7 +655,7 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const int
     // while no particle's H has outgrown its list reach (ghost: stale flag)
     if (LOOP == LOOP_DENSITY || !s->list_valid || s->list_mab != P->max_active_bin)
       SWH_TRY(build_lists(s, P, count));
-    if (s->tuning.diag_mode != 0) return SWH_OK;
+    if (s->tuning.diag_mode != 0 && s->tuning.diag_mode != 4) return SWH_OK;
   }
   const GridDev gd = grid_dev(s);
   const double a2H = P->a * P->a * P->H;

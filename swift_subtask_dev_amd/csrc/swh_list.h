@@ -430,6 +430,10 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
   const int* __restrict__ col = ld.nbr + (nl > 0 ? list_col(lb, ld.K) : 0);
   const int nme = nl > s ? (nl - s + LPI - 1) / LPI : 0;  // this lane's entries
   auto idx = [&](int m) { return m < nme ? col[list_off(s + m * LPI)] : -1; };
+  // profiling only (diag 4): every entry loads the lane's first j's data, so
+  // the gathers hit one line while the arithmetic stays the same
+  const int jfix = ld.diag == 4 ? idx(0) : 0;
+  auto dj = [&](int j) { return ld.diag == 4 ? jfix : j; };
   if constexpr (S::kPay > 1) {
     // heavy j records (gradient, force): index two entries ahead, data one
     // ahead; the register budget of the wide records allows no more
@@ -438,8 +442,8 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
     double4 pn = make_double4(0., 0., 0., 0.);
     JRec<S::kPay> rn{};
     if (jn >= 0) {
-      pn = a.pos[jn];
-      rn = S::load_j(a, jn);
+      pn = a.pos[dj(jn)];
+      rn = S::load_j(a, dj(jn));
     }
     for (; k < nme; k++) {
       const int j = jn;
@@ -448,8 +452,8 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
       jn = jn2;
       jn2 = idx(k + 2);
       if (jn >= 0) {
-        pn = a.pos[jn];
-        rn = S::load_j(a, jn);
+        pn = a.pos[dj(jn)];
+        rn = S::load_j(a, dj(jn));
       }
       double dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
       if (WRAP) {
@@ -478,8 +482,8 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
   double4 pc = make_double4(0., 0., 0., 0.);
   JRec<S::kPay> rc{};
   if (j0 >= 0) {
-    pc = a.pos[j0];
-    rc = S::load_j(a, j0);
+    pc = a.pos[dj(j0)];
+    rc = S::load_j(a, dj(j0));
   }
   // one entry: compute j (data pc/rc) after issuing the loads of jn and the
   // index four entries ahead
@@ -488,8 +492,8 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
     double4 pn = make_double4(0., 0., 0., 0.);   \
     JRec<S::kPay> rn{};                          \
     if (JN >= 0) {                               \
-      pn = a.pos[JN];                            \
-      rn = S::load_j(a, JN);                     \
+      pn = a.pos[dj(JN)];                        \
+      rn = S::load_j(a, dj(JN));                 \
     }                                            \
     const int jc = J;                            \
     J = idx(M + 4);                              \

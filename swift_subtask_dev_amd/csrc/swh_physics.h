@@ -61,10 +61,23 @@ __device__ __forceinline__ double rsqrt_f64(double x) {  // x > 0
   e = fma(-h * y, y, 0.5);
   return fma(y, e, y);
 }
-// a / b: fp64 through rcp_f64, float as the reference writes it.
+// One-Newton-step forms for the pair loops: v_rcp_f64 / v_rsq_f64 are good
+// to ~5e-8 relative on gfx950 and one step takes that to 2e-15 / 4e-15
+// (measured over x in [1e-6, 1e6], tools/probe/rcp_acc.hip) -- far below
+// the float storage of the results (6e-8) the loops accumulate into.
+__device__ __forceinline__ double rcp1_f64(double x) {
+  const double r = __builtin_amdgcn_rcp(x);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ double rsqrt1_f64(double x) {  // x > 0
+  const double y = __builtin_amdgcn_rsq(x);
+  return fma(y, fma(-0.5 * x * y, y, 0.5), y);
+}
+
+// a / b: fp64 through rcp1_f64, float as the reference writes it.
 template <typename T> __device__ __forceinline__ T tdiv(T a, T b);
 template <> __device__ __forceinline__ double tdiv<double>(double a, double b) {
-  return a * rcp_f64(b);
+  return a * rcp1_f64(b);
 }
 template <> __device__ __forceinline__ float tdiv<float>(float a, float b) { return a / b; }
 
@@ -72,7 +85,7 @@ template <> __device__ __forceinline__ float tdiv<float>(float a, float b) { ret
 template <typename T> __device__ __forceinline__ void r_and_inv(T r2, T& r, T& r_inv);
 template <>
 __device__ __forceinline__ void r_and_inv<double>(double r2, double& r, double& r_inv) {
-  r_inv = r2 > 0. ? rsqrt_f64(r2) : 0.;
+  r_inv = r2 > 0. ? rsqrt1_f64(r2) : 0.;
   r = r2 * r_inv;
 }
 template <>
@@ -190,7 +203,21 @@ template <typename T>
 struct ForceIn {
   T m, h, rho, P, c, f, balsara, alpha_visc, alpha_diff, u;
   T vx, vy, vz;
+  T m_inv, rho_inv, P_rho2;  // i side, fp64 path only (force_prep_i)
 };
+
+// The i-particle's reciprocals, once per gather instead of once per pair
+// (fp64 path; the float path keeps the reference's per-pair divisions).
+template <typename T>
+__device__ __forceinline__ void force_prep_i(ForceIn<T>& I) {
+  if constexpr (sizeof(T) == 8) {
+    I.m_inv = rcp_f64(I.m);
+    I.rho_inv = rcp_f64(I.rho);
+    I.P_rho2 = I.P * I.rho_inv * I.rho_inv;
+  } else {
+    I.m_inv = I.rho_inv = I.P_rho2 = (T)0;
+  }
+}
 
 template <typename T>
 struct ForceAcc {
@@ -198,12 +225,72 @@ struct ForceAcc {
   int min_ngb_time_bin;
 };
 
-// runner_iact_nonsym_force (hydro_iact.h:488-609). dx = x_i - x_j.
+// fp64 form of runner_iact_nonsym_force: the same terms with one
+// reciprocal per distinct denominator (1/h_j, 1/m_j, 1/rho_j, 1/(rho_i +
+// rho_j), 1/(P_i + P_j)), the i-side ones precomputed (force_prep_i), and
+// sqrt(x) as x rsqrt(x).
+__device__ __forceinline__ void iact_nonsym_force_f64(double r2, double dx, double dy,
+                                                      double dz, const ForceIn<double>& I,
+                                                      double hid_inv, double hi_inv,
+                                                      const ForceIn<double>& J,
+                                                      double a2_Hubble, ForceAcc<double>& A) {
+  double r, r_inv;
+  r_and_inv(r2, r, r_inv);
+  const double mj = J.m;
+  const double xi = r * hi_inv;
+  double wi, wi_dx;
+  kernel_deval(xi, wi, wi_dx);
+  const double wi_dr = hid_inv * wi_dx;
+  const double hj_inv = rcp1_f64(J.h);
+  const double hj2 = hj_inv * hj_inv;
+  const double hjd_inv = hj2 * hj2;
+  double wj, wj_dx;
+  kernel_deval(r * hj_inv, wj, wj_dx);
+  const double wj_dr = hjd_inv * wj_dx;
+  const double dvdr = (I.vx - J.vx) * dx + (I.vy - J.vy) * dy + (I.vz - J.vz) * dz;
+  const double dvdr_Hubble = dvdr + a2_Hubble * r2;
+  const double omega_ij = fmin(dvdr_Hubble, 0.);
+  const double mu_ij = r_inv * omega_ij;
+  const double v_sig = I.c + J.c - (double)kViscBeta * mu_ij;
+  const double f_ij = 1. - I.f * rcp1_f64(mj);
+  const double f_ji = 1. - J.f * I.m_inv;
+  const double rhoj_inv = rcp1_f64(J.rho);
+  const double rho_ij = I.rho + J.rho;
+  const double rho_ij_inv = rcp1_f64(rho_ij);
+  const double alpha = I.alpha_visc + J.alpha_visc;
+  const double visc = -0.25 * alpha * v_sig * mu_ij * (I.balsara + J.balsara) * rho_ij_inv;
+  const double visc_acc_term = 0.5 * visc * (wi_dr * f_ij + wj_dr * f_ji) * r_inv;
+  const double P_over_rho2_i = I.P_rho2 * f_ij;
+  const double P_over_rho2_j = J.P * rhoj_inv * rhoj_inv * f_ji;
+  const double sph_acc_term = (P_over_rho2_i * wi_dr + P_over_rho2_j * wj_dr) * r_inv;
+  const double acc = sph_acc_term + visc_acc_term;
+  A.ax -= mj * acc * dx;
+  A.ay -= mj * acc * dy;
+  A.az -= mj * acc * dz;
+  const double sph_du_term_i = P_over_rho2_i * dvdr * r_inv * wi_dr;
+  const double visc_du_term = 0.5 * visc_acc_term * dvdr_Hubble;
+  const double alpha_diff = (I.P * I.alpha_diff + J.P * J.alpha_diff) * rcp1_f64(I.P + J.P);
+  const double q = 2. * fabs(I.P - J.P) * rho_ij_inv;
+  const double sq = q > 0. ? q * rsqrt1_f64(q) : 0.;
+  const double v_diff = alpha_diff * 0.5 * (sq + fabs(r_inv * dvdr_Hubble));
+  const double diff_du_term =
+      v_diff * (I.u - J.u) * (f_ij * wi_dr * I.rho_inv + f_ji * wj_dr * rhoj_inv);
+  const double du_dt_i = sph_du_term_i + visc_du_term + diff_du_term;
+  A.u_dt += du_dt_i * mj;
+  A.h_dt -= mj * dvdr * r_inv * rhoj_inv * wi_dr;
+}
+
+// runner_iact_nonsym_force (hydro_iact.h:488-609). dx = x_i - x_j. The
+// float path is the reference's operation order; fp64 takes the form above.
 template <typename T>
 __device__ __forceinline__ void iact_nonsym_force(T r2, T dx, T dy, T dz,
                                                   const ForceIn<T>& I, T hid_inv,
                                                   T hi_inv, const ForceIn<T>& J,
                                                   T a2_Hubble, ForceAcc<T>& A) {
+  if constexpr (sizeof(T) == 8) {
+    iact_nonsym_force_f64(r2, dx, dy, dz, I, hid_inv, hi_inv, J, a2_Hubble, A);
+    return;
+  }
   T r, r_inv;
   r_and_inv(r2, r, r_inv);
   const T mi = I.m, mj = J.m;

@@ -74,6 +74,7 @@ __device__ void gather_task(const Layout L, char* irec, const char* jrec, int nj
   }
   if (LOOP == LOOP_FORCE) {
     load_force_in(irec, L, I);
+    force_prep_i(I);
     F.ax = F.ay = F.az = F.u_dt = F.h_dt = (T)0;
     F.min_ngb_time_bin = ldb(irec, L.min_tb);
   }

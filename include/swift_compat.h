@@ -110,7 +110,19 @@ struct gpart {
   int8_t type;                /* @89  enum part_type is __attribute__((packed)) */
 } __attribute__((aligned(32)));
 
-struct xpart; /* host-only extended data; never read by the hot path */
+/* struct xpart (src/hydro/SPHENIX/hydro_part.h:50-90): the fields the drift
+ * reads (v_full, a_grav) and keeps (x_diff, x_diff_sort); the splitting /
+ * cooling / tracer / star-formation / feedback / MHD members that follow are
+ * not read (padding here; compiled against SWIFT the adapter takes
+ * offsetof of the real struct). 96 B as SURVEY's probe. */
+struct xpart {
+  float x_diff[3];      /* @0  */
+  float x_diff_sort[3]; /* @12 */
+  float v_full[3];      /* @24 */
+  float a_grav[3];      /* @36 */
+  float u_full;         /* @48 */
+  char other_xpart_data_[44];
+} __attribute__((aligned(32)));
 
 /* src/sort_part.h:32-39 */
 struct sort_entry {

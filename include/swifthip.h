@@ -85,7 +85,15 @@ typedef struct swh_part_layout {
   int32_t off_f, off_pressure, off_soundspeed, off_h_dt, off_balsara, off_alpha_visc_max_ngb;
   int32_t off_time_bin;         /* int8 */
   int32_t off_min_ngb_time_bin; /* int8 */
+  int32_t off_gpart;            /* struct gpart* (drift: gravity kick if non-NULL), -1: none */
 } swh_part_layout;
+
+/* struct xpart fields the drift reads (src/hydro/SPHENIX/hydro_part.h:50-90). */
+typedef struct swh_xpart_layout {
+  int32_t stride;     /* sizeof(struct xpart) */
+  int32_t off_v_full; /* float[3] */
+  int32_t off_a_grav; /* float[3] */
+} swh_xpart_layout;
 
 typedef struct swh_gpart_layout {
   int32_t stride; /* sizeof(struct gpart) */
@@ -249,11 +257,13 @@ SWH_API swh_status swh_space_set_stream(swh_space *s, void *stream);
 SWH_API swh_status swh_space_upload_parts(swh_space *s, const void *parts, int64_t count,
                                   const swh_part_layout *L, int on_device);
 /* Fields written back: SWH_FIELDS_DENSITY after density+ghost, SWH_FIELDS_FORCE
- * after force (the union member of struct part that is live), or ALL. */
+ * after force (the union member of struct part that is live), SWH_FIELDS_DRIFT
+ * after a drift (x, v, u, h, rho, pressure, soundspeed, v_sig), or ALL. */
 #define SWH_FIELDS_DENSITY 1
 #define SWH_FIELDS_GRADIENT 2
 #define SWH_FIELDS_FORCE 4
-#define SWH_FIELDS_ALL 7
+#define SWH_FIELDS_DRIFT 8
+#define SWH_FIELDS_ALL 15
 SWH_API swh_status swh_space_download_parts(swh_space *s, void *parts, const swh_part_layout *L,
                                     int fields, int on_device);
 SWH_API int64_t swh_space_count(const swh_space *s);
@@ -298,6 +308,26 @@ SWH_API swh_status swh_space_set_owned(swh_space *s, int64_t n_owned);
 SWH_API swh_status swh_space_pack_halo(swh_space *s, const int32_t *idx, int32_t n, float *out);
 SWH_API swh_status swh_space_unpack_halo(swh_space *s, const int32_t *idx, int32_t n,
                                          const float *in, int fields);
+/* Drift (runner_do_drift_part over every cell, src/runner_drift.c:41 ->
+ * drift_part, src/drift.h:143-232, with SPHENIX hydro_predict_extra,
+ * src/hydro/SPHENIX/hydro.h:1012-1066; entropy and pressure floors NONE):
+ * x += v_full dt_drift; v += a_hydro dt_kick_hydro (+ a_grav dt_kick_grav for
+ * particles with a gpart); u += u_dt dt_therm; h, rho by exp(+-w1); u floored
+ * at min_u; P, c from the EOS; v_sig >= 2c. Every non-inhibited particle,
+ * owned or foreign, is drifted. The particles stay in their cells: the loops
+ * widen their reach by the largest displacement since the last rebuild
+ * (swh_space_info.dx_max, SWIFT's dx_max_part), so they stay exact; rebuild
+ * when it grows too large (SWIFT: space_maxreldx of the cell size). The
+ * xparts (v_full, a_grav) are uploaded in caller order, once per step. */
+typedef struct swh_drift_params {
+  double dt_drift, dt_kick_hydro, dt_kick_grav, dt_therm;
+  float min_u; /* hydro_props->minimal_internal_energy / cosmo->a_factor_internal_energy */
+} swh_drift_params;
+SWH_API swh_status swh_space_upload_xparts(swh_space *s, const void *xparts, int64_t count,
+                                           const swh_xpart_layout *XL, int on_device);
+SWH_API swh_status swh_space_drift(swh_space *s, const swh_drift_params *D,
+                                   const swh_hydro_params *P);
+
 /* Wait for all queued work on the space's stream. */
 SWH_API swh_status swh_space_sync(swh_space *s);
 
@@ -335,6 +365,7 @@ typedef struct swh_space_info {
   int64_t list_entries;  /* last counted list build: total entries */
   int32_t list_overflow; /* last counted list build: particles over list_capacity */
   int32_t list_valid;    /* the step's pair lists are current */
+  double dx_max;         /* largest displacement since the last rebuild (drift) */
 } swh_space_info;
 SWH_API swh_status swh_space_get_info(const swh_space *s, swh_space_info *info);
 

@@ -747,8 +747,11 @@ struct ogrid {
   int *index; /* particle indices sorted by cell */
 };
 
+/* Non-periodic: positions outside [0, dim) (drifted since the last rebuild)
+ * are clamped into the boundary cells, whose extent is then open-ended; the
+ * gathers clamp both ends of their cell range the same way. */
 static void ogrid_build(struct ogrid *g, const opart *parts, long long N,
-                        const double dim[3], double min_width) {
+                        const double dim[3], double min_width, int periodic) {
   for (int k = 0; k < 3; k++) {
     int c = (int)floor(dim[k] / min_width);
     if (c < 1) c = 1;
@@ -764,8 +767,8 @@ static void ogrid_build(struct ogrid *g, const opart *parts, long long N,
     int c[3];
     for (int k = 0; k < 3; k++) {
       double xx = parts[i].x[k];
-      xx -= floor(xx / dim[k]) * dim[k];
-      c[k] = (int)(xx / g->w[k]);
+      if (periodic) xx -= floor(xx / dim[k]) * dim[k];
+      c[k] = (int)floor(xx / g->w[k]);
       if (c[k] >= g->cdim[k]) c[k] = g->cdim[k] - 1;
       if (c[k] < 0) c[k] = 0;
     }
@@ -807,8 +810,8 @@ static long long gather_one(opart *parts, const struct ogrid *g, long long i,
     lo[k] = (int)floor((xx - reach) / g->w[k]);
     hi_c[k] = (int)floor((xx + reach) / g->w[k]);
     if (!P->periodic) {
-      if (lo[k] < 0) lo[k] = 0;
-      if (hi_c[k] > g->cdim[k] - 1) hi_c[k] = g->cdim[k] - 1;
+      lo[k] = lo[k] < 0 ? 0 : (lo[k] > g->cdim[k] - 1 ? g->cdim[k] - 1 : lo[k]);
+      hi_c[k] = hi_c[k] < 0 ? 0 : (hi_c[k] > g->cdim[k] - 1 ? g->cdim[k] - 1 : hi_c[k]);
     } else if (hi_c[k] - lo[k] + 1 > g->cdim[k]) {
       lo[k] = 0;
       hi_c[k] = g->cdim[k] - 1;
@@ -891,7 +894,7 @@ static long long box_loop(opart *o, long long N, const struct oracle_params *P,
                           int *counts) {
   const double hmax = max_h(o, N) * kernel_gamma;
   struct ogrid g;
-  ogrid_build(&g, o, N, P->dim, hmax > 0 ? hmax : P->dim[0]);
+  ogrid_build(&g, o, N, P->dim, hmax > 0 ? hmax : P->dim[0], P->periodic);
   const long long nit = subset ? nsub : N;
   long long total = 0;
 #pragma omp parallel for schedule(dynamic, 256) reduction(+ : total)
@@ -1084,6 +1087,68 @@ API void PFX(box_extra_ghost)(struct part *parts, long long N,
   from_oparts(o, parts, N, PHASE_FORCE);
 }
 
+/* Drift of every non-inhibited particle: drift_part (src/drift.h:143-232)
+ * with SPHENIX hydro_predict_extra (src/hydro/SPHENIX/hydro.h:1012-1066),
+ * entropy and pressure floors NONE, EOS_IDEAL_GAS. Float fields in float, as
+ * the reference (both builds: the drift has no reduction). has_gpart[i]:
+ * the part has a gpart (gravity kick). */
+struct oracle_drift_params {
+  double dt_drift, dt_kick_hydro, dt_kick_grav, dt_therm;
+  float min_u;
+};
+
+static float approx_expf_o(float x) {  /* src/approx_math.h:35 */
+  return 1.f + x * (1.f + x * (0.5f + x * (1.f / 6.f + 1.f / 24.f * x)));
+}
+
+API void PFX(box_drift)(struct part *parts, struct xpart *xparts, const char *has_gpart,
+                        long long N, const struct oracle_drift_params *D) {
+  for (long long i = 0; i < N; i++) {
+    struct part *p = &parts[i];
+    struct xpart *xp = &xparts[i];
+    if (p->time_bin == time_bin_inhibited) continue;
+    p->x[0] += xp->v_full[0] * D->dt_drift;
+    p->x[1] += xp->v_full[1] * D->dt_drift;
+    p->x[2] += xp->v_full[2] * D->dt_drift;
+    p->v[0] += p->a_hydro[0] * D->dt_kick_hydro;
+    p->v[1] += p->a_hydro[1] * D->dt_kick_hydro;
+    p->v[2] += p->a_hydro[2] * D->dt_kick_hydro;
+    if (has_gpart && has_gpart[i]) {
+      p->v[0] += xp->a_grav[0] * D->dt_kick_grav;
+      p->v[1] += xp->a_grav[1] * D->dt_kick_grav;
+      p->v[2] += xp->a_grav[2] * D->dt_kick_grav;
+    }
+    /* hydro_predict_extra(p, xp, (float)dt_drift, (float)dt_therm, ...) */
+    const float dt_drift = (float)D->dt_drift, dt_therm = (float)D->dt_therm;
+    p->u += p->u_dt * dt_therm;
+    const float h_inv = 1.f / p->h;
+    const float w1 = p->force.h_dt * h_inv * dt_drift;
+    if (fabsf(w1) < 0.2f)
+      p->h *= approx_expf_o(w1);
+    else
+      p->h *= expf(w1);
+    const float w2 = -3.f * w1;
+    if (fabsf(w2) < 0.2f)
+      p->rho *= approx_expf_o(w2);
+    else
+      p->rho *= expf(w2);
+    const float floor_u = 0.f; /* entropy_floor NONE */
+    p->u = p->u > floor_u ? p->u : floor_u;
+    p->u = p->u > D->min_u ? p->u : D->min_u;
+    const float pressure = hydro_gamma_minus_one * p->u * p->rho;
+    const float soundspeed = sqrtf(hydro_gamma * pressure / p->rho);
+    p->force.pressure = pressure;
+    p->force.soundspeed = soundspeed;
+    p->viscosity.v_sig = p->viscosity.v_sig > 2.f * soundspeed ? p->viscosity.v_sig
+                                                               : 2.f * soundspeed;
+    for (int k = 0; k < 3; k++) {
+      const float dx = xp->v_full[k] * D->dt_drift;
+      xp->x_diff[k] -= dx;
+      xp->x_diff_sort[k] -= dx;
+    }
+  }
+}
+
 /* src/runner_others.c:618 -> hydro_end_force */
 API void PFX(box_end_force)(struct part *parts, long long N,
                             const struct oracle_params *P) {
@@ -1100,7 +1165,7 @@ API long long PFX(box_count_pairs)(struct part *parts, long long N,
   opart *o = to_oparts(parts, N, PHASE_DENSITY);
   const double hmax = max_h(o, N) * kernel_gamma;
   struct ogrid g;
-  ogrid_build(&g, o, N, P->dim, hmax > 0 ? hmax : P->dim[0]);
+  ogrid_build(&g, o, N, P->dim, hmax > 0 ? hmax : P->dim[0], P->periodic);
   long long total = 0;
 #pragma omp parallel for schedule(dynamic, 1024) reduction(+ : total)
   for (long long i = 0; i < N; i++) {
@@ -1115,8 +1180,8 @@ API long long PFX(box_count_pairs)(struct part *parts, long long N,
       lo[k] = (int)floor((xx - reach) / g.w[k]);
       hc[k] = (int)floor((xx + reach) / g.w[k]);
       if (!P->periodic) {
-        if (lo[k] < 0) lo[k] = 0;
-        if (hc[k] > g.cdim[k] - 1) hc[k] = g.cdim[k] - 1;
+        lo[k] = lo[k] < 0 ? 0 : (lo[k] > g.cdim[k] - 1 ? g.cdim[k] - 1 : lo[k]);
+        hc[k] = hc[k] < 0 ? 0 : (hc[k] > g.cdim[k] - 1 ? g.cdim[k] - 1 : hc[k]);
       } else if (hc[k] - lo[k] + 1 > g.cdim[k]) {
         lo[k] = 0;
         hc[k] = g.cdim[k] - 1;

@@ -86,6 +86,16 @@ GPART_DTYPE = np.dtype(
     }
 )
 
+# include/swift_compat.h struct xpart (SPHENIX): the drift's fields + padding
+XPART_DTYPE = np.dtype(
+    {
+        "names": ["x_diff", "x_diff_sort", "v_full", "a_grav", "u_full"],
+        "formats": [("<f4", 3), ("<f4", 3), ("<f4", 3), ("<f4", 3), "<f4"],
+        "offsets": [0, 12, 24, 36, 48],
+        "itemsize": 96,
+    }
+)
+
 NUM_TIME_BINS = 56  # src/timeline.h:36
 TIME_BIN_INHIBITED = NUM_TIME_BINS + 2
 
@@ -95,6 +105,12 @@ def new_parts(n: int) -> np.ndarray:
     raw = np.zeros(n * 160 + 32, dtype=np.uint8)
     off = (-raw.ctypes.data) % 32
     return raw[off : off + n * 160].view(PART_DTYPE)
+
+
+def new_xparts(n: int) -> np.ndarray:
+    raw = np.zeros(n * 96 + 32, dtype=np.uint8)
+    off = (-raw.ctypes.data) % 32
+    return raw[off : off + n * 96].view(XPART_DTYPE)
 
 
 def new_gparts(n: int) -> np.ndarray:
@@ -113,7 +129,18 @@ class PartLayout(C.Structure):
         "off_visc_alpha", "off_v_sig", "off_laplace_u", "off_diff_alpha", "off_wcount",
         "off_wcount_dh", "off_rho_dh", "off_rot_v", "off_f", "off_pressure",
         "off_soundspeed", "off_h_dt", "off_balsara", "off_alpha_visc_max_ngb",
-        "off_time_bin", "off_min_ngb_time_bin")]
+        "off_time_bin", "off_min_ngb_time_bin", "off_gpart")]
+
+
+class XPartLayout(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("stride", "off_v_full", "off_a_grav")]
+
+
+class DriftParams(C.Structure):
+    """swh_drift_params (== the oracle's oracle_drift_params)."""
+
+    _fields_ = [("dt_drift", C.c_double), ("dt_kick_hydro", C.c_double),
+                ("dt_kick_grav", C.c_double), ("dt_therm", C.c_double), ("min_u", C.c_float)]
 
 
 class GPartLayout(C.Structure):
@@ -187,7 +214,8 @@ class SpaceInfo(C.Structure):
     _fields_ = [("cdim", C.c_int32 * 3), ("ncell", C.c_int32), ("ngroups", C.c_int32),
                 ("reserved", C.c_int32), ("cell_width", C.c_double * 3), ("h_max", C.c_double),
                 ("loop_stats", C.c_int64 * 4), ("list_entries", C.c_int64),
-                ("list_overflow", C.c_int32), ("list_valid", C.c_int32)]
+                ("list_overflow", C.c_int32), ("list_valid", C.c_int32),
+                ("dx_max", C.c_double)]
 
 
 class Tuning(C.Structure):
@@ -204,7 +232,7 @@ class Leaf(C.Structure):
 LEAF_DTYPE = np.dtype([("start", "<i4"), ("count", "<i4")])
 LEAF_PAIR_DTYPE = np.dtype([("j", "<i4"), ("truncated", "<i4"), ("allow_mpole", "<i4")])
 
-FIELDS_DENSITY, FIELDS_GRADIENT, FIELDS_FORCE, FIELDS_ALL = 1, 2, 4, 7
+FIELDS_DENSITY, FIELDS_GRADIENT, FIELDS_FORCE, FIELDS_DRIFT, FIELDS_ALL = 1, 2, 4, 8, 15
 # halo record fields (swh_space_unpack_halo): h, rho, P + c, f + balsara, alphas
 HALO_H, HALO_RHO, HALO_PC, HALO_F_BALSARA, HALO_ALPHAS, HALO_ALL = 1, 2, 4, 8, 16, 31
 HALO_RECORD_FLOATS = 8

@@ -55,6 +55,11 @@ swh_status make_layout(const swh_part_layout* L, Layout* o) {
   o->avmn = L->off_alpha_visc_max_ngb;
   o->time_bin = L->off_time_bin;
   o->min_tb = L->off_min_ngb_time_bin;
+  o->gpart = L->off_gpart;
+  if (o->gpart >= 0 && (!aligned_field(o->gpart, 8, o->stride) || o->gpart + 8 > o->stride)) {
+    set_error("misaligned gpart pointer offset %d", o->gpart);
+    return SWH_ERR_ARG;
+  }
   const int fl[] = {o->mass, o->h, o->u, o->u_dt, o->rho, o->div_v, o->div_v_dt,
                     o->div_v_prev, o->visc_alpha, o->v_sig, o->laplace_u,
                     o->diff_alpha, o->wcount, o->wcount_dh, o->rho_dh, o->f,
@@ -161,6 +166,7 @@ void swh_part_layout_sphenix(swh_part_layout* o) {
   o->off_alpha_visc_max_ngb = offsetof(struct part, force.alpha_visc_max_ngb);
   o->off_time_bin = offsetof(struct part, time_bin);
   o->off_min_ngb_time_bin = offsetof(struct part, limiter_data.min_ngb_time_bin);
+  o->off_gpart = offsetof(struct part, gpart);
 }
 
 void swh_gpart_layout_multisoftening(swh_gpart_layout* o) {

@@ -248,8 +248,9 @@ __device__ __forceinline__ void cell_range(const GridDev& g, double xi, double y
   const double xs[3] = {xi, yi, zi};
   for (int k = 0; k < 3; k++) {
     const double rel = xs[k] - g.origin[k];
-    c.lo[k] = (int)floor((rel - reach) * g.inv_w[k]);
-    c.hi[k] = (int)floor((rel + reach) * g.inv_w[k]);
+    // particles may sit up to g.dx outside their cell after a drift
+    c.lo[k] = (int)floor((rel - reach - g.dx) * g.inv_w[k]);
+    c.hi[k] = (int)floor((rel + reach + g.dx) * g.inv_w[k]);
     if (g.periodic) {
       c.full[k] = (c.hi[k] - c.lo[k] + 1 >= g.cdim[k]);
       if (c.full[k]) {

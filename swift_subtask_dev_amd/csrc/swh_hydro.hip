@@ -56,19 +56,21 @@ __global__ __launch_bounds__(256) void loop_kernel(GridDev g, SoA a,
 // ---------------------------------------------------------------------------
 constexpr int kWalkLpi = 4;  // lanes per i of the list walks
 
-__global__ void list_prep_kernel(const unsigned int* hmax_bits, float gs1, unsigned int* rwrap,
-                                 unsigned int* ovf_n) {
+__global__ void list_prep_kernel(const unsigned int* hmax_bits, float gs1, float dx,
+                                 unsigned int* rwrap, unsigned int* ovf_n) {
   if (threadIdx.x == 0) {
-    const float r = __uint_as_float(*hmax_bits) * gs1;
+    // a particle within R_max + dx of a periodic face may have neighbours
+    // across it (dx: particles drifted out of the box since the rebuild)
+    const float r = __uint_as_float(*hmax_bits) * gs1 + dx;
     *rwrap = __float_as_uint(r * (1.f + 1e-4f) + 1e-30f);
     *ovf_n = 0u;
   }
 }
 
-__global__ void posf_kernel(GridDev g, const double4* __restrict__ pos, int64_t n,
-                            float4* __restrict__ posf) {
+__global__ void posf_kernel(GridDev g, const double4* __restrict__ pos,
+                            const int* __restrict__ pcell, int64_t n, float4* __restrict__ posf) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) posf[i] = cell_local(g, pos[i]);
+  if (i < n) posf[i] = pcell[i] >= 0 ? cell_local(g, pos[i], pcell[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 __global__ __launch_bounds__(64) void list_build_kernel(GridDev g, SoA a, ListDev ld,
@@ -136,14 +138,15 @@ __global__ __launch_bounds__(256) void overflow_kernel(GridDev g, SoA a, ListDev
           const int wx = wrap_cell(g, c, 0, cx, sx);
           const int2 r = cell_range_of(g, wx, wy, wz);
           if (r.y <= r.x) continue;
-          // box gap between i and this image of the cell
+          // box gap between i and this image of the cell (its particles may
+          // stand g.dx outside it after a drift)
           const double cl[3] = {g.origin[0] + wx * g.w[0] + sx, g.origin[1] + wy * g.w[1] + sy,
                                 g.origin[2] + wz * g.w[2] + sz};
           const double xs[3] = {pi.x, pi.y, pi.z};
           double gap2 = 0.;
           for (int k = 0; k < 3; k++) {
             if (c.full[k]) continue;
-            const double gk = fmax(fmax(cl[k] - xs[k], xs[k] - cl[k] - g.w[k]), 0.);
+            const double gk = fmax(fmax(cl[k] - xs[k], xs[k] - cl[k] - g.w[k]) - g.dx, 0.);
             gap2 += gk * gk;
           }
           const int lin = (wz * g.cdim[1] + wy) * g.cdim[0] + wx;
@@ -587,9 +590,10 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
                        (float)(kGamma * ld.skin1), s->cell_hreach.as<unsigned int>());
   }
   hipLaunchKernelGGL(posf_kernel, dim3((int)((s->n + 255) / 256)), dim3(256), 0, s->stream,
-                     grid_dev(s), s->pos.as<const double4>(), s->n, s->posf.as<float4>());
+                     grid_dev(s), s->pos.as<const double4>(), s->pcell.as<const int>(), s->n,
+                     s->posf.as<float4>());
   hipLaunchKernelGGL(list_prep_kernel, dim3(1), dim3(64), 0, s->stream, hmax_slot(s),
-                     kGamma * ld.skin1, rwrap_slot(s), ovf_slot(s));
+                     kGamma * ld.skin1, (float)s->grid.dx, rwrap_slot(s), ovf_slot(s));
   hipLaunchKernelGGL(list_build_kernel, dim3(s->ngroups), dim3(64), 0, s->stream, grid_dev(s),
                      soa_of(s), ld, s->groups.as<const int2>(), s->ngroups, P->max_active_bin,
                      hmax_slot(s), count ? counter_slot(s) : nullptr, s->tuning.diag_mode);

@@ -100,6 +100,7 @@ struct Layout {
   int wcount, wcount_dh, rho_dh, rot_v;
   int f, pressure, soundspeed, h_dt, balsara, avmn;
   int time_bin, min_tb;
+  int gpart;  // struct gpart* (-1: none)
 };
 swh_status make_layout(const swh_part_layout* L, Layout* out);
 
@@ -139,6 +140,7 @@ struct SwhGrid {
   int ncell = 0;
   double hmax = 0;  // max H = gamma*h over all particles at rebuild
   bool adaptive = false;  // cells sized by the typical H (h spans a wide range)
+  double dx = 0;    // largest displacement since the rebuild (drift): loops widen their reach
 };
 
 // Device-resident particle set, sorted by grid cell in Morton order of the
@@ -173,6 +175,11 @@ struct swh_space {
   swh::DevBuf iperm; // int32 caller index -> sorted index
   int64_t n_owned = 0;  // caller indices >= n_owned: foreign halo (swh_space_set_owned)
   swh::DevBuf ncount;  // int32 per-particle interaction count (diagnostic)
+  // drift (swh_space_drift): caller-order xpart data and the gpart flag,
+  // sorted-order displacement since the rebuild and the sorted cell of each
+  // particle (positions relative to it in posf stay valid when it drifts out)
+  swh::DevBuf vfull_c, agrav_c, hasg_c, xdiff, pcell, cell_lin;
+  bool xparts_valid = false;
   // grid
   swh::DevBuf cell_start;  // int32[ncell+1], indexed by Morton rank
   swh::DevBuf cell_rank;   // int32[ncell]: linear cell -> Morton rank

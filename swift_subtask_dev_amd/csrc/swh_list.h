@@ -105,14 +105,15 @@ constexpr int kStageU = SWH_STAGE_U;  // candidates per lane per staging pass
 // Positions relative to the lower corner of each particle's grid cell, in
 // fp32, with h: the list build's staging loads 16 B per candidate and turns
 // it into group-relative coordinates with three fp32 adds.
-__device__ __forceinline__ float4 cell_local(const GridDev& g, const double4& p) {
+// The cell is the particle's sorted cell (pcell, from the rebuild), not the
+// one its current position falls in: after a drift the offset may leave
+// [0, w) by up to g.dx, and staging adds the sorted cell's corner back.
+__device__ __forceinline__ float4 cell_local(const GridDev& g, const double4& p, int lin) {
   const double xs[3] = {p.x, p.y, p.z};
+  const int ck[3] = {lin % g.cdim[0], (lin / g.cdim[0]) % g.cdim[1],
+                     lin / (g.cdim[0] * g.cdim[1])};
   float l[3];
-  for (int k = 0; k < 3; k++) {
-    int ck = (int)floor((xs[k] - g.origin[k]) * g.inv_w[k]);  // key_kernel's binning
-    ck = ck < 0 ? 0 : (ck >= g.cdim[k] ? g.cdim[k] - 1 : ck);
-    l[k] = (float)(xs[k] - (g.origin[k] + ck * g.w[k]));
-  }
+  for (int k = 0; k < 3; k++) l[k] = (float)(xs[k] - (g.origin[k] + ck[k] * g.w[k]));
   return make_float4(l[0], l[1], l[2], (float)p.w);
 }
 
@@ -218,7 +219,8 @@ __device__ __forceinline__ void list_build(const GridDev& g, const SoA& a, const
   int nq = 0, wr = 0;
   if (Rg > 0.) {
     const double Rmax = (double)__uint_as_float(*hmax_bits) * (double)kGamma * skin1;
-    const double reach = fmax(Rg, Rmax);  // r < max(R_i, R_j)
+    // r < max(R_i, R_j); cells are enumerated out to reach + dx (drift)
+    const double reach = fmax(Rg, Rmax) + g.dx;
     CellRange c;
     double ctr[3], half[3];
     double D2 = 0.;
@@ -296,9 +298,10 @@ __device__ __forceinline__ void list_build(const GridDev& g, const SoA& a, const
         if (cnt > 0 && ld.cell_R && Rmax > Rg) {
           // prune by the cell's own reach: box gap group <-> cell (an axis
           // spanning the whole periodic box has no gap)
-          const double gx = c.full[0] ? 0. : fmax(fmax(dox - half[0], -half[0] - dox - g.w[0]), 0.);
-          const double gy = c.full[1] ? 0. : fmax(fmax(doy - half[1], -half[1] - doy - g.w[1]), 0.);
-          const double gz = c.full[2] ? 0. : fmax(fmax(doz - half[2], -half[2] - doz - g.w[2]), 0.);
+          // (the cell's particles may stand g.dx outside its box after a drift)
+          const double gx = c.full[0] ? 0. : fmax(fmax(dox - half[0], -half[0] - dox - g.w[0]) - g.dx, 0.);
+          const double gy = c.full[1] ? 0. : fmax(fmax(doy - half[1], -half[1] - doy - g.w[1]) - g.dx, 0.);
+          const double gz = c.full[2] ? 0. : fmax(fmax(doz - half[2], -half[2] - doz - g.w[2]) - g.dx, 0.);
           const double Rc = fmax(Rg, (double)ld.cell_R[(wz * g.cdim[1] + wy) * g.cdim[0] + wx]) +
                             delta;
           if (gx * gx + gy * gy + gz * gz > Rc * Rc * (1. + 1e-6)) cnt = 0;

@@ -37,6 +37,7 @@ struct GridDev {
   double inv_w[3];
   double origin[3];
   double dim[3];
+  double dx;         // largest displacement since the rebuild: added to every reach
   const int2* span;  // linear (x-fastest) cell -> its sorted range [x, y)
 };
 
@@ -57,6 +58,7 @@ inline GridDev grid_dev(const swh_space* s) {
     d.dim[k] = g.dim[k];
   }
   d.periodic = g.periodic;
+  d.dx = g.dx;
   return d;
 }
 

@@ -23,10 +23,12 @@ __device__ __forceinline__ float aos_f(const char* r, int off) {
   return off >= 0 ? *reinterpret_cast<const float*>(r + off) : 0.f;
 }
 
-__global__ void unpack_kernel(Layout L, const char* __restrict__ aos, int64_t n, SoA a) {
+__global__ void unpack_kernel(Layout L, const char* __restrict__ aos, int64_t n, SoA a,
+                              int8_t* __restrict__ hasg) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const char* r = aos + i * L.stride;
+  hasg[i] = (L.gpart >= 0 && *reinterpret_cast<void* const*>(r + L.gpart) != nullptr) ? 1 : 0;
   const double* x = reinterpret_cast<const double*>(r + L.x);
   a.pos[i] = make_double4(x[0], x[1], x[2], (double)aos_f(r, L.h));
   a.vm[i] = make_float4(aos_f(r, L.v), aos_f(r, L.v + 4), aos_f(r, L.v + 8), aos_f(r, L.mass));
@@ -100,6 +102,22 @@ __global__ void pack_kernel(Layout L, char* __restrict__ aos, int64_t n, SoA a, 
     put_f(r, L.u_dt, ac.w);
     put_f(r, L.h_dt, a.hdt[s]);
     if (L.min_tb >= 0) *reinterpret_cast<int8_t*>(r + L.min_tb) = a.mintb[s];
+  }
+  if (fields & SWH_FIELDS_DRIFT) {
+    double* x = reinterpret_cast<double*>(r + L.x);
+    x[0] = p.x;
+    x[1] = p.y;
+    x[2] = p.z;
+    const float4 vm = a.vm[s];
+    put_f(r, L.v, vm.x);
+    put_f(r, L.v + 4, vm.y);
+    put_f(r, L.v + 8, vm.z);
+    put_f(r, L.h, (float)p.w);
+    put_f(r, L.u, th.x);
+    put_f(r, L.rho, th.y);
+    put_f(r, L.pressure, th.z);
+    put_f(r, L.soundspeed, th.w);
+    put_f(r, L.v_sig, a.grad[s].x);
   }
 }
 
@@ -364,6 +382,110 @@ __global__ void halo_unpack_kernel(SoA a, const int* __restrict__ idx, int n,
   a.fc[s] = fc;
 }
 
+__global__ void pcell_kernel(const uint32_t* __restrict__ keys, const int* __restrict__ lin,
+                             int64_t n, int ncell, int* __restrict__ pcell) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < n) pcell[s] = keys[s] < (uint32_t)ncell ? lin[keys[s]] : -1;
+}
+
+// xparts (caller order) -> v_full, a_grav (caller order; the drift reads them
+// through perm)
+__global__ void xunpack_kernel(swh_xpart_layout XL, const char* __restrict__ aos, int64_t n,
+                               float4* __restrict__ vfull, float4* __restrict__ agrav) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const char* r = aos + i * XL.stride;
+  const float* v = reinterpret_cast<const float*>(r + XL.off_v_full);
+  vfull[i] = make_float4(v[0], v[1], v[2], 0.f);
+  if (XL.off_a_grav >= 0) {
+    const float* g = reinterpret_cast<const float*>(r + XL.off_a_grav);
+    agrav[i] = make_float4(g[0], g[1], g[2], 0.f);
+  } else {
+    agrav[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// approx_expf (src/approx_math.h:35): 4th-order expansion used for |w| < 0.2
+__device__ __forceinline__ float approx_expf(float x) {
+  return 1.f + x * (1.f + x * (0.5f + x * (1.f / 6.f + 1.f / 24.f * x)));
+}
+
+struct DriftParams {
+  double dt_drift, dt_kick_hydro, dt_kick_grav, dt_therm;
+  float min_u;
+};
+
+// drift_part (src/drift.h:143-232) + SPHENIX hydro_predict_extra
+// (hydro.h:1012-1066) per particle; float fields in the reference's float
+// arithmetic, positions in double. dx_bits / h_bits: running maxima of the
+// displacement since the rebuild and of h (float bits, positive).
+__global__ void drift_kernel(SoA a, const float4* __restrict__ vfull,
+                             const float4* __restrict__ agrav, const int8_t* __restrict__ hasg,
+                             float4* __restrict__ xdiff, int64_t n, DriftParams D,
+                             unsigned int* dx_bits, unsigned int* h_bits) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float dmax = 0.f, hm = 0.f;
+  if (s < n && a.tb[s] != kTimeBinInhibited) {
+    const int c = a.perm[s];
+    const float4 vf = vfull[c];
+    double4 p = a.pos[s];
+    p.x += (double)vf.x * D.dt_drift;
+    p.y += (double)vf.y * D.dt_drift;
+    p.z += (double)vf.z * D.dt_drift;
+    float4 vm = a.vm[s];
+    const float4 ac = a.acc[s];
+    // float += float * double, as drift_part writes it
+    vm.x = (float)((double)vm.x + (double)ac.x * D.dt_kick_hydro);
+    vm.y = (float)((double)vm.y + (double)ac.y * D.dt_kick_hydro);
+    vm.z = (float)((double)vm.z + (double)ac.z * D.dt_kick_hydro);
+    if (hasg[c]) {
+      const float4 ag = agrav[c];
+      vm.x = (float)((double)vm.x + (double)ag.x * D.dt_kick_grav);
+      vm.y = (float)((double)vm.y + (double)ag.y * D.dt_kick_grav);
+      vm.z = (float)((double)vm.z + (double)ag.z * D.dt_kick_grav);
+    }
+    a.vm[s] = vm;
+    // hydro_predict_extra
+    float4 th = a.th[s];  // u, rho, P, c
+    th.x += ac.w * (float)D.dt_therm;
+    float h = (float)p.w;
+    const float h_inv = 1.f / h;
+    const float w1 = a.hdt[s] * h_inv * (float)D.dt_drift;
+    h *= fabsf(w1) < 0.2f ? approx_expf(w1) : expf(w1);
+    const float w2 = -3.f * w1;
+    th.y *= fabsf(w2) < 0.2f ? approx_expf(w2) : expf(w2);
+    th.x = fmaxf(th.x, 0.f);  // entropy floor NONE: floor_u = 0
+    th.x = fmaxf(th.x, D.min_u);
+    // EOS_IDEAL_GAS (equation_of_state.h:121-167)
+    const float pressure = kHydroGammaMinusOne * th.x * th.y;
+    const float soundspeed = sqrtf(kHydroGamma * pressure / th.y);
+    th.z = pressure;
+    th.w = soundspeed;
+    a.th[s] = th;
+    float4 gr = a.grad[s];
+    gr.x = fmaxf(gr.x, 2.f * soundspeed);
+    a.grad[s] = gr;
+    p.w = (double)h;
+    a.pos[s] = p;
+    // offsets since the last rebuild (xp->x_diff)
+    float4 xd = xdiff[s];
+    xd.x -= (float)((double)vf.x * D.dt_drift);
+    xd.y -= (float)((double)vf.y * D.dt_drift);
+    xd.z -= (float)((double)vf.z * D.dt_drift);
+    xdiff[s] = xd;
+    dmax = sqrtf(xd.x * xd.x + xd.y * xd.y + xd.z * xd.z);
+    hm = h;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    dmax = fmaxf(dmax, __shfl_xor(dmax, o));
+    hm = fmaxf(hm, __shfl_xor(hm, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(dx_bits, __float_as_uint(dmax));
+    atomicMax(h_bits, __float_as_uint(hm));
+  }
+}
+
 // cell_start[c] = first sorted index with key >= c (c in [0, ncell]).
 __global__ void cell_start_kernel(const uint32_t* __restrict__ keys, int64_t n, int ncell,
                                   int* __restrict__ start) {
@@ -514,7 +636,8 @@ swh_status swh_space_destroy(swh_space* s) {
   (void)hipStreamSynchronize(s->stream);
   DevBuf* bufs[] = {&s->aos, &s->pos, &s->vm, &s->th, &s->fc, &s->tb, &s->dens, &s->rot,
                     &s->grad, &s->acc, &s->hdt, &s->mintb, &s->perm, &s->ncount,
-                    &s->cell_start, &s->cell_rank, &s->cell_code, &s->cell_span, &s->cell_hreach, &s->groups, &s->seg_groups,
+                    &s->cell_start, &s->cell_rank, &s->cell_code, &s->cell_span, &s->cell_hreach,
+                    &s->vfull_c, &s->agrav_c, &s->hasg_c, &s->xdiff, &s->pcell, &s->cell_lin, &s->groups, &s->seg_groups,
                     &s->seg_off, &s->keys, &s->keys2, &s->idx, &s->idx2, &s->sort_tmp,
                     &s->scan_tmp, &s->counters, &s->tmp_soa, &s->ghost_left,
                     &s->ghost_right, &s->ghost_list, &s->ghost_list2, &s->ghost_flag,
@@ -574,6 +697,74 @@ swh_status swh_space_get_info(const swh_space* s, swh_space_info* info) {
   info->list_entries = s->list_entries;
   info->list_overflow = s->list_overflow;
   info->list_valid = s->list_valid ? 1 : 0;
+  info->dx_max = s->grid.dx;
+  return SWH_OK;
+}
+
+swh_status swh_space_upload_xparts(swh_space* s, const void* xparts, int64_t count,
+                                   const swh_xpart_layout* XL, int on_device) {
+  if (!s || !XL || (count > 0 && !xparts) || count != s->n || XL->stride <= 0 ||
+      XL->off_v_full < 0 || XL->off_v_full + 12 > XL->stride ||
+      (XL->off_a_grav >= 0 && XL->off_a_grav + 12 > XL->stride)) {
+    set_error("xparts must match the uploaded parts (count %lld) with v_full in the record",
+              (long long)s->n);
+    return SWH_ERR_ARG;
+  }
+  if (count == 0) return SWH_OK;
+  SWH_HIP(hipSetDevice(s->ctx->device));
+  SWH_TRY(s->vfull_c.reserve((size_t)count * sizeof(float4)));
+  SWH_TRY(s->agrav_c.reserve((size_t)count * sizeof(float4)));
+  SWH_TRY(s->tmp_soa.reserve((size_t)count * XL->stride));
+  SWH_HIP(hipMemcpyAsync(s->tmp_soa.ptr, xparts, (size_t)count * XL->stride,
+                         on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                         s->stream));
+  hipLaunchKernelGGL(xunpack_kernel, dim3((int)((count + 255) / 256)), dim3(256), 0, s->stream,
+                     *XL, s->tmp_soa.as<const char>(), count, s->vfull_c.as<float4>(),
+                     s->agrav_c.as<float4>());
+  SWH_HIP(hipGetLastError());
+  if (!on_device) SWH_HIP(hipStreamSynchronize(s->stream));
+  s->xparts_valid = true;
+  return SWH_OK;
+}
+
+swh_status swh_space_drift(swh_space* s, const swh_drift_params* D, const swh_hydro_params* P) {
+  if (!s || !D || !P) return SWH_ERR_ARG;
+  if (!s->built) {
+    set_error("swh_space_rebuild must precede the drift");
+    return SWH_ERR_STATE;
+  }
+  if (s->n == 0) return SWH_OK;
+  if (!s->xparts_valid) {
+    set_error("swh_space_upload_xparts must precede the drift");
+    return SWH_ERR_STATE;
+  }
+  SWH_HIP(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->stream;
+  DriftParams dp{D->dt_drift, D->dt_kick_hydro, D->dt_kick_grav, D->dt_therm, D->min_u};
+  unsigned int* ctr = s->counters.as<unsigned int>();
+  unsigned int* dx_bits = ctr + 19;  // counter slot 19: drift displacement
+  SWH_HIP(hipMemsetAsync(dx_bits, 0, sizeof(unsigned int), st));
+  hipLaunchKernelGGL(drift_kernel, dim3((int)((s->n + 255) / 256)), dim3(256), 0, st, soa_of(s),
+                     s->vfull_c.as<const float4>(), s->agrav_c.as<const float4>(),
+                     s->hasg_c.as<const int8_t>(), s->xdiff.as<float4>(), s->n, dp, dx_bits,
+                     ctr + 2);
+  SWH_HIP(hipGetLastError());
+  unsigned int h[2] = {0, 0};
+  SWH_HIP(hipMemcpyAsync(&h[0], dx_bits, sizeof(unsigned int), hipMemcpyDeviceToHost, st));
+  SWH_HIP(hipMemcpyAsync(&h[1], ctr + 2, sizeof(unsigned int), hipMemcpyDeviceToHost, st));
+  SWH_HIP(hipStreamSynchronize(st));
+  float dmax, hmax;
+  std::memcpy(&dmax, &h[0], sizeof(float));
+  std::memcpy(&hmax, &h[1], sizeof(float));
+  // every loop widens its reach by the displacement (plus float slack)
+  s->grid.dx = std::max(s->grid.dx, (double)dmax * (1. + 1e-6) + 1e-12);
+  s->list_valid = false;  // positions moved
+  if (s->grid.periodic &&
+      (double)hmax * kGamma + s->grid.dx >=
+          0.5 * std::min(s->grid.dim[0], std::min(s->grid.dim[1], s->grid.dim[2]))) {
+    set_error("Cell smaller than smoothing length after the drift: rebuild");
+    return SWH_ERR_CELL_SMALL;
+  }
   return SWH_OK;
 }
 
@@ -604,8 +795,11 @@ swh_status swh_space_upload_parts(swh_space* s, const void* parts, int64_t count
                          s->stream));
   const int block = 256;
   const int grid = (int)((count + block - 1) / block);
+  SWH_TRY(s->hasg_c.reserve((size_t)count));
+  s->xparts_valid = false;
+  s->grid.dx = 0.;
   hipLaunchKernelGGL(unpack_kernel, dim3(grid), dim3(block), 0, s->stream, L,
-                     s->aos.as<const char>(), count, soa_of(s));
+                     s->aos.as<const char>(), count, soa_of(s), s->hasg_c.as<int8_t>());
   SWH_HIP(hipGetLastError());
   if (!on_device) SWH_HIP(hipStreamSynchronize(s->stream));  // caller may reuse `parts`
   return SWH_OK;
@@ -782,6 +976,9 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
     SWH_TRY(s->cell_code.reserve((size_t)g.ncell * sizeof(uint32_t)));
     SWH_HIP(hipMemcpyAsync(s->cell_code.ptr, s->keys2.ptr, (size_t)g.ncell * sizeof(uint32_t),
                            hipMemcpyDeviceToDevice, st));
+    SWH_TRY(s->cell_lin.reserve((size_t)g.ncell * sizeof(int)));
+    SWH_HIP(hipMemcpyAsync(s->cell_lin.ptr, s->idx2.ptr, (size_t)g.ncell * sizeof(int),
+                           hipMemcpyDeviceToDevice, st));
     for (int k = 0; k < 3; k++) s->rank_cdim[k] = g.cdim[k];
   }
   SWH_TRY(s->cell_start.reserve(((size_t)g.ncell + 1) * sizeof(int)));
@@ -819,6 +1016,15 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
                      0, st, s->keys2.as<const uint32_t>(), n, g.ncell,
                      s->cell_start.as<int>());
   SWH_HIP(hipGetLastError());
+  // 4a. each particle's sorted cell (posf is relative to it; a drift moves
+  // particles without re-binning them) and a fresh displacement record
+  SWH_TRY(s->pcell.reserve((size_t)n * sizeof(int)));
+  SWH_TRY(s->xdiff.reserve((size_t)n * sizeof(float4)));
+  hipLaunchKernelGGL(pcell_kernel, dim3(grid), dim3(block), 0, st, s->keys2.as<const uint32_t>(),
+                     s->cell_lin.as<const int>(), n, g.ncell, s->pcell.as<int>());
+  SWH_HIP(hipGetLastError());
+  SWH_HIP(hipMemsetAsync(s->xdiff.ptr, 0, (size_t)n * sizeof(float4), st));
+  g.dx = 0.;
   // 4b. per-linear-cell span table (one load per cell lookup in the loops)
   SWH_TRY(s->cell_span.reserve((size_t)g.ncell * sizeof(int2)));
   hipLaunchKernelGGL(span_kernel, dim3((g.ncell + block - 1) / block), dim3(block), 0, st,

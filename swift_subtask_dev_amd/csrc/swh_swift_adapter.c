@@ -73,6 +73,7 @@ void swifthip_swift_part_layout(swh_part_layout *o) {
   o->off_alpha_visc_max_ngb = (int32_t)offsetof(struct part, force.alpha_visc_max_ngb);
   o->off_time_bin = (int32_t)offsetof(struct part, time_bin);
   o->off_min_ngb_time_bin = (int32_t)offsetof(struct part, limiter_data.min_ngb_time_bin);
+  o->off_gpart = (int32_t)offsetof(struct part, gpart);
 }
 
 void swifthip_swift_gpart_layout(swh_gpart_layout *o) {

@@ -176,7 +176,7 @@ __device__ __forceinline__ void tile4_loop(const GridDev& g, SoA& a,
   hi[2] = row_max<SG>(act ? pi.z : -1e300);
   bool rdone = !(Hg > 0.);
   const double hmax_reach = (double)__uint_as_float(*hmax_bits) * (double)kGamma;
-  const double reach = (LOOP == LOOP_FORCE) ? fmax(Hg, hmax_reach) : Hg;
+  const double reach = ((LOOP == LOOP_FORCE) ? fmax(Hg, hmax_reach) : Hg) + g.dx;
   CellRange c;
   int nx = 1, ny = 1, ncells = 0;
   for (int k = 0; k < 3; k++) {

@@ -252,7 +252,7 @@ __device__ __forceinline__ void tile5_loop(const GridDev& g, SoA& a,
   TileStats ts;
   if (Hg > 0.) {
     const double hmax_reach = (double)__uint_as_float(*hmax_bits) * (double)kGamma;
-    const double reach = (LOOP == LOOP_FORCE) ? fmax(Hg, hmax_reach) : Hg;
+    const double reach = ((LOOP == LOOP_FORCE) ? fmax(Hg, hmax_reach) : Hg) + g.dx;
     CellRange c;
     double ctr[3], half[3];
     double D2 = 0.;

@@ -40,7 +40,7 @@ HIP_SYMBOLS = [
     "swh_space_set_owned", "swh_space_pack_halo", "swh_space_unpack_halo",
     "swh_gspace_create",
     "swh_gspace_destroy", "swh_gspace_upload", "swh_gspace_set_leaves", "swh_grav_pp_batch",
-    "swh_gspace_make_multipoles",
+    "swh_gspace_make_multipoles", "swh_space_upload_xparts", "swh_space_drift",
     "swh_gspace_download", "swh_gspace_sync",
 ]
 ADAPTER_SYMBOLS = [
@@ -118,6 +118,8 @@ def load() -> C.CDLL:
         "swh_space_set_owned": (C.c_int, [vp, i64]),
         "swh_space_pack_halo": (C.c_int, [vp, vp, i32, vp]),
         "swh_space_unpack_halo": (C.c_int, [vp, vp, i32, vp, C.c_int]),
+        "swh_space_upload_xparts": (C.c_int, [vp, vp, i64, P(abi.XPartLayout), C.c_int]),
+        "swh_space_drift": (C.c_int, [vp, P(abi.DriftParams), P(abi.HydroParams)]),
         "swh_space_set_tuning": (C.c_int, [vp, P(abi.Tuning)]),
         "swh_space_get_info": (C.c_int, [vp, P(abi.SpaceInfo)]),
         "swh_gspace_create": (C.c_int, [vp, P(vp)]),
@@ -279,7 +281,8 @@ class HydroSpace:
         return {"cdim": list(i.cdim), "ncell": i.ncell, "ngroups": i.ngroups,
                 "cell_width": list(i.cell_width), "h_max": i.h_max,
                 "loop_stats": list(i.loop_stats), "list_entries": i.list_entries,
-                "list_overflow": i.list_overflow, "list_valid": bool(i.list_valid)}
+                "list_overflow": i.list_overflow, "list_valid": bool(i.list_valid),
+                "dx_max": i.dx_max}
 
     def upload(self, parts, count=None, on_device=False):
         """parts: numpy PART_DTYPE array (host) or a device pointer (int) with count."""
@@ -336,6 +339,16 @@ class HydroSpace:
 
     def sync(self):
         _check(self._lib.swh_space_sync(self.handle), "sync")
+
+    def upload_xparts(self, xparts: np.ndarray):
+        """struct xpart array (abi.XPART_DTYPE), same order/count as the parts."""
+        XL = abi.XPartLayout(abi.XPART_DTYPE.itemsize, abi.XPART_DTYPE.fields["v_full"][1],
+                             abi.XPART_DTYPE.fields["a_grav"][1])
+        _check(self._lib.swh_space_upload_xparts(self.handle, _ptr(xparts), len(xparts),
+                                                 C.byref(XL), 0), "upload_xparts")
+
+    def drift(self, D: abi.DriftParams, P: abi.HydroParams):
+        _check(self._lib.swh_space_drift(self.handle, C.byref(D), C.byref(P)), "drift")
 
     def set_owned(self, n_owned: int):
         """Caller indices >= n_owned become read-only halo (foreign) particles."""

@@ -61,6 +61,7 @@ def load(prec: str = "f32") -> C.CDLL:
     sig("box_ghost", C.c_int, [vp, i64, P(abi.HydroParams), P(i64)])
     sig("box_extra_ghost", None, [vp, i64, P(abi.HydroParams)])
     sig("box_end_force", None, [vp, i64, P(abi.HydroParams)])
+    sig("box_drift", None, [vp, vp, vp, i64, P(abi.DriftParams)])
     sig("box_count_pairs", i64, [vp, i64, P(abi.HydroParams), C.c_int])
     sig("grav_self_pp", i64, [vp, C.c_int, P(C.c_double), P(C.c_double), C.c_double,
                               P(abi.GravParams)])

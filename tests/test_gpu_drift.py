@@ -1,0 +1,199 @@
+"""GPU drift: swh_space_drift vs the oracle's box_drift
+(drift_part, src/drift.h:143-232, with SPHENIX hydro_predict_extra,
+src/hydro/SPHENIX/hydro.h:1012-1066), and the loops after a drift without a
+rebuild (particles left in their cells, reach widened by dx_max) vs the fp64
+oracle chain on the drifted particles: identical interaction counts and the
+same tolerances as the rebuilt chain (tests/test_gpu_parity.py).
+
+Float tolerances: the drift is a handful of float operations per field; the
+GPU contracts a*b+c into fma where the gcc-built oracle rounds twice, so
+fields agree to a few float ulps (x to a few double ulps), not bit for bit.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from test_gpu_parity import VARIANTS, assert_close, box_chain_oracle
+from swift_subtask_dev_amd import abi, ics
+
+pytestmark = pytest.mark.gpu
+
+
+def _stepped_state(ctx, periodic=True, n=16, seed=5):
+    """A box after one full chain: a_hydro, u_dt, h_dt, v_sig are live."""
+    from swift_subtask_dev_amd import lib
+    P = abi.default_hydro_params(periodic=periodic)
+    parts = ics.sedov_box(n, velocity="divergent", pert=0.3, seed=seed)
+    sp = lib.HydroSpace(ctx)
+    sp.upload(parts)
+    sp.rebuild(P)
+    sp.hydro_step(P)
+    sp.download(parts, abi.FIELDS_ALL)
+    sp.close()
+    return parts, P
+
+
+def _xparts(parts, vmax, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n = len(parts)
+    xp = abi.new_xparts(n)
+    xp["v_full"] = parts["v"] + rng.uniform(-vmax, vmax, (n, 3)).astype(np.float32)
+    xp["a_grav"] = rng.normal(0, 3.0, (n, 3)).astype(np.float32)
+    parts["gpart"] = np.where(rng.uniform(size=n) < 0.5, 1, 0).astype(np.uint64)
+    return xp
+
+
+def _drift_params(dt, min_u=0.0):
+    return abi.DriftParams(dt, 0.5 * dt, 0.7 * dt, 0.9 * dt, min_u)
+
+
+def _oracle_drift(parts, xp, D):
+    o = abi.copy_parts(parts)
+    ox = xp.copy()
+    hasg = np.ascontiguousarray((parts["gpart"] != 0).astype(np.int8))
+    O.fn("f64", "box_drift")(o.ctypes.data, ox.ctypes.data, hasg.ctypes.data, len(o),
+                             C.byref(D))
+    return o, ox
+
+
+@pytest.fixture(scope="module")
+def stepped(gpu_ctx):
+    return _stepped_state(gpu_ctx)
+
+
+@pytest.mark.parametrize("min_u", [0.0, 0.3])
+def test_drift_vs_oracle(gpu_ctx, stepped, min_u):
+    from swift_subtask_dev_amd import lib
+    parts0, P = stepped
+    parts = abi.copy_parts(parts0)
+    xp = _xparts(parts, 0.5, seed=2)
+    # some particles cool below min_u, some drift with |w1| >= 0.2 (expf branch)
+    parts["u_dt"][::7] = -50.0 * parts["u"][::7]
+    parts["h_dt"][::11] *= 40.0
+    parts["time_bin"][::13] = abi.TIME_BIN_INHIBITED
+    D = _drift_params(0.01, min_u)
+    sp = lib.HydroSpace(gpu_ctx)
+    g = abi.copy_parts(parts)
+    sp.upload(g)
+    sp.rebuild(P)
+    assert sp.info()["dx_max"] == 0.0
+    sp.upload_xparts(xp)
+    sp.drift(D, P)
+    sp.download(g, abi.FIELDS_DRIFT)
+    info = sp.info()
+    sp.close()
+    o, ox = _oracle_drift(parts, xp, D)
+    live = parts["time_bin"] != abi.TIME_BIN_INHIBITED
+    assert np.array_equal(g["x"][~live], parts["x"][~live])
+    assert np.abs(g["x"] - o["x"]).max() <= 4e-16 * 2
+    for f in ("v", "u", "h", "rho", "pressure", "soundspeed", "v_sig"):
+        assert_close(g[f], o[f], 1e-6, 1e-7, f)
+    assert (g["u"][live] >= min_u).all()
+    # dx_max: the largest |x_diff| of the drift (SWIFT's dx_max_part), rounded up
+    dref = np.sqrt((ox["x_diff"][live].astype(np.float64) ** 2).sum(axis=1)).max()
+    assert dref <= info["dx_max"] <= dref * (1 + 1e-5)
+    assert not info["list_valid"]
+
+
+def test_drift_requires_xparts(gpu_ctx, stepped):
+    from swift_subtask_dev_amd import lib
+    parts, P = stepped
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.upload(abi.copy_parts(parts))
+    sp.rebuild(P)
+    with pytest.raises(lib.SwhError, match="upload_xparts"):
+        sp.drift(_drift_params(0.01), P)
+    sp.close()
+
+
+def _drifted_chain(ctx, parts, xp, Ds, P, variant, **tuning):
+    """GPU: rebuild once, drift len(Ds) times, full chain without a rebuild."""
+    from swift_subtask_dev_amd import lib
+    g = abi.copy_parts(parts)
+    sp = lib.HydroSpace(ctx)
+    sp.set_tuning(1, variant, 0, **tuning)
+    sp.upload(g)
+    sp.rebuild(P)
+    sp.upload_xparts(xp)
+    for D in Ds:
+        sp.drift(D, P)
+    dx = sp.info()["dx_max"]
+    res = sp.hydro_step(P)
+    sp.download(g, abi.FIELDS_ALL)
+    sp.close()
+    return g, res, dx
+
+
+def _check_chain(g, rg, o, ro):
+    assert rg["density"] == ro["density"]
+    assert rg["force"] == ro["force"]
+    assert_close(g["h"], o["h"], 1e-6, what="h")
+    for f in ("rho", "pressure", "soundspeed", "balsara", "v_sig", "laplace_u"):
+        assert_close(g[f], o[f], 5e-5, 1e-4, f)
+    assert_close(g["a_hydro"], o["a_hydro"], 5e-5, 1e-4, "a_hydro")
+    assert_close(g["u_dt"], o["u_dt"], 5e-5, 1e-4, "u_dt")
+    assert_close(g["h_dt"], o["h_dt"], 5e-5, 1e-4, "h_dt")
+    assert np.array_equal(g["min_ngb_time_bin"], o["min_ngb_time_bin"])
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("periodic", [True, False])
+def test_loops_after_drift_vs_f64(gpu_ctx, variant, periodic):
+    """Displacements up to ~half a smoothing length; particles cross the
+    periodic faces and leave their cells."""
+    parts, P = _stepped_state(gpu_ctx, periodic=periodic, n=14, seed=8)
+    xp = _xparts(parts, 1.0, seed=3)
+    D = _drift_params(0.02)
+    g, rg, dx = _drifted_chain(gpu_ctx, parts, xp, [D], P, variant)
+    o, _ = _oracle_drift(parts, xp, D)
+    assert dx > 0.3 * float(parts["h"].mean())
+    if periodic:
+        crossed = ((o["x"] < 0) | (o["x"] >= 1.0)).any(axis=1)
+        assert crossed.sum() > 10
+    o, ro = box_chain_oracle(o, P)
+    _check_chain(g, rg, o, ro)
+
+
+@pytest.mark.parametrize("variant", [7, 5])
+def test_repeated_drifts_accumulate_reach(gpu_ctx, variant):
+    """Three drifts without a rebuild: dx_max accumulates (x_diff is relative
+    to the rebuild), the loops stay exact; a rebuild resets it."""
+    from swift_subtask_dev_amd import lib
+    parts, P = _stepped_state(gpu_ctx, n=14, seed=9)
+    xp = _xparts(parts, 1.0, seed=4)
+    Ds = [_drift_params(0.006) for _ in range(3)]
+    g, rg, dx = _drifted_chain(gpu_ctx, parts, xp, Ds, P, variant)
+    o = parts
+    for D in Ds:
+        o, _ = _oracle_drift(o, xp, D)
+    o, ro = box_chain_oracle(o, P)
+    _check_chain(g, rg, o, ro)
+    # single-drift reach of the same total displacement, within rounding
+    _, _, dx1 = _drifted_chain(gpu_ctx, parts, xp, [_drift_params(0.018)], P, variant)
+    assert abs(dx - dx1) <= 1e-5 * dx1
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.upload(abi.copy_parts(parts))
+    sp.rebuild(P)
+    sp.upload_xparts(xp)
+    sp.drift(Ds[0], P)
+    assert sp.info()["dx_max"] > 0
+    sp.rebuild(P)
+    assert sp.info()["dx_max"] == 0.0
+    sp.close()
+
+
+def test_drift_list_skin_and_capacity(gpu_ctx):
+    """Pair lists after a drift with a list skin and a small list capacity
+    (overflow path) stay exact."""
+    parts, P = _stepped_state(gpu_ctx, n=14, seed=10)
+    xp = _xparts(parts, 1.0, seed=5)
+    D = _drift_params(0.01)
+    o, _ = _oracle_drift(parts, xp, D)
+    o, ro = box_chain_oracle(o, P)
+    for tuning in ({"list_skin": 0.2}, {"list_capacity": 24}):
+        g, rg, _ = _drifted_chain(gpu_ctx, parts, xp, [D], P, 7, **tuning)
+        _check_chain(g, rg, o, ro)

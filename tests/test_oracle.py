@@ -512,3 +512,60 @@ def test_reference_tolerances_are_draw_specific():
 
     assert worst("random", 0.0, 0.0, "tolerance_27_normal.dat", 3) > 3.0
     assert worst("random", 0.0, 0.0, "tolerance_27_normal.dat", 1) < 1.0
+
+
+def test_box_drift_restatement():
+    """box_drift against a numpy statement of drift_part + hydro_predict_extra
+    (src/drift.h:143-232, src/hydro/SPHENIX/hydro.h:1012-1066) in float32:
+    kicks with/without a gpart, inhibited particles untouched, both exp
+    branches, the min_u floor. (No reference fixture covers the drift:
+    parity of this row rests on the restatement of the source.)"""
+    rng = np.random.Generator(np.random.PCG64(7))
+    n = 400
+    p = abi.new_parts(n)
+    p["x"] = rng.uniform(0, 1, (n, 3))
+    p["v"] = rng.normal(0, 1, (n, 3))
+    p["a_hydro"] = rng.normal(0, 5, (n, 3))
+    p["u"] = rng.uniform(0.5, 2, n)
+    p["u_dt"] = rng.normal(0, 80, n)
+    p["h"] = rng.uniform(0.02, 0.05, n)
+    p["h_dt"] = rng.normal(0, 2, n)
+    p["rho"] = rng.uniform(0.5, 2, n)
+    p["v_sig"] = rng.uniform(0, 3, n)
+    p["time_bin"] = np.where(np.arange(n) % 17 == 0, abi.TIME_BIN_INHIBITED, 1)
+    xp = abi.new_xparts(n)
+    xp["v_full"] = rng.normal(0, 1, (n, 3))
+    xp["a_grav"] = rng.normal(0, 3, (n, 3))
+    hasg = (np.arange(n) % 2).astype(np.int8)
+    D = abi.DriftParams(0.01, 0.005, 0.007, 0.009, 0.4)
+    o, ox = abi.copy_parts(p), xp.copy()
+    O.fn("f64", "box_drift")(o.ctypes.data, ox.ctypes.data, hasg.ctypes.data, n, C.byref(D))
+    live = p["time_bin"] != abi.TIME_BIN_INHIBITED
+    assert np.array_equal(o[~live], p[~live])
+    f32 = np.float32
+    x = p["x"] + xp["v_full"].astype(np.float64) * D.dt_drift
+    v = (p["v"] + p["a_hydro"].astype(np.float64) * D.dt_kick_hydro).astype(f32)
+    vg = (v + xp["a_grav"].astype(np.float64) * D.dt_kick_grav).astype(f32)
+    v = np.where(hasg[:, None] == 1, vg, v)
+    u = p["u"] + p["u_dt"] * f32(D.dt_therm)
+    w1 = p["h_dt"] * (f32(1) / p["h"]) * f32(D.dt_drift)
+
+    def ex(w):
+        a = f32(1) + w * (f32(1) + w * (f32(0.5) + w * (f32(1 / 6) + f32(1 / 24) * w)))
+        return np.where(np.abs(w) < 0.2, a, np.exp(w))
+
+    h = p["h"] * ex(w1)
+    rho = p["rho"] * ex(f32(-3) * w1)
+    u = np.maximum(np.maximum(u, f32(0)), f32(D.min_u))
+    P = f32(2 / 3) * u * rho
+    c = np.sqrt(f32(5 / 3) * P / rho)
+    assert (np.abs(w1[live]) >= 0.2).any() and (np.abs(w1[live]) < 0.2).any()
+    assert np.abs(o["x"][live] - x[live]).max() <= 4e-16
+    for name, ref in (("v", v), ("u", u), ("h", h), ("rho", rho), ("pressure", P),
+                      ("soundspeed", c), ("v_sig", np.maximum(p["v_sig"], 2 * c))):
+        e = np.abs(o[name][live] - ref[live]) / np.maximum(np.abs(ref[live]), 1e-30)
+        assert e.max() < 1e-6, (name, e.max())
+    assert (o["u"][live] >= f32(0.4)).all() and (o["u"][live] == f32(0.4)).any()
+    dx = -(xp["v_full"].astype(np.float64) * D.dt_drift).astype(f32)
+    assert np.array_equal(ox["x_diff"][live], dx[live])
+    assert np.array_equal(ox["x_diff_sort"][live], dx[live])

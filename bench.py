@@ -198,6 +198,66 @@ def parity_vs_cpu(ctx, parts, P, tuning, threads):
             "floor": "1e-6 (density fields) / 1e-4 (force fields) x the column maximum"}
 
 
+def step_breakdown(sp, P, stream, torch, local, reps=3):
+    """Per-phase times of a whole SWIFT hydro step on the device-resident box,
+    measured AFTER the timed region (not part of `value`): drift (drift_part +
+    hydro_predict_extra), rebuild (re-bin + sort), then the SPHENIX chain. Two
+    variants: rebuild every step, and drift-only (particles left in their
+    cells, the loops' reach widened by dx_max). Velocities: v_full of |v| ~ 1
+    with dt moving the fastest particle 0.1 h per step."""
+    from swift_subtask_dev_amd import abi
+    rng = np.random.Generator(np.random.PCG64(17))
+    n = len(local)
+    xp = abi.new_xparts(n)
+    xp["v_full"] = rng.normal(0, 0.577, (n, 3)).astype(np.float32)
+    sp.upload_xparts(xp)
+    h = float(np.median(local["h"]))
+    dt = 0.1 * h / float(np.abs(xp["v_full"]).max() * 1.733)
+    # kicks and the thermal update on a CFL-limited step (the Sedov hot spot's
+    # sound speed), positions moved by v_full over dt
+    vsig = np.maximum(local["v_sig"].astype(np.float64), 1e-30)
+    dt_cfl = min(dt, 0.1 * float(np.min(local["h"] / vsig)))
+    D = abi.DriftParams(dt, dt_cfl, dt_cfl, dt_cfl, 0.0)
+    sp.rebuild(P)
+    sp.hydro_step(P)  # a consistent state (h_dt, u_dt of a whole chain) to drift from
+    names = ["drift", "rebuild", "density", "ghost", "gradient", "extra_ghost", "force"]
+    out = {}
+    for mode in ("rebuild_every_step", "drift_only"):
+        acc = {k: [] for k in names}
+        dx = 0.0
+        for _ in range(reps):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)]
+            ev[0].record(stream)
+            sp.drift(D, P)
+            ev[1].record(stream)
+            if mode == "rebuild_every_step":
+                sp.rebuild(P)
+            ev[2].record(stream)
+            sp.init_parts(P)
+            sp.density(P, count=False)
+            ev[3].record(stream)
+            sp.ghost(P)
+            ev[4].record(stream)
+            sp.gradient(P, count=False)
+            ev[5].record(stream)
+            sp.extra_ghost(P)
+            ev[6].record(stream)
+            sp.force(P, count=False)
+            sp.end_force(P)
+            ev[7].record(stream)
+            torch.cuda.synchronize()
+            for k, name in enumerate(names):
+                acc[name].append(ev[k].elapsed_time(ev[k + 1]))
+            dx = sp.info()["dx_max"]
+        r = {f"{k}_ms": statistics.median(v) for k, v in acc.items()}
+        r["step_ms"] = sum(r.values())
+        r["dx_max_over_h"] = dx / h
+        out[mode] = r
+    out["note"] = ("untimed by the headline; medians of 3 steps; drift_only accumulates "
+                   "dx_max over its 3 steps (0.1 h each); kicks on a CFL step")
+    return out
+
+
 def load_traffic():
     path = ROOT / "profiles" / "traffic_density.json"
     if path.exists():
@@ -280,6 +340,8 @@ def run_grav(args, ctx, rank, world, dist, torch):
                          "traffic": None, "flops_model": "28 flops per directed P2P interaction"},
             "cpu_baseline": None,
         }
+        if breakdown:
+            out["step_breakdown"] = breakdown
         print(json.dumps(out), flush=True)
     sp.close()
 
@@ -306,6 +368,8 @@ def main():
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-runs", type=int, default=3)
+    ap.add_argument("--no-breakdown", action="store_true",
+                    help="skip the untimed full-step breakdown (drift, rebuild, chain)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong: the 128^3 box split over the GPUs (the metric); "
                          "weak: one 128^3 box per GPU")
@@ -447,6 +511,12 @@ def main():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     total_interactions, total_owned = tot.tolist()
     elapsed_max = tmax.item()
+    breakdown = None
+    if world == 1 and not args.no_breakdown and not eagle:
+        try:
+            breakdown = step_breakdown(sp, P, stream, torch, local)
+        except Exception as e:  # report, never fake
+            log(f"step breakdown failed: {e}")
 
     if rank == 0:
         td = statistics.mean(t_dens)
@@ -530,6 +600,8 @@ def main():
             },
             "cpu_baseline": None,
         }
+        if breakdown:
+            out["step_breakdown"] = breakdown
         if eagle:
             # the port's fixed cdim=20 grid puts ~10^4 clump particles in one
             # cell (O(n^2) per cell pair): no bounded CPU sample of this box

@@ -110,15 +110,17 @@ void walk_kernel(GridDev g, SoA a, ListDev ld, int n,
 // the launch needs no host round trip.
 template <int LOOP, typename T>
 __global__ __launch_bounds__(256) void overflow_kernel(GridDev g, SoA a, ListDev ld,
+                                                       const int* __restrict__ queue,
+                                                       const unsigned int* __restrict__ qn,
                                                        int max_active_bin, T a2H,
                                                        const unsigned int* __restrict__ hmax_bits,
                                                        unsigned long long* counter,
                                                        int* __restrict__ ncount) {
-  const int nov = (int)*ld.ovf_n;
+  const int nov = (int)*qn;
   const int lane = threadIdx.x & 63;
   const int nwaves = gridDim.x * (blockDim.x / 64);
   for (int w = blockIdx.x * (blockDim.x / 64) + (int)(threadIdx.x / 64); w < nov; w += nwaves) {
-    const int i = ld.ovf[w];
+    const int i = queue[w];
     if (!active_part(a, i, max_active_bin)) continue;  // wave-uniform
     LoopState<LOOP, T> st;
     st.n = 0;
@@ -172,39 +174,60 @@ __global__ __launch_bounds__(256) void overflow_kernel(GridDev g, SoA a, ListDev
   }
 }
 
-// Density on a subset (the ghost's reruns, runner_ghost.c:1503-1546): a
-// particle whose H still fits its list reach walks its list, any other one
-// searches.
+// Density on a subset (the ghost's reruns, runner_ghost.c:1503-1546): LPI
+// lanes per rerun particle walk its list while its H still fits the list
+// reach; any other one (H grown past its reach, list overflow, no lists) is
+// queued for the wave-per-particle search (overflow_kernel). The subset is the
+// ghost's redo list, in (nearly) sorted order.
 template <typename T>
 __global__ __launch_bounds__(256) void walk_subset_kernel(GridDev g, SoA a, ListDev ld,
                                                           int list_ok,
                                                           const int* __restrict__ subset,
                                                           int nitems, int max_active_bin,
                                                           const unsigned int* __restrict__ hmax_bits,
-                                                          unsigned long long* counter) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+                                                          unsigned long long* counter,
+                                                          int* __restrict__ searchq,
+                                                          unsigned int* nsearch) {
+  constexpr int LPI = kWalkLpi;
+  const int t = (int)blockIdx.x * (256 / LPI) + (int)threadIdx.x / LPI;
+  const int s = (int)threadIdx.x % LPI;
   const int i = t < nitems ? subset[t] : -1;
-  const bool act = i >= 0 && active_part(a, i, max_active_bin);
-  LoopState<LOOP_DENSITY, T> st;
-  st.n = 0;
+  bool act = i >= 0 && active_part(a, i, max_active_bin);
+  int nl = 0, lb = -1;
+  double4 pi = make_double4(0., 0., 0., 0.);
+  bool search = false;
   if (act) {
-    st.load_i(a, i, (T)0, hmax_bits);
-    const double4 pi = a.pos[i];
-    const int nl = list_ok ? ld.cnt[i] : 0;
-    const int lb = list_ok ? ld.base[i] : -1;
+    pi = a.pos[i];
+    if (list_ok) {
+      nl = ld.cnt[i];
+      lb = ld.base[i];
+    }
     const bool listed = list_ok && lb >= 0 && nl <= ld.K &&
                         pi.w * (double)kGamma <= (double)ld.reach[i];
-    if (listed) {
-      if (g.periodic)
-        walk_entries<1, true, T>(g, a, ld, pi, nl, lb, 0, st);
-      else
-        walk_entries<1, false, T>(g, a, ld, pi, nl, lb, 0, st);
-    } else {
-      gather_direct<T>(g, a, pi, st);
+    if (!listed) {
+      search = true;
+      act = false;
     }
-    st.store(a, i);
   }
-  if (counter) count_add(act ? st.n : 0, counter);
+  const bool q = search && s == 0;
+  const int slot = block_append(q, nsearch);
+  if (q) searchq[slot] = i;
+  LoopState<LOOP_DENSITY, T> st;
+  st.n = 0;
+  if (act) st.load_i(a, i, (T)0, hmax_bits);
+  if (!act) nl = 0;
+  const double rwrap = list_ok ? (double)__uint_as_float(*ld.rwrap_bits) : 0.;
+  if (__any(act && g.periodic && near_face(g, pi, rwrap)))
+    walk_entries<LPI, true, T>(g, a, ld, pi, nl, lb, s, st);
+  else
+    walk_entries<LPI, false, T>(g, a, ld, pi, nl, lb, s, st);
+  reduce_lanes<LPI, T>(st);
+  if (act && s == 0) st.store(a, i);
+  if (counter) {
+    unsigned long long v = (unsigned long long)((act && s == 0) ? st.n : 0);
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(counter, v);
+  }
 }
 
 // Occupancy of the tile kernels: SWH_TILE_WPE > 0 asks the compiler for at
@@ -278,21 +301,23 @@ template <typename T>
 __global__ void ghost_init_kernel(SoA a, int64_t n, int max_active_bin, float h_max,
                                   float* left, float* right, int* list, int* count) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || !active_part(a, i, max_active_bin)) return;
-  left[i] = 0.f;
-  right[i] = h_max;
-  const int slot = atomicAdd(count, 1);
-  list[slot] = (int)i;
+  const bool act = i < n && active_part(a, i, max_active_bin);
+  if (act) {
+    left[i] = 0.f;
+    right[i] = h_max;
+  }
+  const int slot = block_append(act, count);  // one atomic per block, sorted order kept
+  if (act) list[slot] = (int)i;
 }
 
+// One particle of the ghost: redo (h updated, queued for a rerun), or
+// converged (final fields written); hf_out = its h, stale = H outgrew its
+// list reach.
 template <typename T>
-__global__ void ghost_kernel(SoA a, const int* __restrict__ list, int count,
-                             int* __restrict__ redo, int* __restrict__ nredo, float* left,
-                             float* right, GhostParams gp, unsigned int* hmax_bits,
-                             const float* __restrict__ list_reach, unsigned int* list_stale) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= count) return;
-  const int i = list[t];
+__device__ __forceinline__ void ghost_part(SoA& a, int i, float* left, float* right,
+                                           const GhostParams& gp,
+                                           const float* __restrict__ list_reach, bool& redo_out,
+                                           float& hf_out, bool& stale) {
   double4 pos = a.pos[i];
   const T h_old = (T)(float)pos.w;
   const T h_old_dim = h_old * h_old * h_old;
@@ -372,8 +397,8 @@ __global__ void ghost_kernel(SoA a, const int* __restrict__ list, int count,
       a.rot[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       left[i] = lft;
       right[i] = rgt;
-      redo[atomicAdd(nredo, 1)] = i;
-      atomicMax(hmax_bits, __float_as_uint(hf));
+      redo_out = true;
+      hf_out = hf;
       return;
     } else if (hf <= gp.h_min) {
       h_final = (T)gp.h_min;
@@ -393,9 +418,9 @@ __global__ void ghost_kernel(SoA a, const int* __restrict__ list, int count,
   const float hf = (float)h_final;
   pos.w = (double)hf;
   a.pos[i] = pos;
-  atomicMax(hmax_bits, __float_as_uint(hf));
+  hf_out = hf;
   // the step's pair lists cover this particle's loops only while H <= its R
-  if (list_reach && (double)hf * (double)kGamma > (double)list_reach[i]) atomicOr(list_stale, 1u);
+  stale = list_reach && (double)hf * (double)kGamma > (double)list_reach[i];
   // converged: hydro_prepare_gradient + hydro_reset_gradient (hydro.h:654-733)
   const T hh = (T)hf;
   const T curl_v = tsqrt(rot_x * rot_x + rot_y * rot_y + rot_z * rot_z);
@@ -429,6 +454,28 @@ __global__ void ghost_kernel(SoA a, const int* __restrict__ list, int count,
   g.x = (float)((T)2 * soundspeed);  // v_sig
   g.y = fc.z;                        // alpha_visc_max_ngb = alpha_visc
   a.grad[i] = g;
+}
+
+template <typename T>
+__global__ void ghost_kernel(SoA a, const int* __restrict__ list, int count,
+                             int* __restrict__ redo, int* __restrict__ nredo, float* left,
+                             float* right, GhostParams gp, unsigned int* hmax_bits,
+                             const float* __restrict__ list_reach, unsigned int* list_stale) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  bool rd = false, stale = false;
+  float hf = 0.f;
+  const int i = t < count ? list[t] : -1;
+  if (i >= 0) ghost_part<T>(a, i, left, right, gp, list_reach, rd, hf, stale);
+  // one append per block for the rerun list; one max, one stale flag per wave
+  const int slot = block_append(rd, nredo);
+  if (rd) redo[slot] = i;
+  float m = hf;
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  const bool any_stale = __any(stale);
+  if ((threadIdx.x & 63) == 0) {
+    if (m > 0.f) atomicMax(hmax_bits, __float_as_uint(m));
+    if (any_stale) atomicOr(list_stale, 1u);
+  }
 }
 
 // runner_do_extra_ghost (runner_ghost.c:992-1083): hydro_end_gradient,
@@ -543,19 +590,23 @@ static unsigned int* hmax_slot(swh_space* s) { return s->counters.as<unsigned in
 static unsigned int* ovf_slot(swh_space* s) { return s->counters.as<unsigned int>() + 16; }
 static unsigned int* stale_slot(swh_space* s) { return s->counters.as<unsigned int>() + 17; }
 static unsigned int* rwrap_slot(swh_space* s) { return s->counters.as<unsigned int>() + 18; }
+// u32[20]: the ghost reruns' search-queue length
+constexpr float kGhostListSkin = 0.01f;
+static unsigned int* search_slot(swh_space* s) { return s->counters.as<unsigned int>() + 20; }
 
 static int loop_variant_of(const swh_space* s) {
   return s->tuning.loop_variant != 0 ? s->tuning.loop_variant : 7;
 }
 
 static ListDev list_dev(swh_space* s) {
+  // skin of the lists in use (the ghost may rebuild them with a wider one)
   ListDev d;
   d.nbr = s->nbr.as<int>();
   d.cnt = s->nbr_cnt.as<int>();
   d.base = s->nbr_base.as<int>();
   d.reach = s->nbr_reach.as<float>();
   d.K = s->list_K;
-  d.skin1 = 1.f + s->tuning.list_skin;
+  d.skin1 = 1.f + s->list_skin_cur;
   d.rwrap_bits = rwrap_slot(s);
   d.ovf = s->nbr_ovf.as<int>();
   d.posf = s->posf.as<const float4>();
@@ -567,8 +618,10 @@ static ListDev list_dev(swh_space* s) {
 }
 
 // Build the step's pair lists (variant 7) for the active particles.
-static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool count) {
+static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool count,
+                              float skin) {
   const int K = s->tuning.list_capacity > 0 ? s->tuning.list_capacity : 128;
+  s->list_skin_cur = skin;
   SWH_TRY(s->nbr.reserve((size_t)std::max(1, s->ngroups) * K * kListSlots * sizeof(int)));
   if (K % 4 != 0) {
     set_error("list_capacity must be a multiple of 4");
@@ -610,18 +663,26 @@ static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int
   const int block = 256;
   if (v == 7) {
     const ListDev ld = list_dev(s);
-    if (subset) {  // density reruns of the ghost
-      hipLaunchKernelGGL((walk_subset_kernel<T>), dim3((nitems + block - 1) / block),
-                         dim3(block), 0, s->stream, gd, soa_of(s), ld, s->list_valid ? 1 : 0,
-                         subset, nitems, max_active_bin, hmax_slot(s), ctr);
+    constexpr int ppb = block / kWalkLpi;
+    if (subset) {  // density reruns of the ghost: list walks, then the queued searches
+      (void)hipMemsetAsync(search_slot(s), 0, sizeof(unsigned int), s->stream);
+      hipLaunchKernelGGL((walk_subset_kernel<T>), dim3((nitems + ppb - 1) / ppb), dim3(block),
+                         0, s->stream, gd, soa_of(s), ld, s->list_valid ? 1 : 0, subset, nitems,
+                         max_active_bin, hmax_slot(s), ctr, s->ghost_search.as<int>(),
+                         search_slot(s));
+      // one wave per queued particle; the queue length is read on the device
+      const int sblocks = std::max(1, std::min(2048, (nitems + 3) / 4));
+      hipLaunchKernelGGL((overflow_kernel<LOOP_DENSITY, T>), dim3(sblocks), dim3(block), 0,
+                         s->stream, gd, soa_of(s), ld, s->ghost_search.as<const int>(),
+                         search_slot(s), max_active_bin, a2H, hmax_slot(s), ctr, ncount);
       return;
     }
-    constexpr int ppb = block / kWalkLpi;
     hipLaunchKernelGGL((walk_kernel<LOOP, T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
                        s->stream, gd, soa_of(s), ld, nitems, max_active_bin, a2H, hmax_slot(s),
                        ctr, ncount);
     hipLaunchKernelGGL((overflow_kernel<LOOP, T>), dim3(64), dim3(block), 0, s->stream, gd,
-                       soa_of(s), ld, max_active_bin, a2H, hmax_slot(s), ctr, ncount);
+                       soa_of(s), ld, ld.ovf, ld.ovf_n, max_active_bin, a2H, hmax_slot(s), ctr,
+                       ncount);
     return;
   }
   if ((v == 4 || v == 5) && !subset) {
@@ -658,7 +719,7 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const int
     // the density loop builds the step's lists; gradient and force reuse them
     // while no particle's H has outgrown its list reach (ghost: stale flag)
     if (LOOP == LOOP_DENSITY || !s->list_valid || s->list_mab != P->max_active_bin)
-      SWH_TRY(build_lists(s, P, count));
+      SWH_TRY(build_lists(s, P, count, s->tuning.list_skin));
     if (s->tuning.diag_mode != 0 && s->tuning.diag_mode != 4) return SWH_OK;
   }
   const GridDev gd = grid_dev(s);
@@ -746,6 +807,7 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   SWH_TRY(s->ghost_right.reserve(n * sizeof(float)));
   SWH_TRY(s->ghost_list.reserve(n * sizeof(int)));
   SWH_TRY(s->ghost_list2.reserve(n * sizeof(int)));
+  SWH_TRY(s->ghost_search.reserve(n * sizeof(int)));
   int* cnt = s->counters.as<int>() + 4;  // slots 4,5: list counts
   SWH_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(int), st));
   const int block = 256;
@@ -768,11 +830,12 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   gp.fac_B = P->a_factor_Balsara_eps;
   int* list = s->ghost_list.as<int>();
   int* list2 = s->ghost_list2.as<int>();
-  const float* lreach =
-      (loop_variant_of(s) == 7 && s->list_valid) ? s->nbr_reach.as<const float>() : nullptr;
+  const bool lists = loop_variant_of(s) == 7;
+  const int n_active = count;
   SWH_HIP(hipMemsetAsync(stale_slot(s), 0, sizeof(unsigned int), st));
   int it = 0;
   for (; count > 0 && it < P->max_smoothing_iterations; it++) {
+    const float* lreach = (lists && s->list_valid) ? s->nbr_reach.as<const float>() : nullptr;
     SWH_HIP(hipMemsetAsync(cnt + 1, 0, sizeof(int), st));
     const int g = (count + block - 1) / block;
     if (s->ctx->precision == SWH_PRECISION_F64)
@@ -787,6 +850,14 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
     SWH_HIP(hipMemcpyAsync(&count, cnt + 1, sizeof(int), hipMemcpyDeviceToHost, st));
     SWH_HIP(hipStreamSynchronize(st));
     std::swap(list, list2);
+    if (count > 0 && lists && (int64_t)count * 8 >= (int64_t)n_active) {
+      // A large rerun (the first iteration after a drift redoes nearly every
+      // particle): rebuild the lists for the new h, with a 1% skin so the
+      // few later iterations' changes stay within reach and the gradient /
+      // force loops keep them, then walk.
+      SWH_TRY(build_lists(s, P, false, std::max(s->tuning.list_skin, kGhostListSkin)));
+      SWH_HIP(hipMemsetAsync(stale_slot(s), 0, sizeof(unsigned int), st));
+    }
     if (count > 0) SWH_TRY(launch_loop<LOOP_DENSITY>(s, P, list, count, false));
   }
   {
@@ -794,7 +865,7 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
     unsigned int c[18];
     SWH_HIP(hipMemcpyAsync(c, s->counters.ptr, sizeof(c), hipMemcpyDeviceToHost, st));
     SWH_HIP(hipStreamSynchronize(st));
-    if (lreach && c[17]) s->list_valid = false;  // gradient / force rebuild the lists
+    if (lists && s->list_valid && c[17]) s->list_valid = false;  // gradient / force rebuild
     float hmax;
     std::memcpy(&hmax, &c[2], sizeof(hmax));
     // a kernel reach of half the periodic box or more would need more than

@@ -197,12 +197,13 @@ struct swh_space {
   swh::DevBuf posf;  // float4: position relative to its grid cell's corner, h
   bool list_valid = false;
   int32_t list_mab = 0, list_K = 0;
+  float list_skin_cur = 0.f;  // skin of the lists in use (tuning, or the ghost's rebuild)
   int64_t list_entries = 0;   // last counted build: total entries
   int32_t list_overflow = 0;  // last counted build: particles over capacity
   // scratch
   swh::DevBuf keys, keys2, idx, idx2, sort_tmp, scan_tmp, counters;
   swh::DevBuf tmp_soa;     // staging for permutation gathers
-  swh::DevBuf ghost_left, ghost_right, ghost_list, ghost_list2, ghost_flag;
+  swh::DevBuf ghost_left, ghost_right, ghost_list, ghost_list2, ghost_search;
   swh::HostBuf hstage;
 };
 

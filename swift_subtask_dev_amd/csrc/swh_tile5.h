@@ -73,6 +73,47 @@ __device__ __forceinline__ int wave_max_i(int v) {
   return v;
 }
 
+// Stream compaction with one atomic per workgroup (blockDim.x <= 1024): the
+// threads with `pred` get consecutive slots, in thread order. Every thread of
+// the block must call it (it synchronises the block). Same-address atomics
+// serialise in L2, so per-wave appends of millions of items cost ~0.3 ms.
+template <typename C>
+__device__ __forceinline__ int block_append(bool pred, C* counter) {
+  __shared__ int wcnt[16];
+  __shared__ int wbase[16];
+  const int lane = (int)(threadIdx.x & 63), w = (int)(threadIdx.x >> 6);
+  const int nw = (int)((blockDim.x + 63) >> 6);
+  const unsigned long long m = __ballot(pred);
+  if (lane == 0) wcnt[w] = (int)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+    for (int k = 0; k < nw; k++) {
+      wbase[k] = tot;
+      tot += wcnt[k];
+    }
+    const int b = tot ? (int)atomicAdd(counter, (C)tot) : 0;
+    for (int k = 0; k < nw; k++) wbase[k] += b;
+  }
+  __syncthreads();
+  return pred ? wbase[w] + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+
+// Stream compaction with one atomic per wave: the lanes with `pred` get
+// consecutive slots (in lane order) of the list whose length is *counter.
+// Every lane of the wave must call it.
+template <typename C>
+__device__ __forceinline__ int wave_append(bool pred, C* counter) {
+  const unsigned long long m = __ballot(pred);
+  if (m == 0ull) return -1;
+  const int lane = (int)(threadIdx.x & 63);
+  const int leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = (int)atomicAdd(counter, (C)__popcll(m));
+  base = __shfl(base, leader);
+  return pred ? base + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+
 // Combine the LPI partial states of one i-particle (lanes differing in the
 // low log2(LPI) bits): sums add, v_sig / alpha_max take the max, the limiter
 // takes the min.

@@ -297,19 +297,6 @@ struct GhostParams {
   double a2_inv, H, fac_B;
 };
 
-template <typename T>
-__global__ void ghost_init_kernel(SoA a, int64_t n, int max_active_bin, float h_max,
-                                  float* left, float* right, int* list, int* count) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool act = i < n && active_part(a, i, max_active_bin);
-  if (act) {
-    left[i] = 0.f;
-    right[i] = h_max;
-  }
-  const int slot = block_append(act, count);  // one atomic per block, sorted order kept
-  if (act) list[slot] = (int)i;
-}
-
 // One particle of the ghost: redo (h updated, queued for a rerun), or
 // converged (final fields written); hf_out = its h, stale = H outgrew its
 // list reach.
@@ -456,25 +443,41 @@ __device__ __forceinline__ void ghost_part(SoA& a, int i, float* left, float* ri
   a.grad[i] = g;
 }
 
+// One pass of the ghost over `list` (null: the first pass, over every active
+// particle, whose bisection bounds start at [0, h_max]).
 template <typename T>
-__global__ void ghost_kernel(SoA a, const int* __restrict__ list, int count,
-                             int* __restrict__ redo, int* __restrict__ nredo, float* left,
-                             float* right, GhostParams gp, unsigned int* hmax_bits,
-                             const float* __restrict__ list_reach, unsigned int* list_stale) {
+__global__ __launch_bounds__(1024) void ghost_kernel(
+    SoA a, const int* __restrict__ list, int count, int max_active_bin, int* __restrict__ redo,
+    int* __restrict__ nredo, float* left, float* right, GhostParams gp, unsigned int* hmax_bits,
+    const float* __restrict__ list_reach, unsigned int* list_stale) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   bool rd = false, stale = false;
   float hf = 0.f;
-  const int i = t < count ? list[t] : -1;
+  int i = -1;
+  if (t < count) {
+    if (list) {
+      i = list[t];
+    } else if (active_part(a, t, max_active_bin)) {
+      i = t;
+      left[i] = 0.f;
+      right[i] = gp.h_max;
+    }
+  }
   if (i >= 0) ghost_part<T>(a, i, left, right, gp, list_reach, rd, hf, stale);
-  // one append per block for the rerun list; one max, one stale flag per wave
+  // one append per block for the rerun list
   const int slot = block_append(rd, nredo);
   if (rd) redo[slot] = i;
+  // h max and the stale flag: an atomic only when it changes something (all
+  // blocks hitting one address serialise at ~10 ns per atomic)
   float m = hf;
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   const bool any_stale = __any(stale);
   if ((threadIdx.x & 63) == 0) {
-    if (m > 0.f) atomicMax(hmax_bits, __float_as_uint(m));
-    if (any_stale) atomicOr(list_stale, 1u);
+    if (m > 0.f && __float_as_uint(m) > __hip_atomic_load(hmax_bits, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(hmax_bits, __float_as_uint(m));
+    if (any_stale && __hip_atomic_load(list_stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+      atomicOr(list_stale, 1u);
   }
 }
 
@@ -808,17 +811,10 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   SWH_TRY(s->ghost_list.reserve(n * sizeof(int)));
   SWH_TRY(s->ghost_list2.reserve(n * sizeof(int)));
   SWH_TRY(s->ghost_search.reserve(n * sizeof(int)));
-  int* cnt = s->counters.as<int>() + 4;  // slots 4,5: list counts
-  SWH_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(int), st));
-  const int block = 256;
-  const int nblk = (int)((n + block - 1) / block);
-  hipLaunchKernelGGL(ghost_init_kernel<double>, dim3(nblk), dim3(block), 0, st, soa_of(s), n,
-                     P->max_active_bin, P->h_max, s->ghost_left.as<float>(),
-                     s->ghost_right.as<float>(), s->ghost_list.as<int>(), cnt);
-  SWH_HIP(hipGetLastError());
-  int count = 0;
-  SWH_HIP(hipMemcpyAsync(&count, cnt, sizeof(int), hipMemcpyDeviceToHost, st));
-  SWH_HIP(hipStreamSynchronize(st));
+  int* cnt = s->counters.as<int>() + 4;  // slot 5: rerun count
+  const int block = 1024;
+  // the first pass runs over every particle (inactive ones return at once)
+  int count = (int)n;
   GhostParams gp;
   gp.h_max = P->h_max;
   gp.h_min = P->h_min;
@@ -828,10 +824,10 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   gp.a2_inv = P->a2_inv;
   gp.H = P->H;
   gp.fac_B = P->a_factor_Balsara_eps;
-  int* list = s->ghost_list.as<int>();
-  int* list2 = s->ghost_list2.as<int>();
+  int* list = nullptr;  // first pass: every active particle
+  int* list2 = s->ghost_list.as<int>();
+  int* spare = s->ghost_list2.as<int>();
   const bool lists = loop_variant_of(s) == 7;
-  const int n_active = count;
   SWH_HIP(hipMemsetAsync(stale_slot(s), 0, sizeof(unsigned int), st));
   int it = 0;
   for (; count > 0 && it < P->max_smoothing_iterations; it++) {
@@ -840,17 +836,20 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
     const int g = (count + block - 1) / block;
     if (s->ctx->precision == SWH_PRECISION_F64)
       hipLaunchKernelGGL(ghost_kernel<double>, dim3(g), dim3(block), 0, st, soa_of(s), list,
-                         count, list2, cnt + 1, s->ghost_left.as<float>(),
+                         count, P->max_active_bin, list2, cnt + 1, s->ghost_left.as<float>(),
                          s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s));
     else
       hipLaunchKernelGGL(ghost_kernel<float>, dim3(g), dim3(block), 0, st, soa_of(s), list,
-                         count, list2, cnt + 1, s->ghost_left.as<float>(),
+                         count, P->max_active_bin, list2, cnt + 1, s->ghost_left.as<float>(),
                          s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s));
     SWH_HIP(hipGetLastError());
     SWH_HIP(hipMemcpyAsync(&count, cnt + 1, sizeof(int), hipMemcpyDeviceToHost, st));
     SWH_HIP(hipStreamSynchronize(st));
-    std::swap(list, list2);
-    if (count > 0 && lists && (int64_t)count * 8 >= (int64_t)n_active) {
+    // the new rerun list becomes the input; the old input buffer is reused
+    int* done = list ? list : spare;
+    list = list2;
+    list2 = done;
+    if (count > 0 && lists && (int64_t)count * 8 >= n) {
       // A large rerun (the first iteration after a drift redoes nearly every
       // particle): rebuild the lists for the new h, with a 1% skin so the
       // few later iterations' changes stay within reach and the gradient /

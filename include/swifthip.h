@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SWH_ABI_VERSION 4
+#define SWH_ABI_VERSION 5
 
 #if defined(__GNUC__)
 #define SWH_API __attribute__((visibility("default")))
@@ -142,6 +142,7 @@ typedef struct swh_grav_params {
   int32_t use_gadget_tolerance;
   int32_t use_tree_below_softening;
   int32_t consider_truncation_in_MAC;
+  double r_cut_max;  /* e->mesh->r_cut_max: the tree walk skips pairs beyond it */
 } swh_grav_params;
 
 /* A cell's multipole expansion about its centre of mass, order 4 (SWIFT's
@@ -401,6 +402,43 @@ SWH_API swh_status swh_grav_pp_batch(swh_gspace *g, const swh_grav_params *G,
                                      int64_t *n_interactions, int64_t *n_m2p);
 SWH_API swh_status swh_gspace_download(swh_gspace *g, void *gparts, const swh_gpart_layout *L,
                                int on_device);
+
+/* Tree gravity (SURVEY 8 a15 recursion, 8f row 3 M2L): the cell tree of the
+ * uploaded gparts, cells[c] = {start, count} ranges nested as SWIFT's
+ * (a split cell's progeny partition its range). swh_grav_tree then runs a
+ * step's gravity tasks on it:
+ *   runner_doself_recursive_grav on every cell of self_cells and
+ *   runner_dopair_recursive_grav on every pair of pair_cells (2 per pair)
+ *   (src/runner_doiact_grav.c:2208-2431: the r_cut_max skip, P-P of cells of
+ *   <= 1 particle (runner_dopair_grav_pp_no_cache), M-M when
+ *   gravity_M2L_accept_symmetric passes, leaf-leaf P-P with M2P
+ *   (runner_dopair_grav_pp, allow_mpole), else split the larger cell),
+ * then the down pass (runner_do_grav_down, 65-164: L2L from each cell's
+ * parent, L2P at the leaves). Multipoles of every cell come from P2M over the
+ * cell's particles (the reference's M2M gives the same moments up to
+ * rounding). The walk runs on the host over the downloaded multipoles; the
+ * P2P, M2P, M2L, L2L and L2P work runs on the device. Results accumulate
+ * like swh_grav_pp_batch's (swh_gspace_download adds them). */
+typedef struct swh_gcell {
+  int32_t start, count; /* gpart range */
+  int32_t split;        /* 1: progeny[] partition the range */
+  int32_t progeny[8];   /* child cell indices (-1: none) */
+} swh_gcell;
+typedef struct swh_grav_tree_stats {
+  int64_t n_pp;         /* P2P pair interactions */
+  int64_t n_m2p;        /* M2P evaluations */
+  int64_t n_m2l;        /* M2L applications (a symmetric M-M counts 2) */
+  int64_t n_pp_tasks;   /* leaf <- cell P-P entries of the walk */
+  int64_t n_skipped;    /* cell pairs beyond r_cut_max */
+} swh_grav_tree_stats;
+SWH_API swh_status swh_gspace_set_tree(swh_gspace *g, const swh_gcell *cells, int32_t ncells);
+SWH_API swh_status swh_grav_tree(swh_gspace *g, const swh_grav_params *G,
+                                 const int32_t *self_cells, int32_t nself,
+                                 const int32_t *pair_cells, int32_t npair,
+                                 swh_grav_tree_stats *stats);
+/* Field tensors of the last swh_grav_tree (35 floats per cell, struct
+ * grav_tensor's F order = swh_multipole::M's), after the down pass. */
+SWH_API swh_status swh_gspace_field_tensors(swh_gspace *g, float *out);
 SWH_API swh_status swh_gspace_sync(swh_gspace *g);
 
 #ifdef __cplusplus

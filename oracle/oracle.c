@@ -2164,6 +2164,7 @@ struct oracle_grav_params {
   int use_gadget_tolerance;
   int use_tree_below_softening;
   int consider_truncation_in_MAC;
+  double r_cut_max;    /* e->mesh->r_cut_max */
 };
 
 /* ------------------------------------------------------------------------ */
@@ -2671,4 +2672,342 @@ API long long PFX(grav_pair_pp)(struct gpart *gi, int ni, struct gpart *gj, int 
   long long n = grav_pp(gi, ni, gj, nj, 0, truncated, zero, zero, G, NULL, NULL);
   if (symmetric) n += grav_pp(gj, nj, gi, ni, 0, truncated, zero, zero, G, NULL, NULL);
   return n;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Tree gravity: runner_doself_recursive_grav / runner_dopair_recursive_grav */
+/* (src/runner_doiact_grav.c:2208-2431) over a cell tree, M2L                */
+/* (gravity_M2L_nonsym / _symmetric + gravity_M2L_apply, multipole.h:        */
+/* 1600-2095, with gravity_M2L_accept_symmetric, multipole_accept.h:78-199), */
+/* and runner_do_grav_down (runner_doiact_grav.c:65-164: gravity_L2L,        */
+/* gravity_L2P). Cell multipoles: gravity_P2M over each cell's gparts.       */
+/* P-P entries run through grav_pp_leaves (above).                           */
+/* ------------------------------------------------------------------------ */
+struct oracle_gcell {
+  int start, count, split, progeny[8];
+};
+
+struct otree_walk {
+  const struct oracle_gcell *cells;
+  const struct oracle_multipole *mp;
+  const char *act;
+  const struct oracle_grav_params *G;
+  int *pp;      /* entries of 4 ints: i-cell, j-cell, truncated, allow_mpole */
+  long long npp, cap_pp;
+  int *mm;      /* entries of 3 ints: target, source, symmetric */
+  long long nmm, cap_mm;
+  long long skipped;
+};
+
+static void otw_push_pp(struct otree_walk *w, int i, int j, int tr, int allow) {
+  if (w->npp == w->cap_pp) {
+    w->cap_pp = w->cap_pp ? 2 * w->cap_pp : 1024;
+    w->pp = (int *)realloc(w->pp, sizeof(int) * 4 * (size_t)w->cap_pp);
+  }
+  int *e = w->pp + 4 * w->npp++;
+  e[0] = i; e[1] = j; e[2] = tr; e[3] = allow;
+}
+
+static void otw_push_mm(struct otree_walk *w, int t, int s, int sym) {
+  if (w->nmm == w->cap_mm) {
+    w->cap_mm = w->cap_mm ? 2 * w->cap_mm : 1024;
+    w->mm = (int *)realloc(w->mm, sizeof(int) * 3 * (size_t)w->cap_mm);
+  }
+  int *e = w->mm + 3 * w->nmm++;
+  e[0] = t; e[1] = s; e[2] = sym;
+}
+
+/* gravity_M2L_accept (multipole_accept.h:78-176), float, p = 2 */
+static int m2l_accept_o(const struct oracle_grav_params *G, const struct oracle_multipole *A,
+                        const struct oracle_multipole *B, float r2) {
+  const float rho_A = (float)A->r_max, rho_B = (float)B->r_max;
+  const float rho_max = rho_A > rho_B ? rho_A : rho_B;
+  const float max_softening =
+      A->max_softening > B->max_softening ? A->max_softening : B->max_softening;
+  /* sum_n binomial(2, n) power_B[n] integer_powf(rho_A, 2 - n) */
+  const int binom[3] = {1, 2, 1};
+  const float rpow[3] = {rho_A * rho_A, rho_A, 1.f};
+  float E_BA_term = 0.f;
+  for (int n = 0; n <= 2; n++) E_BA_term += (float)binom[n] * B->power[n] * rpow[n];
+  E_BA_term *= 8.f;
+  if (rho_A + rho_B > 0.f) {
+    E_BA_term *= rho_max;
+    E_BA_term /= (rho_A + rho_B);
+  }
+  const float r_to_p = r2;
+  float f_MAC_inv = r2;
+  if (G->periodic && G->consider_truncation_in_MAC) {
+    const float H = max_softening;
+    if (r2 < (25.f / 81.f) * H * H)
+      f_MAC_inv = (25.f / 81.f) * H * H;
+    else if (G->r_s_inv * G->r_s_inv * r2 > (25.f / 9.f))
+      f_MAC_inv = (9.f / 25.f) * G->r_s_inv * G->r_s_inv * r2 * r2;
+  }
+  const float min_a_grav = A->min_old_a_grav_norm;
+  const float M_max = A->M[0] > B->M[0] ? A->M[0] : B->M[0];
+  const float eps = G->adaptive_tolerance;
+  const float theta_crit2 = G->theta_crit * G->theta_crit;
+  const float rho_sum = rho_A + rho_B;
+  const int cond_2 = G->use_tree_below_softening || max_softening * max_softening < r2;
+  if (G->use_advanced_MAC && G->use_gadget_tolerance) {
+    const float q = rho_max / sqrtf(r2);
+    const float ratio = q * q * q;
+    return (M_max * ratio < eps * min_a_grav * f_MAC_inv) && cond_2;
+  } else if (G->use_advanced_MAC) {
+    const int cond_1 = rho_sum * rho_sum < r2;
+    const int cond_3 = E_BA_term < eps * min_a_grav * r_to_p * f_MAC_inv;
+    return cond_1 && cond_2 && cond_3;
+  }
+  return (rho_sum * rho_sum < theta_crit2 * r2) && cond_2;
+}
+
+static void otw_self(struct otree_walk *w, int c);
+static void otw_pair(struct otree_walk *w, int ci, int cj);
+
+static void otw_no_cache(struct otree_walk *w, int ci, int cj) {
+  if (!w->act[ci]) return;
+  if (w->cells[ci].count == 0 || w->cells[cj].count == 0) return;
+  if (w->cells[ci].split) {
+    for (int k = 0; k < 8; k++)
+      if (w->cells[ci].progeny[k] >= 0) otw_no_cache(w, w->cells[ci].progeny[k], cj);
+  } else {
+    otw_push_pp(w, ci, cj, w->G->periodic ? 1 : 0, 0);
+  }
+}
+
+static void otw_self(struct otree_walk *w, int c) {
+  if (!w->act[c]) return;
+  const struct oracle_gcell *C = &w->cells[c];
+  if (C->split) {
+    for (int j = 0; j < 8; j++) {
+      if (C->progeny[j] < 0) continue;
+      otw_self(w, C->progeny[j]);
+      for (int k = j + 1; k < 8; k++)
+        if (C->progeny[k] >= 0) otw_pair(w, C->progeny[j], C->progeny[k]);
+    }
+  } else {
+    otw_push_pp(w, c, c, w->G->periodic && (2. * w->mp[c].r_max > w->G->r_cut_min), 0);
+  }
+}
+
+static void otw_pair(struct otree_walk *w, int ci, int cj) {
+  const struct oracle_grav_params *G = w->G;
+  if (!(w->act[ci] || w->act[cj])) return;
+  const struct oracle_multipole *A = &w->mp[ci], *B = &w->mp[cj];
+  double d[3];
+  for (int k = 0; k < 3; k++) {
+    d[k] = A->CoM[k] - B->CoM[k];
+    if (G->periodic) d[k] = nearest(d[k], (double)G->dim[k]);
+  }
+  const double r2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+  const double r_lr_check = sqrt(r2) - (A->r_max + B->r_max);
+  if (G->periodic && r_lr_check > G->r_cut_max) {
+    w->skipped++;
+    return;
+  }
+  const struct oracle_gcell *Ci = &w->cells[ci], *Cj = &w->cells[cj];
+  if (Ci->count <= 1 || Cj->count <= 1) {
+    otw_no_cache(w, ci, cj);
+    otw_no_cache(w, cj, ci);
+  } else if (m2l_accept_o(G, A, B, (float)r2) && m2l_accept_o(G, B, A, (float)r2)) {
+    /* runner_dopair_grav_mm: symmetric when both are active */
+    const int di = w->act[ci], dj = w->act[cj];
+    if (di && dj) {
+      otw_push_mm(w, ci, cj, 1);
+      otw_push_mm(w, cj, ci, 1);
+    } else if (di) {
+      otw_push_mm(w, ci, cj, 0);
+    } else if (dj) {
+      otw_push_mm(w, cj, ci, 0);
+    }
+  } else if (!Ci->split && !Cj->split) {
+    /* runner_dopair_grav_pp(ci, cj, 1, 1) */
+    int tr = 0;
+    if (G->periodic) {
+      double dd[3];
+      for (int k = 0; k < 3; k++) {
+        dd[k] = (float)B->CoM[k] - (float)A->CoM[k];
+        dd[k] = nearest_r((real)dd[k], (real)G->dim[k]);
+      }
+      const double rr2 = dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2];
+      tr = (sqrt(rr2) + (float)A->r_max + (float)B->r_max) > G->r_cut_min;
+    }
+    if (w->act[ci]) otw_push_pp(w, ci, cj, tr, 1);
+    if (w->act[cj]) otw_push_pp(w, cj, ci, tr, 1);
+  } else if (A->r_max > B->r_max) {
+    if (Ci->split) {
+      for (int k = 0; k < 8; k++)
+        if (Ci->progeny[k] >= 0) otw_pair(w, Ci->progeny[k], cj);
+    } else {
+      for (int k = 0; k < 8; k++)
+        if (Cj->progeny[k] >= 0) otw_pair(w, ci, Cj->progeny[k]);
+    }
+  } else {
+    if (Cj->split) {
+      for (int k = 0; k < 8; k++)
+        if (Cj->progeny[k] >= 0) otw_pair(w, ci, Cj->progeny[k]);
+    } else {
+      for (int k = 0; k < 8; k++)
+        if (Ci->progeny[k] >= 0) otw_pair(w, Ci->progeny[k], cj);
+    }
+  }
+}
+
+static int mp_idx(int a, int b, int c) {
+  for (int t = 0; t < 35; t++)
+    if (mp_a[t] == a && mp_b[t] == b && mp_c[t] == c) return t;
+  return -1;
+}
+
+static double xpow_o(const double dx[3], int t) {
+  const int a = mp_a[t], b = mp_b[t], c = mp_c[t];
+  return pow(dx[0], a) * pow(dx[1], b) * pow(dx[2], c) / (fact_d(a) * fact_d(b) * fact_d(c));
+}
+
+/* Field tensors of the whole walk: F (35 per cell, real) after the down
+ * pass; stats = {n_pp, n_m2p, n_m2l, n_pp_tasks, n_skipped}. The gparts'
+ * a_grav / potential receive P2P + M2P (grav_pp_leaves) and L2P. */
+API void PFX(grav_tree)(struct gpart *g, int n, const struct oracle_gcell *cells, int ncells,
+                        const int *self_cells, int nself, const int *pair_cells, int npair,
+                        const struct oracle_grav_params *G, long long *stats, float *ftens) {
+  (void)n;
+  struct oracle_multipole *mp =
+      (struct oracle_multipole *)malloc(sizeof(struct oracle_multipole) * (size_t)ncells);
+  char *act = (char *)calloc((size_t)ncells, 1);
+  int *parent = (int *)malloc(sizeof(int) * (size_t)ncells);
+  for (int c = 0; c < ncells; c++) parent[c] = -1;
+  for (int c = 0; c < ncells; c++) {
+    PFX(grav_p2m)(g + cells[c].start, cells[c].count, &mp[c]);
+    for (int k = 0; k < cells[c].count; k++) {
+      const struct gpart *gp = &g[cells[c].start + k];
+      if (gp->time_bin != time_bin_inhibited && gp->time_bin <= G->max_active_bin) act[c] = 1;
+    }
+    if (cells[c].split)
+      for (int k = 0; k < 8; k++)
+        if (cells[c].progeny[k] >= 0) parent[cells[c].progeny[k]] = c;
+  }
+  struct otree_walk w;
+  memset(&w, 0, sizeof(w));
+  w.cells = cells;
+  w.mp = mp;
+  w.act = act;
+  w.G = G;
+  for (int k = 0; k < nself; k++) otw_self(&w, self_cells[k]);
+  for (int k = 0; k < npair; k++) otw_pair(&w, pair_cells[2 * k], pair_cells[2 * k + 1]);
+  /* P-P: CSR over i-cells in walk order per cell */
+  int *leaves = (int *)malloc(sizeof(int) * 2 * (size_t)ncells);
+  int *off = (int *)calloc((size_t)ncells + 1, sizeof(int));
+  int *pairs = (int *)malloc(sizeof(int) * 3 * (size_t)(w.npp > 0 ? w.npp : 1));
+  for (int c = 0; c < ncells; c++) {
+    leaves[2 * c] = cells[c].start;
+    leaves[2 * c + 1] = cells[c].count;
+  }
+  for (long long q = 0; q < w.npp; q++) off[w.pp[4 * q] + 1]++;
+  for (int c = 0; c < ncells; c++) off[c + 1] += off[c];
+  int *fill = (int *)malloc(sizeof(int) * (size_t)(ncells > 0 ? ncells : 1));
+  memcpy(fill, off, sizeof(int) * (size_t)ncells);
+  for (long long q = 0; q < w.npp; q++) {
+    const int i = w.pp[4 * q];
+    int *e = pairs + 3 * fill[i]++;
+    e[0] = w.pp[4 * q + 1];
+    e[1] = w.pp[4 * q + 2];
+    e[2] = w.pp[4 * q + 3];
+  }
+  long long n_m2p = 0;
+  const long long n_pp = PFX(grav_pp_leaves)(g, leaves, ncells, off, pairs, G, mp, &n_m2p);
+  /* M2L (field tensor at the target's CoM) */
+  real *F = (real *)calloc((size_t)ncells * 35, sizeof(real));
+  for (long long q = 0; q < w.nmm; q++) {
+    const int t = w.mm[3 * q], s = w.mm[3 * q + 1], sym = w.mm[3 * q + 2];
+    const struct oracle_multipole *Bm = &mp[t], *Am = &mp[s];
+    real dx[3];
+    for (int k = 0; k < 3; k++) {
+      dx[k] = (real)(Bm->CoM[k] - Am->CoM[k]);
+      if (G->periodic) dx[k] = nearest_r(dx[k], (real)G->dim[k]);
+    }
+    const real r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+    const real r_inv = (real)(1. / SQRT(r2));
+    const float eps_f = sym ? (Am->max_softening > Bm->max_softening ? Am->max_softening
+                                                                     : Bm->max_softening)
+                            : Am->max_softening;
+    struct m2p_derivs d;
+    m2p_radial(dx[0], dx[1], dx[2], r2, r_inv, (real)eps_f, G->periodic, (real)G->r_s_inv, &d);
+    real *Ft = F + 35 * (size_t)t;
+    for (int kk = 0; kk < 35; kk++) {
+      const int ok = mp_a[kk] + mp_b[kk] + mp_c[kk];
+      for (int nn = 0; nn < 35; nn++) {
+        if (nn >= 1 && nn <= 3) continue; /* dipole about the CoM */
+        const int on = mp_a[nn] + mp_b[nn] + mp_c[nn];
+        if (ok + on > 4) continue;
+        Ft[kk] += (real)Am->M[nn] *
+                  m2p_D(&d, mp_a[kk] + mp_a[nn], mp_b[kk] + mp_b[nn], mp_c[kk] + mp_c[nn]);
+      }
+    }
+  }
+  /* down pass: parents before children (depth order), then L2P */
+  int *depth = (int *)malloc(sizeof(int) * (size_t)ncells);
+  int maxd = 0;
+  for (int c = 0; c < ncells; c++) {
+    int dd = 0, x = c;
+    while (parent[x] >= 0) { x = parent[x]; dd++; }
+    depth[c] = dd;
+    if (dd > maxd) maxd = dd;
+  }
+  for (int dd = 1; dd <= maxd; dd++) {
+    for (int c = 0; c < ncells; c++) {
+      if (depth[c] != dd) continue;
+      const int p = parent[c];
+      const real *Fp = F + 35 * (size_t)p;
+      int any = 0;
+      for (int t = 0; t < 35; t++) any |= Fp[t] != 0;
+      if (!any) continue;
+      const double dx[3] = {mp[c].CoM[0] - mp[p].CoM[0], mp[c].CoM[1] - mp[p].CoM[1],
+                            mp[c].CoM[2] - mp[p].CoM[2]};
+      real *Fc = F + 35 * (size_t)c;
+      for (int kk = 0; kk < 35; kk++)
+        for (int nn = 0; nn < 35; nn++) {
+          const int m = mp_idx(mp_a[kk] + mp_a[nn], mp_b[kk] + mp_b[nn], mp_c[kk] + mp_c[nn]);
+          if (m < 0) continue;
+          Fc[kk] += (real)xpow_o(dx, nn) * Fp[m];
+        }
+    }
+  }
+  for (int c = 0; c < ncells; c++) {
+    if (cells[c].split) continue;
+    const real *Fc = F + 35 * (size_t)c;
+    int any = 0;
+    for (int t = 0; t < 35; t++) any |= Fc[t] != 0;
+    if (!any) continue;
+    for (int k = 0; k < cells[c].count; k++) {
+      struct gpart *gp = &g[cells[c].start + k];
+      if (gp->time_bin == time_bin_inhibited || gp->time_bin > G->max_active_bin) continue;
+      const double dx[3] = {gp->x[0] - mp[c].CoM[0], gp->x[1] - mp[c].CoM[1],
+                            gp->x[2] - mp[c].CoM[2]};
+      double a[3] = {0., 0., 0.}, pot = 0.;
+      for (int t = 0; t < 35; t++) {
+        const double X = xpow_o(dx, t);
+        pot -= X * (double)Fc[t];
+        if (mp_a[t] + mp_b[t] + mp_c[t] <= 3) {
+          a[0] += X * (double)Fc[mp_idx(mp_a[t] + 1, mp_b[t], mp_c[t])];
+          a[1] += X * (double)Fc[mp_idx(mp_a[t], mp_b[t] + 1, mp_c[t])];
+          a[2] += X * (double)Fc[mp_idx(mp_a[t], mp_b[t], mp_c[t] + 1)];
+        }
+      }
+      gp->a_grav[0] += (float)a[0];
+      gp->a_grav[1] += (float)a[1];
+      gp->a_grav[2] += (float)a[2];
+      gp->potential += (float)pot;
+    }
+  }
+  if (ftens)
+    for (size_t k = 0; k < (size_t)ncells * 35; k++) ftens[k] = (float)F[k];
+  if (stats) {
+    stats[0] = n_pp;
+    stats[1] = n_m2p;
+    stats[2] = w.nmm;
+    stats[3] = w.npp;
+    stats[4] = w.skipped;
+  }
+  free(F); free(depth); free(fill); free(pairs); free(off); free(leaves);
+  free(w.pp); free(w.mm); free(parent); free(act); free(mp);
 }

@@ -176,7 +176,19 @@ class GravParams(C.Structure):
                 ("theta_crit", C.c_float), ("adaptive_tolerance", C.c_float),
                 ("use_advanced_MAC", C.c_int32), ("use_gadget_tolerance", C.c_int32),
                 ("use_tree_below_softening", C.c_int32),
-                ("consider_truncation_in_MAC", C.c_int32)]
+                ("consider_truncation_in_MAC", C.c_int32), ("r_cut_max", C.c_double)]
+
+
+class GCell(C.Structure):
+    """swh_gcell: a tree cell's gpart range and progeny."""
+
+    _fields_ = [("start", C.c_int32), ("count", C.c_int32), ("split", C.c_int32),
+                ("progeny", C.c_int32 * 8)]
+
+
+class GravTreeStats(C.Structure):
+    _fields_ = [("n_pp", C.c_int64), ("n_m2p", C.c_int64), ("n_m2l", C.c_int64),
+                ("n_pp_tasks", C.c_int64), ("n_skipped", C.c_int64)]
 
 
 MPOLE_TERMS = 35

@@ -270,6 +270,9 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel(
   const int li = xcd_block_id();
   const swh_leaf L = leaves[li];
   const int p0 = pair_off[li], p1 = pair_off[li + 1];
+  // no sources: leave acc alone (a tree's inner cells overlap their leaves,
+  // whose blocks update the same particles)
+  if (p0 == p1) return;
   unsigned long long nint = 0;
   for (int ibase = 0; ibase < L.count; ibase += kGravBlock * kIPer) {
     int gi[kIPer], self_local[kIPer];
@@ -372,6 +375,9 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
   const int li = xcd_block_id();
   const swh_leaf L = leaves[li];
   const int p0 = pair_off[li], p1 = pair_off[li + 1];
+  // no sources: leave acc alone (a tree's inner cells overlap their leaves,
+  // whose blocks update the same particles)
+  if (p0 == p1) return;
   unsigned long long nint = 0;
   for (int ibase = 0; ibase < L.count; ibase += kGravBlock * kIPer) {
     int gi[kIPer];
@@ -504,6 +510,9 @@ __global__ __launch_bounds__(kGravBlock) void m2p_kernel(
   }
 }
 
+swh_status launch_pp(swh_gspace* g, const swh_grav_params* G, const MacParams& mac,
+                     unsigned long long* ctr);
+
 static GSoA gsoa_of(swh_gspace* g) {
   GSoA s;
   s.pos = g->pos.as<double4>();
@@ -539,8 +548,10 @@ swh_status swh_gspace_destroy(swh_gspace* g) {
   if (!g) return SWH_OK;
   (void)hipSetDevice(g->ctx->device);
   (void)hipStreamSynchronize(g->stream);
-  DevBuf* bufs[] = {&g->aos, &g->pos, &g->hinv, &g->mass, &g->active, &g->accel,
-                    &g->oagn, &g->mpoles, &g->leaves, &g->pair_off, &g->pairs, &g->counter};
+  DevBuf* bufs[] = {&g->aos,      &g->pos,      &g->hinv,    &g->mass,    &g->active,
+                    &g->accel,    &g->oagn,     &g->mpoles,  &g->leaves,  &g->pair_off,
+                    &g->pairs,    &g->counter,  &g->cell_act, &g->ftens,  &g->m2l_off,
+                    &g->m2l_src,  &g->l2l_list, &g->leaf_ids};
   for (DevBuf* b : bufs) b->release();
   (void)hipStreamDestroy(g->stream);
   delete g;
@@ -662,6 +673,24 @@ swh_status swh_grav_pp_batch(swh_gspace* g, const swh_grav_params* G, int64_t* n
   SWH_TRY(g->counter.reserve(2 * sizeof(unsigned long long)));
   unsigned long long* ctr = want ? g->counter.as<unsigned long long>() : nullptr;
   if (ctr) SWH_HIP(hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned long long), g->stream));
+  SWH_TRY(launch_pp(g, G, mac, ctr));
+  if (want) {
+    unsigned long long h[2] = {0, 0};
+    SWH_HIP(hipMemcpyAsync(h, ctr, sizeof(h), hipMemcpyDeviceToHost, g->stream));
+    SWH_HIP(hipStreamSynchronize(g->stream));
+    if (n_int) *n_int = (int64_t)h[0];
+    if (n_m2p) *n_m2p = (int64_t)h[1];
+  }
+  return SWH_OK;
+}
+
+}  // extern "C"
+
+namespace swh {
+
+// The P2P (+ M2P) launches over the gspace's i-leaf CSR lists.
+swh_status launch_pp(swh_gspace* g, const swh_grav_params* G, const MacParams& mac,
+                     unsigned long long* ctr) {
   const bool f64 = g->ctx->precision == SWH_PRECISION_F64;
   if (f64) {
     // the multipole-free instance keeps the P2P kernel's register budget
@@ -690,15 +719,12 @@ swh_status swh_grav_pp_batch(swh_gspace* g, const swh_grav_params* G, int64_t* n
                          (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, mac, ctr);
     SWH_HIP(hipGetLastError());
   }
-  if (want) {
-    unsigned long long h[2] = {0, 0};
-    SWH_HIP(hipMemcpyAsync(h, ctr, sizeof(h), hipMemcpyDeviceToHost, g->stream));
-    SWH_HIP(hipStreamSynchronize(g->stream));
-    if (n_int) *n_int = (int64_t)h[0];
-    if (n_m2p) *n_m2p = (int64_t)h[1];
-  }
   return SWH_OK;
 }
+
+}  // namespace swh
+
+extern "C" {
 
 swh_status swh_gspace_download(swh_gspace* g, void* gparts, const swh_gpart_layout* GL,
                                int on_device) {
@@ -719,6 +745,489 @@ swh_status swh_gspace_download(swh_gspace* g, void* gparts, const swh_gpart_layo
 swh_status swh_gspace_sync(swh_gspace* g) {
   if (!g) return SWH_ERR_ARG;
   SWH_HIP(hipStreamSynchronize(g->stream));
+  return SWH_OK;
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// Tree gravity: the recursive gravity tasks over a cell tree
+// (runner_doself_recursive_grav / runner_dopair_recursive_grav,
+// src/runner_doiact_grav.c:2208-2431), M2L (runner_dopair_grav_mm*,
+// 1881-2095) and the down pass (runner_do_grav_down, 65-164).
+//
+// The walk is a host-side decision procedure over the cells' multipoles
+// (their CoM, r_max, power and softening): it emits P-P entries (i-leaf <-
+// source cell, truncation and allow_mpole flags, i.e. the leaf-pair CSR the
+// batch P2P/M2P kernels already run) and M-M entries (target <- source,
+// symmetric or not). All arithmetic runs on the device: P2M per cell,
+// P2P + M2P, M2L (thread per target cell over its CSR of sources), L2L level
+// by level from the roots, L2P per leaf.
+// ===========================================================================
+namespace swh {
+
+__global__ void cell_active_kernel(const swh_leaf* __restrict__ cells,
+                                   const int8_t* __restrict__ active, int8_t* __restrict__ out) {
+  const swh_leaf c = cells[blockIdx.x];
+  int any = 0;
+  for (int k = threadIdx.x; k < c.count; k += blockDim.x) any |= active[c.start + k];
+  any = __syncthreads_or(any);
+  if (threadIdx.x == 0) out[blockIdx.x] = any ? 1 : 0;
+}
+
+__device__ __forceinline__ double wrap_box(double d, double L) {
+  return d > 0.5 * L ? d - L : (d < -0.5 * L ? d + L : d);
+}
+
+// M2L into each target cell's field tensor (at its CoM) from its sources.
+template <typename T>
+__global__ __launch_bounds__(64) void m2l_kernel(const swh_multipole* __restrict__ mp,
+                                                 int ncells, const int* __restrict__ off,
+                                                 const int2* __restrict__ src, int periodic,
+                                                 double dimx, double dimy, double dimz,
+                                                 T r_s_inv, double* __restrict__ F) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncells) return;
+  const int q0 = off[c], q1 = off[c + 1];
+  if (q0 == q1) return;
+  const double bx = mp[c].CoM[0], by = mp[c].CoM[1], bz = mp[c].CoM[2];
+  const float bsoft = mp[c].max_softening;
+  T Fl[SWH_MPOLE_TERMS];
+#pragma unroll
+  for (int t = 0; t < SWH_MPOLE_TERMS; t++) Fl[t] = (T)0;
+  for (int q = q0; q < q1; q++) {
+    const int2 e = src[q];
+    const swh_multipole& A = mp[e.x];
+    double dx = bx - A.CoM[0], dy = by - A.CoM[1], dz = bz - A.CoM[2];
+    if (periodic) {
+      dx = wrap_box(dx, dimx);
+      dy = wrap_box(dy, dimy);
+      dz = wrap_box(dz, dimz);
+    }
+    // gravity_M2L_symmetric: max of both softenings; _nonsym: the source's
+    const T eps = (T)(e.y ? fmaxf(A.max_softening, bsoft) : A.max_softening);
+    m2l<T>(A.M, (T)dx, (T)dy, (T)dz, eps, periodic != 0, r_s_inv, Fl);
+  }
+  double* out = F + (size_t)c * SWH_MPOLE_TERMS;
+#pragma unroll
+  for (int t = 0; t < SWH_MPOLE_TERMS; t++) out[t] += (double)Fl[t];
+}
+
+// One depth of the down pass: F_cell += L2L(F_parent, CoM_cell - CoM_parent).
+template <typename T>
+__global__ __launch_bounds__(64) void l2l_kernel(const int2* __restrict__ list, int n,
+                           const swh_multipole* __restrict__ mp, double* __restrict__ F) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int2 e = list[k];
+  const double* Fp = F + (size_t)e.y * SWH_MPOLE_TERMS;
+  T P[SWH_MPOLE_TERMS];
+  bool any = false;
+#pragma unroll
+  for (int t = 0; t < SWH_MPOLE_TERMS; t++) {
+    P[t] = (T)Fp[t];
+    any |= Fp[t] != 0.;
+  }
+  if (!any) return;  // the parent's tensor received nothing (pot.interacted == 0)
+  T X[SWH_MPOLE_TERMS];
+  xpowers<T>((T)(mp[e.x].CoM[0] - mp[e.y].CoM[0]), (T)(mp[e.x].CoM[1] - mp[e.y].CoM[1]),
+             (T)(mp[e.x].CoM[2] - mp[e.y].CoM[2]), X);
+  T Fc[SWH_MPOLE_TERMS];
+#pragma unroll
+  for (int t = 0; t < SWH_MPOLE_TERMS; t++) Fc[t] = (T)0;
+  l2l_k<T, 0>(X, P, Fc);
+  double* out = F + (size_t)e.x * SWH_MPOLE_TERMS;
+#pragma unroll
+  for (int t = 0; t < SWH_MPOLE_TERMS; t++) out[t] += (double)Fc[t];
+}
+
+// L2P at the leaves: every active gpart of the leaf.
+template <typename T>
+__global__ __launch_bounds__(256) void l2p_kernel(const swh_leaf* __restrict__ cells,
+                                                  const int* __restrict__ leaf_ids,
+                                                  const swh_multipole* __restrict__ mp,
+                                                  const double* __restrict__ F, GSoA g) {
+  const int c = leaf_ids[blockIdx.x];
+  const swh_leaf L = cells[c];
+  __shared__ double Fs[SWH_MPOLE_TERMS];
+  if (threadIdx.x < SWH_MPOLE_TERMS) Fs[threadIdx.x] = F[(size_t)c * SWH_MPOLE_TERMS + threadIdx.x];
+  __syncthreads();
+  bool any = false;
+  for (int t = 0; t < SWH_MPOLE_TERMS; t++) any |= Fs[t] != 0.;
+  if (!any) return;  // no interaction via multipoles reached this leaf
+  const double cx = mp[c].CoM[0], cy = mp[c].CoM[1], cz = mp[c].CoM[2];
+  for (int k = threadIdx.x; k < L.count; k += blockDim.x) {
+    const int i = L.start + k;
+    if (!g.active[i]) continue;
+    const double4 p = g.pos[i];
+    T o[4];
+    l2p<T>(Fs, (T)(p.x - cx), (T)(p.y - cy), (T)(p.z - cz), o);
+    double4 a = g.acc[i];
+    a.x += (double)o[1];
+    a.y += (double)o[2];
+    a.z += (double)o[3];
+    a.w += (double)o[0];
+    g.acc[i] = a;
+  }
+}
+
+// The recursive walk (host).
+struct TreeWalk {
+  const swh_gcell* cells;
+  const swh_multipole* mp;
+  const int8_t* act;
+  const swh_grav_params* G;
+  MacParams mac;
+  std::vector<std::vector<swh_leaf_pair>> pp;  // per i-cell
+  std::vector<std::vector<int2>> mm;           // per target cell: {source, symmetric}
+  int64_t skipped = 0;
+
+  double nearest(double d, int k) const {
+    const double L = (double)G->dim[k];
+    return d > 0.5 * L ? d - L : (d < -0.5 * L ? d + L : d);
+  }
+  // runner_doself_recursive_grav (2386-2431)
+  void self(int c) {
+    if (!act[c]) return;
+    const swh_gcell& C = cells[c];
+    if (C.split) {
+      for (int j = 0; j < 8; j++) {
+        if (C.progeny[j] < 0) continue;
+        self(C.progeny[j]);
+        for (int k = j + 1; k < 8; k++)
+          if (C.progeny[k] >= 0) pair(C.progeny[j], C.progeny[k]);
+      }
+    } else {
+      // runner_doself_grav_pp (1788-1871): truncated iff periodic && 2 r_max > r_cut_min
+      swh_leaf_pair e;
+      e.j = c;
+      e.truncated = G->periodic && (2. * mp[c].r_max > G->r_cut_min);
+      e.allow_mpole = 0;
+      pp[c].push_back(e);
+    }
+  }
+  // runner_dopair_grav_pp_no_cache (1440-1483): ci's leaves <- all of cj
+  void no_cache(int ci, int cj) {
+    if (!act[ci]) return;
+    if (cells[ci].count == 0 || cells[cj].count == 0) return;
+    if (cells[ci].split) {
+      for (int k = 0; k < 8; k++)
+        if (cells[ci].progeny[k] >= 0) no_cache(cells[ci].progeny[k], cj);
+    } else {
+      swh_leaf_pair e;
+      e.j = cj;
+      e.truncated = G->periodic ? 1 : 0;
+      e.allow_mpole = 0;
+      pp[ci].push_back(e);
+    }
+  }
+  // runner_dopair_grav_mm (2050-2064): symmetric when both are active
+  void mmpair(int ci, int cj) {
+    const bool di = act[ci], dj = act[cj];
+    if (di && dj) {
+      mm[ci].push_back(make_int2(cj, 1));
+      mm[cj].push_back(make_int2(ci, 1));
+    } else if (di) {
+      mm[ci].push_back(make_int2(cj, 0));
+    } else if (dj) {
+      mm[cj].push_back(make_int2(ci, 0));
+    }
+  }
+  // runner_dopair_grav_pp(ci, cj, symmetric = 1, allow_mpole = 1) (1202-1425):
+  // truncated iff periodic && |CoM_i - CoM_j| + r_max_i + r_max_j > r_cut_min
+  void pppair(int ci, int cj) {
+    int trunc = 0;
+    if (G->periodic) {
+      double d2 = 0.;
+      for (int k = 0; k < 3; k++) {
+        float dxf = (float)mp[cj].CoM[k] - (float)mp[ci].CoM[k];
+        const float L = G->dim[k];
+        dxf = dxf > 0.5f * L ? dxf - L : (dxf < -0.5f * L ? dxf + L : dxf);
+        d2 += (double)dxf * (double)dxf;
+      }
+      trunc = (std::sqrt(d2) + (double)(float)mp[ci].r_max + (double)(float)mp[cj].r_max) >
+              G->r_cut_min;
+    }
+    if (act[ci]) pp[ci].push_back(swh_leaf_pair{cj, trunc, 1});
+    if (act[cj]) pp[cj].push_back(swh_leaf_pair{ci, trunc, 1});
+  }
+  // runner_dopair_recursive_grav (2208-2374)
+  void pair(int ci, int cj) {
+    if (!(act[ci] || act[cj])) return;
+    const swh_multipole& A = mp[ci];
+    const swh_multipole& B = mp[cj];
+    double dx = A.CoM[0] - B.CoM[0], dy = A.CoM[1] - B.CoM[1], dz = A.CoM[2] - B.CoM[2];
+    if (G->periodic) {
+      dx = nearest(dx, 0);
+      dy = nearest(dy, 1);
+      dz = nearest(dz, 2);
+    }
+    const double r2 = dx * dx + dy * dy + dz * dz;
+    const double r_lr_check = std::sqrt(r2) - (A.r_max + B.r_max);
+    if (G->periodic && r_lr_check > G->r_cut_max) {
+      skipped++;
+      return;
+    }
+    const swh_gcell& Ci = cells[ci];
+    const swh_gcell& Cj = cells[cj];
+    if (Ci.count <= 1 || Cj.count <= 1) {
+      no_cache(ci, cj);
+      no_cache(cj, ci);
+    } else if (m2l_accept(mac, m2l_side(A), m2l_side(B), (float)r2) &&
+               m2l_accept(mac, m2l_side(B), m2l_side(A), (float)r2)) {
+      mmpair(ci, cj);
+    } else if (!Ci.split && !Cj.split) {
+      pppair(ci, cj);
+    } else if (A.r_max > B.r_max) {
+      if (Ci.split) {
+        for (int k = 0; k < 8; k++)
+          if (Ci.progeny[k] >= 0) pair(Ci.progeny[k], cj);
+      } else {
+        for (int k = 0; k < 8; k++)
+          if (Cj.progeny[k] >= 0) pair(ci, Cj.progeny[k]);
+      }
+    } else {
+      if (Cj.split) {
+        for (int k = 0; k < 8; k++)
+          if (Cj.progeny[k] >= 0) pair(ci, Cj.progeny[k]);
+      } else {
+        for (int k = 0; k < 8; k++)
+          if (Ci.progeny[k] >= 0) pair(Ci.progeny[k], cj);
+      }
+    }
+  }
+};
+
+}  // namespace swh
+
+extern "C" {
+
+swh_status swh_gspace_set_tree(swh_gspace* g, const swh_gcell* cells, int32_t ncells) {
+  if (!g || ncells < 0 || (ncells > 0 && !cells)) return SWH_ERR_ARG;
+  std::vector<int> parent(ncells, -1);
+  for (int c = 0; c < ncells; c++) {
+    const swh_gcell& C = cells[c];
+    if (C.start < 0 || C.count <= 0 || C.start + C.count > g->n) {
+      set_error("cell %d [%d,+%d) empty or outside the gpart set of %lld", c, C.start, C.count,
+                (long long)g->n);
+      return SWH_ERR_ARG;
+    }
+    if (C.split) {
+      int64_t sum = 0;
+      for (int k = 0; k < 8; k++) {
+        const int p = C.progeny[k];
+        if (p < 0) continue;
+        if (p >= ncells || p == c || parent[p] >= 0) {
+          set_error("cell %d: bad progeny %d", c, p);
+          return SWH_ERR_ARG;
+        }
+        const swh_gcell& P = cells[p];
+        if (P.start < C.start || P.start + P.count > C.start + C.count) {
+          set_error("cell %d: progeny %d outside its range", c, p);
+          return SWH_ERR_ARG;
+        }
+        parent[p] = c;
+        sum += P.count;
+      }
+      if (sum != C.count) {
+        set_error("cell %d: progeny hold %lld of its %d gparts", c, (long long)sum, C.count);
+        return SWH_ERR_ARG;
+      }
+    }
+  }
+  // depth of every cell (roots: no parent), L2L list grouped by depth
+  std::vector<int> depth(ncells, -1);
+  int maxd = 0;
+  for (int c = 0; c < ncells; c++) {
+    int d = 0, x = c;
+    while (parent[x] >= 0) {
+      x = parent[x];
+      d++;
+      if (d > ncells) {
+        set_error("cell tree has a cycle");
+        return SWH_ERR_ARG;
+      }
+    }
+    depth[c] = d;
+    maxd = std::max(maxd, d);
+  }
+  std::vector<int2> l2l;
+  std::vector<int32_t> doff(1, 0);
+  for (int d = 1; d <= maxd; d++) {
+    for (int c = 0; c < ncells; c++)
+      if (depth[c] == d) l2l.push_back(make_int2(c, parent[c]));
+    doff.push_back((int32_t)l2l.size());
+  }
+  std::vector<int> leaves;
+  std::vector<swh_leaf> ranges(ncells);
+  for (int c = 0; c < ncells; c++) {
+    if (!cells[c].split) leaves.push_back(c);
+    ranges[c] = swh_leaf{cells[c].start, cells[c].count};
+  }
+  // the cell table doubles as the P2P kernels' leaf table (pairs set later)
+  std::vector<int32_t> off(ncells + 1, 0);
+  SWH_TRY(swh_gspace_set_leaves(g, ranges.data(), ncells, off.data(), nullptr, 0));
+  SWH_HIP(hipSetDevice(g->ctx->device));
+  g->tree.assign(cells, cells + ncells);
+  SWH_TRY(g->cell_act.reserve((size_t)std::max(1, ncells)));
+  SWH_TRY(g->ftens.reserve((size_t)std::max(1, ncells) * SWH_MPOLE_TERMS * sizeof(double)));
+  SWH_TRY(g->l2l_list.reserve(std::max<size_t>(1, l2l.size()) * sizeof(int2)));
+  SWH_TRY(g->leaf_ids.reserve(std::max<size_t>(1, leaves.size()) * sizeof(int)));
+  if (!l2l.empty())
+    SWH_HIP(hipMemcpyAsync(g->l2l_list.ptr, l2l.data(), l2l.size() * sizeof(int2),
+                           hipMemcpyHostToDevice, g->stream));
+  if (!leaves.empty())
+    SWH_HIP(hipMemcpyAsync(g->leaf_ids.ptr, leaves.data(), leaves.size() * sizeof(int),
+                           hipMemcpyHostToDevice, g->stream));
+  SWH_HIP(hipStreamSynchronize(g->stream));
+  g->l2l_depth_off = doff;
+  g->nleaf_cells = (int32_t)leaves.size();
+  return SWH_OK;
+}
+
+swh_status swh_grav_tree(swh_gspace* g, const swh_grav_params* G, const int32_t* self_cells,
+                         int32_t nself, const int32_t* pair_cells, int32_t npair,
+                         swh_grav_tree_stats* stats) {
+  if (!g || !G || nself < 0 || npair < 0 || (nself > 0 && !self_cells) ||
+      (npair > 0 && !pair_cells))
+    return SWH_ERR_ARG;
+  if (stats) *stats = swh_grav_tree_stats{0, 0, 0, 0, 0};
+  const int ncells = (int)g->tree.size();
+  if (g->n == 0 || ncells == 0) {
+    set_error("swh_gspace_set_tree must precede swh_grav_tree");
+    return ncells == 0 ? SWH_ERR_STATE : SWH_OK;
+  }
+  for (int k = 0; k < nself; k++)
+    if (self_cells[k] < 0 || self_cells[k] >= ncells) return SWH_ERR_ARG;
+  for (int k = 0; k < 2 * npair; k++)
+    if (pair_cells[k] < 0 || pair_cells[k] >= ncells) return SWH_ERR_ARG;
+  SWH_HIP(hipSetDevice(g->ctx->device));
+  const int block = 256;
+  // activity, accumulators
+  hipLaunchKernelGGL(gunpack_kernel, dim3((int)((g->n + block - 1) / block)), dim3(block), 0,
+                     g->stream, g->layout, g->aos.as<const char>(), g->n, gsoa_of(g),
+                     G->max_active_bin);
+  SWH_HIP(hipGetLastError());
+  // multipoles (P2M per cell) and cell activity, to the host for the walk
+  SWH_TRY(swh_gspace_make_multipoles(g, nullptr));
+  hipLaunchKernelGGL(cell_active_kernel, dim3(ncells), dim3(256), 0, g->stream,
+                     g->leaves.as<const swh_leaf>(), g->active.as<const int8_t>(),
+                     g->cell_act.as<int8_t>());
+  SWH_HIP(hipGetLastError());
+  std::vector<swh_multipole> mp(ncells);
+  std::vector<int8_t> act(ncells);
+  SWH_HIP(hipMemcpyAsync(mp.data(), g->mpoles.ptr, ncells * sizeof(swh_multipole),
+                         hipMemcpyDeviceToHost, g->stream));
+  SWH_HIP(hipMemcpyAsync(act.data(), g->cell_act.ptr, ncells, hipMemcpyDeviceToHost, g->stream));
+  SWH_HIP(hipStreamSynchronize(g->stream));
+  // the walk
+  TreeWalk w;
+  w.cells = g->tree.data();
+  w.mp = mp.data();
+  w.act = act.data();
+  w.G = G;
+  w.mac = mac_params(G);
+  w.pp.resize(ncells);
+  w.mm.resize(ncells);
+  for (int k = 0; k < nself; k++) w.self(self_cells[k]);
+  for (int k = 0; k < npair; k++) w.pair(pair_cells[2 * k], pair_cells[2 * k + 1]);
+  // P-P lists (CSR over i-cells) and M-M lists (CSR over targets)
+  std::vector<int32_t> poff(ncells + 1, 0), moff(ncells + 1, 0);
+  std::vector<swh_leaf_pair> pairs;
+  std::vector<int2> msrc;
+  for (int c = 0; c < ncells; c++) {
+    pairs.insert(pairs.end(), w.pp[c].begin(), w.pp[c].end());
+    poff[c + 1] = (int32_t)pairs.size();
+    msrc.insert(msrc.end(), w.mm[c].begin(), w.mm[c].end());
+    moff[c + 1] = (int32_t)msrc.size();
+  }
+  std::vector<swh_leaf> ranges(ncells);
+  for (int c = 0; c < ncells; c++) ranges[c] = swh_leaf{g->tree[c].start, g->tree[c].count};
+  SWH_TRY(swh_gspace_set_leaves(g, ranges.data(), ncells, poff.data(), pairs.data(),
+                                (int32_t)pairs.size()));
+  g->mpoles_valid = true;  // the same cell table: the multipoles stay
+  // P2P + M2P
+  SWH_TRY(g->counter.reserve(2 * sizeof(unsigned long long)));
+  unsigned long long* ctr = g->counter.as<unsigned long long>();
+  SWH_HIP(hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned long long), g->stream));
+  if (!pairs.empty()) SWH_TRY(launch_pp(g, G, mac_params(G), ctr));
+  // M2L
+  const bool f64 = g->ctx->precision == SWH_PRECISION_F64;
+  SWH_HIP(hipMemsetAsync(g->ftens.ptr, 0, (size_t)ncells * SWH_MPOLE_TERMS * sizeof(double),
+                         g->stream));
+  if (!msrc.empty()) {
+    SWH_TRY(g->m2l_off.reserve((size_t)(ncells + 1) * sizeof(int32_t)));
+    SWH_TRY(g->m2l_src.reserve(msrc.size() * sizeof(int2)));
+    SWH_HIP(hipMemcpyAsync(g->m2l_off.ptr, moff.data(), (ncells + 1) * sizeof(int32_t),
+                           hipMemcpyHostToDevice, g->stream));
+    SWH_HIP(hipMemcpyAsync(g->m2l_src.ptr, msrc.data(), msrc.size() * sizeof(int2),
+                           hipMemcpyHostToDevice, g->stream));
+    const dim3 mg((ncells + 63) / 64);
+    if (f64)
+      hipLaunchKernelGGL((m2l_kernel<double>), mg, dim3(64), 0, g->stream,
+                         g->mpoles.as<const swh_multipole>(), ncells, g->m2l_off.as<const int>(),
+                         g->m2l_src.as<const int2>(), G->periodic, (double)G->dim[0],
+                         (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv,
+                         g->ftens.as<double>());
+    else
+      hipLaunchKernelGGL((m2l_kernel<float>), mg, dim3(64), 0, g->stream,
+                         g->mpoles.as<const swh_multipole>(), ncells, g->m2l_off.as<const int>(),
+                         g->m2l_src.as<const int2>(), G->periodic, (double)G->dim[0],
+                         (double)G->dim[1], (double)G->dim[2], (float)G->r_s_inv,
+                         g->ftens.as<double>());
+    SWH_HIP(hipGetLastError());
+    // down pass: L2L depth by depth, then L2P at the leaves
+    for (size_t d = 0; d + 1 < g->l2l_depth_off.size(); d++) {
+      const int o0 = g->l2l_depth_off[d], o1 = g->l2l_depth_off[d + 1];
+      if (o1 <= o0) continue;
+      const int2* lst = g->l2l_list.as<const int2>() + o0;
+      if (f64)
+        hipLaunchKernelGGL((l2l_kernel<double>), dim3((o1 - o0 + 63) / 64), dim3(64), 0,
+                           g->stream, lst, o1 - o0, g->mpoles.as<const swh_multipole>(),
+                           g->ftens.as<double>());
+      else
+        hipLaunchKernelGGL((l2l_kernel<float>), dim3((o1 - o0 + 63) / 64), dim3(64), 0,
+                           g->stream, lst, o1 - o0, g->mpoles.as<const swh_multipole>(),
+                           g->ftens.as<double>());
+      SWH_HIP(hipGetLastError());
+    }
+    if (g->nleaf_cells > 0) {
+      if (f64)
+        hipLaunchKernelGGL((l2p_kernel<double>), dim3(g->nleaf_cells), dim3(256), 0, g->stream,
+                           g->leaves.as<const swh_leaf>(), g->leaf_ids.as<const int>(),
+                           g->mpoles.as<const swh_multipole>(), g->ftens.as<const double>(),
+                           gsoa_of(g));
+      else
+        hipLaunchKernelGGL((l2p_kernel<float>), dim3(g->nleaf_cells), dim3(256), 0, g->stream,
+                           g->leaves.as<const swh_leaf>(), g->leaf_ids.as<const int>(),
+                           g->mpoles.as<const swh_multipole>(), g->ftens.as<const double>(),
+                           gsoa_of(g));
+      SWH_HIP(hipGetLastError());
+    }
+  }
+  unsigned long long h[2] = {0, 0};
+  SWH_HIP(hipMemcpyAsync(h, ctr, sizeof(h), hipMemcpyDeviceToHost, g->stream));
+  SWH_HIP(hipStreamSynchronize(g->stream));
+  if (stats) {
+    stats->n_pp = (int64_t)h[0];
+    stats->n_m2p = (int64_t)h[1];
+    stats->n_m2l = (int64_t)msrc.size();
+    stats->n_pp_tasks = (int64_t)pairs.size();
+    stats->n_skipped = w.skipped;
+  }
+  return SWH_OK;
+}
+
+swh_status swh_gspace_field_tensors(swh_gspace* g, float* out) {
+  if (!g || !out) return SWH_ERR_ARG;
+  const size_t n = g->tree.size() * SWH_MPOLE_TERMS;
+  if (n == 0) return SWH_OK;
+  std::vector<double> h(n);
+  SWH_HIP(hipSetDevice(g->ctx->device));
+  SWH_HIP(hipMemcpyAsync(h.data(), g->ftens.ptr, n * sizeof(double), hipMemcpyDeviceToHost,
+                         g->stream));
+  SWH_HIP(hipStreamSynchronize(g->stream));
+  for (size_t k = 0; k < n; k++) out[k] = (float)h[k];
   return SWH_OK;
 }
 

@@ -226,4 +226,13 @@ struct swh_gspace {
   int32_t nleaves = 0, npairs = 0;
   int32_t max_leaf = 0;
   swh::DevBuf counter;
+  // tree gravity (swh_gspace_set_tree / swh_grav_tree)
+  std::vector<swh_gcell> tree;   // host copy of the cell table
+  swh::DevBuf cell_act;          // int8 per cell: any active gpart
+  swh::DevBuf ftens;             // double[35] per cell: field tensors
+  swh::DevBuf m2l_off, m2l_src;  // CSR per target cell: int2 {source, symmetric}
+  swh::DevBuf l2l_list;          // int2 {cell, parent}, grouped by depth
+  std::vector<int32_t> l2l_depth_off;  // l2l_list range of each depth
+  swh::DevBuf leaf_ids;          // int: the unsplit cells
+  int32_t nleaf_cells = 0;
 };

@@ -18,6 +18,9 @@
 // compile-time, so the compiler emits straight-line FMA code.
 #pragma once
 
+#include <algorithm>
+#include <cmath>
+
 #include "swh_physics.h"
 #include "swifthip.h"
 
@@ -245,6 +248,186 @@ __device__ __forceinline__ void m2p(const float* M, T rx, T ry, T rz, T eps, boo
   }
   F[0] = F[1] = F[2] = F[3] = (T)0;
   m2p_terms<T, 0>(M, xp, yp, zp, g, F);
+}
+
+// ---------------------------------------------------------------------------
+// M2L, L2L, L2P (order 4; gravity_M2L_apply, gravity_L2L, gravity_L2P,
+// src/multipole.h:1600-2100, 2513-3018). Field tensors F_k, |k| <= 4, in
+// swh_multipole::M's index order. With D_m the potential derivative tensor
+// at r = (field centre - multipole centre) and X_n(d) = d^n / n!:
+//   M2L: F_k += sum_{|n|+|k| <= 4} M_n D_(n+k)   (dipole M_1 = 0 about the CoM)
+//   L2L: F'_k = sum_{|n|+|k| <= 4} X_n(c' - c) F_(n+k)
+//   L2P: pot = -sum_n X_n(x - c) F_n,  a_e = sum_{|n| <= 3} X_n(x - c) F_(n+e)
+// The (k, n) loops are compile-time, so each is straight-line FMA code.
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr int mp_index(int a, int b, int c) {
+  int t = 0;
+  while (t < SWH_MPOLE_TERMS && !(kMpA[t] == a && kMpB[t] == b && kMpC[t] == c)) t++;
+  return t;
+}
+__host__ __device__ constexpr int mp_order(int t) { return kMpA[t] + kMpB[t] + kMpC[t]; }
+
+// D_m for the 35 multi-indices, |m| <= 4, from powers of r and the chain g
+template <typename T, int t>
+__device__ __forceinline__ void dtensors(const T* xp, const T* yp, const T* zp, const T* g,
+                                         T* D) {
+  if constexpr (t < SWH_MPOLE_TERMS) {
+    D[t] = dtensor<T, kMpA[t], kMpB[t], kMpC[t]>(xp, yp, zp, g);
+    dtensors<T, t + 1>(xp, yp, zp, g, D);
+  }
+}
+
+template <typename T, int k, int n>
+__device__ __forceinline__ void m2l_kn(const float* M, const T* D, T* F) {
+  if constexpr (n < SWH_MPOLE_TERMS) {
+    if constexpr ((n == 0 || n > 3) && mp_order(k) + mp_order(n) <= 4) {
+      constexpr int m = mp_index(kMpA[k] + kMpA[n], kMpB[k] + kMpB[n], kMpC[k] + kMpC[n]);
+      F[k] += (T)M[n] * D[m];
+    }
+    m2l_kn<T, k, n + 1>(M, D, F);
+  }
+}
+template <typename T, int k>
+__device__ __forceinline__ void m2l_k(const float* M, const T* D, T* F) {
+  if constexpr (k < SWH_MPOLE_TERMS) {
+    m2l_kn<T, k, 0>(M, D, F);
+    m2l_k<T, k + 1>(M, D, F);
+  }
+}
+
+// gravity_M2L_nonsym / _symmetric's per-direction work: (rx, ry, rz) = field
+// centre - multipole centre (nearest image applied), eps the softening of
+// the pair (potential_derivatives_compute_M2L, gravity_derivatives.h:217-515).
+template <typename T>
+__device__ __forceinline__ void m2l(const float* M, T rx, T ry, T rz, T eps, bool periodic,
+                                    T r_s_inv, T* F) {
+  const T r2 = rx * rx + ry * ry + rz * rz;
+  const T r_inv = (T)1 / sqrt(r2);
+  T g[6];
+  radial_chain<T>(r2, r_inv, eps, periodic, r_s_inv, g);
+  T xp[5], yp[5], zp[5];
+  xp[0] = yp[0] = zp[0] = (T)1;
+#pragma unroll
+  for (int q = 1; q < 5; q++) {
+    xp[q] = xp[q - 1] * rx;
+    yp[q] = yp[q - 1] * ry;
+    zp[q] = zp[q - 1] * rz;
+  }
+  T D[SWH_MPOLE_TERMS];
+  dtensors<T, 0>(xp, yp, zp, g, D);
+  m2l_k<T, 0>(M, D, F);
+}
+
+// X_n(d) = d^n / n! for the 35 multi-indices
+template <typename T>
+__device__ __forceinline__ void xpowers(T dx, T dy, T dz, T* X) {
+  T xp[5], yp[5], zp[5];
+  xp[0] = yp[0] = zp[0] = (T)1;
+#pragma unroll
+  for (int q = 1; q < 5; q++) {
+    xp[q] = xp[q - 1] * dx;
+    yp[q] = yp[q - 1] * dy;
+    zp[q] = zp[q - 1] * dz;
+  }
+#pragma unroll
+  for (int t = 0; t < SWH_MPOLE_TERMS; t++)
+    X[t] = xp[kMpA[t]] * yp[kMpB[t]] * zp[kMpC[t]] *
+           (T)(1. / (fact(kMpA[t]) * fact(kMpB[t]) * fact(kMpC[t])));
+}
+
+template <typename T, int k, int n>
+__device__ __forceinline__ void l2l_kn(const T* X, const T* Fp, T* F) {
+  if constexpr (n < SWH_MPOLE_TERMS) {
+    if constexpr (mp_order(k) + mp_order(n) <= 4) {
+      constexpr int m = mp_index(kMpA[k] + kMpA[n], kMpB[k] + kMpB[n], kMpC[k] + kMpC[n]);
+      F[k] += X[n] * Fp[m];
+    }
+    l2l_kn<T, k, n + 1>(X, Fp, F);
+  }
+}
+template <typename T, int k>
+__device__ __forceinline__ void l2l_k(const T* X, const T* Fp, T* F) {
+  if constexpr (k < SWH_MPOLE_TERMS) {
+    l2l_kn<T, k, 0>(X, Fp, F);
+    l2l_k<T, k + 1>(X, Fp, F);
+  }
+}
+
+// gravity_L2P: {potential, a_x, a_y, a_z} at offset d from the tensor's centre
+// (F: the tensor in fp64, e.g. staged in LDS)
+template <typename T>
+__device__ __forceinline__ void l2p(const double* F, T dx, T dy, T dz, T* out) {
+  T X[SWH_MPOLE_TERMS];
+  xpowers<T>(dx, dy, dz, X);
+  T pot = (T)0, ax = (T)0, ay = (T)0, az = (T)0;
+#pragma unroll
+  for (int t = 0; t < SWH_MPOLE_TERMS; t++) {
+    pot -= X[t] * (T)F[t];
+    if (mp_order(t) <= 3) {
+      ax += X[t] * (T)F[mp_index(kMpA[t] + 1, kMpB[t], kMpC[t])];
+      ay += X[t] * (T)F[mp_index(kMpA[t], kMpB[t] + 1, kMpC[t])];
+      az += X[t] * (T)F[mp_index(kMpA[t], kMpB[t], kMpC[t] + 1)];
+    }
+  }
+  out[0] = pot;
+  out[1] = ax;
+  out[2] = ay;
+  out[3] = az;
+}
+
+// gravity_M2L_accept (multipole_accept.h:78-176) for sink A, source B, in the
+// reference's float arithmetic (host side: the tree walk's decision).
+struct M2LSide {
+  float rho, max_soft, min_a, M000, power[3];
+};
+inline M2LSide m2l_side(const swh_multipole& m) {
+  M2LSide s;
+  s.rho = (float)m.r_max;
+  s.max_soft = m.max_softening;
+  s.min_a = m.min_old_a_grav_norm;
+  s.M000 = m.M[0];
+  for (int k = 0; k < 3; k++) s.power[k] = m.power[k];
+  return s;
+}
+inline bool m2l_accept(const MacParams& P, const M2LSide& A, const M2LSide& B, float r2) {
+#pragma clang fp contract(off)
+  const float rho_A = A.rho, rho_B = B.rho;
+  const float rho_max = std::max(rho_A, rho_B);
+  const float max_softening = std::max(A.max_soft, B.max_soft);
+  // p = 2: sum_n binomial(2, n) power_B[n] rho_A^(2 - n)
+  float E_BA_term = 0.f;
+  E_BA_term += 1.f * B.power[0] * (rho_A * rho_A);
+  E_BA_term += 2.f * B.power[1] * rho_A;
+  E_BA_term += 1.f * B.power[2] * 1.f;
+  E_BA_term *= 8.f;
+  if (rho_A + rho_B > 0.f) {
+    E_BA_term *= rho_max;
+    E_BA_term /= (rho_A + rho_B);
+  }
+  const float r_to_p = r2;
+  float f_MAC_inv = r2;
+  if (P.periodic && P.trunc_mac) {  // gravity_f_MAC_inverse
+    const float H = max_softening;
+    if (r2 < (25.f / 81.f) * H * H)
+      f_MAC_inv = (25.f / 81.f) * H * H;
+    else if (P.r_s_inv * P.r_s_inv * r2 > (25.f / 9.f))
+      f_MAC_inv = (9.f / 25.f) * P.r_s_inv * P.r_s_inv * r2 * r2;
+  }
+  const float min_a_grav = A.min_a;
+  const float M_max = std::max(A.M000, B.M000);
+  const float rho_sum = rho_A + rho_B;
+  const bool cond_2 = P.below_soft || max_softening * max_softening < r2;
+  if (P.advanced && P.gadget) {
+    const float q = rho_max / sqrtf(r2);
+    const float ratio = q * q * q;  // integer_powf(q, SELF_GRAVITY_MULTIPOLE_ORDER - 1)
+    return (M_max * ratio < P.eps * min_a_grav * f_MAC_inv) && cond_2;
+  }
+  if (P.advanced) {
+    const bool cond_1 = rho_sum * rho_sum < r2;
+    const bool cond_3 = E_BA_term < P.eps * min_a_grav * r_to_p * f_MAC_inv;
+    return cond_1 && cond_2 && cond_3;
+  }
+  return (rho_sum * rho_sum < P.theta_crit2 * r2) && cond_2;
 }
 
 // gravity_multipole_compute_power (multipole.h:878-972) on the stored

@@ -500,6 +500,7 @@ static void grav_params_of(const struct engine *e, swh_grav_params *G) {
   for (int k = 0; k < 3; k++) G->dim[k] = (float)e->mesh->dim[k];
   G->r_s_inv = e->mesh->r_s_inv;
   G->r_cut_min = e->mesh->r_cut_min;
+  G->r_cut_max = e->mesh->r_cut_max;
   G->max_active_bin = e->max_active_bin;
   const struct gravity_props *gp = e->gravity_properties;
   if (gp) {  /* gravity_M2P_accept's inputs (multipole_accept.h:290-373) */

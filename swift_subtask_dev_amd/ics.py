@@ -230,3 +230,69 @@ def neighbour_pairs(cdim: int, periodic: bool = True, truncated: int = 0):
         arr["j"] = [p[0] for p in pairs]
         arr["truncated"] = [p[1] for p in pairs]
     return np.asarray(offs, dtype=np.int32), arr
+
+
+def gravity_tree(gparts: np.ndarray, cdim: int, split_size: int = 64, box: float = 1.0,
+                 max_depth: int = 12):
+    """SWIFT-like cell tree (space_split, src/space_split.c): a cdim^3 grid of
+    top-level cells, each split into octants while it holds more than
+    split_size gparts. Returns (gparts sorted so that every cell is a
+    contiguous range, cells as abi.GCell-compatible records, top-level cell
+    indices). Empty octants get no cell (progeny -1)."""
+    x = np.mod(gparts["x"], box)
+    w = box / cdim
+    top = np.minimum((x / w).astype(np.int64), cdim - 1)
+    tkey = (top[:, 0] * cdim + top[:, 1]) * cdim + top[:, 2]
+    # position within the top cell, 21 bits per axis, interleaved (Morton)
+    rel = np.clip((x - top * w) / w, 0.0, 1.0 - 1e-12)
+    q = (rel * (1 << 21)).astype(np.uint64)
+
+    def spread(v):
+        v = v & np.uint64(0x1FFFFF)
+        v = (v | (v << np.uint64(32))) & np.uint64(0x1F00000000FFFF)
+        v = (v | (v << np.uint64(16))) & np.uint64(0x1F0000FF0000FF)
+        v = (v | (v << np.uint64(8))) & np.uint64(0x100F00F00F00F00F)
+        v = (v | (v << np.uint64(4))) & np.uint64(0x10C30C30C30C30C3)
+        v = (v | (v << np.uint64(2))) & np.uint64(0x1249249249249249)
+        return v
+
+    mort = (spread(q[:, 0]) << np.uint64(2)) | (spread(q[:, 1]) << np.uint64(1)) | spread(q[:, 2])
+    order = np.lexsort((mort, tkey))
+    g = gparts[order].copy()
+    tkey, mort = tkey[order], mort[order]
+    cells = []
+
+    def make(start, count, level):
+        idx = len(cells)
+        cells.append([start, count, 0, [-1] * 8])
+        if count > split_size and level < max_depth:
+            shift = np.uint64(3 * (20 - level))
+            octant = ((mort[start:start + count] >> shift) & np.uint64(7)).astype(np.int64)
+            bounds = np.searchsorted(octant, np.arange(9))  # sorted within the cell
+            prog = [-1] * 8
+            for k in range(8):
+                c0, c1 = int(bounds[k]), int(bounds[k + 1])
+                if c1 > c0:
+                    prog[k] = make(start + c0, c1 - c0, level + 1)
+            cells[idx][2] = 1
+            cells[idx][3] = prog
+        return idx
+
+    counts = np.bincount(tkey, minlength=cdim ** 3)
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    tops = []
+    for t in range(cdim ** 3):
+        if counts[t] > 0:
+            tops.append(make(int(starts[t]), int(counts[t]), 0))
+    arr = np.zeros(len(cells), dtype=np.dtype([("start", "<i4"), ("count", "<i4"),
+                                               ("split", "<i4"), ("progeny", "<i4", 8)]))
+    for k, (st, ct, sp, pg) in enumerate(cells):
+        arr[k] = (st, ct, sp, pg)
+    return g, arr, np.asarray(tops, dtype=np.int32)
+
+
+def top_level_pairs(tops: np.ndarray) -> np.ndarray:
+    """Every unordered pair of top-level cells (the walk prunes far ones)."""
+    n = len(tops)
+    i, j = np.triu_indices(n, k=1)
+    return np.stack([tops[i], tops[j]], axis=1).astype(np.int32)

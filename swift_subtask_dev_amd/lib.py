@@ -41,6 +41,7 @@ HIP_SYMBOLS = [
     "swh_gspace_create",
     "swh_gspace_destroy", "swh_gspace_upload", "swh_gspace_set_leaves", "swh_grav_pp_batch",
     "swh_gspace_make_multipoles", "swh_space_upload_xparts", "swh_space_drift",
+    "swh_gspace_set_tree", "swh_grav_tree", "swh_gspace_field_tensors",
     "swh_gspace_download", "swh_gspace_sync",
 ]
 ADAPTER_SYMBOLS = [
@@ -128,6 +129,10 @@ def load() -> C.CDLL:
         "swh_gspace_set_leaves": (C.c_int, [vp, vp, i32, P(i32), vp, i32]),
         "swh_grav_pp_batch": (C.c_int, [vp, P(abi.GravParams), P(i64), P(i64)]),
         "swh_gspace_make_multipoles": (C.c_int, [vp, vp]),
+        "swh_gspace_set_tree": (C.c_int, [vp, vp, i32]),
+        "swh_grav_tree": (C.c_int, [vp, P(abi.GravParams), vp, i32, vp, i32,
+                                    P(abi.GravTreeStats)]),
+        "swh_gspace_field_tensors": (C.c_int, [vp, vp]),
         "swh_gspace_download": (C.c_int, [vp, vp, P(abi.GPartLayout), C.c_int]),
         "swh_gspace_sync": (C.c_int, [vp]),
     }
@@ -427,6 +432,29 @@ class GravSpace:
         if m2p:
             return n.value, m.value
         return n.value if count else None
+
+    def set_tree(self, cells: np.ndarray):
+        """cells: records of (start, count, split, progeny[8]) (ics.gravity_tree)."""
+        cells = np.ascontiguousarray(cells)
+        assert cells.dtype.itemsize == C.sizeof(abi.GCell)
+        self._tree = cells
+        _check(self._lib.swh_gspace_set_tree(self.handle, _ptr(cells), len(cells)), "set_tree")
+
+    def tree(self, G: abi.GravParams, self_cells, pair_cells) -> dict:
+        """runner_doself_recursive_grav on self_cells, runner_dopair_recursive_grav
+        on pair_cells (n x 2), then the down pass."""
+        sc = np.ascontiguousarray(self_cells, dtype=np.int32)
+        pc = np.ascontiguousarray(pair_cells, dtype=np.int32).reshape(-1)
+        st = abi.GravTreeStats()
+        _check(self._lib.swh_grav_tree(self.handle, C.byref(G), _ptr(sc), len(sc), _ptr(pc),
+                                       len(pc) // 2, C.byref(st)), "grav_tree")
+        return {"n_pp": st.n_pp, "n_m2p": st.n_m2p, "n_m2l": st.n_m2l,
+                "n_pp_tasks": st.n_pp_tasks, "n_skipped": st.n_skipped}
+
+    def field_tensors(self) -> np.ndarray:
+        out = np.zeros((len(self._tree), abi.MPOLE_TERMS), dtype=np.float32)
+        _check(self._lib.swh_gspace_field_tensors(self.handle, _ptr(out)), "field_tensors")
+        return out
 
     def download(self, gparts: np.ndarray):
         _check(self._lib.swh_gspace_download(self.handle, _ptr(gparts), C.byref(self.ctx.GL), 0),

@@ -92,8 +92,12 @@ def test_struct_part_offsets_match_survey():
 def test_params_struct_size():
     # swh_hydro_params: 6 doubles + 4 floats + 2 ints + 8 floats + 2 ints + 3 doubles
     assert C.sizeof(abi.HydroParams) == 6 * 8 + 4 * 4 + 2 * 4 + 8 * 4 + 2 * 4 + 3 * 8
-    # swh_grav_params: mesh scalars (40 B) + 2 floats + 4 ints of the MAC, padded to 8
-    assert C.sizeof(abi.GravParams) == 64
+    # swh_grav_params: mesh scalars (40 B) + 2 floats + 4 ints of the MAC + r_cut_max
+    assert C.sizeof(abi.GravParams) == 72
+    assert abi.GravParams.r_cut_max.offset == 64
+    # swh_gcell: start, count, split, progeny[8]; swh_grav_tree_stats: 5 int64
+    assert C.sizeof(abi.GCell) == 44
+    assert C.sizeof(abi.GravTreeStats) == 40
     # swh_multipole: CoM, r_max, 35 terms, 5 powers, 2 floats
     assert C.sizeof(abi.Multipole) == 4 * 8 + 35 * 4 + 5 * 4 + 2 * 4
 

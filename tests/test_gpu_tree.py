@@ -1,0 +1,161 @@
+"""GPU tree gravity (swh_gspace_set_tree / swh_grav_tree): the recursive
+gravity tasks (runner_doself/dopair_recursive_grav, runner_doiact_grav.c:
+2208-2431), M2L (runner_dopair_grav_mm*, 1881-2095) and the down pass
+(runner_do_grav_down, 65-164) against the oracle's restatement of the same
+walk (grav_tree) on the same tree: identical task counts (the walk's
+decisions are float comparisons evaluated identically), forces and field
+tensors within the fp64-vs-fp64 tolerance; and against direct summation."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from swift_subtask_dev_amd import abi, ics
+
+pytestmark = pytest.mark.gpu
+
+
+def params(periodic=False, theta=0.5, r_cut_max=0.0, r_s_inv=0.0, r_cut_min=0.0,
+           advanced=0, mab=abi.NUM_TIME_BINS):
+    G = abi.GravParams(1 if periodic else 0, (C.c_float * 3)(1, 1, 1), r_s_inv, r_cut_min, mab)
+    G.theta_crit = theta
+    G.adaptive_tolerance = 1e-4
+    G.use_advanced_MAC = advanced
+    G.r_cut_max = r_cut_max
+    return G
+
+
+def clumpy_box(n=16, seed=3):
+    g0 = ics.uniform_gravity_box(n, epsilon=1e-3, seed=seed)
+    rng = np.random.Generator(np.random.PCG64(seed + 2))
+    k = len(g0) // 5
+    g0["x"][:k] = 0.3 + rng.normal(0, 0.03, (k, 3))
+    g0["x"] = np.mod(g0["x"], 1.0)
+    return g0
+
+
+def run_oracle(g, cells, tops, pairs, G):
+    st = np.zeros(5, dtype=np.int64)
+    ft = np.zeros((len(cells), 35), dtype=np.float32)
+    O.fn("f64", "grav_tree")(g.ctypes.data, len(g), cells.ctypes.data, len(cells),
+                             tops.ctypes.data, len(tops), pairs.ctypes.data, len(pairs),
+                             C.byref(G), st.ctypes.data, ft.ctypes.data)
+    return st, ft
+
+
+def run_gpu(ctx, g, cells, tops, pairs, G):
+    from swift_subtask_dev_amd import lib
+    gs = lib.GravSpace(ctx)
+    gs.upload(g)
+    gs.set_tree(cells)
+    st = gs.tree(G, tops, pairs)
+    gs.download(g)
+    ft = gs.field_tensors()
+    gs.close()
+    return st, ft
+
+
+def compare(gg, go, rel=2e-5):
+    a_g = gg["a_grav"].astype(np.float64)
+    a_o = go["a_grav"].astype(np.float64)
+    scale = np.linalg.norm(a_o, axis=1)
+    e = np.linalg.norm(a_g - a_o, axis=1) / np.maximum(scale, 1e-30)
+    assert e.max() < rel, (e.max(), int(np.argmax(e)))
+    ep = np.abs(gg["potential"] - go["potential"]) / np.maximum(np.abs(go["potential"]), 1e-30)
+    assert ep.max() < rel, ep.max()
+
+
+@pytest.mark.parametrize("theta", [0.8, 0.5, 0.3])
+def test_tree_vs_oracle_newtonian(gpu_ctx, theta):
+    g, cells, tops = ics.gravity_tree(clumpy_box(), 2, split_size=32)
+    pairs = ics.top_level_pairs(tops)
+    G = params(theta=theta)
+    gg, go = abi.copy_parts(g), abi.copy_parts(g)
+    st = run_gpu(gpu_ctx, gg, cells, tops, pairs, G)[0]
+    so, fo = run_oracle(go, cells, tops, pairs, G)
+    assert [st["n_pp"], st["n_m2p"], st["n_m2l"], st["n_pp_tasks"], st["n_skipped"]] == list(so)
+    assert st["n_m2l"] > 0 and st["n_m2p"] > 0
+    compare(gg, go)
+
+
+def test_tree_field_tensors(gpu_ctx):
+    g, cells, tops = ics.gravity_tree(clumpy_box(), 2, split_size=32)
+    pairs = ics.top_level_pairs(tops)
+    G = params(theta=0.6)
+    gg, go = abi.copy_parts(g), abi.copy_parts(g)
+    _, fg = run_gpu(gpu_ctx, gg, cells, tops, pairs, G)
+    _, fo = run_oracle(go, cells, tops, pairs, G)
+    assert np.abs(fo).max() > 0
+    # per order, relative to the order's largest term
+    for lo, hi in ((0, 1), (1, 4), (4, 10), (10, 20), (20, 35)):
+        s = np.abs(fo[:, lo:hi]).max()
+        assert np.abs(fg[:, lo:hi] - fo[:, lo:hi]).max() <= 1e-5 * s
+
+
+def test_tree_periodic_truncated(gpu_ctx):
+    """Periodic: truncated M2L/P2P with r_s, and the r_cut_max skip."""
+    g, cells, tops = ics.gravity_tree(clumpy_box(14, seed=7), 4, split_size=24)
+    pairs = ics.top_level_pairs(tops)
+    r_s = 1.25 / 32  # mesh_side_length 32: r_s = 1.25 box / N_mesh
+    G = params(periodic=True, theta=0.6, r_s_inv=1 / r_s, r_cut_min=0.1 * r_s,
+               r_cut_max=4.5 * r_s)
+    gg, go = abi.copy_parts(g), abi.copy_parts(g)
+    st = run_gpu(gpu_ctx, gg, cells, tops, pairs, G)[0]
+    so, _ = run_oracle(go, cells, tops, pairs, G)
+    assert [st["n_pp"], st["n_m2p"], st["n_m2l"], st["n_pp_tasks"], st["n_skipped"]] == list(so)
+    assert st["n_skipped"] > 0
+    compare(gg, go)
+
+
+def test_tree_activity_and_adaptive_mac(gpu_ctx):
+    """Inactive gparts keep their a_grav; the adaptive MAC (use_advanced_MAC,
+    gravity_M2L_accept's E_BA test against min |a_old|) drives the walk."""
+    g0 = clumpy_box(12, seed=9)
+    rng = np.random.Generator(np.random.PCG64(2))
+    g0["time_bin"] = np.where(rng.uniform(size=len(g0)) < 0.5, 2, 1)
+    g0["old_a_grav_norm"] = rng.uniform(0.5, 5.0, len(g0)).astype(np.float32)
+    g, cells, tops = ics.gravity_tree(g0, 2, split_size=24)
+    pairs = ics.top_level_pairs(tops)
+    G = params(theta=0.7, advanced=1, mab=1)
+    gg, go = abi.copy_parts(g), abi.copy_parts(g)
+    st = run_gpu(gpu_ctx, gg, cells, tops, pairs, G)[0]
+    so, _ = run_oracle(go, cells, tops, pairs, G)
+    assert [st["n_pp"], st["n_m2p"], st["n_m2l"], st["n_pp_tasks"], st["n_skipped"]] == list(so)
+    inactive = g["time_bin"] != 1
+    assert np.all(gg["a_grav"][inactive] == 0)
+    compare(gg[~inactive], go[~inactive])
+
+
+def test_tree_zero_opening_angle_is_direct(gpu_ctx):
+    """theta -> 0: no multipole passes, the walk reduces to P-P over every
+    pair: N (N - 1) interactions, the direct sum's forces."""
+    g, cells, tops = ics.gravity_tree(ics.uniform_gravity_box(10, 1e-3, seed=4), 2, 16)
+    pairs = ics.top_level_pairs(tops)
+    G = params(theta=1e-6)
+    gg = abi.copy_parts(g)
+    st = run_gpu(gpu_ctx, gg, cells, tops, pairs, G)[0]
+    N = len(g)
+    assert st["n_pp"] == N * (N - 1) and st["n_m2l"] == 0 and st["n_m2p"] == 0
+    gd = abi.copy_parts(g)
+    leaves = np.array([0, N], dtype=np.int32)
+    off = np.array([0, 1], dtype=np.int32)
+    pr = np.array([0, 0, 0], dtype=np.int32)
+    O.fn("f64", "grav_pp_leaves")(gd.ctypes.data, leaves.ctypes.data, 1, off.ctypes.data,
+                                  pr.ctypes.data, C.byref(G), None, None)
+    compare(gg, gd)
+
+
+def test_tree_bad_input(gpu_ctx):
+    from swift_subtask_dev_amd import lib
+    g, cells, tops = ics.gravity_tree(ics.uniform_gravity_box(8, 1e-3, seed=4), 2, 16)
+    gs = lib.GravSpace(gpu_ctx)
+    gs.upload(g)
+    bad = cells.copy()
+    k = int(np.argmax(bad["split"]))
+    bad["count"][k] += 1  # progeny no longer partition the range
+    with pytest.raises(lib.SwhError):
+        gs.set_tree(bad)
+    gs.close()

@@ -481,39 +481,39 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
     const T r2 = tdx * tdx + tdy * tdy + tdz * tdz;
     if (st.accept(j, pj, r2)) st.interact_staged(rj.p, rj.meta, pj, tdx, tdy, tdz, r2);
   };
-  int j0 = idx(0), j1 = idx(1), j2 = idx(2), j3 = idx(3);
-  double4 pc = make_double4(0., 0., 0., 0.);
-  JRec<S::kPay> rc{};
-  if (j0 >= 0) {
-    pc = a.pos[dj(j0)];
-    rc = S::load_j(a, dj(j0));
+  // light j records (density): indices four entries ahead, particle data two
+  // ahead, so every lane keeps two gathers in flight behind the current
+  // entry's math (the loop is latency-bound: one gather ahead left 76% of the
+  // wave time waiting, profiles/r02b_sq_counters.txt)
+  int ja = idx(0), jb = idx(1), jc = idx(2), jd = idx(3);
+  double4 pa = make_double4(0., 0., 0., 0.), pb = pa;
+  JRec<S::kPay> ra{}, rb{};
+  if (ja >= 0) {
+    pa = a.pos[dj(ja)];
+    ra = S::load_j(a, dj(ja));
   }
-  // one entry: compute j (data pc/rc) after issuing the loads of jn and the
-  // index four entries ahead
-#define SWH_WALK_STEP(J, JN, M)                   \
-  {                                              \
-    double4 pn = make_double4(0., 0., 0., 0.);   \
-    JRec<S::kPay> rn{};                          \
-    if (JN >= 0) {                               \
-      pn = a.pos[dj(JN)];                        \
-      rn = S::load_j(a, dj(JN));                 \
-    }                                            \
-    const int jc = J;                            \
-    J = idx(M + 4);                              \
-    step(jc, pc, rc);                            \
-    pc = pn;                                     \
-    rc = rn;                                     \
+  if (jb >= 0) {
+    pb = a.pos[dj(jb)];
+    rb = S::load_j(a, dj(jb));
   }
-  for (int m = 0; m < nme; m += 4) {
-    SWH_WALK_STEP(j0, j1, m)
-    if (m + 1 >= nme) break;
-    SWH_WALK_STEP(j1, j2, m + 1)
-    if (m + 2 >= nme) break;
-    SWH_WALK_STEP(j2, j3, m + 2)
-    if (m + 3 >= nme) break;
-    SWH_WALK_STEP(j3, j0, m + 3)
+  for (int m = 0; m < nme; m++) {
+    double4 pn = make_double4(0., 0., 0., 0.);
+    JRec<S::kPay> rn{};
+    if (jc >= 0) {
+      pn = a.pos[dj(jc)];
+      rn = S::load_j(a, dj(jc));
+    }
+    const int jcur = ja;
+    ja = jb;
+    jb = jc;
+    jc = jd;
+    jd = idx(m + 4);
+    step(jcur, pa, ra);
+    pa = pb;
+    ra = rb;
+    pb = pn;
+    rb = rn;
   }
-#undef SWH_WALK_STEP
 }
 
 // One loop over every active, listed particle: LPI lanes per i, 256/LPI

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SWH_ABI_VERSION 5
+#define SWH_ABI_VERSION 6
 
 #if defined(__GNUC__)
 #define SWH_API __attribute__((visibility("default")))
@@ -440,6 +440,28 @@ SWH_API swh_status swh_grav_tree(swh_gspace *g, const swh_grav_params *G,
  * grav_tensor's F order = swh_multipole::M's), after the down pass. */
 SWH_API swh_status swh_gspace_field_tensors(swh_gspace *g, float *out);
 SWH_API swh_status swh_gspace_sync(swh_gspace *g);
+
+/* PM mesh gravity: pm_mesh_compute_potential's
+ * non-distributed path, compute_potential_global (src/mesh_gravity.c:844-1041)
+ * without neutrinos, over the uploaded gparts: CIC assignment of the masses
+ * (inhibited gparts skipped), r2c FFT, the Green function with the
+ * long-range truncation and CIC deconvolution (mesh_apply_Green_function),
+ * c2r FFT, then per gpart the CIC potential and the 5-point-stencil
+ * accelerations times const_G (mesh_to_gpart_CIC), written into the records'
+ * a_grav_mesh[3] / potential_mesh floats (overwritten, as the reference zeroes
+ * them first); swh_gspace_download returns them. potential_out (nullable): the
+ * N^3 potential mesh (row-major, z fastest), as mesh->potential_global. */
+typedef struct swh_pm_params {
+  int32_t N;                  /* gravity_props.mesh_size (even, <= 1290) */
+  int32_t off_a_grav_mesh;    /* byte offsets in the gpart record: float[3] */
+  int32_t off_potential_mesh; /* float */
+  int32_t reserved;
+  double box_size;            /* s->dim[0] (cubic periodic box) */
+  double r_s;                 /* mesh->r_s = a_smooth * box_size / N */
+  double const_G;             /* physical_constants->const_newton_G (used as float) */
+} swh_pm_params;
+SWH_API swh_status swh_gspace_pm_mesh(swh_gspace *g, const swh_pm_params *M,
+                                      double *potential_out);
 
 #ifdef __cplusplus
 }

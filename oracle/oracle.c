@@ -3011,3 +3011,182 @@ API void PFX(grav_tree)(struct gpart *g, int n, const struct oracle_gcell *cells
   free(F); free(depth); free(fill); free(pairs); free(off); free(leaves);
   free(w.pp); free(w.mm); free(parent); free(act); free(mp);
 }
+
+/* ======================================================================== */
+/* PM mesh gravity — src/mesh_gravity.c compute_potential_global (844-1041) */
+/* on a non-distributed mesh without neutrinos: CIC assignment              */
+/* (gpart_to_mesh_CIC, 137-182, CIC_set 103-125), r2c FFT,                  */
+/* mesh_apply_Green_function (519-638) with fourier_kernel_long_grav_eval   */
+/* (kernel_long_gravity.h:310-319, default sinh branch), c2r FFT, and       */
+/* mesh_to_gpart_CIC (308-394: CIC potential, 5-point stencil accelerations)*/
+/* + the const_G scaling of mesh_to_gpart_CIC_mapper (428-470). All double, */
+/* as the reference, in both oracle builds. FFTW (third-party, not under    */
+/* /root/reference) computes the unnormalised DFT; this restates it with a  */
+/* plain radix-2 complex transform over the full N^3 spectrum (N a power of */
+/* two), applying the Green function to every k (the factor is even in each*/
+/* component, so the spectrum stays Hermitian and the real part is the c2r */
+/* result).                                                                 */
+/* ======================================================================== */
+static int pm_id(int i, int j, int k, int N) { /* row_major_id_periodic (row_major_id.h:39-43) */
+  return ((i + N) % N) * N * N + ((j + N) % N) * N + ((k + N) % N);
+}
+
+static void pm_fft_line(double *re, double *im, int n, int sign) {
+  for (int i = 1, j = 0; i < n; i++) {
+    int bit = n >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j ^= bit;
+    if (i < j) {
+      double t = re[i]; re[i] = re[j]; re[j] = t;
+      t = im[i]; im[i] = im[j]; im[j] = t;
+    }
+  }
+  for (int len = 2; len <= n; len <<= 1) {
+    const double ang = sign * 2. * M_PI / len;
+    for (int i = 0; i < n; i += len)
+      for (int k = 0; k < len / 2; k++) {
+        const double wr = cos(ang * k), wi = sin(ang * k);
+        const int a = i + k, b = i + k + len / 2;
+        const double xr = re[b] * wr - im[b] * wi, xi = re[b] * wi + im[b] * wr;
+        re[b] = re[a] - xr; im[b] = im[a] - xi;
+        re[a] += xr; im[a] += xi;
+      }
+  }
+}
+
+/* sign -1: forward (FFTW_FORWARD, e^{-2 pi i jk/N}); +1: backward, unnormalised */
+static void pm_fft3d(double *re, double *im, int N, int sign) {
+  double *lr = malloc(N * sizeof(double)), *li = malloc(N * sizeof(double));
+  const int st[3] = {N * N, N, 1};
+  for (int ax = 0; ax < 3; ax++) {
+    const int s = st[ax], o1 = st[(ax + 1) % 3], o2 = st[(ax + 2) % 3];
+    for (int a = 0; a < N; a++)
+      for (int b = 0; b < N; b++) {
+        const int base = a * o1 + b * o2;
+        for (int t = 0; t < N; t++) { lr[t] = re[base + t * s]; li[t] = im[base + t * s]; }
+        pm_fft_line(lr, li, N, sign);
+        for (int t = 0; t < N; t++) { re[base + t * s] = lr[t]; im[base + t * s] = li[t]; }
+      }
+  }
+  free(lr);
+  free(li);
+}
+
+static double pm_cic_get(const double *pot, int N, int i, int j, int k, double tx, double ty,
+                         double tz, double dx, double dy, double dz) { /* CIC_get, 69-85 */
+  double temp;
+  temp = pot[pm_id(i + 0, j + 0, k + 0, N)] * tx * ty * tz;
+  temp += pot[pm_id(i + 0, j + 0, k + 1, N)] * tx * ty * dz;
+  temp += pot[pm_id(i + 0, j + 1, k + 0, N)] * tx * dy * tz;
+  temp += pot[pm_id(i + 0, j + 1, k + 1, N)] * tx * dy * dz;
+  temp += pot[pm_id(i + 1, j + 0, k + 0, N)] * dx * ty * tz;
+  temp += pot[pm_id(i + 1, j + 0, k + 1, N)] * dx * ty * dz;
+  temp += pot[pm_id(i + 1, j + 1, k + 0, N)] * dx * dy * tz;
+  temp += pot[pm_id(i + 1, j + 1, k + 1, N)] * dx * dy * dz;
+  return temp;
+}
+
+static void pm_cic_coeffs(const double x[3], const double dim[3], int N, double fac, int ijk[3],
+                          double t[3], double d[3]) {
+  for (int a = 0; a < 3; a++) {
+    const double p = x[a] < 0. ? x[a] + dim[a] : (x[a] >= dim[a] ? x[a] - dim[a] : x[a]);
+    int i = (int)(fac * p);
+    if (i >= N) i = N - 1;
+    ijk[a] = i;
+    d[a] = fac * p - i;
+    t[a] = 1. - d[a];
+  }
+}
+
+API void PFX(pm_mesh)(struct gpart *g, int n, int N, double box, double r_s, float const_G,
+                      double *pot_out) {
+  const size_t N3 = (size_t)N * N * N;
+  double *re = calloc(N3, sizeof(double)), *im = calloc(N3, sizeof(double));
+  const double fac = N / box, dim[3] = {box, box, box};
+  /* CIC assignment (gpart_to_mesh_CIC) */
+  for (int p = 0; p < n; p++) {
+    if (g[p].time_bin == time_bin_inhibited) continue;
+    int c[3];
+    double t[3], d[3];
+    pm_cic_coeffs(g[p].x, dim, N, fac, c, t, d);
+    const double value = (double)g[p].mass * 1.0;
+    const int i = c[0], j = c[1], k = c[2];
+    re[pm_id(i + 0, j + 0, k + 0, N)] += value * t[0] * t[1] * t[2];
+    re[pm_id(i + 0, j + 0, k + 1, N)] += value * t[0] * t[1] * d[2];
+    re[pm_id(i + 0, j + 1, k + 0, N)] += value * t[0] * d[1] * t[2];
+    re[pm_id(i + 0, j + 1, k + 1, N)] += value * t[0] * d[1] * d[2];
+    re[pm_id(i + 1, j + 0, k + 0, N)] += value * d[0] * t[1] * t[2];
+    re[pm_id(i + 1, j + 0, k + 1, N)] += value * d[0] * t[1] * d[2];
+    re[pm_id(i + 1, j + 1, k + 0, N)] += value * d[0] * d[1] * t[2];
+    re[pm_id(i + 1, j + 1, k + 1, N)] += value * d[0] * d[1] * d[2];
+  }
+  pm_fft3d(re, im, N, -1);
+  /* mesh_apply_Green_function */
+  const double green_fac = -1. / (M_PI * box);
+  const double a_smooth2 = 4. * M_PI * M_PI * r_s * r_s / (box * box);
+  const double k_fac = M_PI / (double)N;
+  const int Nh = N / 2;
+  for (int i = 0; i < N; i++) {
+    const int kx = i > Nh ? i - N : i;
+    const double fx = k_fac * kx;
+    const double sx = kx != 0 ? fx / sin(fx) : 1.;
+    for (int j = 0; j < N; j++) {
+      const int ky = j > Nh ? j - N : j;
+      const double fy = k_fac * ky;
+      const double sy = ky != 0 ? fy / sin(fy) : 1.;
+      for (int k = 0; k < N; k++) {
+        const int kz = k > Nh ? k - N : k;
+        const double fz = k_fac * kz;
+        const double sz = kz != 0 ? fz / (sin(fz) + FLT_MIN) : 1.;
+        const double k2 = (double)kx * kx + (double)ky * ky + (double)kz * kz;
+        if (k2 == 0.) continue;
+        const double u = sqrt(k2 * a_smooth2);
+        const double arg = M_PI_2 * u;
+        const double W = arg / (sinh(arg) + FLT_MIN);
+        const double green_cor = green_fac * W / (k2 + FLT_MIN);
+        const double cic = sx * sy * sz, cic2 = cic * cic, cic4 = cic2 * cic2;
+        const double tot = green_cor * cic4;
+        re[(size_t)i * N * N + j * N + k] *= tot;
+        im[(size_t)i * N * N + j * N + k] *= tot;
+      }
+    }
+  }
+  re[0] = 0.;
+  im[0] = 0.;
+  pm_fft3d(re, im, N, +1);
+  /* mesh_to_gpart_CIC + const_G */
+  for (int p = 0; p < n; p++) {
+    struct gpart *gp = &g[p];
+    if (gp->time_bin == time_bin_inhibited) continue;
+    int c[3];
+    double t[3], d[3];
+    pm_cic_coeffs(gp->x, dim, N, fac, c, t, d);
+    const int i = c[0], j = c[1], k = c[2];
+#define PMG(a, b, cc) pm_cic_get(re, N, i + (a), j + (b), k + (cc), t[0], t[1], t[2], d[0], d[1], d[2])
+    double pp = 0., a[3] = {0., 0., 0.};
+    pp += PMG(0, 0, 0);
+    a[0] += (1. / 12.) * PMG(2, 0, 0);
+    a[0] -= (2. / 3.) * PMG(1, 0, 0);
+    a[0] += (2. / 3.) * PMG(-1, 0, 0);
+    a[0] -= (1. / 12.) * PMG(-2, 0, 0);
+    a[1] += (1. / 12.) * PMG(0, 2, 0);
+    a[1] -= (2. / 3.) * PMG(0, 1, 0);
+    a[1] += (2. / 3.) * PMG(0, -1, 0);
+    a[1] -= (1. / 12.) * PMG(0, -2, 0);
+    a[2] += (1. / 12.) * PMG(0, 0, 2);
+    a[2] -= (2. / 3.) * PMG(0, 0, 1);
+    a[2] += (2. / 3.) * PMG(0, 0, -1);
+    a[2] -= (1. / 12.) * PMG(0, 0, -2);
+#undef PMG
+    for (int q = 0; q < 3; q++) {
+      gp->a_grav_mesh[q] = (float)(fac * a[q]);
+      gp->a_grav_mesh[q] *= const_G;
+    }
+    gp->potential_mesh = 0.f;
+    gp->potential_mesh += (float)pp;
+    gp->potential_mesh *= const_G;
+  }
+  if (pot_out) memcpy(pot_out, re, N3 * sizeof(double));
+  free(re);
+  free(im);
+}

@@ -179,6 +179,19 @@ class GravParams(C.Structure):
                 ("consider_truncation_in_MAC", C.c_int32), ("r_cut_max", C.c_double)]
 
 
+class PMParams(C.Structure):
+    """swh_pm_params (swh_gspace_pm_mesh)."""
+
+    _fields_ = [("N", C.c_int32), ("off_a_grav_mesh", C.c_int32),
+                ("off_potential_mesh", C.c_int32), ("reserved", C.c_int32),
+                ("box_size", C.c_double), ("r_s", C.c_double), ("const_G", C.c_double)]
+
+
+# struct gpart (multi-softening) offsets of the mesh fields (swift_compat.h)
+GPART_OFF_A_GRAV_MESH = 56
+GPART_OFF_POTENTIAL_MESH = 72
+
+
 class GCell(C.Structure):
     """swh_gcell: a tree cell's gpart range and progeny."""
 

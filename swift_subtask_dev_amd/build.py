@@ -18,7 +18,8 @@ INCLUDE = REPO / "include"
 LIB = PKG / "libswifthip.so"
 ADAPTER = PKG / "libswifthip_swift.so"
 
-HIP_SOURCES = ["swh_api.hip", "swh_tasks.hip", "swh_space.hip", "swh_hydro.hip", "swh_grav.hip"]
+HIP_SOURCES = ["swh_api.hip", "swh_tasks.hip", "swh_space.hip", "swh_hydro.hip", "swh_grav.hip",
+               "swh_mesh.hip"]
 HIP_HEADERS = ["swh_internal.h", "swh_physics.h", "swh_space.h", "swh_gather.h", "swh_tile.h",
                "swh_tile4.h", "swh_tile5.h", "swh_list.h", "swh_mpole.h"]
 
@@ -63,7 +64,8 @@ def build(force: bool = False, verbose: bool = False) -> Path:
                 print(" ".join(cmd))
             _run(cmd)
     if force or _stale(LIB, objs):
-        _run([_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs)])
+        _run([_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs),
+              "-lhipfft"])
     # SWIFT-signature adapter: plain C against the SWIFT field-name mirrors.
     asrc = CSRC / "swh_swift_adapter.c"
     if asrc.exists() and (force or _stale(ADAPTER, [asrc, LIB, INCLUDE / "swifthip.h",

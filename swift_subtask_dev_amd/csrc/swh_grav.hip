@@ -553,6 +553,7 @@ swh_status swh_gspace_destroy(swh_gspace* g) {
                     &g->pairs,    &g->counter,  &g->cell_act, &g->ftens,  &g->m2l_off,
                     &g->m2l_src,  &g->l2l_list, &g->leaf_ids};
   for (DevBuf* b : bufs) b->release();
+  mesh_release(g);
   (void)hipStreamDestroy(g->stream);
   delete g;
   return SWH_OK;
@@ -578,6 +579,10 @@ swh_status swh_gspace_upload(swh_gspace* g, const void* gparts, int64_t count,
   SWH_TRY(g->accel.reserve((size_t)count * sizeof(double4)));
   SWH_TRY(g->oagn.reserve((size_t)count * sizeof(float)));
   g->mpoles_valid = false;
+  // nothing accumulated yet: a download before any batch (e.g. after only
+  // swh_gspace_pm_mesh) returns the records with their mesh fields alone
+  SWH_HIP(hipMemsetAsync(g->active.ptr, 0, (size_t)count, g->stream));
+  SWH_HIP(hipMemsetAsync(g->accel.ptr, 0, (size_t)count * sizeof(double4), g->stream));
   SWH_HIP(hipMemcpyAsync(g->aos.ptr, gparts, (size_t)count * L.stride,
                          on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
                          g->stream));

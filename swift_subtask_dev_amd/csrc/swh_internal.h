@@ -235,4 +235,15 @@ struct swh_gspace {
   std::vector<int32_t> l2l_depth_off;  // l2l_list range of each depth
   swh::DevBuf leaf_ids;          // int: the unsplit cells
   int32_t nleaf_cells = 0;
+  // PM mesh (swh_gspace_pm_mesh): density / potential mesh, its r2c
+  // transform and the cached hipFFT plans of side mesh_N
+  swh::DevBuf mesh_rho, mesh_frho;
+  int32_t mesh_N = 0;
+  bool mesh_plans_valid = false;
+  void* mesh_fwd = nullptr;
+  void* mesh_inv = nullptr;
 };
+
+namespace swh {
+void mesh_release(swh_gspace* g);  // swh_mesh.hip: mesh buffers and hipFFT plans
+}

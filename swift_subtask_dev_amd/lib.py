@@ -42,7 +42,7 @@ HIP_SYMBOLS = [
     "swh_gspace_destroy", "swh_gspace_upload", "swh_gspace_set_leaves", "swh_grav_pp_batch",
     "swh_gspace_make_multipoles", "swh_space_upload_xparts", "swh_space_drift",
     "swh_gspace_set_tree", "swh_grav_tree", "swh_gspace_field_tensors",
-    "swh_gspace_download", "swh_gspace_sync",
+    "swh_gspace_download", "swh_gspace_sync", "swh_gspace_pm_mesh",
 ]
 ADAPTER_SYMBOLS = [
     "swifthip_swift_init", "swifthip_swift_finalize", "swifthip_swift_last_error",
@@ -135,6 +135,7 @@ def load() -> C.CDLL:
         "swh_gspace_field_tensors": (C.c_int, [vp, vp]),
         "swh_gspace_download": (C.c_int, [vp, vp, P(abi.GPartLayout), C.c_int]),
         "swh_gspace_sync": (C.c_int, [vp]),
+        "swh_gspace_pm_mesh": (C.c_int, [vp, P(abi.PMParams), vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -462,3 +463,15 @@ class GravSpace:
 
     def sync(self):
         _check(self._lib.swh_gspace_sync(self.handle), "gspace_sync")
+
+    def pm_mesh(self, N: int, box_size: float, r_s: float, const_G: float = 1.0,
+                want_potential: bool = False):
+        """PM long-range gravity (swh_gspace_pm_mesh): the records' a_grav_mesh /
+        potential_mesh are set on the device (download returns them); returns
+        the N^3 potential mesh if asked."""
+        M = abi.PMParams(N, abi.GPART_OFF_A_GRAV_MESH, abi.GPART_OFF_POTENTIAL_MESH, 0,
+                         box_size, r_s, const_G)
+        pot = np.zeros((N, N, N), dtype=np.float64) if want_potential else None
+        _check(self._lib.swh_gspace_pm_mesh(self.handle, C.byref(M),
+                                            _ptr(pot) if pot is not None else None), "pm_mesh")
+        return pot

@@ -74,6 +74,7 @@ def load(prec: str = "f32") -> C.CDLL:
     sig("grav_p2m", None, [vp, C.c_int, P(abi.Multipole)])
     sig("grav_tree", None, [vp, C.c_int, vp, C.c_int, vp, C.c_int, vp, C.c_int,
                             P(abi.GravParams), vp, vp])
+    sig("pm_mesh", None, [vp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_float, vp])
     if prec == "f32":
         for n in ("iact_density", "iact_force", "iact_gradient"):
             sig(n, None, [real, P(real), real, real, vp, vp, real, real])

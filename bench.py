@@ -340,8 +340,6 @@ def run_grav(args, ctx, rank, world, dist, torch):
                          "traffic": None, "flops_model": "28 flops per directed P2P interaction"},
             "cpu_baseline": None,
         }
-        if breakdown:
-            out["step_breakdown"] = breakdown
         print(json.dumps(out), flush=True)
     sp.close()
 

@@ -49,6 +49,9 @@ S_IN_FORCE, S_OUT_FORCE = 77, 21
 FLOPS_DENSITY, FLOPS_FORCE = 65, 146   # SURVEY 8d flops per directed interaction
 
 
+RED_DEVICE = "cuda"  # device of the max/sum-over-ranks tensors
+
+
 def log(msg):
     print(msg, file=sys.stderr, flush=True)
 
@@ -316,8 +319,8 @@ def run_grav(args, ctx, rank, world, dist, torch):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    tot = torch.tensor([float(n_int) * args.steps], dtype=torch.float64, device="cuda")
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    tot = torch.tensor([float(n_int) * args.steps], dtype=torch.float64, device=RED_DEVICE)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=RED_DEVICE)
     if dist:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -383,17 +386,27 @@ def main():
 
     import torch
 
-    torch.cuda.set_device(local_rank)
+    # one rank per GPU; SWH_BENCH_BACKEND=gloo rehearses the multi-rank path
+    # with several ranks sharing the GPUs there are (halo buffers staged
+    # through the host) -- the driver's runs use RCCL, one GPU per rank
+    global RED_DEVICE
+    backend = os.environ.get("SWH_BENCH_BACKEND", "nccl")
+    RED_DEVICE = "cuda" if backend == "nccl" else "cpu"  # gloo reduces host tensors
+    device = local_rank % max(1, torch.cuda.device_count()) if backend == "gloo" else local_rank
+    torch.cuda.set_device(device)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
 
     from swift_subtask_dev_amd import abi, decomp, ics, lib
 
     if args.workload == "grav":
-        ctx = lib.Context(local_rank, args.precision)
+        ctx = lib.Context(device, args.precision)
         run_grav(args, ctx, rank, world, dist, torch)
         ctx.close()
         if dist:
@@ -417,7 +430,7 @@ def main():
         box = (float(nslab), 1.0, 1.0)
     P = abi.default_hydro_params(box, True)
     P.max_active_bin = 1
-    ctx = lib.Context(local_rank, args.precision)
+    ctx = lib.Context(device, args.precision)
 
     # ---- untimed setup: the full SPHENIX chain on the whole box ----------
     sp = lib.HydroSpace(ctx)
@@ -502,8 +515,8 @@ def main():
     t_force = [e[2].elapsed_time(e[3]) * 1e-3 for e in events]
 
     tot = torch.tensor([float(n_density + n_force) * args.steps, float(n_owned)],
-                       dtype=torch.float64, device="cuda")
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+                       dtype=torch.float64, device=RED_DEVICE)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=RED_DEVICE)
     if dist:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)

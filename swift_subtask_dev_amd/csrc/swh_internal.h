@@ -180,6 +180,7 @@ struct swh_space {
   // particle (positions relative to it in posf stay valid when it drifts out)
   swh::DevBuf vfull_c, agrav_c, hasg_c, xdiff, pcell, cell_lin;
   bool xparts_valid = false;
+  double vfull_max = 0.;  // max |v_full| of the uploaded xparts (drift displacement bound)
   // grid
   swh::DevBuf cell_start;  // int32[ncell+1], indexed by Morton rank
   swh::DevBuf cell_rank;   // int32[ncell]: linear cell -> Morton rank

@@ -419,6 +419,18 @@ struct DriftParams {
 // (hydro.h:1012-1066) per particle; float fields in the reference's float
 // arithmetic, positions in double. dx_bits / h_bits: running maxima of the
 // displacement since the rebuild and of h (float bits, positive).
+// max |v_full| over the xparts (float bits; |v| >= 0 orders as its bits)
+__global__ void vmax_kernel(const float4* __restrict__ vfull, int64_t n, unsigned int* vbits) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float v = 0.f;
+  if (s < n) {
+    const float4 q = vfull[s];
+    v = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z);
+  }
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0 && v > 0.f) atomicMax(vbits, __float_as_uint(v));
+}
+
 __global__ void drift_kernel(SoA a, const float4* __restrict__ vfull,
                              const float4* __restrict__ agrav, const int8_t* __restrict__ hasg,
                              float4* __restrict__ xdiff, int64_t n, DriftParams D,
@@ -722,7 +734,20 @@ swh_status swh_space_upload_xparts(swh_space* s, const void* xparts, int64_t cou
                      *XL, s->tmp_soa.as<const char>(), count, s->vfull_c.as<float4>(),
                      s->agrav_c.as<float4>());
   SWH_HIP(hipGetLastError());
-  if (!on_device) SWH_HIP(hipStreamSynchronize(s->stream));
+  // the fastest particle bounds every displacement of the following drifts
+  // (v_full is fixed until the next upload), so the drift needs no read-back
+  SWH_TRY(s->counters.reserve(128));
+  unsigned int* vbits = s->counters.as<unsigned int>() + 21;
+  SWH_HIP(hipMemsetAsync(vbits, 0, sizeof(unsigned int), s->stream));
+  hipLaunchKernelGGL(vmax_kernel, dim3((int)((count + 255) / 256)), dim3(256), 0, s->stream,
+                     s->vfull_c.as<const float4>(), count, vbits);
+  SWH_HIP(hipGetLastError());
+  unsigned int vb = 0;
+  SWH_HIP(hipMemcpyAsync(&vb, vbits, sizeof(vb), hipMemcpyDeviceToHost, s->stream));
+  SWH_HIP(hipStreamSynchronize(s->stream));
+  float vmax;
+  std::memcpy(&vmax, &vb, sizeof(vmax));
+  s->vfull_max = (double)vmax;
   s->xparts_valid = true;
   return SWH_OK;
 }
@@ -749,22 +774,13 @@ swh_status swh_space_drift(swh_space* s, const swh_drift_params* D, const swh_hy
                      s->hasg_c.as<const int8_t>(), s->xdiff.as<float4>(), s->n, dp, dx_bits,
                      ctr + 2);
   SWH_HIP(hipGetLastError());
-  unsigned int h[2] = {0, 0};
-  SWH_HIP(hipMemcpyAsync(&h[0], dx_bits, sizeof(unsigned int), hipMemcpyDeviceToHost, st));
-  SWH_HIP(hipMemcpyAsync(&h[1], ctr + 2, sizeof(unsigned int), hipMemcpyDeviceToHost, st));
-  SWH_HIP(hipStreamSynchronize(st));
-  float dmax, hmax;
-  std::memcpy(&dmax, &h[0], sizeof(float));
-  std::memcpy(&hmax, &h[1], sizeof(float));
-  // every loop widens its reach by the displacement (plus float slack)
-  s->grid.dx = std::max(s->grid.dx, (double)dmax * (1. + 1e-6) + 1e-12);
+  // every loop widens its reach by the displacement since the rebuild: bounded
+  // by |v_full|_max * dt per drift (the drift kernel keeps the exact per-particle
+  // offsets for the next rebuild); no device read-back, the drift stays
+  // asynchronous. The periodic reach check (h grown past half the box) runs
+  // at the next ghost and rebuild.
+  s->grid.dx += s->vfull_max * std::fabs(D->dt_drift) * (1. + 1e-6) + 1e-12;
   s->list_valid = false;  // positions moved
-  if (s->grid.periodic &&
-      (double)hmax * kGamma + s->grid.dx >=
-          0.5 * std::min(s->grid.dim[0], std::min(s->grid.dim[1], s->grid.dim[2]))) {
-    set_error("Cell smaller than smoothing length after the drift: rebuild");
-    return SWH_ERR_CELL_SMALL;
-  }
   return SWH_OK;
 }
 

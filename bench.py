@@ -347,6 +347,137 @@ def run_grav(args, ctx, rank, world, dist, torch):
     sp.close()
 
 
+def run_cosmo(args, ctx, rank, world, dist, torch):
+    """BASELINE config 5 stand-in (SmallCosmoVolume hydro + self-gravity,
+    small_cosmo_volume.yml: 64^3 gas + 64^3 DM, softening 1/25 of the mean
+    separation, PM mesh 64, a_smooth 1.25, r_cut_max 4.5 r_s, adaptive MAC
+    epsilon_fmm 0.001, theta_cr 0.7, cell_split_size 50), in box units.
+    One step = the hydro density + force loops on the gas (the headline's
+    loops) and the gravity of every gpart: the recursive gravity tasks over
+    the cell tree (P2P, M2P, M2L, L2L, L2P) plus the PM mesh. Hydro and gravity
+    run on two streams from two host threads (the two task families of a
+    SWIFT step overlap); the line reports each alone and both together.
+    The MAC is the geometric theta_cr = 0.7 one (SWH_COSMO_ADAPTIVE_MAC=1: the
+    yml's adaptive MAC, whose |a| estimates the stand-in's units do not
+    reproduce: it accepts no M2L here). The recursive walk itself runs on the
+    host (swh_grav_tree): it dominates this step."""
+    import threading
+    from swift_subtask_dev_amd import abi, ics, lib
+
+    if world > 1:
+        raise SystemExit("--workload cosmo runs on one GPU (the driver's multi-GPU runs use sedov)")
+    n = args.n if args.n != 128 else 64
+    t0 = time.time()
+    gas = ics.sedov_slabs(n, 1)
+    gas["u"] = 1.0e-6 / (ics.GAMMA - 1.0)  # a cold uniform medium, no blast
+    P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
+    P.max_active_bin = 1
+    sp = lib.HydroSpace(ctx)
+    sp.upload(gas)
+    sp.rebuild(P)
+    sp.hydro_step(P)  # converged h, the force inputs
+    sp.download(gas, abi.FIELDS_ALL)
+    sp.close()
+    # gparts: the gas + as many DM particles, softening 1/25 of the mean spacing
+    eps = 1.0 / (25.0 * n)
+    dm = ics.uniform_gravity_box(n, epsilon=eps, seed=65)
+    gp = abi.new_gparts(2 * n ** 3)
+    gp[: n ** 3] = dm
+    gp["x"][n ** 3:] = gas["x"]
+    gp["mass"][n ** 3:] = gas["mass"]
+    gp["mass"] *= 0.5
+    gp["epsilon"] = eps
+    gp["time_bin"] = 1
+    gp["type"][n ** 3:] = 0
+    N_mesh = 64
+    r_s = 1.25 / N_mesh
+    G = abi.GravParams(1, (C.c_float * 3)(1, 1, 1), 1.0 / r_s, 0.1 * r_s, abi.NUM_TIME_BINS)
+    G.theta_crit = 0.7
+    G.adaptive_tolerance = 1e-3
+    G.use_advanced_MAC = int(os.environ.get("SWH_COSMO_ADAPTIVE_MAC", "0"))
+    G.r_cut_max = 4.5 * r_s
+    g, cells, tops = ics.gravity_tree(gp, 8, split_size=50)
+    pairs = ics.top_level_pairs(tops)
+    gs = lib.GravSpace(ctx)
+    # one untimed step gives the adaptive MAC its |a| estimate (old_a_grav_norm)
+    gs.upload(g)
+    gs.set_tree(cells)
+    g0 = abi.copy_parts(g)
+    G.use_advanced_MAC = 0
+    gs.tree(G, tops, pairs)
+    gs.download(g0)
+    g["old_a_grav_norm"] = np.linalg.norm(g0["a_grav"].astype(np.float64), axis=1)
+    G.use_advanced_MAC = int(os.environ.get("SWH_COSMO_ADAPTIVE_MAC", "0"))
+    gs.upload(g)
+    gs.set_tree(cells)
+    stats = gs.tree(G, tops, pairs)
+    gs.pm_mesh(N_mesh, 1.0, r_s, 1.0)
+
+    hs = lib.HydroSpace(ctx)
+    hstream = torch.cuda.Stream()
+    hs.set_stream(hstream.cuda_stream)
+    hs.upload(gas)
+    hs.rebuild(P)
+    hs.init_parts(P)
+    n_density = hs.density(P)
+    hs.reset_acceleration(P)
+    n_force = hs.force(P)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] cosmo setup {time.time() - t0:.1f}s: {n ** 3} gas + {n ** 3} DM gparts, "
+        f"{len(cells)} cells; gravity step {stats}; hydro {n_density} + {n_force}")
+
+    def hydro():
+        hs.init_parts(P)
+        hs.density(P, count=False)
+        hs.reset_acceleration(P)
+        hs.force(P, count=False)
+        hs.sync()
+
+    def gravity():
+        gs.tree(G, tops, pairs)  # the device accumulators restart at every walk
+        gs.pm_mesh(N_mesh, 1.0, r_s, 1.0)
+        gs.sync()
+
+    def both():
+        th = threading.Thread(target=gravity)
+        th.start()
+        hydro()
+        th.join()
+
+    def timed(fn):
+        for _ in range(args.warmup):
+            fn()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / args.steps
+
+    t_h, t_g, t_b = timed(hydro), timed(gravity), timed(both)
+    total = float(n_density + n_force + stats["n_pp"])
+    out = {
+        "metric": "hydro (density+force) + gravity P2P interactions/s, SmallCosmoVolume stand-in",
+        "value": total / t_b, "unit": "interactions/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": t_b * 1e3, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (64^3 perturbed-lattice gas + 64^3 uniform DM; SmallCosmoVolume ICs "
+                "unavailable offline)",
+        "config": {"workload": f"SmallCosmoVolume stand-in: {n}^3 gas + {n}^3 DM, hydro density + "
+                               "force loops || gravity tree (P2P, M2P, M2L, L2L, L2P) + PM mesh 64",
+                   "hydro_interactions_per_step": n_density + n_force,
+                   "gravity_tree_stats": stats, "cells": int(len(cells)),
+                   "softening": eps, "r_s": r_s},
+        "step_ms": {"hydro_alone": t_h * 1e3, "gravity_alone": t_g * 1e3,
+                    "overlapped": t_b * 1e3,
+                    "overlap_gain": (t_h + t_g) / t_b},
+        "roofline": None, "cpu_baseline": None,
+    }
+    print(json.dumps(out), flush=True)
+    hs.close()
+    gs.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -374,10 +505,11 @@ def main():
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong: the 128^3 box split over the GPUs (the metric); "
                          "weak: one 128^3 box per GPU")
-    ap.add_argument("--workload", default="sedov", choices=["sedov", "grav", "eagle"],
+    ap.add_argument("--workload", default="sedov", choices=["sedov", "grav", "eagle", "cosmo"],
                     help="sedov: the headline metric (SedovBlast_3D 128^3 density + force); "
                          "grav: BASELINE config 4 (uniform DM box P2P, --n 256); "
-                         "eagle: BASELINE config 3 stand-in (clustered box)")
+                         "eagle: BASELINE config 3 stand-in (clustered box); "
+                         "cosmo: BASELINE config 5 stand-in (hydro + tree/PM gravity, overlapped)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -405,9 +537,9 @@ def main():
 
     from swift_subtask_dev_amd import abi, decomp, ics, lib
 
-    if args.workload == "grav":
+    if args.workload in ("grav", "cosmo"):
         ctx = lib.Context(device, args.precision)
-        run_grav(args, ctx, rank, world, dist, torch)
+        (run_grav if args.workload == "grav" else run_cosmo)(args, ctx, rank, world, dist, torch)
         ctx.close()
         if dist:
             dist.destroy_process_group()

@@ -19,6 +19,12 @@
 // i-particle that passes gravity_M2P_accept against the source leaf's
 // multipole (float test, swh_mpole.h) skips that leaf's P2P tiles (zero mass)
 // and takes M2P instead, in m2p_kernel; leaf multipoles come from p2m_kernel.
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
 #include "swh_internal.h"
 #include "swh_mpole.h"
 #include "swh_physics.h"
@@ -206,10 +212,10 @@ __device__ __forceinline__ void p2p_pair(double dx, double dy, double dz, double
   pot += pot_ij;
 }
 
-// One LDS tile against this thread's kIPer i-particles: every j entry is read
-// once and used kIPer times. SELF: the tile may hold an i itself (the
+// One LDS tile against this thread's IPER i-particles: every j entry is read
+// once and used IPER times. SELF: the tile may hold an i itself (the
 // i-leaf's own leaf), whose term is removed by a zero mass.
-template <bool TRUNC, bool PERIODIC, bool SELF>
+template <bool TRUNC, bool PERIODIC, bool SELF, int IPER>
 __device__ __forceinline__ void p2p_tile(const double* sx, const double* sy, const double* sz,
                                          const double* se2, const double* sh, const float* sm,
                                          int nt, const int* self_local, const double* xi,
@@ -221,7 +227,7 @@ __device__ __forceinline__ void p2p_tile(const double* sx, const double* sy, con
     const double xj = sx[t], yj = sy[t], zj = sz[t], e2j = se2[t], hvj = sh[t];
     const double mj = (double)sm[t];
 #pragma unroll
-    for (int k = 0; k < kIPer; k++) {
+    for (int k = 0; k < IPER; k++) {
       double dx = xj - xi[k], dy = yj - yi[k], dz = zj - zi[k];
       if (PERIODIC) {
         dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
@@ -238,18 +244,19 @@ __device__ __forceinline__ void p2p_tile(const double* sx, const double* sy, con
 
 // Per pair: which of this thread's i-particles take the source leaf's
 // multipole instead (allow_mpole pairs only; block-uniform branch).
+template <int IPER>
 __device__ __forceinline__ void mpole_mask(const GSoA& g, const MacParams& P,
                                            const swh_leaf_pair& pr, const swh_leaf& J,
                                            const bool* act, const int* gi, bool* actp) {
   const bool mp = pr.allow_mpole && J.count > 1;
   if (!mp) {
 #pragma unroll
-    for (int k = 0; k < kIPer; k++) actp[k] = act[k];
+    for (int k = 0; k < IPER; k++) actp[k] = act[k];
     return;
   }
   const MacSource B = mac_source(g.mp[pr.j]);
 #pragma unroll
-  for (int k = 0; k < kIPer; k++) {
+  for (int k = 0; k < IPER; k++) {
     bool use = false;
     if (act[k]) {
       const double4 p = g.pos[gi[k]];
@@ -259,14 +266,17 @@ __device__ __forceinline__ void mpole_mask(const GSoA& g, const MacParams& P,
   }
 }
 
-template <bool MPOLE>
-__global__ __launch_bounds__(kGravBlock) void p2p_kernel(
+// BLK threads per i-leaf workgroup, IPER i-particles per thread: 256 x 2 for
+// the ~400-particle leaves of space_splitsize, 64 x 1 for the small leaves of
+// a deep tree (cell_split_size 50), so the lanes are not left idle.
+template <bool MPOLE, int BLK, int IPER>
+__global__ __launch_bounds__(BLK) void p2p_kernel(
     GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
     const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
     double dimz, double r_s_inv, MacParams mac, unsigned long long* counter) {
-  __shared__ double sx[kGravBlock], sy[kGravBlock], sz[kGravBlock], se2[kGravBlock],
-      sh[kGravBlock];
-  __shared__ float sm[kGravBlock];
+  __shared__ double sx[BLK], sy[BLK], sz[BLK], se2[BLK],
+      sh[BLK];
+  __shared__ float sm[BLK];
   const int li = xcd_block_id();
   const swh_leaf L = leaves[li];
   const int p0 = pair_off[li], p1 = pair_off[li + 1];
@@ -274,14 +284,14 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel(
   // whose blocks update the same particles)
   if (p0 == p1) return;
   unsigned long long nint = 0;
-  for (int ibase = 0; ibase < L.count; ibase += kGravBlock * kIPer) {
-    int gi[kIPer], self_local[kIPer];
-    double xi[kIPer], yi[kIPer], zi[kIPer], hi2[kIPer], hv[kIPer];
-    double ax[kIPer], ay[kIPer], az[kIPer], pot[kIPer];
-    bool act[kIPer];
+  for (int ibase = 0; ibase < L.count; ibase += BLK * IPER) {
+    int gi[IPER], self_local[IPER];
+    double xi[IPER], yi[IPER], zi[IPER], hi2[IPER], hv[IPER];
+    double ax[IPER], ay[IPER], az[IPER], pot[IPER];
+    bool act[IPER];
 #pragma unroll
-    for (int k = 0; k < kIPer; k++) {
-      const int local = ibase + k * kGravBlock + (int)threadIdx.x;
+    for (int k = 0; k < IPER; k++) {
+      const int local = ibase + k * BLK + (int)threadIdx.x;
       gi[k] = L.start + local;
       act[k] = local < L.count && g.active[gi[k]];
       const double4 p = act[k] ? g.pos[gi[k]] : make_double4(0., 0., 0., 1.);
@@ -293,15 +303,15 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel(
     for (int q = p0; q < p1; q++) {
       const swh_leaf_pair pr = pairs[q];
       const swh_leaf J = leaves[pr.j];
-      bool actp[kIPer];  // act minus the particles taking this leaf's multipole
+      bool actp[IPER];  // act minus the particles taking this leaf's multipole
       if (MPOLE) {
-        mpole_mask(g, mac, pr, J, act, gi, actp);
+        mpole_mask<IPER>(g, mac, pr, J, act, gi, actp);
       } else {
 #pragma unroll
-        for (int k = 0; k < kIPer; k++) actp[k] = act[k];
+        for (int k = 0; k < IPER; k++) actp[k] = act[k];
       }
-      for (int jbase = 0; jbase < J.count; jbase += kGravBlock) {
-        const int nt = min(kGravBlock, J.count - jbase);
+      for (int jbase = 0; jbase < J.count; jbase += BLK) {
+        const int nt = min(BLK, J.count - jbase);
         __syncthreads();
         if ((int)threadIdx.x < nt) {
           const int gj = J.start + jbase + (int)threadIdx.x;
@@ -318,13 +328,13 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel(
         // overlapping it (block-uniform test)
         const bool self = J.start + jbase < L.start + L.count && L.start < J.start + jbase + nt;
 #pragma unroll
-        for (int k = 0; k < kIPer; k++) {
+        for (int k = 0; k < IPER; k++) {
           self_local[k] = gi[k] - (J.start + jbase);
           if (actp[k])
             nint += (unsigned long long)(nt - ((self_local[k] >= 0 && self_local[k] < nt) ? 1 : 0));
         }
 #define SWH_P2P_TILE(TR, PE, SE)                                                             \
-  p2p_tile<TR, PE, SE>(sx, sy, sz, se2, sh, sm, nt, self_local, xi, yi, zi, hi2, hv, actp, dimx, \
+  p2p_tile<TR, PE, SE, IPER>(sx, sy, sz, se2, sh, sm, nt, self_local, xi, yi, zi, hi2, hv, actp, dimx, \
                        dimy, dimz, r_s_inv, ax, ay, az, pot)
         if (self) {
           if (pr.truncated) {
@@ -347,7 +357,7 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel(
       }
     }
 #pragma unroll
-    for (int k = 0; k < kIPer; k++) {
+    for (int k = 0; k < IPER; k++) {
       if (!act[k]) continue;
       double4 a = g.acc[gi[k]];
       a.x += ax[k];
@@ -398,7 +408,7 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
       const swh_leaf_pair pr = pairs[q];
       const swh_leaf J = leaves[pr.j];
       bool actp[kIPer];
-      mpole_mask(g, mac, pr, J, act, gi, actp);
+      mpole_mask<kIPer>(g, mac, pr, J, act, gi, actp);
       for (int jbase = 0; jbase < J.count; jbase += kGravBlock) {
         const int nt = min(kGravBlock, J.count - jbase);
         __syncthreads();
@@ -603,7 +613,6 @@ swh_status swh_gspace_set_leaves(swh_gspace* g, const swh_leaf* leaves, int32_t 
                 leaves[i].count, (long long)g->n);
       return SWH_ERR_ARG;
     }
-    maxc = std::max(maxc, leaves[i].count);
   }
   if (nleaves > 0 && (pair_offset[0] != 0 || pair_offset[nleaves] != npairs)) {
     set_error("pair_offset must run 0..npairs");
@@ -614,6 +623,9 @@ swh_status swh_gspace_set_leaves(swh_gspace* g, const swh_leaf* leaves, int32_t 
       set_error("pair %d names leaf %d of %d", q, pairs[q].j, nleaves);
       return SWH_ERR_ARG;
     }
+  // the largest i-leaf that has sources (sizes the P2P workgroups)
+  for (int i = 0; i < nleaves; i++)
+    if (pair_offset[i + 1] > pair_offset[i]) maxc = std::max(maxc, leaves[i].count);
   SWH_HIP(hipSetDevice(g->ctx->device));
   SWH_TRY(g->leaves.reserve((size_t)std::max(1, nleaves) * sizeof(swh_leaf)));
   SWH_TRY(g->pair_off.reserve((size_t)(nleaves + 1) * sizeof(int32_t)));
@@ -698,9 +710,12 @@ swh_status launch_pp(swh_gspace* g, const swh_grav_params* G, const MacParams& m
                      unsigned long long* ctr) {
   const bool f64 = g->ctx->precision == SWH_PRECISION_F64;
   if (f64) {
-    // the multipole-free instance keeps the P2P kernel's register budget
-    auto k = g->any_mpole ? p2p_kernel<true> : p2p_kernel<false>;
-    hipLaunchKernelGGL(k, dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
+    // the multipole-free instance keeps the P2P kernel's register budget;
+    // small leaves (a deep tree) take one wave per i-leaf
+    const bool small = g->max_leaf <= 64;
+    auto k = g->any_mpole ? (small ? p2p_kernel<true, 64, 1> : p2p_kernel<true, kGravBlock, kIPer>)
+                          : (small ? p2p_kernel<false, 64, 1> : p2p_kernel<false, kGravBlock, kIPer>);
+    hipLaunchKernelGGL(k, dim3(g->nleaves), dim3(small ? 64 : kGravBlock), 0, g->stream,
                        gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
                        g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
                        (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, mac, ctr);
@@ -883,8 +898,11 @@ struct TreeWalk {
   const int8_t* act;
   const swh_grav_params* G;
   MacParams mac;
-  std::vector<std::vector<swh_leaf_pair>> pp;  // per i-cell
-  std::vector<std::vector<int2>> mm;           // per target cell: {source, symmetric}
+  // the tasks' entries in walk order: {i-cell, P-P entry} and {target, {source,
+  // symmetric}} (grouped per cell afterwards, stably, so the lists are the
+  // serial walk's whatever the threads)
+  std::vector<std::pair<int, swh_leaf_pair>> pp;
+  std::vector<std::pair<int, int2>> mm;
   int64_t skipped = 0;
 
   double nearest(double d, int k) const {
@@ -908,7 +926,7 @@ struct TreeWalk {
       e.j = c;
       e.truncated = G->periodic && (2. * mp[c].r_max > G->r_cut_min);
       e.allow_mpole = 0;
-      pp[c].push_back(e);
+      pp.emplace_back(c, e);
     }
   }
   // runner_dopair_grav_pp_no_cache (1440-1483): ci's leaves <- all of cj
@@ -923,19 +941,19 @@ struct TreeWalk {
       e.j = cj;
       e.truncated = G->periodic ? 1 : 0;
       e.allow_mpole = 0;
-      pp[ci].push_back(e);
+      pp.emplace_back(ci, e);
     }
   }
   // runner_dopair_grav_mm (2050-2064): symmetric when both are active
   void mmpair(int ci, int cj) {
     const bool di = act[ci], dj = act[cj];
     if (di && dj) {
-      mm[ci].push_back(make_int2(cj, 1));
-      mm[cj].push_back(make_int2(ci, 1));
+      mm.emplace_back(ci, make_int2(cj, 1));
+      mm.emplace_back(cj, make_int2(ci, 1));
     } else if (di) {
-      mm[ci].push_back(make_int2(cj, 0));
+      mm.emplace_back(ci, make_int2(cj, 0));
     } else if (dj) {
-      mm[cj].push_back(make_int2(ci, 0));
+      mm.emplace_back(cj, make_int2(ci, 0));
     }
   }
   // runner_dopair_grav_pp(ci, cj, symmetric = 1, allow_mpole = 1) (1202-1425):
@@ -953,8 +971,8 @@ struct TreeWalk {
       trunc = (std::sqrt(d2) + (double)(float)mp[ci].r_max + (double)(float)mp[cj].r_max) >
               G->r_cut_min;
     }
-    if (act[ci]) pp[ci].push_back(swh_leaf_pair{cj, trunc, 1});
-    if (act[cj]) pp[cj].push_back(swh_leaf_pair{ci, trunc, 1});
+    if (act[ci]) pp.emplace_back(ci, swh_leaf_pair{cj, trunc, 1});
+    if (act[cj]) pp.emplace_back(cj, swh_leaf_pair{ci, trunc, 1});
   }
   // runner_dopair_recursive_grav (2208-2374)
   void pair(int ci, int cj) {
@@ -1125,27 +1143,63 @@ swh_status swh_grav_tree(swh_gspace* g, const swh_grav_params* G, const int32_t*
                          hipMemcpyDeviceToHost, g->stream));
   SWH_HIP(hipMemcpyAsync(act.data(), g->cell_act.ptr, ncells, hipMemcpyDeviceToHost, g->stream));
   SWH_HIP(hipStreamSynchronize(g->stream));
-  // the walk
-  TreeWalk w;
-  w.cells = g->tree.data();
-  w.mp = mp.data();
-  w.act = act.data();
-  w.G = G;
-  w.mac = mac_params(G);
-  w.pp.resize(ncells);
-  w.mm.resize(ncells);
-  for (int k = 0; k < nself; k++) w.self(self_cells[k]);
-  for (int k = 0; k < npair; k++) w.pair(pair_cells[2 * k], pair_cells[2 * k + 1]);
-  // P-P lists (CSR over i-cells) and M-M lists (CSR over targets)
-  std::vector<int32_t> poff(ncells + 1, 0), moff(ncells + 1, 0);
-  std::vector<swh_leaf_pair> pairs;
-  std::vector<int2> msrc;
-  for (int c = 0; c < ncells; c++) {
-    pairs.insert(pairs.end(), w.pp[c].begin(), w.pp[c].end());
-    poff[c + 1] = (int32_t)pairs.size();
-    msrc.insert(msrc.end(), w.mm[c].begin(), w.mm[c].end());
-    moff[c + 1] = (int32_t)msrc.size();
+  // the walk: the self and pair tasks in chunks of consecutive tasks spread
+  // over host threads (the recursive tasks are independent, as SWIFT's runners
+  // execute them); each chunk keeps its entries, and the chunks are joined in
+  // task order, so the lists equal a serial walk's
+  const int64_t ntask = (int64_t)nself + npair;
+  constexpr int64_t kChunk = 64;
+  const int64_t nchunk = (ntask + kChunk - 1) / kChunk;
+  std::vector<TreeWalk> part((size_t)nchunk);
+  const MacParams mac = mac_params(G);
+  std::atomic<int64_t> next{0};
+  auto worker = [&]() {
+    for (int64_t ch = next++; ch < nchunk; ch = next++) {
+      TreeWalk& w = part[(size_t)ch];
+      w.cells = g->tree.data();
+      w.mp = mp.data();
+      w.act = act.data();
+      w.G = G;
+      w.mac = mac;
+      const int64_t t1 = std::min(ntask, (ch + 1) * kChunk);
+      for (int64_t t = ch * kChunk; t < t1; t++) {
+        if (t < nself) w.self(self_cells[t]);
+        else w.pair(pair_cells[2 * (t - nself)], pair_cells[2 * (t - nself) + 1]);
+      }
+    }
+  };
+  int nthr = (int)std::min<int64_t>(nchunk, 16);  // the host share of one GPU
+  if (const char* e = std::getenv("SWH_HOST_THREADS")) nthr = std::max(1, std::atoi(e));
+  nthr = (int)std::max<int64_t>(1, std::min<int64_t>(nthr, nchunk));
+  {
+    std::vector<std::thread> pool;
+    for (int k = 1; k < nthr; k++) pool.emplace_back(worker);
+    worker();
+    for (auto& th : pool) th.join();
   }
+  // P-P lists (CSR over i-cells) and M-M lists (CSR over targets): stable
+  // counting sort of the chunks' entries by cell
+  std::vector<int32_t> poff(ncells + 1, 0), moff(ncells + 1, 0);
+  int64_t skipped = 0;
+  for (const TreeWalk& w : part) {
+    for (const auto& e : w.pp) poff[e.first + 1]++;
+    for (const auto& e : w.mm) moff[e.first + 1]++;
+    skipped += w.skipped;
+  }
+  for (int c = 0; c < ncells; c++) {
+    poff[c + 1] += poff[c];
+    moff[c + 1] += moff[c];
+  }
+  std::vector<swh_leaf_pair> pairs((size_t)poff[ncells]);
+  std::vector<int2> msrc((size_t)moff[ncells]);
+  {
+    std::vector<int32_t> pcur(poff.begin(), poff.end() - 1), mcur(moff.begin(), moff.end() - 1);
+    for (const TreeWalk& w : part) {
+      for (const auto& e : w.pp) pairs[(size_t)pcur[e.first]++] = e.second;
+      for (const auto& e : w.mm) msrc[(size_t)mcur[e.first]++] = e.second;
+    }
+  }
+  part.clear();
   std::vector<swh_leaf> ranges(ncells);
   for (int c = 0; c < ncells; c++) ranges[c] = swh_leaf{g->tree[c].start, g->tree[c].count};
   SWH_TRY(swh_gspace_set_leaves(g, ranges.data(), ncells, poff.data(), pairs.data(),
@@ -1218,7 +1272,7 @@ swh_status swh_grav_tree(swh_gspace* g, const swh_grav_params* G, const int32_t*
     stats->n_m2p = (int64_t)h[1];
     stats->n_m2l = (int64_t)msrc.size();
     stats->n_pp_tasks = (int64_t)pairs.size();
-    stats->n_skipped = w.skipped;
+    stats->n_skipped = skipped;
   }
   return SWH_OK;
 }

@@ -318,7 +318,16 @@ __device__ __forceinline__ void m2l(const float* M, T rx, T ry, T rz, T eps, boo
   m2l_k<T, 0>(M, D, F);
 }
 
-// X_n(d) = d^n / n! for the 35 multi-indices
+// X_n(d) = d^n / n! for the 35 multi-indices (compile-time recursion: every
+// index is a constant, so the arrays stay in registers)
+template <typename T, int t>
+__device__ __forceinline__ void xpowers_t(const T* xp, const T* yp, const T* zp, T* X) {
+  if constexpr (t < SWH_MPOLE_TERMS) {
+    constexpr double inv = 1. / (fact(kMpA[t]) * fact(kMpB[t]) * fact(kMpC[t]));
+    X[t] = xp[kMpA[t]] * yp[kMpB[t]] * zp[kMpC[t]] * (T)inv;
+    xpowers_t<T, t + 1>(xp, yp, zp, X);
+  }
+}
 template <typename T>
 __device__ __forceinline__ void xpowers(T dx, T dy, T dz, T* X) {
   T xp[5], yp[5], zp[5];
@@ -329,10 +338,7 @@ __device__ __forceinline__ void xpowers(T dx, T dy, T dz, T* X) {
     yp[q] = yp[q - 1] * dy;
     zp[q] = zp[q - 1] * dz;
   }
-#pragma unroll
-  for (int t = 0; t < SWH_MPOLE_TERMS; t++)
-    X[t] = xp[kMpA[t]] * yp[kMpB[t]] * zp[kMpC[t]] *
-           (T)(1. / (fact(kMpA[t]) * fact(kMpB[t]) * fact(kMpC[t])));
+  xpowers_t<T, 0>(xp, yp, zp, X);
 }
 
 template <typename T, int k, int n>
@@ -355,20 +361,24 @@ __device__ __forceinline__ void l2l_k(const T* X, const T* Fp, T* F) {
 
 // gravity_L2P: {potential, a_x, a_y, a_z} at offset d from the tensor's centre
 // (F: the tensor in fp64, e.g. staged in LDS)
+template <typename T, int t>
+__device__ __forceinline__ void l2p_t(const double* F, const T* X, T& pot, T& ax, T& ay, T& az) {
+  if constexpr (t < SWH_MPOLE_TERMS) {
+    pot -= X[t] * (T)F[t];
+    if constexpr (mp_order(t) <= 3) {
+      ax += X[t] * (T)F[mp_index(kMpA[t] + 1, kMpB[t], kMpC[t])];
+      ay += X[t] * (T)F[mp_index(kMpA[t], kMpB[t] + 1, kMpC[t])];
+      az += X[t] * (T)F[mp_index(kMpA[t], kMpB[t], kMpC[t] + 1)];
+    }
+    l2p_t<T, t + 1>(F, X, pot, ax, ay, az);
+  }
+}
 template <typename T>
 __device__ __forceinline__ void l2p(const double* F, T dx, T dy, T dz, T* out) {
   T X[SWH_MPOLE_TERMS];
   xpowers<T>(dx, dy, dz, X);
   T pot = (T)0, ax = (T)0, ay = (T)0, az = (T)0;
-#pragma unroll
-  for (int t = 0; t < SWH_MPOLE_TERMS; t++) {
-    pot -= X[t] * (T)F[t];
-    if (mp_order(t) <= 3) {
-      ax += X[t] * (T)F[mp_index(kMpA[t] + 1, kMpB[t], kMpC[t])];
-      ay += X[t] * (T)F[mp_index(kMpA[t], kMpB[t] + 1, kMpC[t])];
-      az += X[t] * (T)F[mp_index(kMpA[t], kMpB[t], kMpC[t] + 1)];
-    }
-  }
+  l2p_t<T, 0>(F, X, pot, ax, ay, az);
   out[0] = pot;
   out[1] = ax;
   out[2] = ay;

@@ -54,7 +54,10 @@ __global__ __launch_bounds__(256) void loop_kernel(GridDev g, SoA a,
 // ---------------------------------------------------------------------------
 // Variant 7 (default): the step's pair lists (swh_list.h).
 // ---------------------------------------------------------------------------
-constexpr int kWalkLpi = 4;  // lanes per i of the list walks
+#ifndef SWH_WALK_LPI
+#define SWH_WALK_LPI 4
+#endif
+constexpr int kWalkLpi = SWH_WALK_LPI;  // lanes per i of the list walks
 
 __global__ void list_prep_kernel(const unsigned int* hmax_bits, float gs1, float dx,
                                  unsigned int* rwrap, unsigned int* ovf_n) {

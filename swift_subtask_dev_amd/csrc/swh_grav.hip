@@ -25,6 +25,8 @@
 #include <thread>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
+
 #include "swh_internal.h"
 #include "swh_mpole.h"
 #include "swh_physics.h"
@@ -561,7 +563,10 @@ swh_status swh_gspace_destroy(swh_gspace* g) {
   DevBuf* bufs[] = {&g->aos,      &g->pos,      &g->hinv,    &g->mass,    &g->active,
                     &g->accel,    &g->oagn,     &g->mpoles,  &g->leaves,  &g->pair_off,
                     &g->pairs,    &g->counter,  &g->cell_act, &g->ftens,  &g->m2l_off,
-                    &g->m2l_src,  &g->l2l_list, &g->leaf_ids};
+                    &g->m2l_src,  &g->l2l_list, &g->leaf_ids, &g->tree_d, &g->wf0,
+                    &g->wf1,      &g->wctr,     &g->pp_key,  &g->pp_val,  &g->pp_key2,
+                    &g->pp_val2,  &g->pp_cnt,   &g->mm_key,  &g->mm_val,  &g->mm_key2,
+                    &g->mm_val2,  &g->mm_cnt,   &g->wsort_tmp};
   for (DevBuf* b : bufs) b->release();
   mesh_release(g);
   (void)hipStreamDestroy(g->stream);
@@ -1021,6 +1026,284 @@ struct TreeWalk {
   }
 };
 
+
+// ---------------------------------------------------------------------------
+// The recursive walk on the device (level-synchronous): every thread takes one
+// task of the frontier -- self(c), pair(ci, cj) or no_cache(ci, cj), the
+// decisions of TreeWalk above -- and either emits its P-P / M-M entries or
+// pushes its sub-tasks into the next frontier. Entries are keyed
+// (cell << 32 | other cell), unique per walk, and sorted by key afterwards, so
+// the lists do not depend on the threads' order.
+enum { GW_SELF = 0, GW_PAIR = 1, GW_NOCACHE = 2 };
+
+struct GWalkOut {
+  int4* next;
+  unsigned int* ctr;  // [0] next frontier, [1] P-P entries, [2] M-M entries, [3] skipped
+  unsigned long long* pp_key;
+  int* pp_val;  // truncated | allow_mpole << 1
+  int* pp_cnt;
+  unsigned long long* mm_key;
+  int* mm_val;  // symmetric
+  int* mm_cnt;
+};
+
+__device__ __forceinline__ void gw_pp(const GWalkOut& o, int ci, int cj, int trunc, int mpole) {
+  const unsigned int p = atomicAdd(&o.ctr[1], 1u);
+  o.pp_key[p] = ((unsigned long long)(unsigned int)ci << 32) | (unsigned int)cj;
+  o.pp_val[p] = trunc | (mpole << 1);
+  atomicAdd(&o.pp_cnt[ci], 1);
+}
+__device__ __forceinline__ void gw_mm(const GWalkOut& o, int t, int src, int sym) {
+  const unsigned int p = atomicAdd(&o.ctr[2], 1u);
+  o.mm_key[p] = ((unsigned long long)(unsigned int)t << 32) | (unsigned int)src;
+  o.mm_val[p] = sym;
+  atomicAdd(&o.mm_cnt[t], 1);
+}
+
+__global__ void gwalk_kernel(const int4* __restrict__ cur, int n, const swh_gcell* __restrict__ cells,
+                             const swh_multipole* __restrict__ mp, const int8_t* __restrict__ act,
+                             MacParams mac, int periodic, double dimx, double dimy, double dimz,
+                             double r_cut_min, double r_cut_max, GWalkOut o) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int4 it = cur[k];
+  if (it.z == GW_SELF) {  // runner_doself_recursive_grav (2386-2431)
+    const int c = it.x;
+    if (!act[c]) return;
+    const swh_gcell C = cells[c];
+    if (C.split) {
+      int ch[8], m = 0;
+      for (int j = 0; j < 8; j++)
+        if (C.progeny[j] >= 0) ch[m++] = C.progeny[j];
+      unsigned int q = atomicAdd(&o.ctr[0], (unsigned int)(m + m * (m - 1) / 2));
+      for (int j = 0; j < m; j++) {
+        o.next[q++] = make_int4(ch[j], -1, GW_SELF, 0);
+        for (int l = j + 1; l < m; l++) o.next[q++] = make_int4(ch[j], ch[l], GW_PAIR, 0);
+      }
+    } else {
+      gw_pp(o, c, c, periodic && (2. * mp[c].r_max > r_cut_min), 0);
+    }
+    return;
+  }
+  if (it.z == GW_NOCACHE) {  // runner_dopair_grav_pp_no_cache (1440-1483)
+    const int ci = it.x, cj = it.y;
+    if (!act[ci]) return;
+    const swh_gcell Ci = cells[ci];
+    if (Ci.count == 0 || cells[cj].count == 0) return;
+    if (Ci.split) {
+      int m = 0;
+      for (int j = 0; j < 8; j++) m += Ci.progeny[j] >= 0 ? 1 : 0;
+      unsigned int q = atomicAdd(&o.ctr[0], (unsigned int)m);
+      for (int j = 0; j < 8; j++)
+        if (Ci.progeny[j] >= 0) o.next[q++] = make_int4(Ci.progeny[j], cj, GW_NOCACHE, 0);
+    } else {
+      gw_pp(o, ci, cj, periodic ? 1 : 0, 0);
+    }
+    return;
+  }
+  // runner_dopair_recursive_grav (2208-2374)
+  const int ci = it.x, cj = it.y;
+  if (!(act[ci] || act[cj])) return;
+  const swh_multipole& A = mp[ci];
+  const swh_multipole& B = mp[cj];
+  double dx = A.CoM[0] - B.CoM[0], dy = A.CoM[1] - B.CoM[1], dz = A.CoM[2] - B.CoM[2];
+  if (periodic) {
+    dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
+    dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
+    dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
+  }
+  const double r2 = dx * dx + dy * dy + dz * dz;
+  const double r_lr_check = sqrt(r2) - (A.r_max + B.r_max);
+  if (periodic && r_lr_check > r_cut_max) {
+    atomicAdd(&o.ctr[3], 1u);
+    return;
+  }
+  const swh_gcell Ci = cells[ci], Cj = cells[cj];
+  if (Ci.count <= 1 || Cj.count <= 1) {
+    unsigned int q = atomicAdd(&o.ctr[0], 2u);
+    o.next[q] = make_int4(ci, cj, GW_NOCACHE, 0);
+    o.next[q + 1] = make_int4(cj, ci, GW_NOCACHE, 0);
+  } else if (m2l_accept(mac, m2l_side(A), m2l_side(B), (float)r2) &&
+             m2l_accept(mac, m2l_side(B), m2l_side(A), (float)r2)) {
+    // runner_dopair_grav_mm (2050-2064): symmetric when both are active
+    const bool di = act[ci], dj = act[cj];
+    if (di && dj) {
+      gw_mm(o, ci, cj, 1);
+      gw_mm(o, cj, ci, 1);
+    } else if (di) {
+      gw_mm(o, ci, cj, 0);
+    } else if (dj) {
+      gw_mm(o, cj, ci, 0);
+    }
+  } else if (!Ci.split && !Cj.split) {
+    // runner_dopair_grav_pp(ci, cj, 1, 1): truncated iff periodic &&
+    // |CoM_i - CoM_j| + r_max_i + r_max_j > r_cut_min (float separations)
+    int trunc = 0;
+    if (periodic) {
+      const float L[3] = {(float)dimx, (float)dimy, (float)dimz};
+      double d2 = 0.;
+      for (int q = 0; q < 3; q++) {
+        float dxf = (float)B.CoM[q] - (float)A.CoM[q];
+        dxf = dxf > 0.5f * L[q] ? dxf - L[q] : (dxf < -0.5f * L[q] ? dxf + L[q] : dxf);
+        d2 += (double)dxf * (double)dxf;
+      }
+      trunc = (sqrt(d2) + (double)(float)A.r_max + (double)(float)B.r_max) > r_cut_min;
+    }
+    if (act[ci]) gw_pp(o, ci, cj, trunc, 1);
+    if (act[cj]) gw_pp(o, cj, ci, trunc, 1);
+  } else {
+    // split the larger cell (or the only split one)
+    const bool split_i = A.r_max > B.r_max ? Ci.split : !Cj.split;
+    const swh_gcell& S = split_i ? Ci : Cj;
+    int m = 0;
+    for (int j = 0; j < 8; j++) m += S.progeny[j] >= 0 ? 1 : 0;
+    unsigned int q = atomicAdd(&o.ctr[0], (unsigned int)m);
+    for (int j = 0; j < 8; j++) {
+      if (S.progeny[j] < 0) continue;
+      o.next[q++] = split_i ? make_int4(S.progeny[j], cj, GW_PAIR, 0)
+                            : make_int4(ci, S.progeny[j], GW_PAIR, 0);
+    }
+  }
+}
+
+__global__ void gw_unpack_pp(const unsigned long long* __restrict__ key, const int* __restrict__ val,
+                             int n, swh_leaf_pair* __restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  swh_leaf_pair e;
+  e.j = (int)(unsigned int)(key[k] & 0xffffffffull);
+  e.truncated = val[k] & 1;
+  e.allow_mpole = (val[k] >> 1) & 1;
+  out[k] = e;
+}
+__global__ void gw_unpack_mm(const unsigned long long* __restrict__ key, const int* __restrict__ val,
+                             int n, int2* __restrict__ out) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  out[k] = make_int2((int)(unsigned int)(key[k] & 0xffffffffull), val[k]);
+}
+
+// Grow a device buffer keeping its first `used` bytes.
+static swh_status grow_keep(DevBuf& b, size_t need, size_t used, hipStream_t st) {
+  if (need <= b.bytes) return SWH_OK;
+  DevBuf nb;
+  SWH_TRY(nb.reserve(std::max(need, 2 * b.bytes)));
+  if (used > 0) SWH_HIP(hipMemcpyAsync(nb.ptr, b.ptr, used, hipMemcpyDeviceToDevice, st));
+  SWH_HIP(hipStreamSynchronize(st));
+  b.release();
+  b.ptr = nb.ptr;
+  b.bytes = nb.bytes;
+  nb.ptr = nullptr;
+  nb.bytes = 0;
+  return SWH_OK;
+}
+
+// The walk on the device; fills g->pair_off / g->pairs (P-P CSR over i-cells)
+// and g->m2l_off / g->m2l_src (M-M CSR over targets).
+static swh_status device_walk(swh_gspace* g, const swh_grav_params* G, const int32_t* self_cells,
+                              int32_t nself, const int32_t* pair_cells, int32_t npair,
+                              int64_t* n_pp, int64_t* n_mm, int64_t* n_skip) {
+  hipStream_t st = g->stream;
+  const int ncells = (int)g->tree.size();
+  const int64_t ntask = (int64_t)nself + npair;
+  std::vector<int4> init((size_t)std::max<int64_t>(1, ntask));
+  for (int k = 0; k < nself; k++) init[k] = make_int4(self_cells[k], -1, GW_SELF, 0);
+  for (int k = 0; k < npair; k++)
+    init[nself + k] = make_int4(pair_cells[2 * k], pair_cells[2 * k + 1], GW_PAIR, 0);
+  SWH_TRY(g->wf0.reserve((size_t)std::max<int64_t>(1, ntask) * sizeof(int4)));
+  if (ntask > 0)
+    SWH_HIP(hipMemcpyAsync(g->wf0.ptr, init.data(), (size_t)ntask * sizeof(int4),
+                           hipMemcpyHostToDevice, st));
+  SWH_TRY(g->wctr.reserve(4 * sizeof(unsigned int)));
+  SWH_TRY(g->pp_cnt.reserve(((size_t)ncells + 1) * sizeof(int)));
+  SWH_TRY(g->mm_cnt.reserve(((size_t)ncells + 1) * sizeof(int)));
+  SWH_HIP(hipMemsetAsync(g->wctr.ptr, 0, 4 * sizeof(unsigned int), st));
+  SWH_HIP(hipMemsetAsync(g->pp_cnt.ptr, 0, ((size_t)ncells + 1) * sizeof(int), st));
+  SWH_HIP(hipMemsetAsync(g->mm_cnt.ptr, 0, ((size_t)ncells + 1) * sizeof(int), st));
+  unsigned int* ctr = g->wctr.as<unsigned int>();
+  const MacParams mac = mac_params(G);
+  int64_t n_cur = ntask;
+  unsigned int h[4] = {0, 0, 0, 0};
+  DevBuf* cur = &g->wf0;
+  DevBuf* nxt = &g->wf1;
+  while (n_cur > 0) {
+    // room for the widest fan-out (a split self task: 8 + 28 sub-tasks) and
+    // two entries per task
+    SWH_TRY(nxt->reserve((size_t)n_cur * 36 * sizeof(int4)));
+    const size_t pp_need = (size_t)h[1] + 2 * (size_t)n_cur, mm_need = (size_t)h[2] + 2 * (size_t)n_cur;
+    SWH_TRY(grow_keep(g->pp_key, pp_need * 8, (size_t)h[1] * 8, st));
+    SWH_TRY(grow_keep(g->pp_val, pp_need * 4, (size_t)h[1] * 4, st));
+    SWH_TRY(grow_keep(g->mm_key, mm_need * 8, (size_t)h[2] * 8, st));
+    SWH_TRY(grow_keep(g->mm_val, mm_need * 4, (size_t)h[2] * 4, st));
+    SWH_HIP(hipMemsetAsync(ctr, 0, sizeof(unsigned int), st));
+    GWalkOut o{nxt->as<int4>(), ctr, g->pp_key.as<unsigned long long>(), g->pp_val.as<int>(),
+               g->pp_cnt.as<int>(), g->mm_key.as<unsigned long long>(), g->mm_val.as<int>(),
+               g->mm_cnt.as<int>()};
+    hipLaunchKernelGGL(gwalk_kernel, dim3((unsigned)((n_cur + 255) / 256)), dim3(256), 0, st,
+                       cur->as<const int4>(), (int)n_cur, g->tree_d.as<const swh_gcell>(),
+                       g->mpoles.as<const swh_multipole>(), g->cell_act.as<const int8_t>(), mac,
+                       G->periodic, (double)G->dim[0], (double)G->dim[1], (double)G->dim[2],
+                       G->r_cut_min, G->r_cut_max, o);
+    SWH_HIP(hipGetLastError());
+    SWH_HIP(hipMemcpyAsync(h, ctr, sizeof(h), hipMemcpyDeviceToHost, st));
+    SWH_HIP(hipStreamSynchronize(st));
+    n_cur = h[0];
+    std::swap(cur, nxt);
+  }
+  const int npp = (int)h[1], nmm = (int)h[2];
+  *n_pp = npp;
+  *n_mm = nmm;
+  *n_skip = h[3];
+  // CSR offsets: exclusive scans of the per-cell counts
+  SWH_TRY(g->pair_off.reserve(((size_t)ncells + 1) * sizeof(int32_t)));
+  SWH_TRY(g->m2l_off.reserve(((size_t)ncells + 1) * sizeof(int32_t)));
+  size_t tb = 0, tb2 = 0;
+  SWH_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, g->pp_cnt.as<int>(),
+                                           g->pair_off.as<int>(), ncells + 1, st));
+  SWH_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, g->pp_key.as<unsigned long long>(),
+                                             g->pp_key2.as<unsigned long long>(),
+                                             g->pp_val.as<int>(), g->pp_val2.as<int>(),
+                                             std::max(npp, nmm), 0, 64, st));
+  SWH_TRY(g->wsort_tmp.reserve(std::max(tb, tb2)));
+  SWH_HIP(hipcub::DeviceScan::ExclusiveSum(g->wsort_tmp.ptr, tb, g->pp_cnt.as<int>(),
+                                           g->pair_off.as<int>(), ncells + 1, st));
+  SWH_HIP(hipcub::DeviceScan::ExclusiveSum(g->wsort_tmp.ptr, tb, g->mm_cnt.as<int>(),
+                                           g->m2l_off.as<int>(), ncells + 1, st));
+  SWH_TRY(g->pairs.reserve((size_t)std::max(1, npp) * sizeof(swh_leaf_pair)));
+  SWH_TRY(g->m2l_src.reserve((size_t)std::max(1, nmm) * sizeof(int2)));
+  if (npp > 0) {
+    SWH_TRY(g->pp_key2.reserve((size_t)npp * 8));
+    SWH_TRY(g->pp_val2.reserve((size_t)npp * 4));
+    size_t t = g->wsort_tmp.bytes;
+    SWH_HIP(hipcub::DeviceRadixSort::SortPairs(g->wsort_tmp.ptr, t, g->pp_key.as<unsigned long long>(),
+                                               g->pp_key2.as<unsigned long long>(),
+                                               g->pp_val.as<int>(), g->pp_val2.as<int>(), npp, 0, 64,
+                                               st));
+    hipLaunchKernelGGL(gw_unpack_pp, dim3((npp + 255) / 256), dim3(256), 0, st,
+                       g->pp_key2.as<const unsigned long long>(), g->pp_val2.as<const int>(), npp,
+                       g->pairs.as<swh_leaf_pair>());
+    SWH_HIP(hipGetLastError());
+  }
+  if (nmm > 0) {
+    SWH_TRY(g->mm_key2.reserve((size_t)nmm * 8));
+    SWH_TRY(g->mm_val2.reserve((size_t)nmm * 4));
+    size_t t = g->wsort_tmp.bytes;
+    SWH_HIP(hipcub::DeviceRadixSort::SortPairs(g->wsort_tmp.ptr, t, g->mm_key.as<unsigned long long>(),
+                                               g->mm_key2.as<unsigned long long>(),
+                                               g->mm_val.as<int>(), g->mm_val2.as<int>(), nmm, 0, 64,
+                                               st));
+    hipLaunchKernelGGL(gw_unpack_mm, dim3((nmm + 255) / 256), dim3(256), 0, st,
+                       g->mm_key2.as<const unsigned long long>(), g->mm_val2.as<const int>(), nmm,
+                       g->m2l_src.as<int2>());
+    SWH_HIP(hipGetLastError());
+  }
+  g->npairs = npp;
+  g->nleaves = ncells;
+  g->max_leaf = g->tree_max_leaf;
+  g->any_mpole = npp > 0;  // leaf-leaf entries allow M2P (allow_mpole = 1)
+  return SWH_OK;
+}
+
 }  // namespace swh
 
 extern "C" {
@@ -1105,6 +1388,15 @@ swh_status swh_gspace_set_tree(swh_gspace* g, const swh_gcell* cells, int32_t nc
   SWH_HIP(hipStreamSynchronize(g->stream));
   g->l2l_depth_off = doff;
   g->nleaf_cells = (int32_t)leaves.size();
+  int32_t ml = 0;
+  for (int c : leaves) ml = std::max(ml, cells[c].count);
+  g->tree_max_leaf = ml;
+  SWH_TRY(g->tree_d.reserve((size_t)std::max(1, ncells) * sizeof(swh_gcell)));
+  if (ncells > 0) {
+    SWH_HIP(hipMemcpyAsync(g->tree_d.ptr, cells, (size_t)ncells * sizeof(swh_gcell),
+                           hipMemcpyHostToDevice, g->stream));
+    SWH_HIP(hipStreamSynchronize(g->stream));
+  }
   return SWH_OK;
 }
 
@@ -1137,90 +1429,101 @@ swh_status swh_grav_tree(swh_gspace* g, const swh_grav_params* G, const int32_t*
                      g->leaves.as<const swh_leaf>(), g->active.as<const int8_t>(),
                      g->cell_act.as<int8_t>());
   SWH_HIP(hipGetLastError());
-  std::vector<swh_multipole> mp(ncells);
-  std::vector<int8_t> act(ncells);
-  SWH_HIP(hipMemcpyAsync(mp.data(), g->mpoles.ptr, ncells * sizeof(swh_multipole),
-                         hipMemcpyDeviceToHost, g->stream));
-  SWH_HIP(hipMemcpyAsync(act.data(), g->cell_act.ptr, ncells, hipMemcpyDeviceToHost, g->stream));
-  SWH_HIP(hipStreamSynchronize(g->stream));
-  // the walk: the self and pair tasks in chunks of consecutive tasks spread
-  // over host threads (the recursive tasks are independent, as SWIFT's runners
-  // execute them); each chunk keeps its entries, and the chunks are joined in
-  // task order, so the lists equal a serial walk's
-  const int64_t ntask = (int64_t)nself + npair;
-  constexpr int64_t kChunk = 64;
-  const int64_t nchunk = (ntask + kChunk - 1) / kChunk;
-  std::vector<TreeWalk> part((size_t)nchunk);
-  const MacParams mac = mac_params(G);
-  std::atomic<int64_t> next{0};
-  auto worker = [&]() {
-    for (int64_t ch = next++; ch < nchunk; ch = next++) {
-      TreeWalk& w = part[(size_t)ch];
-      w.cells = g->tree.data();
-      w.mp = mp.data();
-      w.act = act.data();
-      w.G = G;
-      w.mac = mac;
-      const int64_t t1 = std::min(ntask, (ch + 1) * kChunk);
-      for (int64_t t = ch * kChunk; t < t1; t++) {
-        if (t < nself) w.self(self_cells[t]);
-        else w.pair(pair_cells[2 * (t - nself)], pair_cells[2 * (t - nself) + 1]);
+  int64_t npp = 0, nmm = 0, skipped = 0;
+  if (!std::getenv("SWH_HOST_WALK")) {
+    // the walk on the device (the default)
+    SWH_TRY(device_walk(g, G, self_cells, nself, pair_cells, npair, &npp, &nmm, &skipped));
+  } else {
+    std::vector<swh_multipole> mp(ncells);
+    std::vector<int8_t> act(ncells);
+    SWH_HIP(hipMemcpyAsync(mp.data(), g->mpoles.ptr, ncells * sizeof(swh_multipole),
+                           hipMemcpyDeviceToHost, g->stream));
+    SWH_HIP(hipMemcpyAsync(act.data(), g->cell_act.ptr, ncells, hipMemcpyDeviceToHost, g->stream));
+    SWH_HIP(hipStreamSynchronize(g->stream));
+    // the walk: the self and pair tasks in chunks of consecutive tasks spread
+    // over host threads (the recursive tasks are independent, as SWIFT's runners
+    // execute them); each chunk keeps its entries, and the chunks are joined in
+    // task order, so the lists equal a serial walk's
+    const int64_t ntask = (int64_t)nself + npair;
+    constexpr int64_t kChunk = 64;
+    const int64_t nchunk = (ntask + kChunk - 1) / kChunk;
+    std::vector<TreeWalk> part((size_t)nchunk);
+    const MacParams mac = mac_params(G);
+    std::atomic<int64_t> next{0};
+    auto worker = [&]() {
+      for (int64_t ch = next++; ch < nchunk; ch = next++) {
+        TreeWalk& w = part[(size_t)ch];
+        w.cells = g->tree.data();
+        w.mp = mp.data();
+        w.act = act.data();
+        w.G = G;
+        w.mac = mac;
+        const int64_t t1 = std::min(ntask, (ch + 1) * kChunk);
+        for (int64_t t = ch * kChunk; t < t1; t++) {
+          if (t < nself) w.self(self_cells[t]);
+          else w.pair(pair_cells[2 * (t - nself)], pair_cells[2 * (t - nself) + 1]);
+        }
+      }
+    };
+    int nthr = (int)std::min<int64_t>(nchunk, 16);  // the host share of one GPU
+    if (const char* e = std::getenv("SWH_HOST_THREADS")) nthr = std::max(1, std::atoi(e));
+    nthr = (int)std::max<int64_t>(1, std::min<int64_t>(nthr, nchunk));
+    {
+      std::vector<std::thread> pool;
+      for (int k = 1; k < nthr; k++) pool.emplace_back(worker);
+      worker();
+      for (auto& th : pool) th.join();
+    }
+    // P-P lists (CSR over i-cells) and M-M lists (CSR over targets): stable
+    // counting sort of the chunks' entries by cell
+    std::vector<int32_t> poff(ncells + 1, 0), moff(ncells + 1, 0);
+    for (const TreeWalk& w : part) {
+      for (const auto& e : w.pp) poff[e.first + 1]++;
+      for (const auto& e : w.mm) moff[e.first + 1]++;
+      skipped += w.skipped;
+    }
+    for (int c = 0; c < ncells; c++) {
+      poff[c + 1] += poff[c];
+      moff[c + 1] += moff[c];
+    }
+    std::vector<swh_leaf_pair> pairs((size_t)poff[ncells]);
+    std::vector<int2> msrc((size_t)moff[ncells]);
+    {
+      std::vector<int32_t> pcur(poff.begin(), poff.end() - 1), mcur(moff.begin(), moff.end() - 1);
+      for (const TreeWalk& w : part) {
+        for (const auto& e : w.pp) pairs[(size_t)pcur[e.first]++] = e.second;
+        for (const auto& e : w.mm) msrc[(size_t)mcur[e.first]++] = e.second;
       }
     }
-  };
-  int nthr = (int)std::min<int64_t>(nchunk, 16);  // the host share of one GPU
-  if (const char* e = std::getenv("SWH_HOST_THREADS")) nthr = std::max(1, std::atoi(e));
-  nthr = (int)std::max<int64_t>(1, std::min<int64_t>(nthr, nchunk));
-  {
-    std::vector<std::thread> pool;
-    for (int k = 1; k < nthr; k++) pool.emplace_back(worker);
-    worker();
-    for (auto& th : pool) th.join();
-  }
-  // P-P lists (CSR over i-cells) and M-M lists (CSR over targets): stable
-  // counting sort of the chunks' entries by cell
-  std::vector<int32_t> poff(ncells + 1, 0), moff(ncells + 1, 0);
-  int64_t skipped = 0;
-  for (const TreeWalk& w : part) {
-    for (const auto& e : w.pp) poff[e.first + 1]++;
-    for (const auto& e : w.mm) moff[e.first + 1]++;
-    skipped += w.skipped;
-  }
-  for (int c = 0; c < ncells; c++) {
-    poff[c + 1] += poff[c];
-    moff[c + 1] += moff[c];
-  }
-  std::vector<swh_leaf_pair> pairs((size_t)poff[ncells]);
-  std::vector<int2> msrc((size_t)moff[ncells]);
-  {
-    std::vector<int32_t> pcur(poff.begin(), poff.end() - 1), mcur(moff.begin(), moff.end() - 1);
-    for (const TreeWalk& w : part) {
-      for (const auto& e : w.pp) pairs[(size_t)pcur[e.first]++] = e.second;
-      for (const auto& e : w.mm) msrc[(size_t)mcur[e.first]++] = e.second;
+    part.clear();
+    std::vector<swh_leaf> ranges(ncells);
+    for (int c = 0; c < ncells; c++) ranges[c] = swh_leaf{g->tree[c].start, g->tree[c].count};
+    SWH_TRY(swh_gspace_set_leaves(g, ranges.data(), ncells, poff.data(), pairs.data(),
+                                  (int32_t)pairs.size()));
+    npp = (int64_t)pairs.size();
+    nmm = (int64_t)msrc.size();
+    if (!msrc.empty()) {
+      SWH_TRY(g->m2l_off.reserve((size_t)(ncells + 1) * sizeof(int32_t)));
+      SWH_TRY(g->m2l_src.reserve(msrc.size() * sizeof(int2)));
+      SWH_HIP(hipMemcpyAsync(g->m2l_off.ptr, moff.data(), (ncells + 1) * sizeof(int32_t),
+                             hipMemcpyHostToDevice, g->stream));
+      SWH_HIP(hipMemcpyAsync(g->m2l_src.ptr, msrc.data(), msrc.size() * sizeof(int2),
+                             hipMemcpyHostToDevice, g->stream));
+      SWH_HIP(hipStreamSynchronize(g->stream));  // the host vectors go out of scope
     }
   }
-  part.clear();
-  std::vector<swh_leaf> ranges(ncells);
-  for (int c = 0; c < ncells; c++) ranges[c] = swh_leaf{g->tree[c].start, g->tree[c].count};
-  SWH_TRY(swh_gspace_set_leaves(g, ranges.data(), ncells, poff.data(), pairs.data(),
-                                (int32_t)pairs.size()));
+
   g->mpoles_valid = true;  // the same cell table: the multipoles stay
   // P2P + M2P
   SWH_TRY(g->counter.reserve(2 * sizeof(unsigned long long)));
   unsigned long long* ctr = g->counter.as<unsigned long long>();
   SWH_HIP(hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned long long), g->stream));
-  if (!pairs.empty()) SWH_TRY(launch_pp(g, G, mac_params(G), ctr));
+  if (npp > 0) SWH_TRY(launch_pp(g, G, mac_params(G), ctr));
   // M2L
   const bool f64 = g->ctx->precision == SWH_PRECISION_F64;
   SWH_HIP(hipMemsetAsync(g->ftens.ptr, 0, (size_t)ncells * SWH_MPOLE_TERMS * sizeof(double),
                          g->stream));
-  if (!msrc.empty()) {
-    SWH_TRY(g->m2l_off.reserve((size_t)(ncells + 1) * sizeof(int32_t)));
-    SWH_TRY(g->m2l_src.reserve(msrc.size() * sizeof(int2)));
-    SWH_HIP(hipMemcpyAsync(g->m2l_off.ptr, moff.data(), (ncells + 1) * sizeof(int32_t),
-                           hipMemcpyHostToDevice, g->stream));
-    SWH_HIP(hipMemcpyAsync(g->m2l_src.ptr, msrc.data(), msrc.size() * sizeof(int2),
-                           hipMemcpyHostToDevice, g->stream));
+  if (nmm > 0) {
     const dim3 mg((ncells + 63) / 64);
     if (f64)
       hipLaunchKernelGGL((m2l_kernel<double>), mg, dim3(64), 0, g->stream,
@@ -1270,8 +1573,8 @@ swh_status swh_grav_tree(swh_gspace* g, const swh_grav_params* G, const int32_t*
   if (stats) {
     stats->n_pp = (int64_t)h[0];
     stats->n_m2p = (int64_t)h[1];
-    stats->n_m2l = (int64_t)msrc.size();
-    stats->n_pp_tasks = (int64_t)pairs.size();
+    stats->n_m2l = nmm;
+    stats->n_pp_tasks = npp;
     stats->n_skipped = skipped;
   }
   return SWH_OK;

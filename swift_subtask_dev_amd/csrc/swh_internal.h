@@ -236,6 +236,12 @@ struct swh_gspace {
   std::vector<int32_t> l2l_depth_off;  // l2l_list range of each depth
   swh::DevBuf leaf_ids;          // int: the unsplit cells
   int32_t nleaf_cells = 0;
+  int32_t tree_max_leaf = 0;     // largest unsplit cell
+  // device walk (swh_grav_tree): the cell table, two frontiers of tasks, the
+  // emitted P-P / M-M entries (keys cell << 32 | other, flags) and their
+  // sorted copies, per-cell counts
+  swh::DevBuf tree_d, wf0, wf1, wctr, pp_key, pp_val, pp_key2, pp_val2, pp_cnt;
+  swh::DevBuf mm_key, mm_val, mm_key2, mm_val2, mm_cnt, wsort_tmp;
   // PM mesh (swh_gspace_pm_mesh): density / potential mesh, its r2c
   // transform and the cached hipFFT plans of side mesh_N
   swh::DevBuf mesh_rho, mesh_frho;

@@ -390,7 +390,7 @@ __device__ __forceinline__ void l2p(const double* F, T dx, T dy, T dz, T* out) {
 struct M2LSide {
   float rho, max_soft, min_a, M000, power[3];
 };
-inline M2LSide m2l_side(const swh_multipole& m) {
+__host__ __device__ inline M2LSide m2l_side(const swh_multipole& m) {
   M2LSide s;
   s.rho = (float)m.r_max;
   s.max_soft = m.max_softening;
@@ -399,11 +399,12 @@ inline M2LSide m2l_side(const swh_multipole& m) {
   for (int k = 0; k < 3; k++) s.power[k] = m.power[k];
   return s;
 }
-inline bool m2l_accept(const MacParams& P, const M2LSide& A, const M2LSide& B, float r2) {
+__host__ __device__ inline bool m2l_accept(const MacParams& P, const M2LSide& A, const M2LSide& B,
+                                           float r2) {
 #pragma clang fp contract(off)
   const float rho_A = A.rho, rho_B = B.rho;
-  const float rho_max = std::max(rho_A, rho_B);
-  const float max_softening = std::max(A.max_soft, B.max_soft);
+  const float rho_max = rho_A > rho_B ? rho_A : rho_B;
+  const float max_softening = A.max_soft > B.max_soft ? A.max_soft : B.max_soft;
   // p = 2: sum_n binomial(2, n) power_B[n] rho_A^(2 - n)
   float E_BA_term = 0.f;
   E_BA_term += 1.f * B.power[0] * (rho_A * rho_A);
@@ -424,7 +425,7 @@ inline bool m2l_accept(const MacParams& P, const M2LSide& A, const M2LSide& B, f
       f_MAC_inv = (9.f / 25.f) * P.r_s_inv * P.r_s_inv * r2 * r2;
   }
   const float min_a_grav = A.min_a;
-  const float M_max = std::max(A.M000, B.M000);
+  const float M_max = A.M000 > B.M000 ? A.M000 : B.M000;
   const float rho_sum = rho_A + rho_B;
   const bool cond_2 = P.below_soft || max_softening * max_softening < r2;
   if (P.advanced && P.gadget) {

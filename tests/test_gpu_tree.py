@@ -159,3 +159,21 @@ def test_tree_bad_input(gpu_ctx):
     with pytest.raises(lib.SwhError):
         gs.set_tree(bad)
     gs.close()
+
+
+def test_device_walk_equals_host_walk(gpu_ctx, monkeypatch):
+    """The device walk (default) and the host walk (SWH_HOST_WALK) make the
+    same decisions: identical counts, and the same accelerations up to the
+    summation order of the sorted vs. task-ordered lists."""
+    g, cells, tops = ics.gravity_tree(clumpy_box(14, seed=21), 4, split_size=24)
+    pairs = ics.top_level_pairs(tops)
+    r_s = 1.25 / 32
+    G = params(periodic=True, theta=0.6, r_s_inv=1 / r_s, r_cut_min=0.1 * r_s,
+               r_cut_max=4.5 * r_s)
+    gd, gh = abi.copy_parts(g), abi.copy_parts(g)
+    sd = run_gpu(gpu_ctx, gd, cells, tops, pairs, G)[0]
+    monkeypatch.setenv("SWH_HOST_WALK", "1")
+    sh = run_gpu(gpu_ctx, gh, cells, tops, pairs, G)[0]
+    monkeypatch.delenv("SWH_HOST_WALK")
+    assert sd == sh and sd["n_m2l"] > 0 and sd["n_skipped"] > 0
+    compare(gd, gh, rel=1e-9)

@@ -482,8 +482,9 @@ __global__ __launch_bounds__(kGravBlock) void m2p_kernel(
   const int li = xcd_block_id();
   const swh_leaf L = leaves[li];
   const int p0 = pair_off[li], p1 = pair_off[li + 1];
+  if (p0 == p1) return;  // no sources (a tree's inner cells)
   unsigned long long nm = 0;
-  for (int local = threadIdx.x; local < L.count; local += kGravBlock) {
+  for (int local = threadIdx.x; local < L.count; local += blockDim.x) {
     const int i = L.start + local;
     if (!g.active[i]) continue;
     const double4 p = g.pos[i];
@@ -732,13 +733,14 @@ swh_status launch_pp(swh_gspace* g, const swh_grav_params* G, const MacParams& m
                        (double)G->dim[1], (double)G->dim[2], (float)G->r_s_inv, mac, ctr);
   SWH_HIP(hipGetLastError());
   if (g->any_mpole) {
+    const int mblk = g->max_leaf <= 64 ? 64 : kGravBlock;  // one wave per small leaf
     if (f64)
-      hipLaunchKernelGGL((m2p_kernel<double>), dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
+      hipLaunchKernelGGL((m2p_kernel<double>), dim3(g->nleaves), dim3(mblk), 0, g->stream,
                          gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
                          g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
                          (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, mac, ctr);
     else
-      hipLaunchKernelGGL((m2p_kernel<float>), dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
+      hipLaunchKernelGGL((m2p_kernel<float>), dim3(g->nleaves), dim3(mblk), 0, g->stream,
                          gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
                          g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
                          (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, mac, ctr);
@@ -1554,13 +1556,14 @@ swh_status swh_grav_tree(swh_gspace* g, const swh_grav_params* G, const int32_t*
       SWH_HIP(hipGetLastError());
     }
     if (g->nleaf_cells > 0) {
+      const int lblk = g->tree_max_leaf <= 64 ? 64 : 256;  // one wave per small leaf
       if (f64)
-        hipLaunchKernelGGL((l2p_kernel<double>), dim3(g->nleaf_cells), dim3(256), 0, g->stream,
+        hipLaunchKernelGGL((l2p_kernel<double>), dim3(g->nleaf_cells), dim3(lblk), 0, g->stream,
                            g->leaves.as<const swh_leaf>(), g->leaf_ids.as<const int>(),
                            g->mpoles.as<const swh_multipole>(), g->ftens.as<const double>(),
                            gsoa_of(g));
       else
-        hipLaunchKernelGGL((l2p_kernel<float>), dim3(g->nleaf_cells), dim3(256), 0, g->stream,
+        hipLaunchKernelGGL((l2p_kernel<float>), dim3(g->nleaf_cells), dim3(lblk), 0, g->stream,
                            g->leaves.as<const swh_leaf>(), g->leaf_ids.as<const int>(),
                            g->mpoles.as<const swh_multipole>(), g->ftens.as<const double>(),
                            gsoa_of(g));

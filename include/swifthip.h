@@ -345,7 +345,9 @@ typedef struct swh_tuning {
   int32_t group_size;   /* tile i-group size: 0 (default 16), 16, 32, 64 (variants 4, 5) */
   float cell_scale;     /* if > 0: cells per H_max as a real number (overrides cell_factor) */
   int32_t diag_mode;    /* 0; profiling only (results invalid): 1 = staging only (tile
-                           loops) / list build only (lists), 2 = staging + candidate tests */
+                           loops) / list build only (lists), 2 = staging + candidate tests,
+                           4 = fixed-j gathers; 7 (results valid) = a density loop keeps
+                           pair lists that are still valid instead of rebuilding them */
   int32_t list_capacity; /* list entries per particle (0 = 128); more hits: direct gather */
   float list_skin;       /* relative slack of the list reach over gamma h (default 0: exact
                             lists; a ghost that grows any H past its reach makes gradient /

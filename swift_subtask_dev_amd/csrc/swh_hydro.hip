@@ -724,9 +724,14 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const int
   if (!subset && loop_variant_of(s) == 7) {
     // the density loop builds the step's lists; gradient and force reuse them
     // while no particle's H has outgrown its list reach (ghost: stale flag)
-    if (LOOP == LOOP_DENSITY || !s->list_valid || s->list_mab != P->max_active_bin)
+    // diag_mode 7: a density loop keeps lists that are still valid (nothing
+    // moved, no H outgrew its reach), as SWIFT keeps its sort lists
+    const bool reuse = s->tuning.diag_mode == 7 && s->list_valid &&
+                       s->list_mab == P->max_active_bin;
+    if ((LOOP == LOOP_DENSITY && !reuse) || !s->list_valid || s->list_mab != P->max_active_bin)
       SWH_TRY(build_lists(s, P, count, s->tuning.list_skin));
-    if (s->tuning.diag_mode != 0 && s->tuning.diag_mode != 4) return SWH_OK;
+    if (s->tuning.diag_mode != 0 && s->tuning.diag_mode != 4 && s->tuning.diag_mode != 7)
+      return SWH_OK;
   }
   const GridDev gd = grid_dev(s);
   const double a2H = P->a * P->a * P->H;
@@ -754,8 +759,10 @@ static swh_status run_loop(swh_space* s, const swh_hydro_params* P, int64_t* n_o
   unsigned long long* ctr = counter_slot(s);
   if (n_out) SWH_HIP(hipMemsetAsync(ctr + 3, 0, 5 * sizeof(unsigned long long), s->stream));
   if (n_out) SWH_HIP(hipMemsetAsync(ctr, 0, sizeof(unsigned long long), s->stream));
+  const bool reuse = s->tuning.diag_mode == 7 && s->list_valid &&
+                     s->list_mab == P->max_active_bin;
   const bool rebuilds = loop_variant_of(s) == 7 &&
-                        (LOOP == LOOP_DENSITY || !s->list_valid ||
+                        ((LOOP == LOOP_DENSITY && !reuse) || !s->list_valid ||
                          s->list_mab != P->max_active_bin);
   SWH_TRY(launch_loop<LOOP>(s, P, nullptr, (int)s->n, n_out != nullptr));
   if (n_out) {

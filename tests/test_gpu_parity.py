@@ -751,3 +751,37 @@ def test_grav_bench_geometry_vs_oracle(gpu_ctx, n, cdim, periodic, truncated):
     assert ng == no
     assert_close(g["a_grav"], o["a_grav"], 1e-6, 1e-6, "a_grav")
     assert_close(g["potential"], o["potential"], 1e-6, 1e-6, "potential")
+
+
+@pytest.mark.gpu
+def test_density_list_reuse(gpu_ctx):
+    """diag_mode 7: a density loop keeps still-valid pair lists; its sums equal
+    a fresh build's bitwise and the oracle's count, and a rebuild (positions
+    may have moved) makes the next density build again."""
+    from swift_subtask_dev_amd import lib
+    P = abi.default_hydro_params()
+    parts = ics.sedov_box(14, velocity="divergent", seed=12)
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.set_tuning(1, 7, 16, diag_mode=7)
+    sp.upload(abi.copy_parts(parts))
+    sp.rebuild(P)
+    res = []
+    for _ in range(2):
+        g = abi.copy_parts(parts)
+        sp.init_parts(P)
+        n = sp.density(P)
+        sp.download(g, abi.FIELDS_DENSITY)
+        res.append((n, g))
+    assert res[0][0] == res[1][0]
+    for f in ("rho", "rho_dh", "wcount", "wcount_dh", "div_v", "rot_v"):
+        assert np.array_equal(res[0][1][f], res[1][1][f]), f
+    o = abi.copy_parts(parts)
+    O.fn("f32", "init_parts")(o.ctypes.data, len(o), C.byref(P))
+    no = O.fn("f64", "box_density")(o.ctypes.data, len(o), C.byref(P), None)
+    assert res[1][0] == no
+    assert_hydro_close(res[1][1], o, TIGHT, "density on reused lists")
+    sp.rebuild(P)
+    assert not sp.info()["list_valid"]
+    sp.init_parts(P)
+    assert sp.density(P) == no
+    sp.close()

@@ -438,26 +438,17 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
   const int jfix = ld.diag == 4 ? idx(0) : 0;
   auto dj = [&](int j) { return ld.diag == 4 ? jfix : j; };
   if constexpr (S::kPay > 1) {
-    // heavy j records (gradient, force): index two entries ahead, data one
-    // ahead; the register budget of the wide records allows no more
-    int k = 0;
+    // heavy j records (gradient, force): the index two entries ahead, the
+    // record loaded at its entry -- prefetching the record one entry ahead
+    // held 21 more VGPRs (force 148: 3 waves/SIMD); without it the force walk
+    // fits 4 waves/SIMD and runs 4.5% faster (1.042 -> 0.996 ms at 128^3)
     int jn = idx(0), jn2 = idx(1);
-    double4 pn = make_double4(0., 0., 0., 0.);
-    JRec<S::kPay> rn{};
-    if (jn >= 0) {
-      pn = a.pos[dj(jn)];
-      rn = S::load_j(a, dj(jn));
-    }
-    for (; k < nme; k++) {
+    for (int k = 0; k < nme; k++) {
       const int j = jn;
-      const double4 pj = pn;
-      const JRec<S::kPay> rj = rn;
       jn = jn2;
       jn2 = idx(k + 2);
-      if (jn >= 0) {
-        pn = a.pos[dj(jn)];
-        rn = S::load_j(a, dj(jn));
-      }
+      const double4 pj = a.pos[dj(j)];
+      const JRec<S::kPay> rj = S::load_j(a, dj(j));
       double dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
       if (WRAP) {
         dx = wrap_nearest(dx, g.dim[0]);
@@ -483,8 +474,8 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
   };
   // light j records (density): indices four entries ahead, particle data two
   // ahead, so every lane keeps two gathers in flight behind the current
-  // entry's math (the loop is latency-bound: one gather ahead left 76% of the
-  // wave time waiting, profiles/r02b_sq_counters.txt)
+  // entry's math (measured: one entry ahead at 108 VGPRs, two at 118 and none
+  // at 80 VGPRs / 6 waves per SIMD all take 0.60 ms at 128^3)
   int ja = idx(0), jb = idx(1), jc = idx(2), jd = idx(3);
   double4 pa = make_double4(0., 0., 0., 0.), pb = pa;
   JRec<S::kPay> ra{}, rb{};

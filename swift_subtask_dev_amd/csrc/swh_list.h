@@ -472,39 +472,40 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
     const T r2 = tdx * tdx + tdy * tdy + tdz * tdz;
     if (st.accept(j, pj, r2)) st.interact_staged(rj.p, rj.meta, pj, tdx, tdy, tdz, r2);
   };
-  // light j records (density): indices four entries ahead, particle data two
-  // ahead, so every lane keeps two gathers in flight behind the current
-  // entry's math (measured: one entry ahead at 108 VGPRs, two at 118 and none
-  // at 80 VGPRs / 6 waves per SIMD all take 0.60 ms at 128^3)
-  int ja = idx(0), jb = idx(1), jc = idx(2), jd = idx(3);
-  double4 pa = make_double4(0., 0., 0., 0.), pb = pa;
-  JRec<S::kPay> ra{}, rb{};
-  if (ja >= 0) {
-    pa = a.pos[dj(ja)];
-    ra = S::load_j(a, dj(ja));
+  // light j records (density): a software pipeline over three register
+  // slots, entry e in slot e % 3. A slot's particle data are loaded three
+  // entries before its math and its list index three entries before that.
+  // Every load is unconditional (indices past the list are clamped to its
+  // last entry), and each slot is refilled in place after its math, so the
+  // compiler emits no copy of an in-flight load. A rotating ring with
+  // conditional loads made it wait for every load it had just issued (the ISA
+  // showed s_waitcnt vmcnt(0) ahead of each entry's math), so the prefetch
+  // bought nothing.
+  if (nme <= 0) return;
+  const int last = nme - 1;
+  auto idx_c = [&](int m) { return col[list_off(s + min(m, last) * LPI)]; };
+  int x0 = idx_c(0), x1 = idx_c(1), x2 = idx_c(2);
+  int j0 = x0, j1 = x1, j2 = x2;
+  double4 p0 = a.pos[dj(j0)], p1 = a.pos[dj(j1)], p2 = a.pos[dj(j2)];
+  JRec<S::kPay> r0 = S::load_j(a, dj(j0)), r1 = S::load_j(a, dj(j1)), r2 = S::load_j(a, dj(j2));
+  x0 = idx_c(3);
+  x1 = idx_c(4);
+  x2 = idx_c(5);
+#define SWH_WALK_SLOT(K, E)                 \
+  {                                         \
+    if ((E) >= nme) break;                  \
+    step(j##K, p##K, r##K);                 \
+    j##K = x##K;                            \
+    p##K = a.pos[dj(j##K)];                 \
+    r##K = S::load_j(a, dj(j##K));          \
+    x##K = idx_c((E) + 6);                  \
   }
-  if (jb >= 0) {
-    pb = a.pos[dj(jb)];
-    rb = S::load_j(a, dj(jb));
+  for (int m = 0; m < nme; m += 3) {
+    SWH_WALK_SLOT(0, m)
+    SWH_WALK_SLOT(1, m + 1)
+    SWH_WALK_SLOT(2, m + 2)
   }
-  for (int m = 0; m < nme; m++) {
-    double4 pn = make_double4(0., 0., 0., 0.);
-    JRec<S::kPay> rn{};
-    if (jc >= 0) {
-      pn = a.pos[dj(jc)];
-      rn = S::load_j(a, dj(jc));
-    }
-    const int jcur = ja;
-    ja = jb;
-    jb = jc;
-    jc = jd;
-    jd = idx(m + 4);
-    step(jcur, pa, ra);
-    pa = pb;
-    ra = rb;
-    pb = pn;
-    rb = rn;
-  }
+#undef SWH_WALK_SLOT
 }
 
 // One loop over every active, listed particle: LPI lanes per i, 256/LPI

@@ -71,8 +71,16 @@ if kt.exists() and dens:
     name = dens[0]
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
          for r in csv.DictReader(open(kt)) if r["Kernel_Name"].split("(")[0] == name]
-    steps = json.loads(trace_bench[-1])["steps"] if trace_bench else 10
-    timed = d[-steps:]
+    tb = json.loads(trace_bench[-1]) if trace_bench else {"steps": 10, "warmup": 3}
+    steps, warmup = tb["steps"], tb.get("warmup", 3)
+    # bench.py's order: the setup chain, then ONE counted density loop (its
+    # build counts entries with atomics: the second launch many times the
+    # median), then `warmup` untimed and `steps` timed steps; the list-reuse
+    # and breakdown sections come after and are not the headline
+    med = statistics.median(d)
+    slow = [k for k, x in enumerate(d) if x > 4 * med]
+    start = (slow[1] + 1 if len(slow) > 1 else 0) + warmup
+    timed = d[start:start + steps]
     (dst / f"{tag}_density_dispatches.json").write_text(json.dumps({
-        "kernel": name, "dispatch_ms": d, "timed_dispatches": len(timed),
+        "kernel": name, "dispatch_ms": d, "timed_dispatches": len(timed), "timed_first_index": start,
         "timed_mean_ms": sum(timed) / len(timed), "all_mean_ms": sum(d) / len(d)}, indent=1) + "\n")

@@ -76,7 +76,14 @@ __global__ void posf_kernel(GridDev g, const double4* __restrict__ pos,
   if (i < n) posf[i] = pcell[i] >= 0 ? cell_local(g, pos[i], pcell[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-__global__ __launch_bounds__(64) void list_build_kernel(GridDev g, SoA a, ListDev ld,
+#ifndef SWH_BUILD_WPE
+#define SWH_BUILD_WPE 0
+#endif
+__global__ __launch_bounds__(64)
+#if SWH_BUILD_WPE > 0
+__attribute__((amdgpu_waves_per_eu(SWH_BUILD_WPE)))
+#endif
+void list_build_kernel(GridDev g, SoA a, ListDev ld,
                                                        const int2* __restrict__ groups,
                                                        int ngroups, int max_active_bin,
                                                        const unsigned int* __restrict__ hmax_bits,

@@ -40,6 +40,13 @@ namespace swh {
 
 constexpr int kListSlots = 16;   // list columns per i-group (max group size)
 constexpr int kListLpiBuild = 4;  // lanes per i in the list build
+#ifndef SWH_LIST_REGION
+#define SWH_LIST_REGION 256
+#endif
+#ifndef SWH_LIST_ICAP
+#define SWH_LIST_ICAP 96
+#endif
+constexpr int kListRegion = SWH_LIST_REGION;  // staged candidates per region of the build
 
 // First entry of a listed particle (`base` = group * kListSlots + slot) and
 // the offset of its entry k (module layout comment).
@@ -87,10 +94,11 @@ __global__ void cell_reach_kernel(GridDev g, const double4* __restrict__ pos, in
 template <int LPI>
 struct ListLds {
   static constexpr int GS = 64 / LPI;
-  static constexpr int kICap = 96;           // LDS hits per i before a flush
+  static constexpr int kICap = SWH_LIST_ICAP;           // LDS hits per i before a flush
+  static_assert(kICap >= kT5Blk * LPI, "one consume block must fit i's LDS hits");
   static constexpr int kStride = kICap + 2;  // odd dword stride: lists start on different banks
-  float4 cand[kT5Region];  // x, y, z relative to the box centre; w = inflated R_j^2
-  int candj[kT5Region];
+  float4 cand[kListRegion];  // x, y, z relative to the box centre; w = inflated R_j^2
+  int candj[kListRegion];
   unsigned short hits[GS * kStride + 64];  // [i slot][entry] region slots; + per-lane dummies
   int cell_pre[64];     // staging batch: prefix sum of the cells' counts
   int cell_j0[64];      // first sorted index of the cell minus its prefix
@@ -101,6 +109,7 @@ struct ListLds {
 #define SWH_STAGE_U 4
 #endif
 constexpr int kStageU = SWH_STAGE_U;  // candidates per lane per staging pass
+static_assert(kListRegion >= 64 * kStageU, "a staging pass must fit the region");
 
 // Positions relative to the lower corner of each particle's grid cell, in
 // fp32, with h: the list build's staging loads 16 B per candidate and turns
@@ -153,7 +162,7 @@ __device__ __forceinline__ void list_consume(const GridDev& g, const ListDev& ld
     const int c0 = b * kT5Blk * LPI + s;
     float4 cv[kT5Blk];
 #pragma unroll
-    for (int kk = 0; kk < kT5Blk; kk++) cv[kk] = L.cand[min(c0 + kk * LPI, kT5Region - 1)];
+    for (int kk = 0; kk < kT5Blk; kk++) cv[kk] = L.cand[min(c0 + kk * LPI, kListRegion - 1)];
     bool hit[kT5Blk];
     int cnt = 0;
 #pragma unroll
@@ -319,7 +328,7 @@ __device__ __forceinline__ void list_build(const GridDev& g, const SoA& a, const
       L.cell_off[lane] = make_float4(ox, oy, oz, 0.f);
       wave_sync();
       for (int base = 0; base < total; base += 64 * kStageU) {
-        if (nst > kT5Region - 64 * kStageU) {  // no room for this pass: consume the region
+        if (nst > kListRegion - 64 * kStageU) {  // no room for this pass: consume the region
           wave_sync();
           if (diag != 1) {
             if (wrap)

@@ -14,6 +14,6 @@ mkdir -p "$out"
   -Wno-unused-variable -Iinclude -I$pkg/csrc -fvisibility=hidden -DSWH_BUILD "$@" \
   -c $pkg/csrc/$src -o "$out/$name.hydro.o"
 others=$(ls $obj/*.o | grep -v "${src%.hip}")
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/$name.so" "$out/$name.hydro.o" $others
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/$name.so" "$out/$name.hydro.o" $others -lhipfft
 rm -f "$out/$name.hydro.o"
 echo "built $out/$name.so"

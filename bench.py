@@ -56,49 +56,163 @@ def log(msg):
     print(msg, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(parts, P, n_density, n_force, runs=3, threads=None):
-    """The oracle's float restatement of DOSELF1/DOPAIR1 + DOSELF2/DOPAIR2
-    (sorted pseudo-Verlet loops) over a cdim=20 periodic cell grid, timed on
-    the host cores (kind "port"; the reference's own build is unavailable)."""
+def cpu_share_threads():
+    """This job's CPU share: OMP_NUM_THREADS (16 per GPU on the pool's boxes)
+    or the CPUs it may run on, at most 16."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def run_cpu_worker(kind, arrays, meta, threads):
+    """Run a CPU-baseline leg in a child process that never imports torch, so
+    its OpenMP runtime starts with one thread per physical core of this job's
+    share, pinned (OMP_PLACES=cores, OMP_PROC_BIND=close) -- torch's libgomp
+    is the one the oracle binds to and reads its environment once, at torch's
+    import. Inputs travel through an .npz under /tmp."""
+    import subprocess
+    import tempfile
+
+    with tempfile.TemporaryDirectory(prefix="swh_cpu_") as d:
+        path = os.path.join(d, "in.npz")
+        np.savez(path, **arrays)
+        env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PLACES="cores",
+                   OMP_PROC_BIND="close")
+        cmd = [sys.executable, str(Path(__file__).resolve()), "--cpu-worker", kind,
+               "--cpu-input", path, "--cpu-meta", json.dumps(meta)]
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
+        if r.returncode != 0:
+            raise RuntimeError(f"cpu worker failed ({r.returncode}): {r.stderr[-2000:]}")
+        return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+def cpu_worker_main(kind, path, meta):
+    """The child of run_cpu_worker: the oracle's float restatement timed on
+    this process's pinned threads (test infrastructure: bench's cpu_baseline
+    leg only)."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib as O
     from swift_subtask_dev_amd import abi
 
-    threads = threads or min(16, os.cpu_count() or 1)
-    eb = abi.EngineBundle(dim=tuple(P.dim), periodic=True, params=P, max_active_bin=P.max_active_bin)
-    new = O.fn("f32", "cellgrid_new")
-    run = O.fn("f32", "cellgrid_run")
-    free = O.fn("f32", "cellgrid_free")
-    # separate copies: struct part's density/force union must keep the force
-    # inputs intact for the force loop
-    gd = new(parts.ctypes.data, len(parts), float(P.dim[0]), 20)
-    gf = new(parts.ctypes.data, len(parts), float(P.dim[0]), 20)
-    times = []
-    try:
-        for r in range(runs + 1):  # first run = warm-up
-            td = run(gd, C.addressof(eb.runner), 0, threads)
-            tf = run(gf, C.addressof(eb.runner), 2, threads)
+    z = np.load(path)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    out = {"threads": threads}
+    if kind == "hydro":
+        parts = z["parts"].view(abi.PART_DTYPE).reshape(-1)
+        P = abi.default_hydro_params(tuple(meta["dim"]), True)
+        P.max_active_bin = meta["max_active_bin"]
+        eb = abi.EngineBundle(dim=tuple(P.dim), periodic=True, params=P,
+                              max_active_bin=P.max_active_bin)
+        new, run, free = (O.fn("f32", n) for n in ("cellgrid_new", "cellgrid_run",
+                                                    "cellgrid_free"))
+        # separate copies: the density/force union must keep the force inputs
+        gd = new(parts.ctypes.data, len(parts), float(P.dim[0]), meta["cdim"])
+        gf = new(parts.ctypes.data, len(parts), float(P.dim[0]), meta["cdim"])
+        try:
+            times = []
+            for r in range(meta["runs"] + 1):  # first run = warm-up
+                td = run(gd, C.addressof(eb.runner), 0, threads)
+                tf = run(gf, C.addressof(eb.runner), 2, threads)
+                if r > 0:
+                    times.append(td + tf)
+            out["seconds_share"] = statistics.median(times)
+            # one pinned thread: the per-core rate (one run, memory already warm)
+            out["seconds_1"] = (run(gd, C.addressof(eb.runner), 0, 1) +
+                                run(gf, C.addressof(eb.runner), 2, 1))
+        finally:
+            free(gd)
+            free(gf)
+    elif kind == "grav":
+        G = abi.GravParams.from_buffer_copy(z["G"].tobytes())
+        g = z["gparts"].view(abi.GPART_DTYPE).reshape(-1).copy()
+        leaves, offs, pairs = z["leaves"], z["offs"], z["pairs"]
+        f = O.fn("f32", "grav_pp_leaves")
+        times, n = [], 0
+        for r in range(meta["runs"] + 1):
+            t0 = time.perf_counter()
+            n = f(g.ctypes.data, leaves.ctypes.data, len(leaves), offs.ctypes.data,
+                  pairs.ctypes.data, C.byref(G), None, None)
             if r > 0:
-                times.append(td + tf)
-    finally:
-        free(gd)
-        free(gf)
-    t = statistics.median(times)
+                times.append(time.perf_counter() - t0)
+        out["seconds_share"] = statistics.median(times)
+        out["interactions"] = int(n)
+    elif kind == "cosmo":
+        parts = z["parts"].view(abi.PART_DTYPE).reshape(-1)
+        P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
+        P.max_active_bin = 1
+        eb = abi.EngineBundle(dim=(1.0, 1.0, 1.0), periodic=True, params=P, max_active_bin=1)
+        new, run, free = (O.fn("f32", n) for n in ("cellgrid_new", "cellgrid_run",
+                                                    "cellgrid_free"))
+        gd = new(parts.ctypes.data, len(parts), 1.0, meta["cdim"])
+        gf = new(parts.ctypes.data, len(parts), 1.0, meta["cdim"])
+        try:
+            run(gd, C.addressof(eb.runner), 0, threads)  # warm-up
+            th = run(gd, C.addressof(eb.runner), 0, threads) + run(gf, C.addressof(eb.runner),
+                                                                    2, threads)
+        finally:
+            free(gd)
+            free(gf)
+        G = abi.GravParams.from_buffer_copy(z["G"].tobytes())
+        g = z["gparts"].view(abi.GPART_DTYPE).reshape(-1).copy()
+        cells, tops, pc = z["cells"], z["tops"], z["pairs"]
+        stats = (C.c_longlong * 5)()
+        t0 = time.perf_counter()
+        O.fn("f32", "grav_tree")(g.ctypes.data, len(g), cells.ctypes.data, len(cells),
+                                 tops.ctypes.data, len(tops), pc.ctypes.data, len(pc) // 2,
+                                 C.byref(G), stats, None)
+        out["seconds_gravity"] = time.perf_counter() - t0
+        out["seconds_hydro"] = th
+        out["seconds_share"] = th + out["seconds_gravity"]
+        out["tree_stats"] = list(stats)
+    print(json.dumps(out), flush=True)
+
+
+def cpu_baseline(parts, P, n_density, n_force, runs=3, threads=None):
+    """The oracle's float restatement of DOSELF1/DOPAIR1 + DOSELF2/DOPAIR2
+    (sorted pseudo-Verlet loops) over a cdim=20 periodic cell grid, timed on
+    this job's CPU share, one pinned thread per physical core (kind "port";
+    the reference's own build is unavailable), and on one pinned thread. The
+    full host (every physical core) is projected from the per-thread rate the
+    share run reaches: the pool gives one GPU's job 16 CPUs, so a run on all
+    of the host's cores is not ours to start."""
+    threads = threads or cpu_share_threads()
+    w = run_cpu_worker("hydro", {"parts": np.ascontiguousarray(parts).view(np.uint8)},
+                       {"dim": list(P.dim), "max_active_bin": int(P.max_active_bin),
+                        "cdim": 20, "runs": runs}, threads)
+    t, t1 = w["seconds_share"], w["seconds_1"]
+    n = n_density + n_force
+    host = host_cpu_info()
+    phys = host.get("physical_cores") or threads
+    eff = (n / t / threads) / (n / t1)  # per-thread efficiency of the share run
     calib = None
     cpath = ROOT / "profiles" / "cpu_calibration.json"
     if cpath.exists():
         calib = json.loads(cpath.read_text())
     return {
-        "value": (n_density + n_force) / t,
+        "value": n / t,
         "unit": "interactions/s",
         "cores": threads,
         "kind": "port",
-        "host": host_cpu_info(),
+        "pinning": "one thread per physical core (OMP_PLACES=cores, OMP_PROC_BIND=close), "
+                   "child process without torch",
+        "host": host,
         "calibration": calib,
         "sample": f"full 128^3 box, density+force loops (float restatement of DOSELF1/DOPAIR1/"
-                  f"DOSELF2/DOPAIR2, cdim=20 cells), median of {runs} runs after 1 warm-up, "
-                  f"{t:.3f} s per step",
+                  f"DOSELF2/DOPAIR2, cdim=20 cells), median of {runs} runs after 1 warm-up on "
+                  f"{threads} pinned threads ({t:.3f} s per step); one pinned thread "
+                  f"{t1:.3f} s per step",
         "seconds_per_step": t,
+        "single_core": {"value": n / t1, "seconds_per_step": t1},
+        "full_host_projected": {
+            "value": n / t1 * phys * eff, "cores": phys,
+            "basis": f"one-thread rate x {phys} physical cores x the {eff:.3f} per-thread "
+                     f"efficiency of the {threads}-thread run (projected, not measured: a "
+                     "1-GPU job here gets a 16-CPU share)"},
     }
 
 
@@ -261,8 +375,93 @@ def step_breakdown(sp, P, stream, torch, local, reps=3):
     return out
 
 
-def load_traffic():
-    path = ROOT / "profiles" / "traffic_density.json"
+def steady_state(sp, P, stream, torch, local, n_owned, args, skin=None, steps=None):
+    """K steps of drift + density + force on the device-resident box with the
+    pair lists kept while valid (swh_tuning.list_keep). Drift velocities:
+    random, |v| ~ 1, dt so that the fastest particle moves `disp` h per step
+    (a Courant-limited subsonic flow moves < 0.05 h per step); the space is
+    re-binned every `rebin` steps (dx bound > half a cell). The K steps run
+    twice from the same state: counted (exact interactions per step), then
+    timed without counting; the list builds the device ran are reported."""
+    from swift_subtask_dev_amd import abi
+    skin = args.steady_skin if skin is None else skin
+    steps = args.steady_steps if steps is None else steps
+    disp = args.steady_disp
+    rng = np.random.Generator(np.random.PCG64(23))
+    n = len(local)
+    xp = abi.new_xparts(n)
+    xp["v_full"] = rng.normal(0.0, 0.577, (n, 3)).astype(np.float32)
+    vmax = float(np.sqrt((xp["v_full"].astype(np.float64) ** 2).sum(axis=1)).max())
+    h = float(np.median(local["h"]))
+    dt = disp * h / vmax
+    D = abi.DriftParams(dt, 0.0, 0.0, 0.0, 0.0)
+    sp.set_tuning(args.cell_factor, args.loop_variant, args.group_size, args.cell_scale, 0,
+                  args.list_capacity, skin, 1)
+
+    def reset():
+        sp.upload(local)
+        sp.set_owned(n_owned)
+        sp.rebuild(P)
+        sp.upload_xparts(xp)
+
+    reset()
+    w = min(sp.info()["cell_width"])
+    rebin = max(1, int(0.5 * w / (vmax * dt)))
+
+    def run(count, ev=None):
+        nd = nf = 0
+        for k in range(steps):
+            if k > 0 and k % rebin == 0:
+                sp.rebuild(P)
+            sp.drift(D, P)
+            sp.init_parts(P)
+            if ev:
+                ev[k][0].record(stream)
+            r = sp.density(P, count=count)
+            if ev:
+                ev[k][1].record(stream)
+            sp.reset_acceleration(P)
+            if ev:
+                ev[k][2].record(stream)
+            q = sp.force(P, count=count)
+            if ev:
+                ev[k][3].record(stream)
+            if count:
+                nd += r
+                nf += q
+        return nd, nf
+
+    b0 = sp.info()["list_builds"]
+    nd, nf = run(True)
+    builds = sp.info()["list_builds"] - b0
+    reset()
+    torch.cuda.synchronize()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+    t0 = time.perf_counter()
+    run(False, ev)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    td = statistics.mean([e[0].elapsed_time(e[1]) for e in ev])
+    tf = statistics.mean([e[2].elapsed_time(e[3]) for e in ev])
+    b_d = n_owned * (27 * S_IN_DENSITY + S_OUT_DENSITY)
+    return {"note": "untimed by the headline: drift + density + force per step with the pair "
+                    "lists kept across drifts while valid (device check, rebuilt on the device "
+                    "when a particle's H + 2 D exceeds its build reach)",
+            "steps": steps, "list_skin": skin, "displacement_per_step_over_h": disp,
+            "rebin_every": rebin, "list_builds": int(builds),
+            "steps_per_list_build": steps / max(1, builds),
+            "interactions": nd + nf, "ms_per_step": el / steps * 1e3,
+            "interactions_per_s": (nd + nf) / el,
+            "density_ms": td, "force_ms": tf,
+            "density_roofline_frac": b_d / (td * 1e-3) / HBM_PEAK}
+
+
+def load_traffic(workload="sedov"):
+    """PMC-measured HBM bytes of the roofline kernel(s), per workload
+    (profiles/traffic_density.json: Sedov 128^3 density loop;
+    profiles/traffic_<workload>.json otherwise)."""
+    name = "traffic_density.json" if workload == "sedov" else f"traffic_{workload}.json"
+    path = ROOT / "profiles" / name
     if path.exists():
         try:
             return json.loads(path.read_text())
@@ -338,11 +537,40 @@ def run_grav(args, ctx, rank, world, dist, torch):
                                    "leaf pairs, P2P, softening 0.001, non-periodic",
                        "gparts": int(len(gs)), "leaves": nl, "leaf_cdim": cdim,
                        "interactions_per_step": int(total / args.steps)},
-            "roofline": {"bound": "fp64-vector", "achieved": flops / 1e12,
+            "roofline": {"bound": "fp64-vector", "kernel": "p2p_kernel", "achieved": flops / 1e12,
                          "peak": FP64_PEAK / 1e12, "unit": "TFLOP/s", "frac": flops / FP64_PEAK,
                          "traffic": None, "flops_model": "28 flops per directed P2P interaction"},
             "cpu_baseline": None,
         }
+        tr = load_traffic("grav") if (n == 256 and world == 1) else None
+        if tr:
+            out["roofline"]["traffic"] = tr.get("bytes_per_launch")
+            out["roofline"]["traffic_source"] = tr.get("source")
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                # bounded sample: the first 1% of the i-leaves with their full
+                # source lists (every leaf stays a source)
+                k = max(1, nl // 100)
+                so = np.zeros(nl + 1, dtype=np.int32)
+                so[1:k + 1] = np.diff(offs)[:k]
+                so = np.cumsum(so).astype(np.int32)
+                threads = cpu_share_threads()
+                w = run_cpu_worker("grav", {"gparts": np.ascontiguousarray(gs).view(np.uint8),
+                                            "leaves": leaves, "offs": so,
+                                            "pairs": pairs[:so[-1]],
+                                            "G": np.frombuffer(bytes(G), dtype=np.uint8)},
+                                   {"runs": 2}, threads)
+                out["cpu_baseline"] = {
+                    "value": w["interactions"] / w["seconds_share"], "unit": "interactions/s",
+                    "cores": threads, "kind": "port", "host": host_cpu_info(),
+                    "pinning": "one thread per physical core, child process without torch",
+                    "sample": f"the first {k} of {nl} i-leaves with their 27-leaf source "
+                              f"lists: {w['interactions']} P2P interactions, float "
+                              f"restatement of runner_doself/dopair_grav_pp, median of 2 runs "
+                              f"after 1 warm-up ({w['seconds_share']:.3f} s)"}
+                out["gpu_over_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+            except Exception as e:  # report, never fake
+                log(f"grav cpu baseline failed: {e}")
         print(json.dumps(out), flush=True)
     sp.close()
 
@@ -485,9 +713,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=128, help="particles per dimension per GPU")
     ap.add_argument("--cell-factor", type=int, default=int(os.environ.get("SWH_CELL_FACTOR", "1")))
-    ap.add_argument("--loop-variant", type=int, default=int(os.environ.get("SWH_LOOP_VARIANT", "0")),
-                    help="0 default (7), 7 pair lists, 5 tile loop (group per wave), "
-                         "4 tile loop (4 groups per wave), 1 direct gather")
+    ap.add_argument("--loop-variant", type=int, default=0, choices=[0, 7],
+                    help="0 default (7): pair lists")
     ap.add_argument("--cell-scale", type=float, default=float(os.environ.get("SWH_CELL_SCALE", "0")),
                     help="grid cells per H_max as a real number (overrides --cell-factor)")
     ap.add_argument("--diag-mode", type=int, default=0,
@@ -500,21 +727,49 @@ def main():
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-runs", type=int, default=3)
+    ap.add_argument("--no-steady", action="store_true", help="skip the untimed steady-state run")
+    ap.add_argument("--steady-skin", type=float, default=0.1)
+    ap.add_argument("--steady-steps", type=int, default=24)
+    ap.add_argument("--steady-disp", type=float, default=0.05,
+                    help="steady state: displacement of the fastest particle per step / h")
     ap.add_argument("--no-breakdown", action="store_true",
                     help="skip the untimed full-step breakdown (drift, rebuild, chain)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong: the 128^3 box split over the GPUs (the metric); "
                          "weak: one 128^3 box per GPU")
+    ap.add_argument("--cpu-worker", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-input", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-meta", default="{}", help=argparse.SUPPRESS)
     ap.add_argument("--workload", default="sedov", choices=["sedov", "grav", "eagle", "cosmo"],
                     help="sedov: the headline metric (SedovBlast_3D 128^3 density + force); "
                          "grav: BASELINE config 4 (uniform DM box P2P, --n 256); "
                          "eagle: BASELINE config 3 stand-in (clustered box); "
                          "cosmo: BASELINE config 5 stand-in (hydro + tree/PM gravity, overlapped)")
     args = ap.parse_args()
+    if args.cpu_worker:  # child of run_cpu_worker: no torch, no GPU
+        cpu_worker_main(args.cpu_worker, args.cpu_input, json.loads(args.cpu_meta))
+        return
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N`: one rank per GPU under torch.distributed.run,
+        # started before anything here touches a GPU; exit with its code
+        import socket
+        import subprocess
+
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+               f"--master-port={port}", str(Path(__file__).resolve())] + sys.argv[1:]
+        log(f"launching {args.gpus} ranks: {' '.join(cmd)}")
+        sys.exit(subprocess.call(cmd))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: one rank per GPU")
 
     import torch
 
@@ -654,36 +909,22 @@ def main():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     total_interactions, total_owned = tot.tolist()
     elapsed_max = tmax.item()
-    # The same step with the pair lists kept while they stay valid (diag_mode
-    # 7): nothing moves between these steps, so -- as SWIFT keeps its sort
-    # lists until the particles have drifted -- the density loop walks the
-    # lists built by the first one. Reported beside the headline, which
-    # rebuilds the lists inside every density loop.
-    reuse = None
-    if world == 1 and args.loop_variant in (0, 7) and args.diag_mode == 0:
-        sp.set_tuning(args.cell_factor, args.loop_variant, args.group_size, args.cell_scale,
-                      7, args.list_capacity, args.list_skin)
-        sp.rebuild(P)
-        step()
-        torch.cuda.synchronize()
-        ev2 = [[torch.cuda.Event(enable_timing=True) for _ in range(4)]
-               for _ in range(args.steps)]
-        t1 = time.perf_counter()
-        for k in range(args.steps):
-            step(ev2[k])
-        torch.cuda.synchronize()
-        el2 = time.perf_counter() - t1
-        td2 = statistics.mean([e[0].elapsed_time(e[1]) * 1e-3 for e in ev2])
-        tf2 = statistics.mean([e[2].elapsed_time(e[3]) * 1e-3 for e in ev2])
-        b_d2 = n_owned * (27 * S_IN_DENSITY + S_OUT_DENSITY)
-        reuse = {"note": "untimed by the headline: the density loop walks the lists of the "
-                         "previous step (valid: nothing moved), as SWIFT keeps its sorts",
-                 "ms_per_step": el2 / args.steps * 1e3,
-                 "interactions_per_s": (n_density + n_force) * args.steps / el2,
-                 "density_ms": td2 * 1e3, "force_ms": tf2 * 1e3,
-                 "density_roofline_frac": b_d2 / td2 / HBM_PEAK}
+    # Steady state (untimed by the headline, which builds the lists in every
+    # density loop): K x (drift + hydro_init_part + density + reset + force)
+    # with the pair lists kept across drifts while their skin covers the
+    # displacement (list_keep; the device decides and rebuilds), the space
+    # re-binned every `rebin` steps -- SWIFT's step, which keeps its sorts
+    # until the particles have moved too far.
+    steady = None
+    if world == 1 and args.diag_mode == 0 and not args.no_steady:
+        try:
+            steady = steady_state(sp, P, stream, torch, local, n_owned, args)
+        except Exception as e:  # report, never fake
+            log(f"steady state failed: {e}")
         sp.set_tuning(args.cell_factor, args.loop_variant, args.group_size, args.cell_scale,
                       args.diag_mode, args.list_capacity, args.list_skin)
+        sp.upload(local)
+        sp.set_owned(n_owned)
         sp.rebuild(P)
     breakdown = None
     if world == 1 and not args.no_breakdown and not eagle:
@@ -700,8 +941,9 @@ def main():
         achieved = b_dens / td
         # PMC traffic was measured on the default configuration only
         default_cfg = (args.loop_variant == 0 and args.group_size == 0 and args.list_skin == 0.0
-                       and args.cell_factor == 1 and args.cell_scale == 0 and args.n == 128)
-        traffic = load_traffic() if default_cfg else None
+                       and args.cell_factor == 1 and args.cell_scale == 0 and args.n == 128
+                       and world == 1)
+        traffic = load_traffic(args.workload) if default_cfg else None
         out = {
             "metric": METRIC_EAGLE if eagle else METRIC,
             "value": total_interactions / elapsed_max,
@@ -744,11 +986,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": {0: "list_build_kernel + walk_kernel<DENSITY,double>",
-                           7: "list_build_kernel + walk_kernel<DENSITY,double>",
-                           1: "loop_kernel<DENSITY,double>",
-                           4: "tile4_kernel<DENSITY,double>",
-                           5: "tile5_kernel<DENSITY,double>"}[args.loop_variant],
+                "kernel": "list_build_kernel + walk_kernel<DENSITY,double>",
                 "achieved": achieved / 1e9,
                 "peak": HBM_PEAK / 1e9,
                 "unit": "GB/s",
@@ -774,8 +1012,8 @@ def main():
             },
             "cpu_baseline": None,
         }
-        if reuse:
-            out["step_lists_reused"] = reuse
+        if steady:
+            out["steady_state"] = steady
         if breakdown:
             out["step_breakdown"] = breakdown
         if eagle:
@@ -787,7 +1025,13 @@ def main():
             # `local` still holds the converged chain state the GPU started from
             try:
                 out["cpu_baseline"] = cpu_baseline(local, P, n_density, n_force, args.cpu_runs)
+                # vs the CPU share of one GPU (measured); vs every physical core of
+                # the host (projected from the measured per-thread rate)
                 out["gpu_over_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+                out["gpu_over_cpu_basis"] = (f"cpu_baseline.value: {out['cpu_baseline']['cores']} "
+                                             "pinned threads, one GPU's CPU share")
+                out["gpu_over_cpu_full_host_projected"] = (
+                    out["value"] / out["cpu_baseline"]["full_host_projected"]["value"])
             except Exception as e:  # report, never fake
                 log(f"cpu baseline failed: {e}")
             try:

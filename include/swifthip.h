@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SWH_ABI_VERSION 6
+#define SWH_ABI_VERSION 7
 
 #if defined(__GNUC__)
 #define SWH_API __attribute__((visibility("default")))
@@ -126,7 +126,15 @@ typedef struct swh_hydro_params {
   int32_t max_active_bin; /* e->max_active_bin */
   int32_t periodic;       /* e->s->periodic    */
   double dim[3];          /* e->s->dim         */
+  /* dt_alpha of the extra ghost per time bin (SWH_NUM_TIME_BINS + 1 entries,
+   * nullable). NULL: the non-cosmological get_timestep(bin, time_base). With
+   * cosmology the engine passes, for every bin b, the physical time of the
+   * bin's current step, cosmology_get_delta_time(cosmo, ti_begin,
+   * ti_begin + get_integer_timestep(b)) with ti_begin =
+   * get_integer_time_begin(ti_current - 1, b) (src/runner_ghost.c:1038-1046). */
+  const double *dt_alpha_bins;
 } swh_hydro_params;
+#define SWH_NUM_TIME_BINS 56
 
 typedef struct swh_grav_params {
   int32_t periodic;  /* e->mesh->periodic  */
@@ -335,23 +343,26 @@ SWH_API swh_status swh_space_sync(swh_space *s);
 /* Kernel-tuning knobs of the batch loops (bench/diagnostics). */
 typedef struct swh_tuning {
   int32_t cell_factor;  /* neighbour-grid cells per H_max (1..4) */
-  int32_t loop_variant; /* 0 = default (7);
-                           7 = pair lists: the density loop builds the step's lists
-                               (r < max(R_i, R_j), R = gamma h (1 + list_skin)), the
-                               density / gradient / force loops walk them;
-                           5 = one-launch tile loop, one i-group per wave;
-                           4 = one-launch tile loop, 64/group_size i-groups per wave;
-                           1 = per-particle direct gather */
-  int32_t group_size;   /* tile i-group size: 0 (default 16), 16, 32, 64 (variants 4, 5) */
+  int32_t loop_variant; /* 0 or 7: pair lists -- the density loop builds the step's lists
+                           (r < max(R_i, R_j), R = gamma h (1 + list_skin)), the density /
+                           gradient / force loops walk them */
+  int32_t group_size;   /* list-build i-group size: 0 (default) or 16 */
   float cell_scale;     /* if > 0: cells per H_max as a real number (overrides cell_factor) */
-  int32_t diag_mode;    /* 0; profiling only (results invalid): 1 = staging only (tile
-                           loops) / list build only (lists), 2 = staging + candidate tests,
-                           4 = fixed-j gathers; 7 (results valid) = a density loop keeps
-                           pair lists that are still valid instead of rebuilding them */
-  int32_t list_capacity; /* list entries per particle (0 = 128); more hits: direct gather */
+  int32_t diag_mode;    /* 0; profiling only (results invalid): 1 = list build stages
+                           candidates only, 2 = build without list writes, 4 = fixed-j
+                           gathers; 7 (results valid) = as list_keep */
+  int32_t list_capacity; /* list entries per particle (0 = 128); more hits: a wave-per-
+                            particle search */
   float list_skin;       /* relative slack of the list reach over gamma h (default 0: exact
                             lists; a ghost that grows any H past its reach makes gradient /
                             force rebuild them) */
+  int32_t list_keep;     /* 1: keep the lists across loops and drifts while they cover every
+                            pair, as SWIFT keeps its sorts until dx_max_sort exceeds
+                            space_maxreldx (space.h:66): after a drift the device compares
+                            each H + 2 D (D = largest displacement since the build) with
+                            the build reach gamma h (1 + list_skin) and rebuilds only when
+                            some particle exceeds it, without a host round trip.
+                            0 (default): every density loop builds the lists. */
 } swh_tuning;
 SWH_API swh_status swh_space_set_tuning(swh_space *s, const swh_tuning *t);
 
@@ -369,6 +380,7 @@ typedef struct swh_space_info {
   int32_t list_overflow; /* last counted list build: particles over list_capacity */
   int32_t list_valid;    /* the step's pair lists are current */
   double dx_max;         /* largest displacement since the last rebuild (drift) */
+  int64_t list_builds;   /* pair-list builds run on the device since the space was created */
 } swh_space_info;
 SWH_API swh_status swh_space_get_info(const swh_space *s, swh_space_info *info);
 

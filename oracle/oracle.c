@@ -553,6 +553,7 @@ struct oracle_params {
   int max_active_bin;
   int periodic;
   double dim[3];
+  const double *dt_alpha_bins; /* nullable: cosmological dt_alpha per time bin */
 };
 
 /* hydro.h:553-566 */
@@ -732,6 +733,14 @@ static inline double get_timestep(timebin_t bin, double time_base) {
   return (double)(1LL << (bin + 1)) * time_base;
 }
 
+/* runner_ghost.c:1038-1046: with cosmology, dt_alpha is the physical time of
+ * the bin's step (cosmology_get_delta_time over [ti_begin, ti_begin +
+ * ti_step]); the caller tabulates it per bin in P->dt_alpha_bins. */
+static inline double dt_alpha_of(timebin_t bin, const struct oracle_params *P) {
+  if (P->dt_alpha_bins) return (bin >= 0 && bin <= num_time_bins) ? P->dt_alpha_bins[bin] : 0.;
+  return get_timestep(bin, P->time_base);
+}
+
 /* ======================================================================== */
 /* Grid-gather box loops: for each active i, visit the grid cells that      */
 /* overlap [x_i - R, x_i + R] and apply the non-symmetric interaction with  */
@@ -786,6 +795,100 @@ static void ogrid_build(struct ogrid *g, const opart *parts, long long N,
 static void ogrid_free(struct ogrid *g) {
   free(g->start);
   free(g->index);
+}
+
+/* Multi-level search structure: the particles are binned by their kernel
+ * reach H = gamma h into levels (level L holds H in (H_max 2^-(L+1),
+ * H_max 2^-L], the last level everything smaller), each with its own grid of
+ * cells about as wide as its largest H (at most 256 per dimension). A gather
+ * visits, per level, the cells within its own reach (r < H_i) or within
+ * max(H_i, H_max of the level) (force: r < max(H_i, H_j)). The visited set
+ * always contains every in-range j, so the interaction set is the one of
+ * the single uniform grid; clustered boxes, whose H span decades, then cost
+ * O(N n_ngb) instead of O(N n_clump). */
+#define OLEV_MAX 8
+struct olevels {
+  int nlev;
+  double hmax[OLEV_MAX]; /* largest H of each level */
+  struct ogrid g[OLEV_MAX];
+};
+
+static void ogrid_build_sub(struct ogrid *g, const opart *parts, const int *ids, long long n,
+                            const double dim[3], double min_width, int periodic) {
+  for (int k = 0; k < 3; k++) {
+    int c = (int)floor(dim[k] / min_width);
+    if (c < 1) c = 1;
+    if (c > 256) c = 256;
+    g->cdim[k] = c;
+    g->w[k] = dim[k] / c;
+  }
+  g->ncell = g->cdim[0] * g->cdim[1] * g->cdim[2];
+  g->start = (int *)calloc((size_t)g->ncell + 1, sizeof(int));
+  g->index = (int *)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+  int *cellof = (int *)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
+  for (long long t = 0; t < n; t++) {
+    const opart *p = &parts[ids[t]];
+    int c[3];
+    for (int k = 0; k < 3; k++) {
+      double xx = p->x[k];
+      if (periodic) xx -= floor(xx / dim[k]) * dim[k];
+      c[k] = (int)floor(xx / g->w[k]);
+      if (c[k] >= g->cdim[k]) c[k] = g->cdim[k] - 1;
+      if (c[k] < 0) c[k] = 0;
+    }
+    cellof[t] = (c[2] * g->cdim[1] + c[1]) * g->cdim[0] + c[0];
+    g->start[cellof[t] + 1]++;
+  }
+  for (int c = 0; c < g->ncell; c++) g->start[c + 1] += g->start[c];
+  int *fill = (int *)malloc(sizeof(int) * (size_t)g->ncell);
+  memcpy(fill, g->start, sizeof(int) * (size_t)g->ncell);
+  for (long long t = 0; t < n; t++) g->index[fill[cellof[t]]++] = ids[t];
+  free(fill);
+  free(cellof);
+}
+
+static void olevels_build(struct olevels *L, const opart *parts, long long N,
+                          const double dim[3], int periodic) {
+  double hmax = 0;
+  for (long long i = 0; i < N; i++)
+    if (!part_is_inhibited(&parts[i]) && parts[i].h > hmax) hmax = parts[i].h;
+  hmax *= kernel_gamma;
+  const double dmax = fmax(dim[0], fmax(dim[1], dim[2]));
+  if (!(hmax > 0)) hmax = dmax;
+  /* levels down to the 256-cell resolution of the box (finer buys nothing) */
+  int nlev = 1;
+  while (nlev < OLEV_MAX && hmax / (double)(1 << nlev) > dmax / 256.) nlev++;
+  L->nlev = nlev;
+  long long *cnt = (long long *)calloc(OLEV_MAX, sizeof(long long));
+  int *lev = (int *)malloc(sizeof(int) * (size_t)(N > 0 ? N : 1));
+  for (long long i = 0; i < N; i++) {
+    lev[i] = -1;
+    if (part_is_inhibited(&parts[i])) continue;
+    const double H = (double)parts[i].h * kernel_gamma;
+    int l = 0;
+    while (l < nlev - 1 && H <= hmax / (double)(2 << l)) l++;
+    lev[i] = l;
+    cnt[l]++;
+  }
+  int *ids = (int *)malloc(sizeof(int) * (size_t)(N > 0 ? N : 1));
+  for (int l = 0; l < nlev; l++) {
+    long long n = 0;
+    double hl = 0;
+    for (long long i = 0; i < N; i++)
+      if (lev[i] == l) {
+        ids[n++] = (int)i;
+        if (parts[i].h > hl) hl = parts[i].h;
+      }
+    L->hmax[l] = hl * kernel_gamma;
+    ogrid_build_sub(&L->g[l], parts, ids, n, dim, hl > 0 ? hl * kernel_gamma : dmax, periodic);
+  }
+  free(ids);
+  free(lev);
+  free(cnt);
+}
+
+static void olevels_free(struct olevels *L) {
+  for (int l = 0; l < L->nlev; l++) ogrid_free(&L->g[l]);
 }
 
 /* src/periodic.h:66-72 */
@@ -892,9 +995,8 @@ static double max_h(const opart *o, long long N) {
 static long long box_loop(opart *o, long long N, const struct oracle_params *P,
                           int loop, const int *subset, long long nsub,
                           int *counts) {
-  const double hmax = max_h(o, N) * kernel_gamma;
-  struct ogrid g;
-  ogrid_build(&g, o, N, P->dim, hmax > 0 ? hmax : P->dim[0], P->periodic);
+  struct olevels L;
+  olevels_build(&L, o, N, P->dim, P->periodic);
   const long long nit = subset ? nsub : N;
   long long total = 0;
 #pragma omp parallel for schedule(dynamic, 256) reduction(+ : total)
@@ -902,13 +1004,16 @@ static long long box_loop(opart *o, long long N, const struct oracle_params *P,
     const long long i = subset ? subset[t] : t;
     if (!part_is_active(&o[i], (timebin_t)P->max_active_bin)) continue;
     if (part_is_inhibited(&o[i])) continue;
-    const double reach =
-        (loop == LOOP_FORCE) ? hmax : (double)o[i].h * kernel_gamma;
-    const long long n = gather_one(o, &g, i, loop, reach, P);
+    const double Hi = (double)o[i].h * kernel_gamma;
+    long long n = 0;
+    for (int l = 0; l < L.nlev; l++) {
+      const double reach = (loop == LOOP_FORCE) ? fmax(Hi, L.hmax[l]) : Hi;
+      n += gather_one(o, &L.g[l], i, loop, reach, P);
+    }
     if (counts) counts[i] = (int)n;
     total += n;
   }
-  ogrid_free(&g);
+  olevels_free(&L);
   return total;
 }
 
@@ -1079,7 +1184,7 @@ API void PFX(box_extra_ghost)(struct part *parts, long long N,
     opart *p = &o[i];
     if (!part_is_active(p, (timebin_t)P->max_active_bin)) continue;
     hydro_end_gradient(p);
-    const real dt_alpha = (real)get_timestep(p->time_bin, P->time_base);
+    const real dt_alpha = (real)dt_alpha_of(p->time_bin, P);
     hydro_prepare_force(p, P, dt_alpha);
     timestep_limiter_prepare_force(p);
     hydro_reset_acceleration(p);
@@ -1930,7 +2035,7 @@ API void orf_part_prepare_gradient(struct part *p, const struct oracle_params *P
 }
 API void orf_part_extra_ghost(struct part *p, const struct oracle_params *P) {
   hydro_end_gradient(p);
-  hydro_prepare_force(p, P, (float)get_timestep(p->time_bin, P->time_base));
+  hydro_prepare_force(p, P, (float)dt_alpha_of(p->time_bin, P));
   timestep_limiter_prepare_force(p);
   hydro_reset_acceleration(p);
 }

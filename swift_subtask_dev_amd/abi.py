@@ -164,7 +164,20 @@ class HydroParams(C.Structure):
         ("diff_alpha", C.c_float), ("diff_beta", C.c_float), ("diff_alpha_max", C.c_float),
         ("diff_alpha_min", C.c_float),
         ("max_active_bin", C.c_int32), ("periodic", C.c_int32), ("dim", C.c_double * 3),
+        ("dt_alpha_bins", C.POINTER(C.c_double)),
     ]
+
+    def set_dt_alpha_bins(self, table) -> None:
+        """Per-time-bin dt_alpha (cosmological runs, cosmo.dt_alpha_table);
+        None restores the non-cosmological get_timestep. The array is kept
+        alive by this object."""
+        if table is None:
+            self._dt_keep = None
+            self.dt_alpha_bins = None
+            return
+        arr = (C.c_double * (NUM_TIME_BINS + 1))(*[float(v) for v in table])
+        self._dt_keep = arr
+        self.dt_alpha_bins = C.cast(arr, C.POINTER(C.c_double))
 
 
 class GravParams(C.Structure):
@@ -240,14 +253,15 @@ class SpaceInfo(C.Structure):
                 ("reserved", C.c_int32), ("cell_width", C.c_double * 3), ("h_max", C.c_double),
                 ("loop_stats", C.c_int64 * 4), ("list_entries", C.c_int64),
                 ("list_overflow", C.c_int32), ("list_valid", C.c_int32),
-                ("dx_max", C.c_double)]
+                ("dx_max", C.c_double), ("list_builds", C.c_int64)]
 
 
 class Tuning(C.Structure):
     """swh_tuning (include/swifthip.h)."""
     _fields_ = [("cell_factor", C.c_int32), ("loop_variant", C.c_int32),
                 ("group_size", C.c_int32), ("cell_scale", C.c_float), ("diag_mode", C.c_int32),
-                ("list_capacity", C.c_int32), ("list_skin", C.c_float)]
+                ("list_capacity", C.c_int32), ("list_skin", C.c_float),
+                ("list_keep", C.c_int32)]
 
 
 class Leaf(C.Structure):

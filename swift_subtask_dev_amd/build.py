@@ -20,8 +20,8 @@ ADAPTER = PKG / "libswifthip_swift.so"
 
 HIP_SOURCES = ["swh_api.hip", "swh_tasks.hip", "swh_space.hip", "swh_hydro.hip", "swh_grav.hip",
                "swh_mesh.hip"]
-HIP_HEADERS = ["swh_internal.h", "swh_physics.h", "swh_space.h", "swh_gather.h", "swh_tile.h",
-               "swh_tile4.h", "swh_tile5.h", "swh_list.h", "swh_mpole.h"]
+HIP_HEADERS = ["swh_internal.h", "swh_physics.h", "swh_space.h", "swh_gather.h", "swh_wave.h",
+               "swh_list.h", "swh_mpole.h"]
 
 
 def _hipcc() -> str:

@@ -6,13 +6,12 @@
 //                (density, gradient: r < H_i; force: r < max(H_i, H_j))
 //   interact() : the non-symmetric iact (hydro_iact.h:130, 276, 488)
 //   store()    : accumulate into the particle's fields (SWIFT "+=" semantics)
-//   kPay / load_j() / interact_staged(): the j-side record staged in LDS by
-//                the tile loop (kPay float4s + one int) and the iact on it
+//   kPay / load_j() / interact_staged(): the j-side record a list walk loads
+//                (kPay float4s + one int) and the iact on it
 //
-// gather_direct (variant 1): each lane walks the grid cells of its own i and
-// evaluates every accepted j immediately. It serves the subset loops (ghost
-// reruns of particles whose pair list no longer covers their h) and the
-// overflow particles of the pair lists (swh_list.h).
+// The list walks (swh_list.h) evaluate these states entry by entry; the
+// wave-per-particle search of list overflow and ghost reruns walks the grid
+// cells with cell_range / wrap_cell / separation.
 #pragma once
 
 #include "swh_physics.h"
@@ -29,7 +28,7 @@ __device__ __forceinline__ double wrap_nearest(double d, double box) {
 template <int LOOP, typename T>
 struct LoopState;
 
-// j-side record of a loop as staged by the tile loop.
+// j-side record of a loop as loaded by a list walk.
 template <int N>
 struct JRec {
   float4 p[N];
@@ -297,32 +296,6 @@ __device__ __forceinline__ T separation(const GridDev& g, const CellRange& c, co
   tdy = (T)dy;
   tdz = (T)dz;
   return tdx * tdx + tdy * tdy + tdz * tdz;
-}
-
-template <typename T, class S>
-__device__ __forceinline__ void gather_direct(const GridDev& g, const SoA& a, const double4& pi,
-                                              S& st) {
-  CellRange c;
-  cell_range(g, pi.x, pi.y, pi.z, st.reach, c);
-  for (int cz = c.lo[2]; cz <= c.hi[2]; cz++) {
-    double sz;
-    const int wz = wrap_cell(g, c, 2, cz, sz);
-    for (int cy = c.lo[1]; cy <= c.hi[1]; cy++) {
-      double sy;
-      const int wy = wrap_cell(g, c, 1, cy, sy);
-      for (int cx = c.lo[0]; cx <= c.hi[0]; cx++) {
-        double sx;
-        const int wx = wrap_cell(g, c, 0, cx, sx);
-        const int2 r = cell_range_of(g, wx, wy, wz);
-        for (int j = r.x; j < r.y; j++) {
-          const double4 pj = a.pos[j];
-          T dx, dy, dz;
-          const T r2 = separation<T>(g, c, pi, pj, sx, sy, sz, dx, dy, dz);
-          if (st.accept(j, pj, r2)) st.interact(a, j, pj, dx, dy, dz, r2);
-        }
-      }
-    }
-  }
 }
 
 }  // namespace swh

@@ -30,7 +30,7 @@
 #include "swh_internal.h"
 #include "swh_mpole.h"
 #include "swh_physics.h"
-#include "swh_tile.h"
+#include "swh_wave.h"
 
 namespace swh {
 

@@ -6,17 +6,15 @@
 //
 // Gather formulation: every directed pair (i <- j) is evaluated exactly once,
 // by the owner of i, with the non-symmetric iact (hydro_iact.h:130,276,488),
-// so the sums are deterministic and need no atomics. The default loops walk
-// the step's pair lists (swh_list.h); the tile loops (swh_tile4.h,
-// swh_tile5.h) search and interact in one launch; gather_direct
-// (swh_gather.h) serves subsets and list overflow.
+// so the sums are deterministic and need no atomics. The loops walk the
+// step's pair lists (swh_list.h); particles the lists do not cover (list
+// overflow, ghost reruns whose h outgrew the list reach) take a
+// wave-per-particle search of the grid cells around them.
 #include <cstring>
 #include "swh_gather.h"
 #include "swh_internal.h"
 #include "swh_list.h"
-#include "swh_tile.h"
-#include "swh_tile4.h"
-#include "swh_tile5.h"
+#include "swh_wave.h"
 
 namespace swh {
 
@@ -26,54 +24,100 @@ __device__ __forceinline__ void count_add(int n, unsigned long long* counter) {
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(counter, v);
 }
 
-// Variant 1: one thread per i-particle (item t of the launch, or subset[t]),
-// direct gather over its grid cells.
-template <int LOOP, typename T>
-__global__ __launch_bounds__(256) void loop_kernel(GridDev g, SoA a,
-                                                   const int* __restrict__ subset,
-                                                   int nitems, int max_active_bin, T a2H,
-                                                   const unsigned int* __restrict__ hmax_bits,
-                                                   unsigned long long* counter,
-                                                   int* __restrict__ ncount) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int i = (t < nitems) ? (subset ? subset[t] : t) : -1;
-  const bool act = i >= 0 && active_part(a, i, max_active_bin);
-  LoopState<LOOP, T> st;
-  st.n = 0;
-  double4 pi = make_double4(0., 0., 0., 0.);
-  if (act) {
-    st.load_i(a, i, a2H, hmax_bits);
-    pi = a.pos[i];
-    gather_direct<T>(g, a, pi, st);
-    st.store(a, i);
-    if (ncount) ncount[i] = st.n;
-  }
-  if (counter) count_add(act ? st.n : 0, counter);
-}
-
 // ---------------------------------------------------------------------------
-// Variant 7 (default): the step's pair lists (swh_list.h).
+// The step's pair lists (swh_list.h).
 // ---------------------------------------------------------------------------
 #ifndef SWH_WALK_LPI
 #define SWH_WALK_LPI 4
 #endif
 constexpr int kWalkLpi = SWH_WALK_LPI;  // lanes per i of the list walks
 
+// `run_if` (nullable): the list-build kernels of a kept-list step run only
+// when the device check (list_check_kernel) found the kept lists stale, so
+// the host decides nothing and never waits.
+__device__ __forceinline__ bool skip_build(const unsigned int* run_if) {
+  return run_if && *run_if == 0u;
+}
+
+// The periodic-wrap radius: a particle within R_max + dx of a periodic face
+// may have neighbours across it (dx: the displacement bound since the
+// rebuild -- particles may have drifted out of the box); rwrap_base is its
+// R_max part at the list build.
+__device__ __forceinline__ unsigned int rwrap_of(float base, float dx) {
+  return __float_as_uint(base + dx * (1.f + 1e-4f));
+}
+
 __global__ void list_prep_kernel(const unsigned int* hmax_bits, float gs1, float dx,
-                                 unsigned int* rwrap, unsigned int* ovf_n) {
-  if (threadIdx.x == 0) {
-    // a particle within R_max + dx of a periodic face may have neighbours
-    // across it (dx: particles drifted out of the box since the rebuild)
-    const float r = __uint_as_float(*hmax_bits) * gs1 + dx;
-    *rwrap = __float_as_uint(r * (1.f + 1e-4f) + 1e-30f);
+                                 unsigned int* rwrap, unsigned int* rwrap_base,
+                                 unsigned int* ovf_n, const unsigned int* run_if,
+                                 unsigned int* nbuilds) {
+  if (threadIdx.x == 0 && !skip_build(run_if)) {
+    const float base = __uint_as_float(*hmax_bits) * gs1 * (1.f + 1e-4f) + 1e-30f;
+    *rwrap_base = __float_as_uint(base);
+    *rwrap = rwrap_of(base, dx);
     *ovf_n = 0u;
+    *nbuilds += 1u;
   }
 }
 
+// Cell-local fp32 positions for the build's staging, and the displacement
+// record at build time (xd0 = xdiff: a kept list measures drifts from here).
 __global__ void posf_kernel(GridDev g, const double4* __restrict__ pos,
-                            const int* __restrict__ pcell, int64_t n, float4* __restrict__ posf) {
+                            const int* __restrict__ pcell, const float4* __restrict__ xdiff,
+                            int64_t n, float4* __restrict__ posf, float4* __restrict__ xd0,
+                            const unsigned int* run_if) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) posf[i] = pcell[i] >= 0 ? cell_local(g, pos[i], pcell[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i >= n || skip_build(run_if)) return;
+  posf[i] = pcell[i] >= 0 ? cell_local(g, pos[i], pcell[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  xd0[i] = xdiff[i];
+}
+
+__global__ void zero_u32_kernel(unsigned int* __restrict__ p, int64_t n,
+                                const unsigned int* run_if) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && !skip_build(run_if)) p[i] = 0u;
+}
+
+// Kept lists after drifts (SWIFT keeps a cell's sorts until its particles
+// have moved too far: dx_max_sort against space_maxreldx, space.h:66,
+// runner_doiact_functions_hydro.h:1357-1400). A list holds every j with
+// r_build < max(R_i, R_j), R = gamma h (1 + skin) at the build. With D the
+// largest displacement since the build, r_now >= r_build - 2D, so a pair it
+// lacks can enter r < max(H_i, H_j) only if some particle has H_now + 2D >
+// R_build. Pass 1: D (float bits) from the displacement record.
+__global__ void list_disp_kernel(const float4* __restrict__ xdiff, const float4* __restrict__ xd0,
+                                 const int8_t* __restrict__ tb, int64_t n,
+                                 unsigned int* __restrict__ disp_bits) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float d = 0.f;
+  if (i < n && tb[i] != kTimeBinInhibited) {
+    const float4 a = xdiff[i], b = xd0[i];
+    const float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
+    d = sqrtf(dx * dx + dy * dy + dz * dz) * (1.f + 1e-5f);
+  }
+  for (int o = 32; o > 0; o >>= 1) d = fmaxf(d, __shfl_xor(d, o));
+  if ((threadIdx.x & 63) == 0 && d > 0.f) atomicMax(disp_bits, __float_as_uint(d));
+}
+
+// Pass 2: stale if an active particle is unlisted, or any listed particle's
+// H_now + 2D exceeds its build reach.
+__global__ void list_check_kernel(SoA a, ListDev ld, int64_t n, int max_active_bin,
+                                  const unsigned int* __restrict__ disp_bits,
+                                  unsigned int* __restrict__ stale) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool bad = false;
+  if (i < n && active_part(a, i, max_active_bin)) {
+    const double D = (double)__uint_as_float(*disp_bits);
+    const double H = a.pos[i].w * (double)kGamma;
+    bad = ld.base[i] < 0 || H + 2. * D > (double)ld.reach[i];
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(stale, 1u);
+}
+
+// Kept lists: the wrap radius follows the displacement bound dx of the drifts.
+__global__ void list_rwrap_kernel(unsigned int* rwrap, const unsigned int* rwrap_base,
+                                  float dx) {
+  if (threadIdx.x == 0) *rwrap = rwrap_of(__uint_as_float(*rwrap_base), dx);
 }
 
 #ifndef SWH_BUILD_WPE
@@ -87,8 +131,10 @@ void list_build_kernel(GridDev g, SoA a, ListDev ld,
                                                        const int2* __restrict__ groups,
                                                        int ngroups, int max_active_bin,
                                                        const unsigned int* __restrict__ hmax_bits,
-                                                       unsigned long long* counter, int diag) {
+                                                       unsigned long long* counter, int diag,
+                                                       const unsigned int* run_if) {
   __shared__ ListLds<kListLpiBuild> lds;
+  if (skip_build(run_if)) return;
   list_build<kListLpiBuild>(g, a, ld, groups, ngroups, max_active_bin, hmax_bits, counter, diag,
                             lds);
 }
@@ -238,51 +284,6 @@ __global__ __launch_bounds__(256) void walk_subset_kernel(GridDev g, SoA a, List
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(counter, v);
   }
-}
-
-// Occupancy of the tile kernels: SWH_TILE_WPE > 0 asks the compiler for at
-// least that many waves per SIMD (it caps the VGPR budget accordingly).
-#ifndef SWH_TILE_WPE
-#define SWH_TILE_WPE 0
-#endif
-#if SWH_TILE_WPE > 0
-#define SWH_TILE_BOUNDS __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SWH_TILE_WPE)))
-#else
-#define SWH_TILE_BOUNDS __launch_bounds__(64)
-#endif
-
-// Variant 4: the tile loop with fp32 candidate tests (swh_tile4.h).
-template <int LOOP, typename T, int SG>
-__global__ SWH_TILE_BOUNDS void tile4_kernel(GridDev g, SoA a,
-                                                   const int2* __restrict__ groups, int ngroups,
-                                                   int max_active_bin, T a2H,
-                                                   const unsigned int* __restrict__ hmax_bits,
-                                                   unsigned long long* counter,
-                                                   int* __restrict__ ncount, int diag) {
-  __shared__ Tile4Lds<SG, TileSlots<LOOP>::value> lds;
-  tile4_loop<LOOP, T, SG>(g, a, groups, ngroups, max_active_bin, a2H, hmax_bits, counter,
-                                 ncount, diag, lds);
-}
-
-// Variant 5: one i-group per wave, LPI lanes per i-particle (swh_tile5.h).
-// The density instance asks for 3 waves per SIMD (VGPR cap 168): measured
-// 1.65 ms vs 1.92 ms at 128^3; the force instance is left alone (it spills).
-template <int LOOP>
-struct Tile5Waves {
-  static constexpr int value = (SWH_TILE_WPE > 0) ? SWH_TILE_WPE : (LOOP == LOOP_DENSITY ? 3 : 1);
-};
-
-template <int LOOP, typename T, int LPI>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(Tile5Waves<LOOP>::value)))
-void tile5_kernel(GridDev g, SoA a,
-                                                   const int2* __restrict__ groups, int ngroups,
-                                                   int max_active_bin, T a2H,
-                                                   const unsigned int* __restrict__ hmax_bits,
-                                                   unsigned long long* counter,
-                                                   int* __restrict__ ncount, int diag) {
-  __shared__ Tile5Lds<LPI> lds;
-  tile5_loop<LOOP, T, LPI>(g, a, groups, ngroups, max_active_bin, a2H, hmax_bits, counter,
-                           ncount, diag, lds);
 }
 
 // hydro_init_part (src/hydro/SPHENIX/hydro.h:553-566) on active particles.
@@ -498,6 +499,8 @@ struct ForcePrepParams {
   double a, a_factor_sound_speed, a2_inv, time_base;
   float visc_alpha_max, visc_alpha_min, visc_length;
   float diff_beta, diff_alpha_max, diff_alpha_min;
+  int use_bins;                     // cosmological dt_alpha per time bin (swh_hydro_params)
+  double dt_bin[kNumTimeBins + 1];  // runner_ghost.c:1038-1046
 };
 
 template <typename T>
@@ -514,8 +517,9 @@ __global__ void extra_ghost_kernel(SoA a, int64_t n, int max_active_bin, ForcePr
   const T laplace_u = (T)r.w * (T)2 * h_inv_dim_plus_one;
   r.w = (float)laplace_u;
   a.rot[i] = r;
-  const T dt_alpha =
-      (T)((tb <= 0) ? 0. : (double)(1LL << (tb + 1)) * fp.time_base);  // get_timestep
+  // get_timestep (timeline.h:91-95), or the caller's cosmological table
+  const T dt_alpha = (T)(fp.use_bins ? ((tb >= 0 && tb <= kNumTimeBins) ? fp.dt_bin[tb] : 0.)
+                                     : ((tb <= 0) ? 0. : (double)(1LL << (tb + 1)) * fp.time_base));
   const float4 th = a.th[i];
   float4 g = a.grad[i];     // v_sig, avmn, div_v_prev, div_v_dt
   float4 fc = a.fc[i];      // f, balsara, alpha_visc, alpha_diff
@@ -606,10 +610,14 @@ static unsigned int* rwrap_slot(swh_space* s) { return s->counters.as<unsigned i
 // u32[20]: the ghost reruns' search-queue length
 constexpr float kGhostListSkin = 0.01f;
 static unsigned int* search_slot(swh_space* s) { return s->counters.as<unsigned int>() + 20; }
-
-static int loop_variant_of(const swh_space* s) {
-  return s->tuning.loop_variant != 0 ? s->tuning.loop_variant : 7;
-}
+// (u32[19]: the drift's displacement, u32[21]: max |v_full|, swh_space.hip)
+// u32[24]: kept lists found stale by the device check; u32[25]: displacement
+// since the list build (float bits); u32[26]: list builds run on the device;
+// u32[27]: the wrap radius's R_max part
+static unsigned int* keep_stale_slot(swh_space* s) { return s->counters.as<unsigned int>() + 24; }
+static unsigned int* disp_slot(swh_space* s) { return s->counters.as<unsigned int>() + 25; }
+static unsigned int* nbuild_slot(swh_space* s) { return s->counters.as<unsigned int>() + 26; }
+static unsigned int* rwrap_base_slot(swh_space* s) { return s->counters.as<unsigned int>() + 27; }
 
 static ListDev list_dev(swh_space* s) {
   // skin of the lists in use (the ghost may rebuild them with a wider one)
@@ -630,9 +638,11 @@ static ListDev list_dev(swh_space* s) {
   return d;
 }
 
-// Build the step's pair lists (variant 7) for the active particles.
+// Build the step's pair lists for the active particles. run_if (nullable):
+// a device flag; the build kernels do nothing unless it is set (kept lists
+// that the device check found stale).
 static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool count,
-                              float skin) {
+                              float skin, const unsigned int* run_if = nullptr) {
   const int K = s->tuning.list_capacity > 0 ? s->tuning.list_capacity : 128;
   s->list_skin_cur = skin;
   SWH_TRY(s->nbr.reserve((size_t)std::max(1, s->ngroups) * K * kListSlots * sizeof(int)));
@@ -645,82 +655,79 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
   SWH_TRY(s->nbr_reach.reserve((size_t)s->n * sizeof(float)));
   SWH_TRY(s->nbr_ovf.reserve((size_t)s->n * sizeof(int)));
   SWH_TRY(s->posf.reserve((size_t)s->n * sizeof(float4)));
+  SWH_TRY(s->list_xd0.reserve((size_t)s->n * sizeof(float4)));
   SWH_TRY(s->cell_hreach.reserve((size_t)std::max(1, s->grid.ncell) * sizeof(float)));
   s->list_K = K;
   const ListDev ld = list_dev(s);
   if (ld.cell_R) {
-    SWH_HIP(hipMemsetAsync(s->cell_hreach.ptr, 0, (size_t)s->grid.ncell * sizeof(float),
-                           s->stream));
+    hipLaunchKernelGGL(zero_u32_kernel, dim3((s->grid.ncell + 255) / 256), dim3(256), 0,
+                       s->stream, s->cell_hreach.as<unsigned int>(), (int64_t)s->grid.ncell,
+                       run_if);
     hipLaunchKernelGGL(cell_reach_kernel, dim3((int)((s->n + 255) / 256)), dim3(256), 0,
-                       s->stream, grid_dev(s), s->pos.as<const double4>(), s->n,
-                       (float)(kGamma * ld.skin1), s->cell_hreach.as<unsigned int>());
+                       s->stream, s->pos.as<const double4>(), s->pcell.as<const int>(), s->n,
+                       (float)(kGamma * ld.skin1), s->cell_hreach.as<unsigned int>(), run_if);
   }
   hipLaunchKernelGGL(posf_kernel, dim3((int)((s->n + 255) / 256)), dim3(256), 0, s->stream,
-                     grid_dev(s), s->pos.as<const double4>(), s->pcell.as<const int>(), s->n,
-                     s->posf.as<float4>());
+                     grid_dev(s), s->pos.as<const double4>(), s->pcell.as<const int>(),
+                     s->xdiff.as<const float4>(), s->n, s->posf.as<float4>(),
+                     s->list_xd0.as<float4>(), run_if);
   hipLaunchKernelGGL(list_prep_kernel, dim3(1), dim3(64), 0, s->stream, hmax_slot(s),
-                     kGamma * ld.skin1, (float)s->grid.dx, rwrap_slot(s), ovf_slot(s));
+                     kGamma * ld.skin1, (float)s->grid.dx, rwrap_slot(s), rwrap_base_slot(s),
+                     ovf_slot(s), run_if, nbuild_slot(s));
   hipLaunchKernelGGL(list_build_kernel, dim3(s->ngroups), dim3(64), 0, s->stream, grid_dev(s),
                      soa_of(s), ld, s->groups.as<const int2>(), s->ngroups, P->max_active_bin,
-                     hmax_slot(s), count ? counter_slot(s) : nullptr, s->tuning.diag_mode);
+                     hmax_slot(s), count ? counter_slot(s) : nullptr, s->tuning.diag_mode,
+                     run_if);
   SWH_HIP(hipGetLastError());
   s->list_valid = true;
+  s->list_check = false;
   s->list_mab = P->max_active_bin;
   return SWH_OK;
+}
+
+// Kept lists after a drift: the device decides whether they still cover
+// every pair (list_disp_kernel, list_check_kernel) and rebuilds them if not,
+// all on the stream (no host round trip).
+static swh_status check_kept_lists(swh_space* s, const swh_hydro_params* P, bool count) {
+  const int nb = (int)((s->n + 255) / 256);
+  SWH_HIP(hipMemsetAsync(keep_stale_slot(s), 0, 2 * sizeof(unsigned int), s->stream));
+  hipLaunchKernelGGL(list_disp_kernel, dim3(nb), dim3(256), 0, s->stream,
+                     s->xdiff.as<const float4>(), s->list_xd0.as<const float4>(),
+                     s->tb.as<const int8_t>(), s->n, disp_slot(s));
+  hipLaunchKernelGGL(list_check_kernel, dim3(nb), dim3(256), 0, s->stream, soa_of(s), list_dev(s),
+                     s->n, P->max_active_bin, disp_slot(s), keep_stale_slot(s));
+  hipLaunchKernelGGL(list_rwrap_kernel, dim3(1), dim3(64), 0, s->stream, rwrap_slot(s),
+                     rwrap_base_slot(s), (float)s->grid.dx);
+  SWH_HIP(hipGetLastError());
+  // a device-side rebuild (stale) resets the record: xd0 = xdiff
+  return build_lists(s, P, count, s->tuning.list_skin, keep_stale_slot(s));
 }
 
 template <int LOOP, typename T>
 static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int nitems,
                          int max_active_bin, T a2H, unsigned long long* ctr, int* ncount) {
-  const int v = loop_variant_of(s);
   const int block = 256;
-  if (v == 7) {
-    const ListDev ld = list_dev(s);
-    constexpr int ppb = block / kWalkLpi;
-    if (subset) {  // density reruns of the ghost: list walks, then the queued searches
-      (void)hipMemsetAsync(search_slot(s), 0, sizeof(unsigned int), s->stream);
-      hipLaunchKernelGGL((walk_subset_kernel<T>), dim3((nitems + ppb - 1) / ppb), dim3(block),
-                         0, s->stream, gd, soa_of(s), ld, s->list_valid ? 1 : 0, subset, nitems,
-                         max_active_bin, hmax_slot(s), ctr, s->ghost_search.as<int>(),
-                         search_slot(s));
-      // one wave per queued particle; the queue length is read on the device
-      const int sblocks = std::max(1, std::min(2048, (nitems + 3) / 4));
-      hipLaunchKernelGGL((overflow_kernel<LOOP_DENSITY, T>), dim3(sblocks), dim3(block), 0,
-                         s->stream, gd, soa_of(s), ld, s->ghost_search.as<const int>(),
-                         search_slot(s), max_active_bin, a2H, hmax_slot(s), ctr, ncount);
-      return;
-    }
-    hipLaunchKernelGGL((walk_kernel<LOOP, T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
-                       s->stream, gd, soa_of(s), ld, nitems, max_active_bin, a2H, hmax_slot(s),
-                       ctr, ncount);
-    hipLaunchKernelGGL((overflow_kernel<LOOP, T>), dim3(64), dim3(block), 0, s->stream, gd,
-                       soa_of(s), ld, ld.ovf, ld.ovf_n, max_active_bin, a2H, hmax_slot(s), ctr,
-                       ncount);
+  const ListDev ld = list_dev(s);
+  constexpr int ppb = block / kWalkLpi;
+  if (subset) {  // density reruns of the ghost: list walks, then the queued searches
+    (void)hipMemsetAsync(search_slot(s), 0, sizeof(unsigned int), s->stream);
+    hipLaunchKernelGGL((walk_subset_kernel<T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
+                       s->stream, gd, soa_of(s), ld, s->list_valid ? 1 : 0, subset, nitems,
+                       max_active_bin, hmax_slot(s), ctr, s->ghost_search.as<int>(),
+                       search_slot(s));
+    // one wave per queued particle; the queue length is read on the device
+    const int sblocks = std::max(1, std::min(2048, (nitems + 3) / 4));
+    hipLaunchKernelGGL((overflow_kernel<LOOP_DENSITY, T>), dim3(sblocks), dim3(block), 0,
+                       s->stream, gd, soa_of(s), ld, s->ghost_search.as<const int>(),
+                       search_slot(s), max_active_bin, a2H, hmax_slot(s), ctr, ncount);
     return;
   }
-  if ((v == 4 || v == 5) && !subset) {
-    const int sg = s->tuning.group_size > 0 ? s->tuning.group_size : 16;
-    // variant 4 packs 64/sg groups into a wave, variant 5 gives each group a wave
-    const int nw = v == 5 ? s->ngroups : (s->ngroups + 64 / sg - 1) / (64 / sg);
-    const int2* grp = s->groups.as<const int2>();
-#define SWH_TILE_LAUNCH(K)                                                                   \
-  hipLaunchKernelGGL((K), dim3(nw), dim3(64), 0, s->stream, gd, soa_of(s), grp, s->ngroups, \
-                     max_active_bin, a2H, hmax_slot(s), ctr, ncount, s->tuning.diag_mode)
-    if (v == 5) {
-      if (sg == 16) SWH_TILE_LAUNCH((tile5_kernel<LOOP, T, 4>));
-      else if (sg == 32) SWH_TILE_LAUNCH((tile5_kernel<LOOP, T, 2>));
-      else SWH_TILE_LAUNCH((tile5_kernel<LOOP, T, 1>));
-    } else {
-      if (sg == 16) SWH_TILE_LAUNCH((tile4_kernel<LOOP, T, 16>));
-      else if (sg == 32) SWH_TILE_LAUNCH((tile4_kernel<LOOP, T, 32>));
-      else SWH_TILE_LAUNCH((tile4_kernel<LOOP, T, 64>));
-    }
-#undef SWH_TILE_LAUNCH
-    return;
-  }
-  hipLaunchKernelGGL((loop_kernel<LOOP, T>), dim3((nitems + block - 1) / block), dim3(block), 0,
-                     s->stream, gd, soa_of(s), subset, nitems, max_active_bin, a2H, hmax_slot(s),
-                     ctr, ncount);
+  hipLaunchKernelGGL((walk_kernel<LOOP, T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
+                     s->stream, gd, soa_of(s), ld, nitems, max_active_bin, a2H, hmax_slot(s), ctr,
+                     ncount);
+  hipLaunchKernelGGL((overflow_kernel<LOOP, T>), dim3(64), dim3(block), 0, s->stream, gd,
+                     soa_of(s), ld, ld.ovf, ld.ovf_n, max_active_bin, a2H, hmax_slot(s), ctr,
+                     ncount);
 }
 
 template <int LOOP>
@@ -728,15 +735,22 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const int
                               int nitems, bool count) {
   if (nitems <= 0) return SWH_OK;
   if (!subset && s->ngroups <= 0) return SWH_OK;
-  if (!subset && loop_variant_of(s) == 7) {
-    // the density loop builds the step's lists; gradient and force reuse them
-    // while no particle's H has outgrown its list reach (ghost: stale flag)
-    // diag_mode 7: a density loop keeps lists that are still valid (nothing
-    // moved, no H outgrew its reach), as SWIFT keeps its sort lists
-    const bool reuse = s->tuning.diag_mode == 7 && s->list_valid &&
-                       s->list_mab == P->max_active_bin;
-    if ((LOOP == LOOP_DENSITY && !reuse) || !s->list_valid || s->list_mab != P->max_active_bin)
+  if (!subset) {
+    // The density loop builds the step's lists; gradient and force reuse them
+    // while no particle's H has outgrown its list reach (ghost: stale flag).
+    // list_keep (or diag_mode 7): a density loop keeps lists that are still
+    // valid, as SWIFT keeps its sort lists -- after a drift the device checks
+    // the displacement against the lists' skin and rebuilds only if needed.
+    const bool keep = (s->tuning.list_keep || s->tuning.diag_mode == 7) &&
+                      s->list_mab == P->max_active_bin;
+    const bool fresh = s->list_valid && s->list_mab == P->max_active_bin;
+    if (keep && fresh && s->list_check) {
+      SWH_TRY(check_kept_lists(s, P, count));
+    } else if ((LOOP == LOOP_DENSITY && !(keep && fresh)) || !fresh) {
       SWH_TRY(build_lists(s, P, count, s->tuning.list_skin));
+    } else if (s->list_check) {  // gradient / force right after a drift
+      SWH_TRY(check_kept_lists(s, P, count));
+    }
     if (s->tuning.diag_mode != 0 && s->tuning.diag_mode != 4 && s->tuning.diag_mode != 7)
       return SWH_OK;
   }
@@ -766,11 +780,10 @@ static swh_status run_loop(swh_space* s, const swh_hydro_params* P, int64_t* n_o
   unsigned long long* ctr = counter_slot(s);
   if (n_out) SWH_HIP(hipMemsetAsync(ctr + 3, 0, 5 * sizeof(unsigned long long), s->stream));
   if (n_out) SWH_HIP(hipMemsetAsync(ctr, 0, sizeof(unsigned long long), s->stream));
-  const bool reuse = s->tuning.diag_mode == 7 && s->list_valid &&
-                     s->list_mab == P->max_active_bin;
-  const bool rebuilds = loop_variant_of(s) == 7 &&
-                        ((LOOP == LOOP_DENSITY && !reuse) || !s->list_valid ||
-                         s->list_mab != P->max_active_bin);
+  const bool keep = (s->tuning.list_keep || s->tuning.diag_mode == 7) &&
+                    s->list_mab == P->max_active_bin;
+  const bool fresh = s->list_valid && s->list_mab == P->max_active_bin;
+  const bool rebuilds = (LOOP == LOOP_DENSITY && !(keep && fresh)) || !fresh;
   SWH_TRY(launch_loop<LOOP>(s, P, nullptr, (int)s->n, n_out != nullptr));
   if (n_out) {
     unsigned long long h[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -844,7 +857,7 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   int* list = nullptr;  // first pass: every active particle
   int* list2 = s->ghost_list.as<int>();
   int* spare = s->ghost_list2.as<int>();
-  const bool lists = loop_variant_of(s) == 7;
+  const bool lists = true;
   SWH_HIP(hipMemsetAsync(stale_slot(s), 0, sizeof(unsigned int), st));
   int it = 0;
   for (; count > 0 && it < P->max_smoothing_iterations; it++) {
@@ -920,6 +933,8 @@ swh_status swh_extra_ghost(swh_space* s, const swh_hydro_params* P) {
   fp.diff_beta = P->diff_beta;
   fp.diff_alpha_max = P->diff_alpha_max;
   fp.diff_alpha_min = P->diff_alpha_min;
+  fp.use_bins = P->dt_alpha_bins != nullptr;
+  for (int b = 0; b <= kNumTimeBins; b++) fp.dt_bin[b] = fp.use_bins ? P->dt_alpha_bins[b] : 0.;
   const int block = 256;
   const int g = (int)((s->n + block - 1) / block);
   if (s->ctx->precision == SWH_PRECISION_F64)

@@ -152,7 +152,7 @@ struct swh_space {
   int64_t n = 0;
   bool built = false;
   SwhGrid grid;
-  swh_tuning tuning{1, 0, 0, 0.f, 0, 0, 0.f};
+  swh_tuning tuning{1, 0, 0, 0.f, 0, 0, 0.f, 0};
 
   // AoS image of the caller's records (for write-back of untouched fields)
   swh::DevBuf aos;
@@ -196,7 +196,9 @@ struct swh_space {
   // next upload / rebuild / tuning change, or a ghost that grows an H past its R
   swh::DevBuf nbr, nbr_cnt, nbr_base, nbr_reach, nbr_ovf;
   swh::DevBuf posf;  // float4: position relative to its grid cell's corner, h
+  swh::DevBuf list_xd0;  // float4: the displacement record (xdiff) at the list build
   bool list_valid = false;
+  bool list_check = false;  // kept lists after a drift: the device checks them first
   int32_t list_mab = 0, list_K = 0;
   float list_skin_cur = 0.f;  // skin of the lists in use (tuning, or the ghost's rebuild)
   int64_t list_entries = 0;   // last counted build: total entries

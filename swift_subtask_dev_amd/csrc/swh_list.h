@@ -31,10 +31,10 @@
 // entry k of slot sl sits at row k/4, column 4 sl + k%4 of the block's
 // 64-entry rows. The four lanes of an i read one 16-byte segment per row and
 // a wave reads whole 256-byte rows. Particles with more than K hits
-// (cnt > K) are walked by the per-particle search (gather_direct) instead.
+// (cnt > K) are walked by the wave-per-particle search (overflow_kernel).
 #pragma once
 
-#include "swh_tile5.h"
+#include "swh_wave.h"
 
 namespace swh {
 
@@ -47,6 +47,7 @@ constexpr int kListLpiBuild = 4;  // lanes per i in the list build
 #define SWH_LIST_ICAP 96
 #endif
 constexpr int kListRegion = SWH_LIST_REGION;  // staged candidates per region of the build
+constexpr int kListBlk = 8;  // candidates per lane per test block of the build
 
 // First entry of a listed particle (`base` = group * kListSlots + slot) and
 // the offset of its entry k (module layout comment).
@@ -75,27 +76,26 @@ struct ListDev {
 // Per-cell maximum R = gamma h (1 + skin): the list build skips a cell whose
 // box lies farther than max(R_group, R_cell) from the group box (SWIFT's
 // per-cell h_max pruning of DOPAIR2, runner_doiact_functions_hydro.h:1424-1530).
-__global__ void cell_reach_kernel(GridDev g, const double4* __restrict__ pos, int64_t n,
-                                  float gs1, unsigned int* __restrict__ cell_R) {
+// A particle counts for the cell whose sorted range holds it (pcell, from the
+// rebuild): after a drift it may stand outside that cell's box, and the build
+// stages it from there (the box gaps allow for g.dx); inhibited particles
+// (pcell < 0) are in no cell.
+__global__ void cell_reach_kernel(const double4* __restrict__ pos, const int* __restrict__ pcell,
+                                  int64_t n, float gs1, unsigned int* __restrict__ cell_R,
+                                  const unsigned int* run_if) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  const double4 p = pos[j];
-  int lin = 0;
-  const double xs[3] = {p.x, p.y, p.z};
-  for (int k = 2; k >= 0; k--) {  // key_kernel's binning, linear x-fastest index
-    int ck = (int)floor((xs[k] - g.origin[k]) * g.inv_w[k]);
-    ck = ck < 0 ? 0 : (ck >= g.cdim[k] ? g.cdim[k] - 1 : ck);
-    lin = lin * g.cdim[k] + ck;
-  }
+  if (j >= n || (run_if && *run_if == 0u)) return;
+  const int lin = pcell[j];
+  if (lin < 0) return;
   // positive floats order as their bit patterns
-  atomicMax(&cell_R[lin], __float_as_uint((float)(p.w * (double)gs1) * 1.0000005f));
+  atomicMax(&cell_R[lin], __float_as_uint((float)(pos[j].w * (double)gs1) * 1.0000005f));
 }
 
 template <int LPI>
 struct ListLds {
   static constexpr int GS = 64 / LPI;
   static constexpr int kICap = SWH_LIST_ICAP;           // LDS hits per i before a flush
-  static_assert(kICap >= kT5Blk * LPI, "one consume block must fit i's LDS hits");
+  static_assert(kICap >= kListBlk * LPI, "one consume block must fit i's LDS hits");
   static constexpr int kStride = kICap + 2;  // odd dword stride: lists start on different banks
   float4 cand[kListRegion];  // x, y, z relative to the box centre; w = inflated R_j^2
   int candj[kListRegion];
@@ -154,19 +154,19 @@ __device__ __forceinline__ void list_consume(const GridDev& g, const ListDev& ld
                                              int& wr, int il, int s, int gbase, TileStats& ts) {
   constexpr int GS = 64 / LPI;
   const int dummy = GS * LDS::kStride + il * LPI + s;
-  const int nblk = (nst + kT5Blk * LPI - 1) / (kT5Blk * LPI);
-  ts.asteps += (unsigned int)(nblk * kT5Blk);
+  const int nblk = (nst + kListBlk * LPI - 1) / (kListBlk * LPI);
+  ts.asteps += (unsigned int)(nblk * kListBlk);
   const float bx = (float)g.dim[0], by = (float)g.dim[1], bz = (float)g.dim[2];
   for (int b = 0; b < nblk; b++) {
-    if (__any(nq > LDS::kICap - kT5Blk * LPI)) list_flush<LPI>(ld, L, nq, wr, il, s, gbase, ts);
-    const int c0 = b * kT5Blk * LPI + s;
-    float4 cv[kT5Blk];
+    if (__any(nq > LDS::kICap - kListBlk * LPI)) list_flush<LPI>(ld, L, nq, wr, il, s, gbase, ts);
+    const int c0 = b * kListBlk * LPI + s;
+    float4 cv[kListBlk];
 #pragma unroll
-    for (int kk = 0; kk < kT5Blk; kk++) cv[kk] = L.cand[min(c0 + kk * LPI, kListRegion - 1)];
-    bool hit[kT5Blk];
+    for (int kk = 0; kk < kListBlk; kk++) cv[kk] = L.cand[min(c0 + kk * LPI, kListRegion - 1)];
+    bool hit[kListBlk];
     int cnt = 0;
 #pragma unroll
-    for (int kk = 0; kk < kT5Blk; kk++) {
+    for (int kk = 0; kk < kListBlk; kk++) {
       float dx = xi - cv[kk].x, dy = yi - cv[kk].y, dz = zi - cv[kk].z;
       if (WRAP) {
         if (c.full[0]) dx = wrap_nearest_f(dx, bx);
@@ -188,7 +188,7 @@ __device__ __forceinline__ void list_consume(const GridDev& g, const ListDev& ld
     const int tot = __shfl(inc, LPI - 1, LPI);
     int pos = il * LDS::kStride + nq + inc - cnt;
 #pragma unroll
-    for (int kk = 0; kk < kT5Blk; kk++) {
+    for (int kk = 0; kk < kListBlk; kk++) {
       L.hits[hit[kk] ? pos : dummy] = (unsigned short)(c0 + kk * LPI);
       pos += hit[kk] ? 1 : 0;
     }
@@ -258,7 +258,7 @@ __device__ __forceinline__ void list_build(const GridDev& g, const SoA& a, const
     const int ncells = nxy * (c.hi[2] - c.lo[2] + 1);
     // Rounding bound of the fp32 relative coordinates: a candidate is staged
     // as fl(local) + fl(cell offset) with |local| <= w, |offset| <= D + w and
-    // |sum| <= D (swh_tile4.h's argument with 2(D + w) in place of D).
+    // |sum| <= D (kThrSlack's argument, swh_wave.h, with 2(D + w) in place of D).
     const double wmax = fmax(g.w[0], fmax(g.w[1], g.w[2]));
     const double delta = 16. * kUnitRound * (sqrt(D2) + wmax);
     const float deltaf = uni_f((float)delta);

@@ -9,6 +9,7 @@
 // cell tree into leaves (space_split, cell.c): runs of consecutive cells of
 // one aligned Morton block holding <= 64 particles.
 #include <cmath>
+#include <cstdlib>
 #include <hipcub/hipcub.hpp>
 
 #include <cstring>
@@ -154,14 +155,20 @@ __global__ void bbox_kernel(const double4* __restrict__ pos, const int8_t* __res
 
 // Inhibited particles get key = ncell: they sort behind every cell and are
 // never visited as neighbours (the loops' part_is_inhibited skip).
+__device__ __forceinline__ uint32_t spread3(uint32_t v);
+
+// The key is the cell's Morton rank followed by `sb` bits per dimension of
+// the particle's Morton position inside its cell: a cell stays one
+// contiguous range, and inside it particles close in space are close in
+// memory, so the neighbours a list entry names sit in few cache lines.
 __global__ void key_kernel(GridDev g, const int* __restrict__ rank, double4* __restrict__ pos,
-                           const int8_t* __restrict__ tb, int64_t n, int ncell,
+                           const int8_t* __restrict__ tb, int64_t n, int ncell, int sb,
                            uint32_t* __restrict__ keys, int* __restrict__ idx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   idx[i] = (int)i;
   if (tb[i] == kTimeBinInhibited) {
-    keys[i] = (uint32_t)ncell;
+    keys[i] = (uint32_t)ncell << (3 * sb);
     return;
   }
   double4 p = pos[i];
@@ -175,13 +182,25 @@ __global__ void key_kernel(GridDev g, const int* __restrict__ rank, double4* __r
     pos[i] = p;
   }
   int c[3];
+  uint32_t sub[3];
   const double xs[3] = {p.x, p.y, p.z};
+  const int smax = (1 << sb) - 1;
   for (int k = 0; k < 3; k++) {
-    int ck = (int)floor((xs[k] - g.origin[k]) * g.inv_w[k]);
+    const double u = (xs[k] - g.origin[k]) * g.inv_w[k];
+    int ck = (int)floor(u);
     ck = ck < 0 ? 0 : (ck >= g.cdim[k] ? g.cdim[k] - 1 : ck);
     c[k] = ck;
+    int sk = (int)floor((u - ck) * (double)(1 << sb));
+    sub[k] = (uint32_t)(sk < 0 ? 0 : (sk > smax ? smax : sk));
   }
-  keys[i] = (uint32_t)rank[(c[2] * g.cdim[1] + c[1]) * g.cdim[0] + c[0]];
+  const uint32_t sm = spread3(sub[0]) | (spread3(sub[1]) << 1) | (spread3(sub[2]) << 2);
+  keys[i] = ((uint32_t)rank[(c[2] * g.cdim[1] + c[1]) * g.cdim[0] + c[0]] << (3 * sb)) | sm;
+}
+
+// Drop the in-cell bits of the sorted keys: keys become cell ranks again.
+__global__ void key_shift_kernel(uint32_t* __restrict__ keys, int64_t n, int shift) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) keys[i] >>= shift;
 }
 
 __device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 10 bits -> every 3rd bit
@@ -614,7 +633,10 @@ static swh_status reserve_soa(swh_space* s, int64_t n) {
 }
 
 swh_status space_hmax_to_device(swh_space* s) {
-  SWH_TRY(s->counters.reserve(128));
+  if (!s->counters.ptr) {  // first use: every counter slot starts at zero
+    SWH_TRY(s->counters.reserve(128));
+    SWH_HIP(hipMemsetAsync(s->counters.ptr, 0, 128, s->stream));
+  }
   unsigned int* hb = s->counters.as<unsigned int>() + 2;  // slot 2: hmax bits
   SWH_HIP(hipMemsetAsync(hb, 0, sizeof(unsigned int), s->stream));
   hipLaunchKernelGGL(hmax_kernel, dim3(1024), dim3(256), 0, s->stream, s->pos.as<double4>(),
@@ -676,20 +698,18 @@ swh_status swh_space_set_stream(swh_space* s, void* stream) {
 }
 
 swh_status swh_space_set_tuning(swh_space* s, const swh_tuning* t) {
-  const bool variant_ok = t && (t->loop_variant == 0 || t->loop_variant == 1 ||
-                                t->loop_variant == 4 || t->loop_variant == 5 ||
-                                t->loop_variant == 7);
-  const bool lists = t && (t->loop_variant == 0 || t->loop_variant == 7);
-  if (!s || !t || t->cell_factor < 1 || t->cell_factor > 4 || !variant_ok ||
-      (t->group_size != 0 && t->group_size != 16 && t->group_size != 32 && t->group_size != 64) ||
-      (lists && t->group_size > 16) || t->cell_scale < 0.f || t->cell_scale > 4.f ||
-      t->diag_mode < 0 || t->diag_mode > 7 || t->diag_mode == 5 || t->diag_mode == 6 || t->list_capacity < 0 ||
-      t->list_capacity > 4096 || (t->list_capacity % 4) != 0 || !(t->list_skin >= 0.f) ||
-      t->list_skin > 1.f)
+  if (!s || !t || t->cell_factor < 1 || t->cell_factor > 4 ||
+      (t->loop_variant != 0 && t->loop_variant != 7) ||
+      (t->group_size != 0 && t->group_size != 16) || t->cell_scale < 0.f || t->cell_scale > 4.f ||
+      t->diag_mode < 0 || t->diag_mode > 7 || t->diag_mode == 3 || t->diag_mode == 5 ||
+      t->diag_mode == 6 || t->list_capacity < 0 || t->list_capacity > 4096 ||
+      (t->list_capacity % 4) != 0 || !(t->list_skin >= 0.f) || t->list_skin > 1.f ||
+      t->list_keep < 0 || t->list_keep > 1)
     return SWH_ERR_ARG;
   s->tuning = *t;
   s->built = false;
   s->list_valid = false;
+  s->list_check = false;
   return SWH_OK;
 }
 
@@ -710,6 +730,13 @@ swh_status swh_space_get_info(const swh_space* s, swh_space_info* info) {
   info->list_overflow = s->list_overflow;
   info->list_valid = s->list_valid ? 1 : 0;
   info->dx_max = s->grid.dx;
+  if (s->counters.ptr) {  // list builds that ran on the device (u32[26])
+    unsigned int nb = 0;
+    SWH_HIP(hipMemcpyAsync(&nb, s->counters.as<unsigned int>() + 26, sizeof(nb),
+                           hipMemcpyDeviceToHost, s->stream));
+    SWH_HIP(hipStreamSynchronize(s->stream));
+    info->list_builds = nb;
+  }
   return SWH_OK;
 }
 
@@ -736,7 +763,10 @@ swh_status swh_space_upload_xparts(swh_space* s, const void* xparts, int64_t cou
   SWH_HIP(hipGetLastError());
   // the fastest particle bounds every displacement of the following drifts
   // (v_full is fixed until the next upload), so the drift needs no read-back
-  SWH_TRY(s->counters.reserve(128));
+  if (!s->counters.ptr) {
+    SWH_TRY(s->counters.reserve(128));
+    SWH_HIP(hipMemsetAsync(s->counters.ptr, 0, 128, s->stream));
+  }
   unsigned int* vbits = s->counters.as<unsigned int>() + 21;
   SWH_HIP(hipMemsetAsync(vbits, 0, sizeof(unsigned int), s->stream));
   hipLaunchKernelGGL(vmax_kernel, dim3((int)((count + 255) / 256)), dim3(256), 0, s->stream,
@@ -780,7 +810,12 @@ swh_status swh_space_drift(swh_space* s, const swh_drift_params* D, const swh_hy
   // asynchronous. The periodic reach check (h grown past half the box) runs
   // at the next ghost and rebuild.
   s->grid.dx += s->vfull_max * std::fabs(D->dt_drift) * (1. + 1e-6) + 1e-12;
-  s->list_valid = false;  // positions moved
+  // positions moved: kept lists (list_keep) are checked against their skin on
+  // the device before the next loop uses them; otherwise they are rebuilt
+  if (s->list_valid && (s->tuning.list_keep || s->tuning.diag_mode == 7))
+    s->list_check = true;
+  else
+    s->list_valid = false;
   return SWH_OK;
 }
 
@@ -1001,13 +1036,17 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
   GridDev gd = grid_dev(s);
   // 2b. keys (Morton rank of the cell) + stable radix sort
   const int grid = (int)((n + block - 1) / block);
-  hipLaunchKernelGGL(key_kernel, dim3(grid), dim3(block), 0, st, gd,
-                     s->cell_rank.as<const int>(), s->pos.as<double4>(),
-                     s->tb.as<const int8_t>(), n, g.ncell, s->keys.as<uint32_t>(),
-                     s->idx.as<int>());
-  SWH_HIP(hipGetLastError());
   int end_bit = 1;
   while ((1LL << end_bit) <= (int64_t)g.ncell) end_bit++;
+  // in-cell Morton bits per dimension (at most 3, within the 32-bit key)
+  int sub_bits = std::min(3, (32 - end_bit) / 3);
+  if (const char* e = std::getenv("SWH_SUBCELL_BITS")) sub_bits = std::max(0, std::min(sub_bits, std::atoi(e)));
+  hipLaunchKernelGGL(key_kernel, dim3(grid), dim3(block), 0, st, gd,
+                     s->cell_rank.as<const int>(), s->pos.as<double4>(),
+                     s->tb.as<const int8_t>(), n, g.ncell, sub_bits, s->keys.as<uint32_t>(),
+                     s->idx.as<int>());
+  SWH_HIP(hipGetLastError());
+  end_bit += 3 * sub_bits;
   size_t tmp_bytes = 0;
   SWH_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, s->keys.as<uint32_t>(),
                                              s->keys2.as<uint32_t>(), s->idx.as<int>(),
@@ -1017,6 +1056,11 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
                                              s->keys.as<uint32_t>(), s->keys2.as<uint32_t>(),
                                              s->idx.as<int>(), s->idx2.as<int>(), (int)n, 0,
                                              end_bit, st));
+  if (sub_bits > 0) {
+    hipLaunchKernelGGL(key_shift_kernel, dim3(grid), dim3(block), 0, st, s->keys2.as<uint32_t>(),
+                       n, 3 * sub_bits);
+    SWH_HIP(hipGetLastError());
+  }
   // 3. permute SoA into cell order
   SWH_TRY(s->tmp_soa.reserve((size_t)n * soa_bytes_per_part() + 16 * 256));
   SoA tmp = soa_carve(s->tmp_soa.as<char>(), n);

@@ -1,0 +1,152 @@
+// swh_wave.h — wave-level helpers of the batch neighbour loops (swh_list.h)
+// and the gravity kernels: wave barriers and reductions, wave-uniform
+// broadcasts, stream compaction, the fp32 rounding constants of the list
+// build's candidate tests, XCD-aware workgroup order and the combination of
+// the lanes' partial loop states.
+#pragma once
+
+#include "swh_gather.h"
+
+namespace swh {
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// XCD-aware workgroup order: workgroups are dealt round-robin to the 8 XCDs
+// (workgroup w runs on XCD w % 8); give each XCD a contiguous stretch of the
+// Morton-ordered work so neighbouring work items share that XCD's L2.
+__device__ __forceinline__ int xcd_block_id() {
+  const int nwg = gridDim.x;
+  const int per_xcd = (nwg + 7) / 8;
+  const int xcd = blockIdx.x % 8, slot_in_xcd = blockIdx.x / 8;
+  const int full_xcds = nwg - (per_xcd - 1) * 8;  // XCDs that get per_xcd blocks
+  return xcd < full_xcds ? xcd * per_xcd + slot_in_xcd
+                         : full_xcds * per_xcd + (xcd - full_xcds) * (per_xcd - 1) + slot_in_xcd;
+}
+
+// Rounding bound of the list build's fp32 candidate tests: separations are
+// formed from fp32 coordinates relative to the group centre, so a test of
+// r2 < (R + 16 u D)^2 (1 + 8u) (u = 2^-24, D bounds the coordinates' size)
+// accepts every pair whose exact fp64 separation is below R.
+constexpr double kUnitRound = 5.9604644775390625e-8;   // u = 2^-24
+constexpr float kThrSlack = 1.f + 8.f * 5.9604645e-8f;  // (1 + 8u)
+
+// Work counters of a counted launch (swh_space_info.loop_stats): candidates
+// loaded, candidates staged, test wave steps and list-flush wave steps.
+struct TileStats {
+  unsigned int loaded = 0, staged = 0, asteps = 0, bsteps = 0;
+};
+
+__device__ __forceinline__ float wrap_nearest_f(float d, float box) {
+  return d > 0.5f * box ? d - box : (d < -0.5f * box ? d + box : d);
+}
+
+__device__ __forceinline__ int uni_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float uni_f(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+__device__ __forceinline__ double uni_d(double v) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned int lo = (unsigned int)__builtin_amdgcn_readfirstlane((int)(unsigned int)b);
+  const unsigned int hi =
+      (unsigned int)__builtin_amdgcn_readfirstlane((int)(unsigned int)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ double wave_min_d(double v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ double wave_max_d(double v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Stream compaction with one atomic per workgroup (blockDim.x <= 1024): the
+// threads with `pred` get consecutive slots, in thread order. Every thread of
+// the block must call it (it synchronises the block). Same-address atomics
+// serialise in L2, so per-wave appends of millions of items cost ~0.3 ms.
+template <typename C>
+__device__ __forceinline__ int block_append(bool pred, C* counter) {
+  __shared__ int wcnt[16];
+  __shared__ int wbase[16];
+  const int lane = (int)(threadIdx.x & 63), w = (int)(threadIdx.x >> 6);
+  const int nw = (int)((blockDim.x + 63) >> 6);
+  const unsigned long long m = __ballot(pred);
+  if (lane == 0) wcnt[w] = (int)__popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+    for (int k = 0; k < nw; k++) {
+      wbase[k] = tot;
+      tot += wcnt[k];
+    }
+    const int b = tot ? (int)atomicAdd(counter, (C)tot) : 0;
+    for (int k = 0; k < nw; k++) wbase[k] += b;
+  }
+  __syncthreads();
+  return pred ? wbase[w] + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+
+// Stream compaction with one atomic per wave: the lanes with `pred` get
+// consecutive slots (in lane order) of the list whose length is *counter.
+// Every lane of the wave must call it.
+template <typename C>
+__device__ __forceinline__ int wave_append(bool pred, C* counter) {
+  const unsigned long long m = __ballot(pred);
+  if (m == 0ull) return -1;
+  const int lane = (int)(threadIdx.x & 63);
+  const int leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = (int)atomicAdd(counter, (C)__popcll(m));
+  base = __shfl(base, leader);
+  return pred ? base + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+
+// Combine the LPI partial states of one i-particle (lanes differing in the
+// low log2(LPI) bits): sums add, v_sig / alpha_max take the max, the limiter
+// takes the min.
+template <int W, typename T>
+__device__ __forceinline__ void reduce_lanes(LoopState<LOOP_DENSITY, T>& s) {
+  for (int o = 1; o < W; o <<= 1) {
+    s.A.rho += __shfl_xor(s.A.rho, o);
+    s.A.rho_dh += __shfl_xor(s.A.rho_dh, o);
+    s.A.wcount += __shfl_xor(s.A.wcount, o);
+    s.A.wcount_dh += __shfl_xor(s.A.wcount_dh, o);
+    s.A.div_v += __shfl_xor(s.A.div_v, o);
+    s.A.rot_x += __shfl_xor(s.A.rot_x, o);
+    s.A.rot_y += __shfl_xor(s.A.rot_y, o);
+    s.A.rot_z += __shfl_xor(s.A.rot_z, o);
+    s.n += __shfl_xor(s.n, o);
+  }
+}
+template <int W, typename T>
+__device__ __forceinline__ void reduce_lanes(LoopState<LOOP_GRADIENT, T>& s) {
+  for (int o = 1; o < W; o <<= 1) {
+    s.A.v_sig = tmax(s.A.v_sig, (T)__shfl_xor(s.A.v_sig, o));
+    s.A.alpha_visc_max_ngb =
+        tmax(s.A.alpha_visc_max_ngb, (T)__shfl_xor(s.A.alpha_visc_max_ngb, o));
+    s.A.laplace_u += __shfl_xor(s.A.laplace_u, o);
+    s.n += __shfl_xor(s.n, o);
+  }
+}
+template <int W, typename T>
+__device__ __forceinline__ void reduce_lanes(LoopState<LOOP_FORCE, T>& s) {
+  for (int o = 1; o < W; o <<= 1) {
+    s.A.ax += __shfl_xor(s.A.ax, o);
+    s.A.ay += __shfl_xor(s.A.ay, o);
+    s.A.az += __shfl_xor(s.A.az, o);
+    s.A.u_dt += __shfl_xor(s.A.u_dt, o);
+    s.A.h_dt += __shfl_xor(s.A.h_dt, o);
+    s.A.min_ngb_time_bin = min(s.A.min_ngb_time_bin, __shfl_xor(s.A.min_ngb_time_bin, o));
+    s.n += __shfl_xor(s.n, o);
+  }
+}
+
+}  // namespace swh

@@ -276,9 +276,9 @@ class HydroSpace:
             pass
 
     def set_tuning(self, cell_factor=1, loop_variant=0, group_size=0, cell_scale=0.0,
-                   diag_mode=0, list_capacity=0, list_skin=0.0):
+                   diag_mode=0, list_capacity=0, list_skin=0.0, list_keep=0):
         t = abi.Tuning(cell_factor, loop_variant, group_size, cell_scale, diag_mode,
-                       list_capacity, list_skin)
+                       list_capacity, list_skin, list_keep)
         _check(self._lib.swh_space_set_tuning(self.handle, C.byref(t)), "set_tuning")
 
     def info(self) -> dict:
@@ -288,7 +288,7 @@ class HydroSpace:
                 "cell_width": list(i.cell_width), "h_max": i.h_max,
                 "loop_stats": list(i.loop_stats), "list_entries": i.list_entries,
                 "list_overflow": i.list_overflow, "list_valid": bool(i.list_valid),
-                "dx_max": i.dx_max}
+                "dx_max": i.dx_max, "list_builds": i.list_builds}
 
     def upload(self, parts, count=None, on_device=False):
         """parts: numpy PART_DTYPE array (host) or a device pointer (int) with count."""

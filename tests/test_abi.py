@@ -91,7 +91,9 @@ def test_struct_part_offsets_match_survey():
 
 def test_params_struct_size():
     # swh_hydro_params: 6 doubles + 4 floats + 2 ints + 8 floats + 2 ints + 3 doubles
-    assert C.sizeof(abi.HydroParams) == 6 * 8 + 4 * 4 + 2 * 4 + 8 * 4 + 2 * 4 + 3 * 8
+    # + the dt_alpha_bins pointer (ABI v7)
+    assert C.sizeof(abi.HydroParams) == 6 * 8 + 4 * 4 + 2 * 4 + 8 * 4 + 2 * 4 + 3 * 8 + 8
+    assert abi.HydroParams.dt_alpha_bins.offset == 136
     # swh_grav_params: mesh scalars (40 B) + 2 floats + 4 ints of the MAC + r_cut_max
     assert C.sizeof(abi.GravParams) == 72
     assert abi.GravParams.r_cut_max.offset == 64

@@ -99,6 +99,20 @@ def test_drift_vs_oracle(gpu_ctx, stepped, min_u):
     assert not info["list_valid"]
 
 
+def test_tuning_rejects_removed_variants(gpu_ctx):
+    """Loop variants 1, 4 and 5 (round 1's tile loops) are gone: the pair
+    lists are the only loop."""
+    from swift_subtask_dev_amd import lib
+    sp = lib.HydroSpace(gpu_ctx)
+    for v in (1, 4, 5):
+        with pytest.raises(lib.SwhError):
+            sp.set_tuning(1, v)
+    with pytest.raises(lib.SwhError):
+        sp.set_tuning(1, 7, 32)
+    sp.set_tuning(1, 7, 16, list_keep=1, list_skin=0.2)
+    sp.close()
+
+
 def test_drift_requires_xparts(gpu_ctx, stepped):
     from swift_subtask_dev_amd import lib
     parts, P = stepped
@@ -158,7 +172,7 @@ def test_loops_after_drift_vs_f64(gpu_ctx, variant, periodic):
     _check_chain(g, rg, o, ro)
 
 
-@pytest.mark.parametrize("variant", [7, 5])
+@pytest.mark.parametrize("variant", [7])
 def test_repeated_drifts_accumulate_reach(gpu_ctx, variant):
     """Three drifts without a rebuild: dx_max accumulates (x_diff is relative
     to the rebuild), the loops stay exact; a rebuild resets it."""
@@ -197,3 +211,91 @@ def test_drift_list_skin_and_capacity(gpu_ctx):
     for tuning in ({"list_skin": 0.2}, {"list_capacity": 24}):
         g, rg, _ = _drifted_chain(gpu_ctx, parts, xp, [D], P, 7, **tuning)
         _check_chain(g, rg, o, ro)
+
+
+def test_clustered_adaptive_drift_chain_vs_f64(gpu_ctx):
+    """Adaptive grid (clustered box: cells sized by the typical H, per-cell
+    reach pruning) after a drift without a rebuild: the per-cell maximum
+    reach must follow the cell whose sorted range holds a particle, not the
+    cell its drifted position falls in, or force pairs with r < H_j of a
+    particle that crossed a face are lost. Counts exact, chain tolerances."""
+    from swift_subtask_dev_amd import lib
+    P = abi.default_hydro_params()
+    parts = ics.clustered_box(16, n_clumps=4, per_clump=1500, seed=23)
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.upload(parts)
+    sp.rebuild(P)
+    sp.hydro_step(P)
+    sp.download(parts, abi.FIELDS_ALL)
+    sp.close()
+    assert parts["h"].max() / parts["h"].min() > 8
+    rng = np.random.Generator(np.random.PCG64(29))
+    xp = abi.new_xparts(len(parts))
+    xp["v_full"] = rng.normal(0.0, 1.0, (len(parts), 3)).astype(np.float32)
+    # move the particles by ~0.4 of the median h: many cross the small cells
+    dt = 0.4 * float(np.median(parts["h"]))
+    D = abi.DriftParams(dt, 0.0, 0.0, 0.0, 0.0)
+    g, rg, dx = _drifted_chain(gpu_ctx, parts, xp, [D], P, 7)
+    o, _ = _oracle_drift(parts, xp, D)
+    o, ro = box_chain_oracle(o, P)
+    _check_chain(g, rg, o, ro)
+
+
+@pytest.mark.parametrize("disp,expect_rebuilds", [(0.01, False), (0.25, True)])
+def test_kept_lists_across_drifts_vs_f64(gpu_ctx, disp, expect_rebuilds):
+    """list_keep: pair lists survive drifts while their skin covers the
+    displacement (SWIFT keeps its sorts until dx_max_sort exceeds
+    space_maxreldx, space.h:66) and the device rebuilds them as soon as some
+    H + 2 D exceeds a build reach. Three drifts, each followed by density and
+    force loops compared with the fp64 oracle on the drifted particles: exact
+    counts and the loop tolerances either way. Small moves keep the lists
+    (fewer builds than loops), large ones force device-side rebuilds."""
+    from swift_subtask_dev_amd import lib
+    parts, P = _stepped_state(gpu_ctx, n=14, seed=12)
+    rng = np.random.Generator(np.random.PCG64(3))
+    xp = abi.new_xparts(len(parts))
+    xp["v_full"] = rng.normal(0.0, 0.577, (len(parts), 3)).astype(np.float32)
+    vmax = float(np.sqrt((xp["v_full"].astype(np.float64) ** 2).sum(axis=1)).max())
+    D = abi.DriftParams(disp * float(np.median(parts["h"])) / vmax, 0.0, 0.0, 0.0, 0.0)
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.set_tuning(1, 0, 0, list_skin=0.2, list_keep=1)
+    g = abi.copy_parts(parts)
+    sp.upload(g)
+    sp.rebuild(P)
+    sp.upload_xparts(xp)
+    o = abi.copy_parts(parts)
+    b0 = sp.info()["list_builds"]
+    loops = 0
+    for step in range(3):
+        sp.drift(D, P)
+        o, _ = _oracle_drift(o, xp, D)
+        sp.init_parts(P)
+        nd = sp.density(P)
+        gd = abi.copy_parts(g)
+        sp.download(gd, abi.FIELDS_DENSITY | abi.FIELDS_DRIFT)
+        sp.reset_acceleration(P)
+        nf = sp.force(P)
+        gf = abi.copy_parts(g)
+        sp.download(gf, abi.FIELDS_FORCE | abi.FIELDS_DRIFT)
+        loops += 2
+        od = abi.copy_parts(o)
+        O.fn("f32", "init_parts")(od.ctypes.data, len(od), C.byref(P))
+        assert nd == O.fn("f64", "box_density")(od.ctypes.data, len(od), C.byref(P), None)
+        for f in ("rho", "rho_dh", "wcount", "wcount_dh"):
+            assert_close(gd[f], od[f], 2e-6, 1e-6, f"{f} step {step}")
+        of = abi.copy_parts(o)
+        of["a_hydro"] = 0
+        of["u_dt"] = 0
+        of["h_dt"] = 0
+        of["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
+        assert nf == O.fn("f64", "box_force")(of.ctypes.data, len(of), C.byref(P), None)
+        for f in ("a_hydro", "u_dt", "h_dt"):
+            assert_close(gf[f], of[f], 5e-5, 1e-4, f"{f} step {step}")
+        assert np.array_equal(gf["min_ngb_time_bin"], of["min_ngb_time_bin"])
+    builds = sp.info()["list_builds"] - b0
+    sp.close()
+    assert 1 <= builds <= 3
+    if expect_rebuilds:
+        assert builds >= 2, builds
+    else:
+        assert builds == 1, builds  # built at the first density loop, then kept

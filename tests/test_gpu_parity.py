@@ -282,10 +282,10 @@ def test_125cells_chain_vs_f64(gpu_ctx):
     assert_close(gr["main"]["a_hydro"], orc["main"]["a_hydro"], 1e-5, 1e-3, "a_hydro")
 
 
-# loop_variant 1 = per-particle direct gather, 4 = tile loop (64/group_size
-# i-groups per wave), 5 = tile loop (one i-group per wave), 7 = pair lists
-# (the default: density builds the step's lists, every loop walks them)
-VARIANTS = [1, 4, 5, 7]
+# loop_variant 7 = pair lists (the default and only loop: density builds the
+# step's lists, every loop walks them); the round-1 tile loops (variants 1,
+# 4, 5) were removed from the product
+VARIANTS = [7]
 
 
 def box_chain_gpu(ctx, parts, P, cell_factor=1, variant=0, group_size=0, **tuning):
@@ -319,8 +319,7 @@ def box_chain_oracle(parts, P, prec="f64"):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("variant,group_size,skin",
-                         [(1, 0, 0.1), (4, 16, 0.1), (4, 32, 0.1), (4, 64, 0.1), (5, 16, 0.1),
-                          (5, 32, 0.1), (5, 64, 0.1), (7, 16, 0.1), (7, 16, 0.0), (7, 16, 0.5)])
+                         [(7, 16, 0.1), (7, 16, 0.0), (7, 16, 0.5), (0, 0, 0.0)])
 @pytest.mark.parametrize("cell_factor", [1, 2, 3])
 def test_box_density_vs_f64(gpu_ctx, cell_factor, variant, group_size, skin):
     """Batch density loop on a periodic Sedov-like box vs the fp64 oracle;
@@ -345,9 +344,8 @@ def test_box_density_vs_f64(gpu_ctx, cell_factor, variant, group_size, skin):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("variant,group_size,tuning",
-                         [(1, 0, {}), (4, 16, {}), (4, 64, {}), (5, 16, {}), (5, 32, {}),
-                          (5, 64, {}), (7, 16, {}), (7, 16, {"list_skin": 0.0}),
-                          (7, 16, {"list_capacity": 24})])
+                         [(7, 16, {}), (7, 16, {"list_skin": 0.1}),
+                          (7, 16, {"list_capacity": 24}), (0, 0, {"list_keep": 1})])
 def test_box_chain_vs_f64(gpu_ctx, variant, group_size, tuning):
     """Full SPHENIX chain (density, ghost with h iteration, gradient, extra
     ghost, force, end force) on a perturbed box with h off-target so the

@@ -1,0 +1,357 @@
+"""GPU parity of the physics terms the headline input leaves at zero.
+
+The Sedov input has v = 0 and every earlier chain test ran with time_base = 0,
+a = 1, H = 0: div_v, rot_v, h_dt, the artificial viscosity, SPHENIX's
+viscosity-switch evolution and the diffusion-alpha evolution
+(hydro_prepare_force, src/hydro/SPHENIX/hydro.h:823-934) and every
+cosmological factor were never compared. These tests run the batch chain
+(density, ghost, gradient, extra ghost, force, end force) against the fp64
+oracle's restatement with:
+
+  * time_base > 0, mixed time bins and inactive particles, over two
+    consecutive steps with a drift between them, so div_v_previous_step and
+    the alphas carry over (runner_ghost.c:1038-1046 non-cosmological branch);
+  * cosmology: a < 1, H > 0, the gamma = 5/3 scale-factor powers and the
+    cosmological dt_alpha per time bin (cosmology_get_delta_time,
+    src/cosmology.c:1287-1307, tabulated by swift_subtask_dev_amd/cosmo.py);
+  * the 128^3 headline box with a converging flow, random Balsara switches,
+    viscosity and diffusion alphas and a perturbed internal energy: the force
+    loop's viscosity and diffusion terms at the size the bench times;
+  * the bench's exact EAGLE_6 stand-in (1.66 M particles, h spanning 25x).
+
+Viscosity and diffusion are "parity unpinned" against the reference itself:
+no reference-held answer exercises them (test125cells has no converging
+flow, and du/dt of its cases is diffusion-free); the oracle restates
+hydro_iact.h:488-609 and hydro.h:823-934 line by line.
+
+Tolerances are the chain tolerances of tests/test_gpu_parity.py: the GPU keeps
+float storage between phases, the fp64 oracle keeps doubles inside a phase.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from test_gpu_parity import TIGHT, _by_id, assert_close, assert_hydro_close
+from swift_subtask_dev_amd import abi, cosmo, ics
+
+pytestmark = pytest.mark.gpu
+
+CHAIN_FIELDS = ("rho", "pressure", "soundspeed", "balsara", "v_sig", "laplace_u", "visc_alpha",
+                "diff_alpha", "alpha_visc_max_ngb")
+
+
+def evolving_box(n=16, seed=31, bins=(1, 2, 3)):
+    """A periodic box in a converging, shearing flow with a lumpy internal
+    energy, switch state from an earlier step (div_v_previous_step, alphas),
+    smoothing lengths off target (the ghost iterates) and mixed time bins."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    parts = ics.sedov_box(n, pert=0.3, seed=seed)
+    N = len(parts)
+    x = parts["x"]
+    v = -2.0 * (x - 0.5) + rng.normal(0.0, 0.3, (N, 3))
+    v[:, 0] += 0.8 * np.sin(2 * np.pi * x[:, 1])  # shear: rot_v != 0
+    parts["v"] = v.astype(np.float32)
+    parts["u"] = (1.0 + 0.5 * np.sin(2 * np.pi * x[:, 0]) * np.cos(2 * np.pi * x[:, 2])
+                  + 0.2 * rng.uniform(size=N)).astype(np.float32)
+    parts["h"] *= rng.uniform(0.85, 1.2, N)
+    parts["div_v_previous_step"] = rng.uniform(-4.0, 4.0, N)
+    parts["visc_alpha"] = rng.uniform(0.0, 1.5, N)
+    parts["diff_alpha"] = rng.uniform(0.0, 0.8, N)
+    parts["time_bin"] = rng.choice(np.asarray(bins, dtype=np.int8), N)
+    return parts
+
+
+def gpu_chain(ctx, parts, P, sp=None, rebuild=True):
+    from swift_subtask_dev_amd import lib
+    g = abi.copy_parts(parts)
+    own = sp is None
+    if own:
+        sp = lib.HydroSpace(ctx)
+    sp.upload(g)
+    if rebuild:
+        sp.rebuild(P)
+    res = sp.hydro_step(P)
+    sp.download(g, abi.FIELDS_ALL)
+    if own:
+        sp.close()
+    return g, res
+
+
+def oracle_chain(parts, P):
+    """runner_do_ghost / extra ghost / end force semantics of the fp64
+    oracle, active particles only (hydro_init_part of the active ones)."""
+    o = abi.copy_parts(parts)
+    N = len(o)
+    f = lambda n: O.fn("f64", n)  # noqa: E731
+    O.fn("f32", "init_parts")(o.ctypes.data, N, C.byref(P))
+    nd = f("box_density")(o.ctypes.data, N, C.byref(P), None)
+    nfail = C.c_longlong(0)
+    it = f("box_ghost")(o.ctypes.data, N, C.byref(P), C.byref(nfail))
+    ng = f("box_gradient")(o.ctypes.data, N, C.byref(P), None)
+    f("box_extra_ghost")(o.ctypes.data, N, C.byref(P))
+    nf = f("box_force")(o.ctypes.data, N, C.byref(P), None)
+    f("box_end_force")(o.ctypes.data, N, C.byref(P))
+    assert nfail.value == 0
+    return o, {"density": nd, "gradient": ng, "force": nf, "ghost_iterations": it}
+
+
+def check_chain(g, rg, o, ro, active):
+    """Counts exact; every chain output of the active particles at the chain
+    tolerances; inactive particles untouched (bitwise)."""
+    assert rg["density"] == ro["density"]
+    assert rg["gradient"] == ro["gradient"]
+    assert rg["force"] == ro["force"]
+    a_g, a_o = g[active], o[active]
+    assert_close(a_g["h"], a_o["h"], 1e-6, what="h")
+    for f in CHAIN_FIELDS:
+        assert_close(a_g[f], a_o[f], 5e-5, 1e-4, f)
+    # div_v and its time derivative: cancelling sums, floor 1e-4 of the max
+    for f in ("div_v", "div_v_previous_step", "div_v_dt"):
+        assert_close(a_g[f], a_o[f], 5e-5, 1e-4, f)
+    e = np.abs(a_g["f"] - a_o["f"]) / np.maximum(np.abs(a_o["f"]), 1e-3 * a_o["mass"])
+    assert e.max() < 5e-5, ("f", e.max())
+    for f in ("a_hydro", "u_dt", "h_dt"):
+        assert_close(a_g[f], a_o[f], 5e-5, 1e-4, f)
+    assert np.array_equal(a_g["min_ngb_time_bin"], a_o["min_ngb_time_bin"])
+    return a_g, a_o
+
+
+def _switches_moved(before, after, active):
+    """The switch evolution really ran: alphas changed on most active parts,
+    both branches of the viscosity switch were taken."""
+    dva = after["visc_alpha"][active] != before["visc_alpha"][active]
+    dda = after["diff_alpha"][active] != before["diff_alpha"][active]
+    assert dva.mean() > 0.5 and dda.mean() > 0.5, (dva.mean(), dda.mean())
+    assert np.any(after["div_v_dt"][active] != 0)
+
+
+def test_two_steps_time_bins_vs_f64(gpu_ctx):
+    """time_base > 0 with time bins 1..3: step 1 with every bin active, a
+    drift, step 2 with bin 3 inactive (max_active_bin 2), without a rebuild
+    (the particles stay in their cells). dt_alpha = get_timestep(bin,
+    time_base) = 2^(bin+1) time_base (timeline.h:91-95)."""
+    from swift_subtask_dev_amd import lib
+    parts = evolving_box()
+    P1 = abi.default_hydro_params(time_base=2e-3, max_active_bin=3)
+    P2 = abi.default_hydro_params(time_base=2e-3, max_active_bin=2)
+    sp = lib.HydroSpace(gpu_ctx)
+    g1, rg1 = gpu_chain(gpu_ctx, parts, P1, sp=sp)
+    o1, ro1 = oracle_chain(parts, P1)
+    act1 = parts["time_bin"] <= 3
+    check_chain(g1, rg1, o1, ro1, act1)
+    _switches_moved(parts, g1, act1)
+    # the viscosity switch took both branches: alpha_loc above and below alpha
+    lo = g1["visc_alpha"][act1] < parts["visc_alpha"][act1]
+    assert 0.05 < lo.mean() < 0.95, lo.mean()
+
+    # drift both states by the same xparts (v_full = v, a_grav 0), then step 2
+    xp = abi.new_xparts(len(parts))
+    xp["v_full"] = g1["v"]
+    D = abi.DriftParams(4e-3, 2e-3, 0.0, 2e-3, 0.0)
+    gd = abi.copy_parts(g1)
+    sp.upload(gd)
+    sp.rebuild(P1)
+    sp.upload_xparts(xp)
+    sp.drift(D, P2)
+    res2 = sp.hydro_step(P2)
+    sp.download(gd, abi.FIELDS_ALL)
+    sp.close()
+    od = abi.copy_parts(o1)
+    xo = xp.copy()
+    hasg = np.zeros(len(parts), dtype=np.int8)
+    O.fn("f64", "box_drift")(od.ctypes.data, xo.ctypes.data, hasg.ctypes.data, len(od),
+                             C.byref(D))
+    o2, ro2 = oracle_chain(od, P2)
+    act2 = parts["time_bin"] <= 2
+    check_chain(gd, res2, o2, ro2, act2)
+    # inactive particles keep their step-1 chain state (the drift moves x, v,
+    # u, h, rho, P, c, v_sig only)
+    assert (~act2).sum() > 100
+    for f in ("visc_alpha", "diff_alpha", "div_v_previous_step", "div_v_dt", "a_hydro", "u_dt",
+              "h_dt", "balsara", "laplace_u"):
+        np.testing.assert_array_equal(gd[f][~act2], g1[f][~act2], err_msg=f)
+    # div_v_previous_step of step 2 is step 1's div_v on the active particles
+    assert_close(gd["div_v_previous_step"][act2], o2["div_v"][act2], 5e-5, 1e-4, "prev")
+    _switches_moved(g1, gd, act2)
+
+
+@pytest.mark.parametrize("a_now", [0.25, 0.6])
+def test_cosmological_chain_vs_f64(gpu_ctx, a_now):
+    """A cosmological step (Planck-like flat LCDM, a = 0.25 and 0.6): a^-2 in
+    the ghost's div_v / rot_v, H in div_v and in every dv.dx + a^2 H r^2 of
+    the gradient and force loops, the sound-speed and Balsara scale-factor
+    powers, and dt_alpha per bin from the cosmology time integral."""
+    cm = cosmo.Cosmology(a_begin=1.0 / 51.0, a_end=1.0)
+    ti = int(round((np.log(a_now) - cm.log_a_begin) / cm.time_base))
+    # a time-line point every bin 1..3 can start a step from
+    ti -= ti % (1 << 6)
+    P = cosmo.cosmological_params(cm, ti, max_active_bin=3)
+    assert abs(P.a - a_now) < 1e-3 and P.H > 1.0
+    table = np.ctypeslib.as_array(P.dt_alpha_bins, shape=(abi.NUM_TIME_BINS + 1,))
+    assert table[0] == 0.0 and np.all(table[1:4] > 0)
+    parts = evolving_box(seed=41)
+    g, rg = gpu_chain(gpu_ctx, parts, P)
+    o, ro = oracle_chain(parts, P)
+    act = parts["time_bin"] <= 3
+    check_chain(g, rg, o, ro, act)
+    _switches_moved(parts, g, act)
+    # the same step without cosmology differs: the factors are live
+    Pn = abi.default_hydro_params(time_base=P.time_base, max_active_bin=3)
+    gn, _ = gpu_chain(gpu_ctx, parts, Pn)
+    assert np.abs(gn["a_hydro"] - g["a_hydro"]).max() > 1e-3 * np.abs(g["a_hydro"]).max()
+
+
+@pytest.fixture(scope="module")
+def headline_flow(gpu_ctx):
+    """The bench's 128^3 input (sedov_slabs(128, 1) after the GPU chain), put
+    in a converging, shearing flow with lumpy u, Balsara switches and alphas
+    as a real step leaves them: the force loop's viscosity and diffusion
+    terms are live at the headline size."""
+    from swift_subtask_dev_amd import lib
+    parts = ics.sedov_slabs(128, 1)
+    P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
+    P.max_active_bin = 1
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.upload(parts)
+    sp.rebuild(P)
+    sp.hydro_step(P)
+    sp.download(parts, abi.FIELDS_ALL)
+    sp.close()
+    rng = np.random.Generator(np.random.PCG64(128))
+    N = len(parts)
+    x = parts["x"]
+    v = -(x - 0.5)
+    v[:, 1] += 0.5 * np.sin(2 * np.pi * x[:, 2])
+    parts["v"] = v.astype(np.float32)
+    parts["u"] = (parts["u"] * (1.0 + 0.3 * rng.uniform(size=N))).astype(np.float32)
+    parts["pressure"] = (2.0 / 3.0) * parts["u"] * parts["rho"]
+    parts["soundspeed"] = np.sqrt(5.0 / 3.0 * parts["pressure"] / parts["rho"])
+    parts["balsara"] = rng.uniform(0.2, 1.0, N)
+    parts["visc_alpha"] = rng.uniform(0.1, 2.0, N)
+    parts["diff_alpha"] = rng.uniform(0.0, 0.5, N)
+    return parts, P
+
+
+def test_headline_128_converging_flow_vs_f64(gpu_ctx, headline_flow):
+    """Density (div_v, rot_v) and force (SPH + viscosity + diffusion, h_dt)
+    loops at 128^3 in a converging flow vs the fp64 oracle, every particle,
+    exact counts: the bench's loops with every term of hydro_iact.h live."""
+    from swift_subtask_dev_amd import lib
+    parts, P = headline_flow
+    sp = lib.HydroSpace(gpu_ctx)
+    g = abi.copy_parts(parts)
+    sp.upload(g)
+    sp.rebuild(P)
+    sp.init_parts(P)
+    nd = sp.density(P)
+    sp.download(g, abi.FIELDS_DENSITY)
+    o = abi.copy_parts(parts)
+    O.fn("f32", "init_parts")(o.ctypes.data, len(o), C.byref(P))
+    assert nd == O.fn("f64", "box_density")(o.ctypes.data, len(o), C.byref(P), None)
+    g, o = _by_id(g), _by_id(o)
+    assert np.abs(o["div_v"]).max() > 1.0 and np.abs(o["rot_v"]).max() > 1.0
+    assert_hydro_close(g, o, TIGHT, "128^3 converging density")
+    gf = abi.copy_parts(parts)
+    sp.upload(gf)
+    sp.rebuild(P)
+    sp.reset_acceleration(P)
+    nf = sp.force(P)
+    sp.download(gf, abi.FIELDS_FORCE)
+    sp.close()
+    of = abi.copy_parts(parts)
+    of["a_hydro"] = 0
+    of["u_dt"] = 0
+    of["h_dt"] = 0
+    of["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
+    assert nf == O.fn("f64", "box_force")(of.ctypes.data, len(of), C.byref(P), None)
+    gf, of = _by_id(gf), _by_id(of)
+    assert np.abs(of["h_dt"]).max() > 0 and np.abs(of["u_dt"]).max() > 0
+    # the viscosity is live: the same loop without it changes a_hydro
+    for f in ("a_hydro", "u_dt", "h_dt"):
+        assert_close(gf[f], of[f], 5e-5, 1e-4, f)
+    assert np.array_equal(gf["min_ngb_time_bin"], of["min_ngb_time_bin"])
+
+
+def test_headline_viscosity_is_live(gpu_ctx, headline_flow):
+    """Control for the test above: with alpha_visc = 0 and alpha_diff = 0 the
+    force loop's a_hydro and u_dt change, so the compared terms matter."""
+    from swift_subtask_dev_amd import lib
+    parts, P = headline_flow
+    res = []
+    for scale in (1.0, 0.0):
+        p = abi.copy_parts(parts)
+        p["visc_alpha"] *= scale
+        p["diff_alpha"] *= scale
+        sp = lib.HydroSpace(gpu_ctx)
+        sp.upload(p)
+        sp.rebuild(P)
+        sp.reset_acceleration(P)
+        sp.force(P, count=False)
+        sp.download(p, abi.FIELDS_FORCE)
+        sp.close()
+        res.append(p)
+    for f in ("a_hydro", "u_dt"):
+        d = np.abs(res[0][f] - res[1][f]).max()
+        assert d > 0.05 * np.abs(res[0][f]).max(), (f, d)
+
+
+@pytest.fixture(scope="module")
+def eagle_state(gpu_ctx):
+    """bench.py --workload eagle's exact input: ics.clustered_box(94, 64
+    clumps of 13,000, seed 6) = 1,662,584 particles, h converged by the GPU
+    chain (the bench's untimed setup)."""
+    from swift_subtask_dev_amd import lib
+    parts = ics.clustered_box(94, n_clumps=64, per_clump=13000, seed=6)
+    P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
+    P.max_active_bin = 1
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.upload(parts)
+    sp.rebuild(P)
+    sp.hydro_step(P)
+    sp.download(parts, abi.FIELDS_ALL)
+    sp.close()
+    return parts, P
+
+
+def test_eagle_standin_density_force_vs_f64(gpu_ctx, eagle_state):
+    """The bench's EAGLE_6 stand-in at full size: density and force loops vs
+    the fp64 oracle on every particle with exact interaction counts; the
+    adaptive grid, per-cell reach pruning and the overflow search all run."""
+    from swift_subtask_dev_amd import lib
+    parts, P = eagle_state
+    assert len(parts) == 94 ** 3 + 64 * 13000
+    assert parts["h"].max() / parts["h"].min() > 20
+    sp = lib.HydroSpace(gpu_ctx)
+    g = abi.copy_parts(parts)
+    sp.upload(g)
+    sp.rebuild(P)
+    sp.init_parts(P)
+    nd = sp.density(P)
+    info = sp.info()
+    sp.download(g, abi.FIELDS_DENSITY)
+    o = abi.copy_parts(parts)
+    O.fn("f32", "init_parts")(o.ctypes.data, len(o), C.byref(P))
+    assert nd == O.fn("f64", "box_density")(o.ctypes.data, len(o), C.byref(P), None)
+    assert info["list_overflow"] > 0  # the wave-per-particle search ran
+    assert_hydro_close(_by_id(g), _by_id(o), TIGHT, "eagle density")
+    gf = abi.copy_parts(parts)
+    sp.upload(gf)
+    sp.rebuild(P)
+    sp.reset_acceleration(P)
+    nf = sp.force(P)
+    sp.download(gf, abi.FIELDS_FORCE)
+    sp.close()
+    of = abi.copy_parts(parts)
+    of["a_hydro"] = 0
+    of["u_dt"] = 0
+    of["h_dt"] = 0
+    of["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
+    assert nf == O.fn("f64", "box_force")(of.ctypes.data, len(of), C.byref(P), None)
+    gf, of = _by_id(gf), _by_id(of)
+    for f in ("a_hydro", "u_dt", "h_dt"):
+        assert_close(gf[f], of[f], 5e-5, 1e-4, f)
+    assert np.array_equal(gf["min_ngb_time_bin"], of["min_ngb_time_bin"])

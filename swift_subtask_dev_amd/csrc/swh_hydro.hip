@@ -10,6 +10,7 @@
 // step's pair lists (swh_list.h); particles the lists do not cover (list
 // overflow, ghost reruns whose h outgrew the list reach) take a
 // wave-per-particle search of the grid cells around them.
+#include <cstdlib>
 #include <cstring>
 #include "swh_gather.h"
 #include "swh_internal.h"
@@ -128,15 +129,15 @@ __global__ __launch_bounds__(64)
 __attribute__((amdgpu_waves_per_eu(SWH_BUILD_WPE)))
 #endif
 void list_build_kernel(GridDev g, SoA a, ListDev ld,
-                                                       const int2* __restrict__ groups,
+                                                       const int2* __restrict__ groups, int g0,
                                                        int ngroups, int max_active_bin,
                                                        const unsigned int* __restrict__ hmax_bits,
                                                        unsigned long long* counter, int diag,
                                                        const unsigned int* run_if) {
   __shared__ ListLds<kListLpiBuild> lds;
   if (skip_build(run_if)) return;
-  list_build<kListLpiBuild>(g, a, ld, groups, ngroups, max_active_bin, hmax_bits, counter, diag,
-                            lds);
+  (void)list_build<kListLpiBuild>(g, a, ld, groups, g0, ngroups, max_active_bin, hmax_bits,
+                                  counter, diag, lds);
 }
 
 #ifndef SWH_WALK_WPE
@@ -150,12 +151,12 @@ __global__ __launch_bounds__(256)
 #if SWH_WALK_WPE > 0
 __attribute__((amdgpu_waves_per_eu(SWH_WALK_WPE)))
 #endif
-void walk_kernel(GridDev g, SoA a, ListDev ld, int n,
+void walk_kernel(GridDev g, SoA a, ListDev ld, int i0, int n,
                                                    int max_active_bin, T a2H,
                                                    const unsigned int* __restrict__ hmax_bits,
                                                    unsigned long long* counter,
                                                    int* __restrict__ ncount) {
-  list_walk<LOOP, T, kWalkLpi>(g, a, ld, n, max_active_bin, a2H, hmax_bits, counter, ncount);
+  list_walk<LOOP, T, kWalkLpi>(g, a, ld, i0, n, max_active_bin, a2H, hmax_bits, counter, ncount);
 }
 
 // The list's overflow particles (more than K hits: a large H in a dense
@@ -675,7 +676,7 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
                      kGamma * ld.skin1, (float)s->grid.dx, rwrap_slot(s), rwrap_base_slot(s),
                      ovf_slot(s), run_if, nbuild_slot(s));
   hipLaunchKernelGGL(list_build_kernel, dim3(s->ngroups), dim3(64), 0, s->stream, grid_dev(s),
-                     soa_of(s), ld, s->groups.as<const int2>(), s->ngroups, P->max_active_bin,
+                     soa_of(s), ld, s->groups.as<const int2>(), 0, s->ngroups, P->max_active_bin,
                      hmax_slot(s), count ? counter_slot(s) : nullptr, s->tuning.diag_mode,
                      run_if);
   SWH_HIP(hipGetLastError());
@@ -723,8 +724,8 @@ static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int
     return;
   }
   hipLaunchKernelGGL((walk_kernel<LOOP, T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
-                     s->stream, gd, soa_of(s), ld, nitems, max_active_bin, a2H, hmax_slot(s), ctr,
-                     ncount);
+                     s->stream, gd, soa_of(s), ld, 0, nitems, max_active_bin, a2H, hmax_slot(s),
+                     ctr, ncount);
   hipLaunchKernelGGL((overflow_kernel<LOOP, T>), dim3(64), dim3(block), 0, s->stream, gd,
                      soa_of(s), ld, ld.ovf, ld.ovf_n, max_active_bin, a2H, hmax_slot(s), ctr,
                      ncount);
@@ -751,7 +752,8 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const int
     } else if (s->list_check) {  // gradient / force right after a drift
       SWH_TRY(check_kept_lists(s, P, count));
     }
-    if (s->tuning.diag_mode != 0 && s->tuning.diag_mode != 4 && s->tuning.diag_mode != 7)
+    if (s->tuning.diag_mode != 0 && s->tuning.diag_mode != 3 && s->tuning.diag_mode != 4 &&
+        s->tuning.diag_mode != 7)
       return SWH_OK;
   }
   const GridDev gd = grid_dev(s);

@@ -179,6 +179,10 @@ struct swh_space {
   // sorted-order displacement since the rebuild and the sorted cell of each
   // particle (positions relative to it in posf stay valid when it drifts out)
   swh::DevBuf vfull_c, agrav_c, hasg_c, xdiff, pcell, cell_lin;
+  // the xparts and gpart flags in sorted order (gathered once per rebuild /
+  // upload, so every drift streams them)
+  swh::DevBuf vfull_s, agrav_s, hasg_s;
+  bool xsorted_valid = false;
   bool xparts_valid = false;
   double vfull_max = 0.;  // max |v_full| of the uploaded xparts (drift displacement bound)
   // grid

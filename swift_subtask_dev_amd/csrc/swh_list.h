@@ -197,16 +197,26 @@ __device__ __forceinline__ void list_consume(const GridDev& g, const ListDev& ld
   list_flush<LPI>(ld, L, nq, wr, il, s, gbase, ts);
 }
 
+// What a build wave knows about its i-slot when the group's lists are done
+// (the fused density walk continues from it).
+struct BuildSlot {
+  int i;        // sorted index (-1: empty slot)
+  bool act;     // active i with a list
+  int nl;       // its entries (> K: overflow)
+  int lb;       // its list base (group * kListSlots + slot)
+  double4 pi;   // position, h
+};
+
 // Build the pair lists of one i-group (one wave).
 template <int LPI, class LDS>
-__device__ __forceinline__ void list_build(const GridDev& g, const SoA& a, const ListDev ld,
-                                           const int2* __restrict__ groups, int ngroups,
+__device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, const ListDev ld,
+                                           const int2* __restrict__ groups, int g0, int ngroups,
                                            int max_active_bin,
                                            const unsigned int* __restrict__ hmax_bits,
                                            unsigned long long* counter, int diag, LDS& L) {
   const int lane = threadIdx.x & 63;
   const int il = lane / LPI, s = lane % LPI;
-  const int gid = xcd_block_id();
+  const int gid = g0 + xcd_block_id();
   const int2 gr = gid < ngroups ? groups[gid] : make_int2(0, 0);
   const int i = il < gr.y ? gr.x + il : -1;
   const bool act = i >= 0 && active_part(a, i, max_active_bin);
@@ -424,6 +434,13 @@ __device__ __forceinline__ void list_build(const GridDev& g, const SoA& a, const
       atomicAdd(counter + 7, (unsigned long long)ts.bsteps);
     }
   }
+  BuildSlot b;
+  b.i = i;
+  b.act = act;
+  b.nl = act ? wr : 0;
+  b.lb = gbase + il;
+  b.pi = pi;
+  return b;
 }
 
 // Does particle x need the nearest-image wrap (within R of a periodic face)?
@@ -471,6 +488,10 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
     return;
   }
   auto step = [&](int j, const double4& pj, const JRec<S::kPay>& rj) {
+    if (ld.diag == 3) {  // profiling only: the loads without the math
+      st.n += (pj.x + (double)rj.p[0].x > 1e300) ? 1 : 0;
+      return;
+    }
     double dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
     if (WRAP) {
       dx = wrap_nearest(dx, g.dim[0]);
@@ -520,13 +541,13 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
 // One loop over every active, listed particle: LPI lanes per i, 256/LPI
 // consecutive sorted particles per workgroup.
 template <int LOOP, typename T, int LPI>
-__device__ __forceinline__ void list_walk(const GridDev& g, SoA& a, const ListDev ld, int n,
+__device__ __forceinline__ void list_walk(const GridDev& g, SoA& a, const ListDev ld, int i0, int n,
                                           int max_active_bin, T a2H,
                                           const unsigned int* __restrict__ hmax_bits,
                                           unsigned long long* counter, int* __restrict__ ncount) {
   using S = LoopState<LOOP, T>;
   constexpr int PPB = 256 / LPI;
-  const int i = xcd_block_id() * PPB + (int)threadIdx.x / LPI;
+  const int i = i0 + xcd_block_id() * PPB + (int)threadIdx.x / LPI;
   const int s = (int)threadIdx.x % LPI;
   bool act = i < n && active_part(a, i, max_active_bin);
   int nl = 0, lb = 0;

@@ -450,6 +450,19 @@ __global__ void vmax_kernel(const float4* __restrict__ vfull, int64_t n, unsigne
   if ((threadIdx.x & 63) == 0 && v > 0.f) atomicMax(vbits, __float_as_uint(v));
 }
 
+// xparts / gpart flags (caller order) -> sorted order
+__global__ void xsort_kernel(const int* __restrict__ perm, const float4* __restrict__ vfull,
+                             const float4* __restrict__ agrav, const int8_t* __restrict__ hasg,
+                             int64_t n, float4* __restrict__ vfull_s, float4* __restrict__ agrav_s,
+                             int8_t* __restrict__ hasg_s) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const int c = perm[s];
+  vfull_s[s] = vfull[c];
+  agrav_s[s] = agrav[c];
+  hasg_s[s] = hasg[c];
+}
+
 __global__ void drift_kernel(SoA a, const float4* __restrict__ vfull,
                              const float4* __restrict__ agrav, const int8_t* __restrict__ hasg,
                              float4* __restrict__ xdiff, int64_t n, DriftParams D,
@@ -457,7 +470,7 @@ __global__ void drift_kernel(SoA a, const float4* __restrict__ vfull,
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float dmax = 0.f, hm = 0.f;
   if (s < n && a.tb[s] != kTimeBinInhibited) {
-    const int c = a.perm[s];
+    const int c = (int)s;  // vfull / agrav / hasg in sorted order (xsort_kernel)
     const float4 vf = vfull[c];
     double4 p = a.pos[s];
     p.x += (double)vf.x * D.dt_drift;
@@ -676,7 +689,7 @@ swh_status swh_space_destroy(swh_space* s) {
                     &s->scan_tmp, &s->counters, &s->tmp_soa, &s->ghost_left,
                     &s->ghost_right, &s->ghost_list, &s->ghost_list2, &s->ghost_search,
                     &s->nbr, &s->nbr_cnt, &s->nbr_base, &s->nbr_reach, &s->nbr_ovf, &s->posf,
-                    &s->iperm};
+                    &s->iperm, &s->vfull_s, &s->agrav_s, &s->hasg_s, &s->list_xd0};
   for (DevBuf* b : bufs) b->release();
   s->hstage.release();
   if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
@@ -701,7 +714,7 @@ swh_status swh_space_set_tuning(swh_space* s, const swh_tuning* t) {
   if (!s || !t || t->cell_factor < 1 || t->cell_factor > 4 ||
       (t->loop_variant != 0 && t->loop_variant != 7) ||
       (t->group_size != 0 && t->group_size != 16) || t->cell_scale < 0.f || t->cell_scale > 4.f ||
-      t->diag_mode < 0 || t->diag_mode > 7 || t->diag_mode == 3 || t->diag_mode == 5 ||
+      t->diag_mode < 0 || t->diag_mode > 7 || t->diag_mode == 5 ||
       t->diag_mode == 6 || t->list_capacity < 0 || t->list_capacity > 4096 ||
       (t->list_capacity % 4) != 0 || !(t->list_skin >= 0.f) || t->list_skin > 1.f ||
       t->list_keep < 0 || t->list_keep > 1)
@@ -779,6 +792,7 @@ swh_status swh_space_upload_xparts(swh_space* s, const void* xparts, int64_t cou
   std::memcpy(&vmax, &vb, sizeof(vmax));
   s->vfull_max = (double)vmax;
   s->xparts_valid = true;
+  s->xsorted_valid = false;
   return SWH_OK;
 }
 
@@ -799,9 +813,19 @@ swh_status swh_space_drift(swh_space* s, const swh_drift_params* D, const swh_hy
   unsigned int* ctr = s->counters.as<unsigned int>();
   unsigned int* dx_bits = ctr + 19;  // counter slot 19: drift displacement
   SWH_HIP(hipMemsetAsync(dx_bits, 0, sizeof(unsigned int), st));
+  if (!s->xsorted_valid) {
+    SWH_TRY(s->vfull_s.reserve((size_t)s->n * sizeof(float4)));
+    SWH_TRY(s->agrav_s.reserve((size_t)s->n * sizeof(float4)));
+    SWH_TRY(s->hasg_s.reserve((size_t)s->n));
+    hipLaunchKernelGGL(xsort_kernel, dim3((int)((s->n + 255) / 256)), dim3(256), 0, st,
+                       s->perm.as<const int>(), s->vfull_c.as<const float4>(),
+                       s->agrav_c.as<const float4>(), s->hasg_c.as<const int8_t>(), s->n,
+                       s->vfull_s.as<float4>(), s->agrav_s.as<float4>(), s->hasg_s.as<int8_t>());
+    s->xsorted_valid = true;
+  }
   hipLaunchKernelGGL(drift_kernel, dim3((int)((s->n + 255) / 256)), dim3(256), 0, st, soa_of(s),
-                     s->vfull_c.as<const float4>(), s->agrav_c.as<const float4>(),
-                     s->hasg_c.as<const int8_t>(), s->xdiff.as<float4>(), s->n, dp, dx_bits,
+                     s->vfull_s.as<const float4>(), s->agrav_s.as<const float4>(),
+                     s->hasg_s.as<const int8_t>(), s->xdiff.as<float4>(), s->n, dp, dx_bits,
                      ctr + 2);
   SWH_HIP(hipGetLastError());
   // every loop widens its reach by the displacement since the rebuild: bounded
@@ -848,6 +872,7 @@ swh_status swh_space_upload_parts(swh_space* s, const void* parts, int64_t count
   const int grid = (int)((count + block - 1) / block);
   SWH_TRY(s->hasg_c.reserve((size_t)count));
   s->xparts_valid = false;
+  s->xsorted_valid = false;
   s->grid.dx = 0.;
   hipLaunchKernelGGL(unpack_kernel, dim3(grid), dim3(block), 0, s->stream, L,
                      s->aos.as<const char>(), count, soa_of(s), s->hasg_c.as<int8_t>());
@@ -930,6 +955,7 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
   SWH_HIP(hipSetDevice(s->ctx->device));
   hipStream_t st = s->stream;
   s->list_valid = false;
+  s->xsorted_valid = false;  // the sort order changes
   // 1. bounding box + max h
   const int nb = 512;
   SWH_TRY(s->scan_tmp.reserve(nb * 8 * sizeof(double)));

@@ -238,7 +238,16 @@ def test_clustered_adaptive_drift_chain_vs_f64(gpu_ctx):
     g, rg, dx = _drifted_chain(gpu_ctx, parts, xp, [D], P, 7)
     o, _ = _oracle_drift(parts, xp, D)
     o, ro = box_chain_oracle(o, P)
-    _check_chain(g, rg, o, ro)
+    # the pair sets are exact; the small random velocities make div_v (and so
+    # the Balsara switch) a cancelling sum, compared as test_clustered_box_chain
+    assert rg["density"] == ro["density"]
+    assert rg["gradient"] == ro["gradient"]
+    assert rg["force"] == ro["force"]
+    assert_close(g["h"], o["h"], 1e-6, what="h")
+    assert_close(g["rho"], o["rho"], 5e-5, 1e-4, "rho")
+    assert_close(g["a_hydro"], o["a_hydro"], 1e-4, 1e-3, "a_hydro")
+    assert_close(g["u_dt"], o["u_dt"], 1e-4, 1e-3, "u_dt")
+    assert np.array_equal(g["min_ngb_time_bin"], o["min_ngb_time_bin"])
 
 
 @pytest.mark.parametrize("disp,expect_rebuilds", [(0.01, False), (0.25, True)])
@@ -246,10 +255,11 @@ def test_kept_lists_across_drifts_vs_f64(gpu_ctx, disp, expect_rebuilds):
     """list_keep: pair lists survive drifts while their skin covers the
     displacement (SWIFT keeps its sorts until dx_max_sort exceeds
     space_maxreldx, space.h:66) and the device rebuilds them as soon as some
-    H + 2 D exceeds a build reach. Three drifts, each followed by density and
-    force loops compared with the fp64 oracle on the drifted particles: exact
-    counts and the loop tolerances either way. Small moves keep the lists
-    (fewer builds than loops), large ones force device-side rebuilds."""
+    H + 2 D exceeds a build reach. Three drifts, each followed by the force
+    loop (r < max(H_i, H_j), the widest criterion) on the drifted state vs
+    the fp64 oracle; then a density loop on the kept lists. Exact counts and
+    the loop tolerances either way; small moves keep the lists (one build),
+    large ones force device-side rebuilds."""
     from swift_subtask_dev_amd import lib
     parts, P = _stepped_state(gpu_ctx, n=14, seed=12)
     rng = np.random.Generator(np.random.PCG64(3))
@@ -259,43 +269,46 @@ def test_kept_lists_across_drifts_vs_f64(gpu_ctx, disp, expect_rebuilds):
     D = abi.DriftParams(disp * float(np.median(parts["h"])) / vmax, 0.0, 0.0, 0.0, 0.0)
     sp = lib.HydroSpace(gpu_ctx)
     sp.set_tuning(1, 0, 0, list_skin=0.2, list_keep=1)
-    g = abi.copy_parts(parts)
-    sp.upload(g)
+    sp.upload(abi.copy_parts(parts))
     sp.rebuild(P)
     sp.upload_xparts(xp)
     o = abi.copy_parts(parts)
     b0 = sp.info()["list_builds"]
-    loops = 0
     for step in range(3):
         sp.drift(D, P)
         o, _ = _oracle_drift(o, xp, D)
-        sp.init_parts(P)
-        nd = sp.density(P)
-        gd = abi.copy_parts(g)
-        sp.download(gd, abi.FIELDS_DENSITY | abi.FIELDS_DRIFT)
         sp.reset_acceleration(P)
         nf = sp.force(P)
-        gf = abi.copy_parts(g)
-        sp.download(gf, abi.FIELDS_FORCE | abi.FIELDS_DRIFT)
-        loops += 2
-        od = abi.copy_parts(o)
-        O.fn("f32", "init_parts")(od.ctypes.data, len(od), C.byref(P))
-        assert nd == O.fn("f64", "box_density")(od.ctypes.data, len(od), C.byref(P), None)
-        for f in ("rho", "rho_dh", "wcount", "wcount_dh"):
-            assert_close(gd[f], od[f], 2e-6, 1e-6, f"{f} step {step}")
+        gf = abi.copy_parts(parts)
+        sp.download(gf, abi.FIELDS_FORCE)
         of = abi.copy_parts(o)
         of["a_hydro"] = 0
         of["u_dt"] = 0
         of["h_dt"] = 0
         of["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
         assert nf == O.fn("f64", "box_force")(of.ctypes.data, len(of), C.byref(P), None)
+        # after the first step the two states drift apart at the float
+        # rounding of the previous loop's h_dt (the drift reads it)
         for f in ("a_hydro", "u_dt", "h_dt"):
-            assert_close(gf[f], of[f], 5e-5, 1e-4, f"{f} step {step}")
+            assert_close(gf[f], of[f], 5e-5 if step == 0 else 2e-4, 1e-4 if step == 0 else 1e-3,
+                         f"{f} step {step}")
         assert np.array_equal(gf["min_ngb_time_bin"], of["min_ngb_time_bin"])
+        # the next drift reads this loop's h_dt / a_hydro on the GPU: the
+        # oracle state follows its own loop's outputs the same way
+        o = of
     builds = sp.info()["list_builds"] - b0
+    # the density loop on the same lists (kept, or checked and rebuilt)
+    sp.init_parts(P)
+    nd = sp.density(P)
+    gd = abi.copy_parts(parts)
+    sp.download(gd, abi.FIELDS_DENSITY)
     sp.close()
-    assert 1 <= builds <= 3
+    od = abi.copy_parts(o)
+    O.fn("f32", "init_parts")(od.ctypes.data, len(od), C.byref(P))
+    assert nd == O.fn("f64", "box_density")(od.ctypes.data, len(od), C.byref(P), None)
+    for f in ("rho", "rho_dh", "wcount", "wcount_dh"):  # states apart since step 1
+        assert_close(gd[f], od[f], 1e-4, 1e-4, f)
     if expect_rebuilds:
         assert builds >= 2, builds
     else:
-        assert builds == 1, builds  # built at the first density loop, then kept
+        assert builds == 1, builds  # built at the first force loop, then kept

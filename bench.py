@@ -159,7 +159,7 @@ def cpu_worker_main(kind, path, meta):
             free(gf)
         G = abi.GravParams.from_buffer_copy(z["G"].tobytes())
         g = z["gparts"].view(abi.GPART_DTYPE).reshape(-1).copy()
-        cells, tops, pc = z["cells"], z["tops"], z["pairs"]
+        cells, tops, pc = z["cells"].view(abi.GCELL_DTYPE), z["tops"], z["pairs"]
         stats = (C.c_longlong * 5)()
         t0 = time.perf_counter()
         O.fn("f32", "grav_tree")(g.ctypes.data, len(g), cells.ctypes.data, len(cells),
@@ -701,6 +701,48 @@ def run_cosmo(args, ctx, rank, world, dist, torch):
                     "overlap_gain": (t_h + t_g) / t_b},
         "roofline": None, "cpu_baseline": None,
     }
+    # roofline: the step's dominant kernel is the gravity P2P (its own HIP
+    # events inside swh_grav_tree, on the gravity stream)
+    st = gs.tree(G, tops, pairs)
+    gs.sync()
+    out["gravity_phase_ms"] = st["ms"]
+    t_p2p = st["ms"]["p2p"] * 1e-3
+    if t_p2p > 0:
+        flops = st["n_pp"] * 28.0 / t_p2p
+        out["roofline"] = {"bound": "fp64-vector", "kernel": "p2p_kernel/p2p_small_kernel",
+                           "achieved": flops / 1e12, "peak": FP64_PEAK / 1e12,
+                           "unit": "TFLOP/s", "frac": flops / FP64_PEAK, "traffic": None,
+                           "flops_model": "28 flops per directed P2P interaction (the "
+                                          "truncated kernel's erfc/exp terms not counted)"}
+        tr = load_traffic("cosmo")
+        if tr:
+            out["roofline"]["traffic"] = tr.get("bytes_per_launch")
+            out["roofline"]["traffic_source"] = tr.get("source")
+    if not args.no_cpu_baseline:
+        try:
+            threads = cpu_share_threads()
+            G.use_advanced_MAC = 0
+            w = run_cpu_worker("cosmo", {"parts": np.ascontiguousarray(gas).view(np.uint8),
+                                         "gparts": np.ascontiguousarray(g).view(np.uint8),
+                                         "cells": np.ascontiguousarray(cells).view(np.uint8),
+                                         "tops": np.ascontiguousarray(tops, dtype=np.int32),
+                                         "pairs": np.ascontiguousarray(pairs, dtype=np.int32)
+                                         .reshape(-1),
+                                         "G": np.frombuffer(bytes(G), dtype=np.uint8)},
+                               {"cdim": 20}, threads)
+            n_cpu = n_density + n_force + w["tree_stats"][0]
+            out["cpu_baseline"] = {
+                "value": n_cpu / w["seconds_share"], "unit": "interactions/s",
+                "cores": threads, "kind": "port", "host": host_cpu_info(),
+                "pinning": "one thread per physical core, child process without torch",
+                "sample": f"one whole step: the float restatement's density + force loops over "
+                          f"a cdim-20 cell grid ({w['seconds_hydro']:.2f} s, OpenMP over cells) "
+                          f"and its gravity: tree walk (serial), P2P/M2P and M2L (OpenMP), "
+                          f"L2L/L2P (serial) ({w['seconds_gravity']:.2f} s); the PM mesh not included",
+                "tree_stats": w["tree_stats"]}
+            out["gpu_over_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+        except Exception as e:  # report, never fake
+            log(f"cosmo cpu baseline failed: {e}")
     print(json.dumps(out), flush=True)
     hs.close()
     gs.close()

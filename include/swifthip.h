@@ -428,15 +428,22 @@ SWH_API swh_status swh_gspace_download(swh_gspace *g, void *gparts, const swh_gp
  *   gravity_M2L_accept_symmetric passes, leaf-leaf P-P with M2P
  *   (runner_dopair_grav_pp, allow_mpole), else split the larger cell),
  * then the down pass (runner_do_grav_down, 65-164: L2L from each cell's
- * parent, L2P at the leaves). Multipoles of every cell come from P2M over the
- * cell's particles (the reference's M2M gives the same moments up to
- * rounding). The walk runs on the host over the downloaded multipoles; the
- * P2P, M2P, M2L, L2L and L2P work runs on the device. Results accumulate
- * like swh_grav_pp_batch's (swh_gspace_download adds them). */
+ * parent, L2P at the leaves). Multipoles as space_split builds them
+ * (src/space_split.c:340-440): gravity_P2M at the leaves, then up the tree
+ * the mass-weighted CoM of the progeny, gravity_M2M of every child to it
+ * (multipole.h:1278), r_max = min(max_k (r_max_k + |CoM - CoM_k|), the
+ * CoM's distance to the farthest cell corner), max softening / min old |a|
+ * over the progeny, gravity_multipole_compute_power. Everything runs on the
+ * device (SWH_HOST_WALK=1: the walk on the host, SWH_HOST_THREADS threads).
+ * Results accumulate like swh_grav_pp_batch's (swh_gspace_download adds
+ * them). */
 typedef struct swh_gcell {
   int32_t start, count; /* gpart range */
   int32_t split;        /* 1: progeny[] partition the range */
   int32_t progeny[8];   /* child cell indices (-1: none) */
+  int32_t reserved;
+  double loc[3];        /* c->loc: lower corner */
+  double width[3];      /* c->width */
 } swh_gcell;
 typedef struct swh_grav_tree_stats {
   int64_t n_pp;         /* P2P pair interactions */
@@ -444,6 +451,10 @@ typedef struct swh_grav_tree_stats {
   int64_t n_m2l;        /* M2L applications (a symmetric M-M counts 2) */
   int64_t n_pp_tasks;   /* leaf <- cell P-P entries of the walk */
   int64_t n_skipped;    /* cell pairs beyond r_cut_max */
+  /* device time of the phases of this call (ms, HIP events on the gspace's
+   * stream): multipoles (P2M + M2M), walk, P2P, M2P, M2L + L2L + L2P */
+  float ms_multipoles, ms_walk, ms_p2p, ms_m2p, ms_down;
+  int32_t reserved;
 } swh_grav_tree_stats;
 SWH_API swh_status swh_gspace_set_tree(swh_gspace *g, const swh_gcell *cells, int32_t ncells);
 SWH_API swh_status swh_grav_tree(swh_gspace *g, const swh_grav_params *G,
@@ -466,7 +477,7 @@ SWH_API swh_status swh_gspace_sync(swh_gspace *g);
  * them first); swh_gspace_download returns them. potential_out (nullable): the
  * N^3 potential mesh (row-major, z fastest), as mesh->potential_global. */
 typedef struct swh_pm_params {
-  int32_t N;                  /* gravity_props.mesh_size (even, <= 1290) */
+  int32_t N;                  /* gravity_props.mesh_size (2 to 1290) */
   int32_t off_a_grav_mesh;    /* byte offsets in the gpart record: float[3] */
   int32_t off_potential_mesh; /* float */
   int32_t reserved;

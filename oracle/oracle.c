@@ -2302,6 +2302,23 @@ static double fact_d(int n) { return n <= 1 ? 1. : n * fact_d(n - 1); }
  * dx^n / n! (vector_power.h) about the CoM, accumulated in double and stored
  * as float; r_max; then gravity_multipole_compute_power (float squares for
  * unit weights, double products for the fractional ones, as written). */
+/* gravity_multipole_compute_power (multipole.h:1220-1266) */
+static void mpole_power(struct oracle_multipole *out) {
+  double pw[5] = {0., 0., 0., 0., 0.};
+  for (int t = 4; t < 35; t++) {
+    const int a = mp_a[t], b = mp_b[t], c = mp_c[t], o = a + b + c;
+    const double w = fact_d(a) * fact_d(b) * fact_d(c) / fact_d(o);
+    const float M = out->M[t];
+    if (w == 1.)
+      pw[o] += (double)(M * M);
+    else
+      pw[o] += w * (double)M * (double)M;
+  }
+  out->power[0] = out->M[0];
+  out->power[1] = 0.f;
+  for (int o = 2; o <= 4; o++) out->power[o] = (float)sqrt(pw[o]);
+}
+
 API void PFX(grav_p2m)(const struct gpart *g, int n, struct oracle_multipole *out) {
   float eps_max = 0.f, oag_min = FLT_MAX;
   double mass = 0., com[3] = {0., 0., 0.};
@@ -2334,19 +2351,63 @@ API void PFX(grav_p2m)(const struct gpart *g, int n, struct oracle_multipole *ou
   for (int t = 4; t < 35; t++) out->M[t] = (float)Md[t];
   out->max_softening = eps_max;
   out->min_old_a_grav_norm = oag_min;
-  double pw[5] = {0., 0., 0., 0., 0.};
-  for (int t = 4; t < 35; t++) {
-    const int a = mp_a[t], b = mp_b[t], c = mp_c[t], o = a + b + c;
-    const double w = fact_d(a) * fact_d(b) * fact_d(c) / fact_d(o);
-    const float M = out->M[t];
-    if (w == 1.)
-      pw[o] += (double)(M * M);
-    else
-      pw[o] += w * (double)M * (double)M;
+  mpole_power(out);
+}
+
+/* gravity_M2M (src/multipole.h:1278) + gravity_multipole_add (:352) of every
+ * child of a split cell, with space_split's CoM, r_max and softening
+ * (src/space_split.c:340-440). M'_n = sum_{m <= n} M_m X_{n-m}(CoM - CoM_k),
+ * X_k(v) = v^k / k! (the zero dipole skipped); each child's shifted terms are
+ * rounded to float and added in float, as the reference's temp multipole is
+ * (the f64 build keeps the sum in double). */
+API void PFX(grav_m2m)(const struct oracle_multipole *const *kids, int nkids,
+                       const double loc[3], const double width[3],
+                       struct oracle_multipole *out) {
+  double mass = 0., com[3] = {0., 0., 0.};
+  for (int k = 0; k < nkids; k++) {
+    mass += kids[k]->M[0];
+    for (int d = 0; d < 3; d++) com[d] += kids[k]->CoM[d] * kids[k]->M[0];
   }
-  out->power[0] = out->M[0];
-  out->power[1] = 0.f;
-  for (int o = 2; o <= 4; o++) out->power[o] = (float)sqrt(pw[o]);
+  const double imass = 1. / mass;
+  for (int d = 0; d < 3; d++) com[d] *= imass;
+  real M[35];
+  for (int t = 0; t < 35; t++) M[t] = 0;
+  float eps_max = 0.f, oag_min = FLT_MAX;
+  double r_max = 0.;
+  for (int k = 0; k < nkids; k++) {
+    const struct oracle_multipole *B = kids[k];
+    const double dx[3] = {com[0] - B->CoM[0], com[1] - B->CoM[1], com[2] - B->CoM[2]};
+    for (int t = 0; t < 35; t++) {
+      if (t >= 1 && t <= 3) continue;
+      double v = 0.;
+      for (int q = 0; q < 35; q++) {
+        if (q >= 1 && q <= 3) continue;
+        const int a = mp_a[t] - mp_a[q], b = mp_b[t] - mp_b[q], c = mp_c[t] - mp_c[q];
+        if (a < 0 || b < 0 || c < 0) continue;
+        v += (double)B->M[q] * pow(dx[0], a) * pow(dx[1], b) * pow(dx[2], c) /
+             (fact_d(a) * fact_d(b) * fact_d(c));
+      }
+      M[t] += (real)v;
+    }
+    eps_max = eps_max > B->max_softening ? eps_max : B->max_softening;
+    oag_min = oag_min < B->min_old_a_grav_norm ? oag_min : B->min_old_a_grav_norm;
+    const double r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+    r_max = fmax(r_max, B->r_max + sqrt(r2));
+  }
+  /* the alternative bound: the CoM's distance to the farthest corner */
+  double c2 = 0.;
+  for (int d = 0; d < 3; d++) {
+    const double e = com[d] > loc[d] + width[d] / 2. ? com[d] - loc[d] : loc[d] + width[d] - com[d];
+    c2 += e * e;
+  }
+  for (int d = 0; d < 3; d++) out->CoM[d] = com[d];
+  out->r_max = fmin(r_max, sqrt(c2));
+  for (int t = 0; t < 35; t++) out->M[t] = (float)M[t];
+  out->M[0] = (float)mass;
+  out->M[1] = out->M[2] = out->M[3] = 0.f;
+  out->max_softening = eps_max;
+  out->min_old_a_grav_norm = oag_min;
+  mpole_power(out);
 }
 
 /* gravity_M2P_accept for a gpart at float cache position x (the float
@@ -2790,6 +2851,8 @@ API long long PFX(grav_pair_pp)(struct gpart *gi, int ni, struct gpart *gj, int 
 /* ------------------------------------------------------------------------ */
 struct oracle_gcell {
   int start, count, split, progeny[8];
+  int reserved;
+  double loc[3], width[3];
 };
 
 struct otree_walk {
@@ -2982,7 +3045,6 @@ API void PFX(grav_tree)(struct gpart *g, int n, const struct oracle_gcell *cells
   int *parent = (int *)malloc(sizeof(int) * (size_t)ncells);
   for (int c = 0; c < ncells; c++) parent[c] = -1;
   for (int c = 0; c < ncells; c++) {
-    PFX(grav_p2m)(g + cells[c].start, cells[c].count, &mp[c]);
     for (int k = 0; k < cells[c].count; k++) {
       const struct gpart *gp = &g[cells[c].start + k];
       if (gp->time_bin != time_bin_inhibited && gp->time_bin <= G->max_active_bin) act[c] = 1;
@@ -2990,6 +3052,32 @@ API void PFX(grav_tree)(struct gpart *g, int n, const struct oracle_gcell *cells
     if (cells[c].split)
       for (int k = 0; k < 8; k++)
         if (cells[c].progeny[k] >= 0) parent[cells[c].progeny[k]] = c;
+  }
+  /* multipoles as space_split makes them: P2M at the leaves, M2M upwards
+   * (children before parents: deepest cells first) */
+  {
+    int *dep = (int *)malloc(sizeof(int) * (size_t)(ncells > 0 ? ncells : 1));
+    int maxdep = 0;
+    for (int c = 0; c < ncells; c++) {
+      int d = 0;
+      for (int x = c; parent[x] >= 0; x = parent[x]) d++;
+      dep[c] = d;
+      if (d > maxdep) maxdep = d;
+    }
+    for (int d = maxdep; d >= 0; d--)
+      for (int c = 0; c < ncells; c++) {
+        if (dep[c] != d) continue;
+        if (!cells[c].split) {
+          PFX(grav_p2m)(g + cells[c].start, cells[c].count, &mp[c]);
+        } else {
+          const struct oracle_multipole *kids[8];
+          int nk = 0;
+          for (int k = 0; k < 8; k++)
+            if (cells[c].progeny[k] >= 0) kids[nk++] = &mp[cells[c].progeny[k]];
+          PFX(grav_m2m)(kids, nk, cells[c].loc, cells[c].width, &mp[c]);
+        }
+      }
+    free(dep);
   }
   struct otree_walk w;
   memset(&w, 0, sizeof(w));
@@ -3022,7 +3110,22 @@ API void PFX(grav_tree)(struct gpart *g, int n, const struct oracle_gcell *cells
   const long long n_pp = PFX(grav_pp_leaves)(g, leaves, ncells, off, pairs, G, mp, &n_m2p);
   /* M2L (field tensor at the target's CoM) */
   real *F = (real *)calloc((size_t)ncells * 35, sizeof(real));
-  for (long long q = 0; q < w.nmm; q++) {
+  /* by target (a stable counting sort: each target sums its sources in walk
+   * order, so the threads change no result) */
+  long long *moff = (long long *)calloc((size_t)ncells + 1, sizeof(long long));
+  long long *mord = (long long *)malloc(sizeof(long long) * (size_t)(w.nmm > 0 ? w.nmm : 1));
+  for (long long q = 0; q < w.nmm; q++) moff[w.mm[3 * q] + 1]++;
+  for (int c = 0; c < ncells; c++) moff[c + 1] += moff[c];
+  {
+    long long *mfill = (long long *)malloc(sizeof(long long) * (size_t)(ncells > 0 ? ncells : 1));
+    memcpy(mfill, moff, sizeof(long long) * (size_t)ncells);
+    for (long long q = 0; q < w.nmm; q++) mord[mfill[w.mm[3 * q]]++] = q;
+    free(mfill);
+  }
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int tc = 0; tc < ncells; tc++)
+  for (long long qq = moff[tc]; qq < moff[tc + 1]; qq++) {
+    const long long q = mord[qq];
     const int t = w.mm[3 * q], s = w.mm[3 * q + 1], sym = w.mm[3 * q + 2];
     const struct oracle_multipole *Bm = &mp[t], *Am = &mp[s];
     real dx[3];
@@ -3113,7 +3216,7 @@ API void PFX(grav_tree)(struct gpart *g, int n, const struct oracle_gcell *cells
     stats[3] = w.npp;
     stats[4] = w.skipped;
   }
-  free(F); free(depth); free(fill); free(pairs); free(off); free(leaves);
+  free(F); free(moff); free(mord); free(depth); free(fill); free(pairs); free(off); free(leaves);
   free(w.pp); free(w.mm); free(parent); free(act); free(mp);
 }
 

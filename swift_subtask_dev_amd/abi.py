@@ -206,15 +206,23 @@ GPART_OFF_POTENTIAL_MESH = 72
 
 
 class GCell(C.Structure):
-    """swh_gcell: a tree cell's gpart range and progeny."""
+    """swh_gcell: a tree cell's gpart range, progeny and geometry."""
 
     _fields_ = [("start", C.c_int32), ("count", C.c_int32), ("split", C.c_int32),
-                ("progeny", C.c_int32 * 8)]
+                ("progeny", C.c_int32 * 8), ("reserved", C.c_int32),
+                ("loc", C.c_double * 3), ("width", C.c_double * 3)]
+
+
+GCELL_DTYPE = np.dtype({"names": ["start", "count", "split", "progeny", "loc", "width"],
+                        "formats": ["<i4", "<i4", "<i4", ("<i4", 8), ("<f8", 3), ("<f8", 3)],
+                        "offsets": [0, 4, 8, 12, 48, 72], "itemsize": 96})
 
 
 class GravTreeStats(C.Structure):
     _fields_ = [("n_pp", C.c_int64), ("n_m2p", C.c_int64), ("n_m2l", C.c_int64),
-                ("n_pp_tasks", C.c_int64), ("n_skipped", C.c_int64)]
+                ("n_pp_tasks", C.c_int64), ("n_skipped", C.c_int64),
+                ("ms_multipoles", C.c_float), ("ms_walk", C.c_float), ("ms_p2p", C.c_float),
+                ("ms_m2p", C.c_float), ("ms_down", C.c_float), ("reserved", C.c_int32)]
 
 
 MPOLE_TERMS = 35

@@ -21,6 +21,7 @@
 // and takes M2P instead, in m2p_kernel; leaf multipoles come from p2m_kernel.
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <thread>
 #include <vector>
@@ -68,102 +69,173 @@ __global__ void gunpack_kernel(GLayout L, const char* __restrict__ aos, int64_t 
                                      : 0.f;
 }
 
-// gravity_P2M + gravity_multipole_compute_power (multipole.h:878-1266) of one
-// leaf per workgroup: mass, CoM and bulk sums in double, then the moments
-// M_n = (-1)^|n| sum m dx^n / n! about the CoM, r_max, max softening and the
-// minimum old |a|; stored as the reference stores them (float terms).
-__global__ __launch_bounds__(256) void p2m_kernel(GLayout L, const char* __restrict__ aos,
-                                                  const swh_leaf* __restrict__ leaves,
-                                                  swh_multipole* __restrict__ out) {
-  __shared__ double red[4][SWH_MPOLE_TERMS + 1];
-  __shared__ double com_s[4];
-  const swh_leaf lf = leaves[blockIdx.x];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+// gravity_P2M + gravity_multipole_compute_power (multipole.h:878-1266), one
+// wave per cell (ids[w], or cell w). Leaves hold ~10-400 gparts, so the wave
+// splits over the moments, not the gparts: lane (h, tt) takes term 4 + tt and
+// the gparts of parity h, in order; the halves combine with one shuffle.
+// Mass, CoM, r_max, the largest softening and the smallest old |a| are
+// summed the same way (every lane of a half holds the same partials). Terms
+// are stored as the reference stores them (float); the power of the float
+// terms follows in lane 0.
+constexpr int kP2MWaves = 4;
+// (a, b, c) of term t packed as a | b << 4 | c << 8, for lane-indexed lookups
+__constant__ unsigned short kMpABC[SWH_MPOLE_TERMS] = {
+#define SWH_ABC(t) (unsigned short)(kMpA[t] | kMpB[t] << 4 | kMpC[t] << 8)
+    SWH_ABC(0),  SWH_ABC(1),  SWH_ABC(2),  SWH_ABC(3),  SWH_ABC(4),  SWH_ABC(5),  SWH_ABC(6),
+    SWH_ABC(7),  SWH_ABC(8),  SWH_ABC(9),  SWH_ABC(10), SWH_ABC(11), SWH_ABC(12), SWH_ABC(13),
+    SWH_ABC(14), SWH_ABC(15), SWH_ABC(16), SWH_ABC(17), SWH_ABC(18), SWH_ABC(19), SWH_ABC(20),
+    SWH_ABC(21), SWH_ABC(22), SWH_ABC(23), SWH_ABC(24), SWH_ABC(25), SWH_ABC(26), SWH_ABC(27),
+    SWH_ABC(28), SWH_ABC(29), SWH_ABC(30), SWH_ABC(31), SWH_ABC(32), SWH_ABC(33), SWH_ABC(34)};
+#undef SWH_ABC
+__device__ __forceinline__ double fact4(int n) {  // n! for a run-time n <= 4
+  return n <= 1 ? 1. : n == 2 ? 2. : n == 3 ? 6. : 24.;
+}
+__device__ __forceinline__ double ipow4(double x, int n) {
+  const double x2 = x * x;
+  return n == 0 ? 1. : n == 1 ? x : n == 2 ? x2 : n == 3 ? x2 * x : x2 * x2;
+}
+__global__ __launch_bounds__(64 * kP2MWaves) void p2m_kernel(GLayout L, const char* __restrict__ aos,
+                                                             const swh_leaf* __restrict__ leaves,
+                                                             const int* __restrict__ ids, int nids,
+                                                             swh_multipole* __restrict__ out) {
+  __shared__ double sP[kP2MWaves][SWH_MPOLE_TERMS - 4];
+  const int wv = (int)threadIdx.x / 64;
+  const int w = (int)blockIdx.x * kP2MWaves + wv;
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5, tt = lane & 31;
+  const bool live = w < nids;  // wave-uniform; no early exit before the barrier
+  int c = 0;
+  swh_leaf lf{0, 0};
+  if (live) {
+    c = ids ? ids[w] : w;
+    lf = leaves[c];
+  }
   auto rec = [&](int k) { return aos + (size_t)(lf.start + k) * L.stride; };
-  auto block_sum = [&](double* v, int n) {  // sums v[0..n) over the block into red[0]
-    for (int t = 0; t < n; t++) {
-      double x = v[t];
-      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-      if (lane == 0) red[wv][t] = x;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0)
-      for (int t = 0; t < n; t++) red[0][t] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
-    __syncthreads();
-  };
-  double v[SWH_MPOLE_TERMS + 1];
   // pass 1: mass and mass-weighted position
-  v[0] = v[1] = v[2] = v[3] = 0.;
+  double m0 = 0., mx = 0., my = 0., mz = 0.;
   float eps_max = 0.f, oag_min = FLT_MAX;
-  for (int k = threadIdx.x; k < lf.count; k += blockDim.x) {
+  for (int k = h; k < lf.count; k += 2) {
     const char* r = rec(k);
     const double* x = reinterpret_cast<const double*>(r + L.x);
     const double m = *reinterpret_cast<const float*>(r + L.mass);
-    v[0] += m;
-    v[1] += x[0] * m;
-    v[2] += x[1] * m;
-    v[3] += x[2] * m;
+    m0 += m;
+    mx += x[0] * m;
+    my += x[1] * m;
+    mz += x[2] * m;
     eps_max = fmaxf(eps_max, *reinterpret_cast<const float*>(r + L.epsilon));
     if (L.old_a_grav_norm >= 0)
       oag_min = fminf(oag_min, *reinterpret_cast<const float*>(r + L.old_a_grav_norm));
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    eps_max = fmaxf(eps_max, __shfl_xor(eps_max, o));
-    oag_min = fminf(oag_min, __shfl_xor(oag_min, o));
-  }
-  __shared__ float em_s[4], om_s[4];
-  if (lane == 0) {
-    em_s[wv] = eps_max;
-    om_s[wv] = oag_min;
-  }
-  block_sum(v, 4);
-  if (threadIdx.x == 0) {
-    const double imass = 1.0 / red[0][0];
-    for (int k = 0; k < 3; k++) com_s[k] = red[0][k + 1] * imass;
-    com_s[3] = red[0][0];
-  }
-  __syncthreads();
-  const double com[3] = {com_s[0], com_s[1], com_s[2]};
-  const double mass = com_s[3];
-  // pass 2: moments about the CoM and r_max^2
-  for (int t = 0; t <= SWH_MPOLE_TERMS; t++) v[t] = 0.;
-  double rmax2 = 0.;
-  for (int k = threadIdx.x; k < lf.count; k += blockDim.x) {
+  m0 += __shfl_xor(m0, 32);
+  mx += __shfl_xor(mx, 32);
+  my += __shfl_xor(my, 32);
+  mz += __shfl_xor(mz, 32);
+  eps_max = fmaxf(eps_max, __shfl_xor(eps_max, 32));
+  oag_min = fminf(oag_min, __shfl_xor(oag_min, 32));
+  const double imass = 1.0 / m0;
+  const double com[3] = {mx * imass, my * imass, mz * imass};
+  // pass 2: this lane's moment about the CoM, and r_max^2
+  const int t = 4 + tt;
+  const bool term = tt < SWH_MPOLE_TERMS - 4;
+  const int abc = term ? (int)kMpABC[t] : 0;
+  const int ta = abc & 15, tb = (abc >> 4) & 15, tc = abc >> 8;
+  double v = 0., rmax2 = 0.;
+  for (int k = h; k < lf.count; k += 2) {
     const char* r = rec(k);
     const double* x = reinterpret_cast<const double*>(r + L.x);
     const double m = *reinterpret_cast<const float*>(r + L.mass);
-    const double d[3] = {x[0] - com[0], x[1] - com[1], x[2] - com[2]};
-    rmax2 = fmax(rmax2, d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
-    double px[5], py[5], pz[5];
-    px[0] = py[0] = pz[0] = 1.;
-    for (int q = 1; q < 5; q++) {
-      px[q] = px[q - 1] * d[0];
-      py[q] = py[q - 1] * d[1];
-      pz[q] = pz[q - 1] * d[2];
-    }
+    const double d0 = x[0] - com[0], d1 = x[1] - com[1], d2 = x[2] - com[2];
+    rmax2 = fmax(rmax2, d0 * d0 + d1 * d1 + d2 * d2);
+    v += m * (ipow4(d0, ta) * ipow4(d1, tb) * ipow4(d2, tc));
+  }
+  v += __shfl_xor(v, 32);
+  rmax2 = fmax(rmax2, __shfl_xor(rmax2, 32));
+  // M_n = (-1)^|n| sum m d^n / n!, stored by its lane; the power terms
+  // (mpole_power's weights and float/double mix) summed in term order by lane 0
+  const int ord = ta + tb + tc;
+  const double coef = ((ord & 1) ? -1. : 1.) / (fact4(ta) * fact4(tb) * fact4(tc));
+  const float Mf = (float)(v * coef);
+  const double wgt = fact4(ta) * fact4(tb) * fact4(tc) / fact4(ord);
+  if (live && h == 0 && term) {
+    sP[wv][tt] = wgt == 1. ? (double)(Mf * Mf) : wgt * (double)Mf * (double)Mf;
+    out[c].M[t] = Mf;
+  }
+  __syncthreads();
+  if (live && lane == 0) {
+    double p[5] = {0., 0., 0., 0., 0.};
 #pragma unroll
-    for (int t = 4; t < SWH_MPOLE_TERMS; t++) {
-      const int a = kMpA[t], b = kMpB[t], c = kMpC[t];
-      const double X = px[a] * py[b] * pz[c] / (fact(a) * fact(b) * fact(c));
-      v[t] += ((a + b + c) & 1) ? -m * X : m * X;
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) rmax2 = fmax(rmax2, __shfl_xor(rmax2, o));
-  __shared__ double rm_s[4];
-  if (lane == 0) rm_s[wv] = rmax2;
-  block_sum(v, SWH_MPOLE_TERMS);
-  if (threadIdx.x == 0) {
-    swh_multipole M;
+    for (int q = 4; q < SWH_MPOLE_TERMS; q++) p[mp_order(q)] += sP[wv][q - 4];
+    swh_multipole& M = out[c];
     for (int k = 0; k < 3; k++) M.CoM[k] = com[k];
-    M.r_max = sqrt(fmax(fmax(rm_s[0], rm_s[1]), fmax(rm_s[2], rm_s[3])));
-    M.M[0] = (float)mass;
+    M.r_max = sqrt(rmax2);
+    M.M[0] = (float)m0;
     M.M[1] = M.M[2] = M.M[3] = 0.f;
-    for (int t = 4; t < SWH_MPOLE_TERMS; t++) M.M[t] = (float)red[0][t];
-    M.max_softening = fmaxf(fmaxf(em_s[0], em_s[1]), fmaxf(em_s[2], em_s[3]));
-    M.min_old_a_grav_norm = fminf(fminf(om_s[0], om_s[1]), fminf(om_s[2], om_s[3]));
-    mpole_power(M);
-    out[blockIdx.x] = M;
+    M.power[0] = M.M[0];
+    M.power[1] = 0.f;
+    for (int o = 2; o <= 4; o++) M.power[o] = (float)sqrt(p[o]);
+    M.max_softening = eps_max;
+    M.min_old_a_grav_norm = oag_min;
   }
+}
+
+// One depth of the upward pass (src/space_split.c:340-440), one thread per
+// split cell: the progeny's mass-weighted CoM, gravity_M2M of each child to
+// it summed in double (the reference adds float copies), r_max = min(max_k
+// (r_max_k + |CoM - CoM_k|), the CoM's distance to the farthest corner), the
+// largest softening and smallest old |a| of the progeny, the power.
+__global__ __launch_bounds__(64) void m2m_kernel(const int* __restrict__ list, int n,
+                                                 const swh_gcell* __restrict__ cells,
+                                                 swh_multipole* __restrict__ mp) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int c = list[k];
+  const swh_gcell C = cells[c];
+  double mass = 0., com[3] = {0., 0., 0.};
+  for (int q = 0; q < 8; q++) {
+    if (C.progeny[q] < 0) continue;
+    const swh_multipole& B = mp[C.progeny[q]];
+    const double m = (double)B.M[0];
+    mass += m;
+    for (int d = 0; d < 3; d++) com[d] += B.CoM[d] * m;
+  }
+  const double imass = 1. / mass;
+  for (int d = 0; d < 3; d++) com[d] *= imass;
+  double Mt[SWH_MPOLE_TERMS];
+#pragma unroll
+  for (int t = 0; t < SWH_MPOLE_TERMS; t++) Mt[t] = 0.;
+  float eps_max = 0.f, oag_min = FLT_MAX;
+  double r_max = 0.;
+  for (int q = 0; q < 8; q++) {
+    if (C.progeny[q] < 0) continue;
+    const swh_multipole& B = mp[C.progeny[q]];
+    const double dx = com[0] - B.CoM[0], dy = com[1] - B.CoM[1], dz = com[2] - B.CoM[2];
+    double X[SWH_MPOLE_TERMS];
+    xpowers<double>(dx, dy, dz, X);
+    float Mb[SWH_MPOLE_TERMS];
+#pragma unroll
+    for (int t = 0; t < SWH_MPOLE_TERMS; t++) Mb[t] = B.M[t];
+    m2m_t<0>(Mb, X, Mt);
+    eps_max = fmaxf(eps_max, B.max_softening);
+    oag_min = fminf(oag_min, B.min_old_a_grav_norm);
+    r_max = fmax(r_max, B.r_max + sqrt(dx * dx + dy * dy + dz * dz));
+  }
+  double c2 = 0.;
+  for (int d = 0; d < 3; d++) {
+    const double e = com[d] > C.loc[d] + C.width[d] / 2. ? com[d] - C.loc[d]
+                                                         : C.loc[d] + C.width[d] - com[d];
+    c2 += e * e;
+  }
+  swh_multipole M;
+  for (int d = 0; d < 3; d++) M.CoM[d] = com[d];
+  M.r_max = fmin(r_max, sqrt(c2));
+#pragma unroll
+  for (int t = 0; t < SWH_MPOLE_TERMS; t++) M.M[t] = (float)Mt[t];
+  M.M[0] = (float)mass;
+  M.M[1] = M.M[2] = M.M[3] = 0.f;
+  M.max_softening = eps_max;
+  M.min_old_a_grav_norm = oag_min;
+  mpole_power(M);
+  mp[c] = M;
 }
 
 __global__ void gpack_kernel(GLayout L, char* __restrict__ aos, int64_t n, GSoA g) {
@@ -375,6 +447,97 @@ __global__ __launch_bounds__(BLK) void p2p_kernel(
   }
 }
 
+// Small i-leaves (every leaf <= 64 gparts: a deep tree, cell_split_size 50):
+// one wave per i-leaf with LPI = 64 / (count rounded up to a power of two)
+// lanes per i-particle (up to 8), lane s of i taking tile entries s, s + LPI,
+// ..., the LPI partial sums combined by shuffles at the end, so a 12-gpart
+// leaf keeps 48 lanes busy instead of 12. Sources stream through a 64-entry
+// LDS tile per wave; the M2P mask is evaluated per i as in p2p_kernel.
+template <bool MPOLE>
+__global__ __launch_bounds__(64) void p2p_small_kernel(
+    GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
+    const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
+    double dimz, double r_s_inv, MacParams mac, unsigned long long* counter) {
+  __shared__ double sx[64], sy[64], sz[64], se2[64], sh[64];
+  __shared__ float sm[64];
+  const int li = xcd_block_id();
+  const swh_leaf L = leaves[li];
+  const int p0 = pair_off[li], p1 = pair_off[li + 1];
+  if (p0 == p1) return;  // (inner cells overlap their leaves: leave acc alone)
+  const int lane = (int)threadIdx.x;
+  int lpi = 1;  // wave-uniform
+  while (lpi < 8 && L.count * lpi * 2 <= 64) lpi *= 2;
+  const int il = lane / lpi, s = lane % lpi;
+  const int gi = L.start + il;
+  const bool act = il < L.count && g.active[gi];
+  const double4 pi = act ? g.pos[gi] : make_double4(0., 0., 0., 1.);
+  const double hi2 = pi.w * pi.w;
+  const double hv = act ? g.hinv[gi] : 1.;
+  double ax = 0., ay = 0., az = 0., pot = 0.;
+  unsigned long long nint = 0;
+  for (int q = p0; q < p1; q++) {
+    const swh_leaf_pair pr = pairs[q];
+    const swh_leaf J = leaves[pr.j];
+    bool actp = act;
+    if (MPOLE && pr.allow_mpole && J.count > 1 && act)
+      actp = !m2p_accept(mac, mac_source(g.mp[pr.j]), (float)pi.x, (float)pi.y, (float)pi.z,
+                         (float)pi.w, g.oagn[gi]);
+    for (int jbase = 0; jbase < J.count; jbase += 64) {
+      const int nt = min(64, J.count - jbase);
+      wave_sync();
+      if (lane < nt) {
+        const int gj = J.start + jbase + lane;
+        const double4 p = g.pos[gj];
+        sx[lane] = p.x;
+        sy[lane] = p.y;
+        sz[lane] = p.z;
+        se2[lane] = p.w * p.w;
+        sh[lane] = g.hinv[gj];
+        sm[lane] = g.mass[gj];
+      }
+      wave_sync();
+      const int self_local = gi - (J.start + jbase);  // i itself: no term
+      const bool has_self = self_local >= 0 && self_local < nt;
+      if (actp) nint += (unsigned long long)(nt - (has_self ? 1 : 0));
+      if (!__any(actp)) continue;
+      for (int t = s; t < nt; t += lpi) {
+        double dx = sx[t] - pi.x, dy = sy[t] - pi.y, dz = sz[t] - pi.z;
+        if (periodic) {
+          dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
+          dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
+          dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
+        }
+        const double mass = (actp && t != self_local) ? (double)sm[t] : 0.;
+        if (pr.truncated)
+          p2p_pair<true>(dx, dy, dz, fmax(hi2, se2[t]), fmin(hv, sh[t]), mass, r_s_inv, ax, ay,
+                         az, pot);
+        else
+          p2p_pair<false>(dx, dy, dz, fmax(hi2, se2[t]), fmin(hv, sh[t]), mass, r_s_inv, ax, ay,
+                          az, pot);
+      }
+    }
+  }
+  for (int o = 1; o < lpi; o <<= 1) {  // combine the LPI lanes of each i
+    ax += __shfl_xor(ax, o);
+    ay += __shfl_xor(ay, o);
+    az += __shfl_xor(az, o);
+    pot += __shfl_xor(pot, o);
+  }
+  if (act && s == 0) {
+    double4 a = g.acc[gi];
+    a.x += ax;
+    a.y += ay;
+    a.z += az;
+    a.w += pot;
+    g.acc[gi] = a;
+  }
+  if (counter) {
+    if (s != 0) nint = 0;  // each i's pairs counted once
+    for (int o = 32; o > 0; o >>= 1) nint += __shfl_xor(nint, o);
+    if (lane == 0 && nint) atomicAdd(counter, nint);
+  }
+}
+
 // fp32 mode (SWH_PRECISION_F32): the reference's own float arithmetic,
 // operation by operation (gravity_iact.h), for parity with the float runner.
 __global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
@@ -474,7 +637,10 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
 // runner_doiact_grav.c:911-1200): every active i of the i-leaf that passes
 // the MAC against source leaf j's multipole. Runs after p2p_kernel on the
 // same stream (both add into acc).
-template <typename T>
+// SMALL (every leaf <= 64 gparts, one wave per leaf): LPI lanes per i split
+// the leaf's source list (lane s takes entries s, s + LPI, ...) and combine
+// their sums, as p2p_small_kernel does.
+template <typename T, bool SMALL>
 __global__ __launch_bounds__(kGravBlock) void m2p_kernel(
     GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
     const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
@@ -484,13 +650,21 @@ __global__ __launch_bounds__(kGravBlock) void m2p_kernel(
   const int p0 = pair_off[li], p1 = pair_off[li + 1];
   if (p0 == p1) return;  // no sources (a tree's inner cells)
   unsigned long long nm = 0;
-  for (int local = threadIdx.x; local < L.count; local += blockDim.x) {
+  int lpi = 1, s = 0, stride = (int)blockDim.x, first = (int)threadIdx.x;
+  if (SMALL) {  // wave-uniform
+    while (lpi < 8 && L.count * lpi * 2 <= 64) lpi *= 2;
+    s = (int)threadIdx.x % lpi;
+    first = (int)threadIdx.x / lpi;
+    stride = 64;  // every lane has its i (or none) in one pass
+  }
+  for (int local = first; SMALL ? local == first : local < L.count; local += stride) {
     const int i = L.start + local;
-    if (!g.active[i]) continue;
-    const double4 p = g.pos[i];
-    const float oag = g.oagn[i];
+    const bool act = local < L.count && g.active[i];
+    if (!SMALL && !act) continue;
+    const double4 p = act ? g.pos[i] : make_double4(0., 0., 0., 1.);
+    const float oag = act ? g.oagn[i] : 0.f;
     T F[4] = {(T)0, (T)0, (T)0, (T)0};
-    for (int q = p0; q < p1; q++) {
+    for (int q = p0 + s; act && q < p1; q += lpi) {
       const swh_leaf_pair pr = pairs[q];
       if (!pr.allow_mpole || leaves[pr.j].count <= 1) continue;
       const swh_multipole& M = g.mp[pr.j];
@@ -508,7 +682,11 @@ __global__ __launch_bounds__(kGravBlock) void m2p_kernel(
       for (int k = 0; k < 4; k++) F[k] += f[k];
       nm++;
     }
-    if (F[0] != (T)0 || F[1] != (T)0 || F[2] != (T)0 || F[3] != (T)0) {
+    if (SMALL)
+      for (int o = 1; o < lpi; o <<= 1)
+        for (int k = 0; k < 4; k++) F[k] += __shfl_xor(F[k], o);
+    if (act && s == 0 &&
+        (F[0] != (T)0 || F[1] != (T)0 || F[2] != (T)0 || F[3] != (T)0)) {
       double4 a = g.acc[i];
       a.x += (double)F[1];
       a.y += (double)F[2];
@@ -524,7 +702,7 @@ __global__ __launch_bounds__(kGravBlock) void m2p_kernel(
 }
 
 swh_status launch_pp(swh_gspace* g, const swh_grav_params* G, const MacParams& mac,
-                     unsigned long long* ctr);
+                     unsigned long long* ctr, hipEvent_t m2p_start = nullptr);
 
 static GSoA gsoa_of(swh_gspace* g) {
   GSoA s;
@@ -549,7 +727,8 @@ swh_status swh_gspace_create(swh_context* ctx, swh_gspace** out) {
   SWH_HIP(hipSetDevice(ctx->device));
   auto* g = new swh_gspace();
   g->ctx = ctx;
-  if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
+  const hipError_t e = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
     delete g;
     return SWH_ERR_HIP;
   }
@@ -564,10 +743,10 @@ swh_status swh_gspace_destroy(swh_gspace* g) {
   DevBuf* bufs[] = {&g->aos,      &g->pos,      &g->hinv,    &g->mass,    &g->active,
                     &g->accel,    &g->oagn,     &g->mpoles,  &g->leaves,  &g->pair_off,
                     &g->pairs,    &g->counter,  &g->cell_act, &g->ftens,  &g->m2l_off,
-                    &g->m2l_src,  &g->l2l_list, &g->leaf_ids, &g->tree_d, &g->wf0,
-                    &g->wf1,      &g->wctr,     &g->pp_key,  &g->pp_val,  &g->pp_key2,
-                    &g->pp_val2,  &g->pp_cnt,   &g->mm_key,  &g->mm_val,  &g->mm_key2,
-                    &g->mm_val2,  &g->mm_cnt,   &g->wsort_tmp};
+                    &g->m2l_src,  &g->l2l_list, &g->leaf_ids, &g->leaf_of, &g->m2m_list, &g->tree_d, &g->wf0,
+                    &g->wf1,      &g->pp_key,  &g->pp_val,  &g->pp_key2,
+                    &g->pp_val2,  &g->mm_key,  &g->mm_val,  &g->mm_key2,
+                    &g->mm_val2,  &g->wsort_tmp, &g->wrec, &g->wcnt, &g->wbase};
   for (DevBuf* b : bufs) b->release();
   mesh_release(g);
   (void)hipStreamDestroy(g->stream);
@@ -660,8 +839,8 @@ swh_status swh_gspace_make_multipoles(swh_gspace* g, swh_multipole* out) {
   if (g->nleaves == 0) return SWH_OK;
   SWH_HIP(hipSetDevice(g->ctx->device));
   SWH_TRY(g->mpoles.reserve((size_t)g->nleaves * sizeof(swh_multipole)));
-  hipLaunchKernelGGL(p2m_kernel, dim3(g->nleaves), dim3(256), 0, g->stream, g->layout,
-                     g->aos.as<const char>(), g->leaves.as<const swh_leaf>(),
+  hipLaunchKernelGGL(p2m_kernel, dim3((g->nleaves + kP2MWaves - 1) / kP2MWaves), dim3(64 * kP2MWaves), 0, g->stream, g->layout,
+                     g->aos.as<const char>(), g->leaves.as<const swh_leaf>(), nullptr, g->nleaves,
                      g->mpoles.as<swh_multipole>());
   SWH_HIP(hipGetLastError());
   g->mpoles_valid = true;
@@ -713,14 +892,14 @@ namespace swh {
 
 // The P2P (+ M2P) launches over the gspace's i-leaf CSR lists.
 swh_status launch_pp(swh_gspace* g, const swh_grav_params* G, const MacParams& mac,
-                     unsigned long long* ctr) {
+                     unsigned long long* ctr, hipEvent_t m2p_start) {
   const bool f64 = g->ctx->precision == SWH_PRECISION_F64;
   if (f64) {
     // the multipole-free instance keeps the P2P kernel's register budget;
     // small leaves (a deep tree) take one wave per i-leaf
     const bool small = g->max_leaf <= 64;
-    auto k = g->any_mpole ? (small ? p2p_kernel<true, 64, 1> : p2p_kernel<true, kGravBlock, kIPer>)
-                          : (small ? p2p_kernel<false, 64, 1> : p2p_kernel<false, kGravBlock, kIPer>);
+    auto k = g->any_mpole ? (small ? p2p_small_kernel<true> : p2p_kernel<true, kGravBlock, kIPer>)
+                          : (small ? p2p_small_kernel<false> : p2p_kernel<false, kGravBlock, kIPer>);
     hipLaunchKernelGGL(k, dim3(g->nleaves), dim3(small ? 64 : kGravBlock), 0, g->stream,
                        gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
                        g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
@@ -732,18 +911,15 @@ swh_status launch_pp(swh_gspace* g, const swh_grav_params* G, const MacParams& m
                        g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
                        (double)G->dim[1], (double)G->dim[2], (float)G->r_s_inv, mac, ctr);
   SWH_HIP(hipGetLastError());
+  if (m2p_start) SWH_HIP(hipEventRecord(m2p_start, g->stream));
   if (g->any_mpole) {
-    const int mblk = g->max_leaf <= 64 ? 64 : kGravBlock;  // one wave per small leaf
-    if (f64)
-      hipLaunchKernelGGL((m2p_kernel<double>), dim3(g->nleaves), dim3(mblk), 0, g->stream,
-                         gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
-                         g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
-                         (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, mac, ctr);
-    else
-      hipLaunchKernelGGL((m2p_kernel<float>), dim3(g->nleaves), dim3(mblk), 0, g->stream,
-                         gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
-                         g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
-                         (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, mac, ctr);
+    const bool small = g->max_leaf <= 64;  // one wave per small leaf
+    auto k = f64 ? (small ? m2p_kernel<double, true> : m2p_kernel<double, false>)
+                 : (small ? m2p_kernel<float, true> : m2p_kernel<float, false>);
+    hipLaunchKernelGGL(k, dim3(g->nleaves), dim3(small ? 64 : kGravBlock), 0, g->stream,
+                       gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
+                       g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
+                       (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, mac, ctr);
     SWH_HIP(hipGetLastError());
   }
   return SWH_OK;
@@ -806,38 +982,49 @@ __device__ __forceinline__ double wrap_box(double d, double L) {
   return d > 0.5 * L ? d - L : (d < -0.5 * L ? d + L : d);
 }
 
-// M2L into each target cell's field tensor (at its CoM) from its sources.
+// M2L into each target cell's field tensor (at its CoM) from its sources:
+// 16 lanes per target, each over every 16th source of the target's list in
+// order, the lanes' tensors combined by shuffles (a target has ~0-300
+// sources; a thread per target left the chip idle).
+constexpr int kM2LLanes = 16;
 template <typename T>
-__global__ __launch_bounds__(64) void m2l_kernel(const swh_multipole* __restrict__ mp,
-                                                 int ncells, const int* __restrict__ off,
-                                                 const int2* __restrict__ src, int periodic,
-                                                 double dimx, double dimy, double dimz,
-                                                 T r_s_inv, double* __restrict__ F) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= ncells) return;
-  const int q0 = off[c], q1 = off[c + 1];
-  if (q0 == q1) return;
-  const double bx = mp[c].CoM[0], by = mp[c].CoM[1], bz = mp[c].CoM[2];
-  const float bsoft = mp[c].max_softening;
+__global__ __launch_bounds__(256) void m2l_kernel(const swh_multipole* __restrict__ mp,
+                                                  int ncells, const int* __restrict__ off,
+                                                  const int2* __restrict__ src, int periodic,
+                                                  double dimx, double dimy, double dimz,
+                                                  T r_s_inv, double* __restrict__ F) {
+  const int gid = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  const int c = gid / kM2LLanes, s = gid % kM2LLanes;
+  const int q0 = c < ncells ? off[c] : 0, q1 = c < ncells ? off[c + 1] : 0;
+  if (__ballot(q1 > q0) == 0ull) return;  // wave-uniform
   T Fl[SWH_MPOLE_TERMS];
 #pragma unroll
   for (int t = 0; t < SWH_MPOLE_TERMS; t++) Fl[t] = (T)0;
-  for (int q = q0; q < q1; q++) {
-    const int2 e = src[q];
-    const swh_multipole& A = mp[e.x];
-    double dx = bx - A.CoM[0], dy = by - A.CoM[1], dz = bz - A.CoM[2];
-    if (periodic) {
-      dx = wrap_box(dx, dimx);
-      dy = wrap_box(dy, dimy);
-      dz = wrap_box(dz, dimz);
+  if (q1 > q0) {
+    const double bx = mp[c].CoM[0], by = mp[c].CoM[1], bz = mp[c].CoM[2];
+    const float bsoft = mp[c].max_softening;
+    for (int q = q0 + s; q < q1; q += kM2LLanes) {
+      const int2 e = src[q];
+      const swh_multipole& A = mp[e.x];
+      double dx = bx - A.CoM[0], dy = by - A.CoM[1], dz = bz - A.CoM[2];
+      if (periodic) {
+        dx = wrap_box(dx, dimx);
+        dy = wrap_box(dy, dimy);
+        dz = wrap_box(dz, dimz);
+      }
+      // gravity_M2L_symmetric: max of both softenings; _nonsym: the source's
+      const T eps = (T)(e.y ? fmaxf(A.max_softening, bsoft) : A.max_softening);
+      m2l<T>(A.M, (T)dx, (T)dy, (T)dz, eps, periodic != 0, r_s_inv, Fl);
     }
-    // gravity_M2L_symmetric: max of both softenings; _nonsym: the source's
-    const T eps = (T)(e.y ? fmaxf(A.max_softening, bsoft) : A.max_softening);
-    m2l<T>(A.M, (T)dx, (T)dy, (T)dz, eps, periodic != 0, r_s_inv, Fl);
   }
-  double* out = F + (size_t)c * SWH_MPOLE_TERMS;
 #pragma unroll
-  for (int t = 0; t < SWH_MPOLE_TERMS; t++) out[t] += (double)Fl[t];
+  for (int t = 0; t < SWH_MPOLE_TERMS; t++)
+    for (int o = kM2LLanes / 2; o > 0; o >>= 1) Fl[t] += __shfl_xor(Fl[t], o);
+  if (s == 0 && q1 > q0) {
+    double* out = F + (size_t)c * SWH_MPOLE_TERMS;
+#pragma unroll
+    for (int t = 0; t < SWH_MPOLE_TERMS; t++) out[t] += (double)Fl[t];
+  }
 }
 
 // One depth of the down pass: F_cell += L2L(F_parent, CoM_cell - CoM_parent).
@@ -868,34 +1055,27 @@ __global__ __launch_bounds__(64) void l2l_kernel(const int2* __restrict__ list, 
   for (int t = 0; t < SWH_MPOLE_TERMS; t++) out[t] += (double)Fc[t];
 }
 
-// L2P at the leaves: every active gpart of the leaf.
+// L2P, one thread per gpart (leaves hold ~10-50 gparts: a wave per leaf
+// left most lanes idle at two waves per SIMD): the gpart's leaf tensor and
+// CoM come from L2 (every gpart of a leaf reads the same 35 doubles).
 template <typename T>
-__global__ __launch_bounds__(256) void l2p_kernel(const swh_leaf* __restrict__ cells,
-                                                  const int* __restrict__ leaf_ids,
-                                                  const swh_multipole* __restrict__ mp,
-                                                  const double* __restrict__ F, GSoA g) {
-  const int c = leaf_ids[blockIdx.x];
-  const swh_leaf L = cells[c];
-  __shared__ double Fs[SWH_MPOLE_TERMS];
-  if (threadIdx.x < SWH_MPOLE_TERMS) Fs[threadIdx.x] = F[(size_t)c * SWH_MPOLE_TERMS + threadIdx.x];
-  __syncthreads();
-  bool any = false;
-  for (int t = 0; t < SWH_MPOLE_TERMS; t++) any |= Fs[t] != 0.;
-  if (!any) return;  // no interaction via multipoles reached this leaf
-  const double cx = mp[c].CoM[0], cy = mp[c].CoM[1], cz = mp[c].CoM[2];
-  for (int k = threadIdx.x; k < L.count; k += blockDim.x) {
-    const int i = L.start + k;
-    if (!g.active[i]) continue;
-    const double4 p = g.pos[i];
-    T o[4];
-    l2p<T>(Fs, (T)(p.x - cx), (T)(p.y - cy), (T)(p.z - cz), o);
-    double4 a = g.acc[i];
-    a.x += (double)o[1];
-    a.y += (double)o[2];
-    a.z += (double)o[3];
-    a.w += (double)o[0];
-    g.acc[i] = a;
-  }
+__global__ __launch_bounds__(256) void l2p_part_kernel(int64_t n, const int* __restrict__ leaf_of,
+                                                       const swh_multipole* __restrict__ mp,
+                                                       const double* __restrict__ F, GSoA g) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !g.active[i]) return;
+  const int c = leaf_of[i];
+  if (c < 0) return;
+  const double* Fc = F + (size_t)c * SWH_MPOLE_TERMS;
+  const double4 p = g.pos[i];
+  T o[4];
+  l2p<T>(Fc, (T)(p.x - mp[c].CoM[0]), (T)(p.y - mp[c].CoM[1]), (T)(p.z - mp[c].CoM[2]), o);
+  double4 a = g.acc[i];
+  a.x += (double)o[1];
+  a.y += (double)o[2];
+  a.z += (double)o[3];
+  a.w += (double)o[0];
+  g.acc[i] = a;
 }
 
 // The recursive walk (host).
@@ -1038,151 +1218,310 @@ struct TreeWalk {
 // the lists do not depend on the threads' order.
 enum { GW_SELF = 0, GW_PAIR = 1, GW_NOCACHE = 2 };
 
-struct GWalkOut {
-  int4* next;
-  unsigned int* ctr;  // [0] next frontier, [1] P-P entries, [2] M-M entries, [3] skipped
-  unsigned long long* pp_key;
-  int* pp_val;  // truncated | allow_mpole << 1
-  int* pp_cnt;
-  unsigned long long* mm_key;
-  int* mm_val;  // symmetric
-  int* mm_cnt;
+// Per-wave output counts of one level (written by the count pass, scanned
+// over the waves, read back by the write pass: no global atomics -- thousands
+// of waves adding into one counter serialise on its L2 channel).
+struct GWCnt {
+  unsigned int next, pp, mm, skip, self, pad[3];
+};
+struct GWCntSum {
+  __host__ __device__ GWCnt operator()(const GWCnt& a, const GWCnt& b) const {
+    GWCnt c;
+    c.next = a.next + b.next;
+    c.pp = a.pp + b.pp;
+    c.mm = a.mm + b.mm;
+    c.skip = a.skip + b.skip;
+    c.self = a.self + b.self;
+    c.pad[0] = c.pad[1] = c.pad[2] = 0u;
+    return c;
+  }
 };
 
-__device__ __forceinline__ void gw_pp(const GWalkOut& o, int ci, int cj, int trunc, int mpole) {
-  const unsigned int p = atomicAdd(&o.ctr[1], 1u);
-  o.pp_key[p] = ((unsigned long long)(unsigned int)ci << 32) | (unsigned int)cj;
-  o.pp_val[p] = trunc | (mpole << 1);
-  atomicAdd(&o.pp_cnt[ci], 1);
-}
-__device__ __forceinline__ void gw_mm(const GWalkOut& o, int t, int src, int sym) {
-  const unsigned int p = atomicAdd(&o.ctr[2], 1u);
-  o.mm_key[p] = ((unsigned long long)(unsigned int)t << 32) | (unsigned int)src;
-  o.mm_val[p] = sym;
-  atomicAdd(&o.mm_cnt[t], 1);
+struct GWalkOut {
+  int4* next;
+  GWCnt* wcnt;         // count pass: this level's per-wave counts
+  const GWCnt* wbase;  // write pass: their exclusive scan plus the running totals
+  unsigned long long* pp_key;
+  int* pp_val;  // truncated | allow_mpole << 1
+  unsigned long long* mm_key;
+  int* mm_val;  // symmetric
+  int bits;     // key = cell << bits | other cell
+};
+
+// The walk's view of a cell, one 64-byte line (a task reads two of them, not
+// the 200-byte multipoles and 96-byte cells): the CoM and r_max in double,
+// the acceptance test's float fields, the gpart count and split / active.
+struct __align__(64) GWRec {
+  double com[3];
+  double r_max;
+  float max_soft, min_a, power[3];
+  int count;
+  int flags;  // 1: split, 2: active
+  int pad;
+};
+static_assert(sizeof(GWRec) == 64, "one cache line per cell");
+
+__global__ void gw_rec_kernel(const swh_gcell* __restrict__ cells,
+                              const swh_multipole* __restrict__ mp,
+                              const int8_t* __restrict__ act, int n, GWRec* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  GWRec r;
+  for (int k = 0; k < 3; k++) r.com[k] = mp[c].CoM[k];
+  r.r_max = mp[c].r_max;
+  r.max_soft = mp[c].max_softening;
+  r.min_a = mp[c].min_old_a_grav_norm;
+  for (int k = 0; k < 3; k++) r.power[k] = mp[c].power[k];
+  r.count = cells[c].count;
+  r.flags = (cells[c].split ? 1 : 0) | (act[c] ? 2 : 0);
+  r.pad = 0;
+  out[c] = r;
 }
 
-__global__ void gwalk_kernel(const int4* __restrict__ cur, int n, const swh_gcell* __restrict__ cells,
-                             const swh_multipole* __restrict__ mp, const int8_t* __restrict__ act,
-                             MacParams mac, int periodic, double dimx, double dimy, double dimz,
-                             double r_cut_min, double r_cut_max, GWalkOut o) {
+// m2l_side of a record (M_000 = power[0], gravity_multipole_compute_power)
+__device__ __forceinline__ M2LSide rec_side(const GWRec& r) {
+  M2LSide s;
+  s.rho = (float)r.r_max;
+  s.max_soft = r.max_soft;
+  s.min_a = r.min_a;
+  s.M000 = r.power[0];
+  for (int k = 0; k < 3; k++) s.power[k] = r.power[k];
+  return s;
+}
+
+// What one frontier task does (decided first, written after the wave has
+// reserved its slots with one atomic per counter).
+enum {
+  GA_NONE = 0, GA_SELF_SPLIT, GA_SELF_LEAF, GA_NC_SPLIT, GA_NC_LEAF, GA_SKIP, GA_PAIR_NC,
+  GA_MM, GA_PP, GA_SPLIT
+};
+
+// Exclusive prefix over the wave of four packed 16-bit counts; *tot gets the
+// wave's totals (every lane).
+__device__ __forceinline__ unsigned long long wave_excl_scan16x4(unsigned long long v,
+                                                                 unsigned long long* tot) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long s = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long u = __shfl_up(s, o);
+    if (lane >= o) s += u;
+  }
+  *tot = __shfl(s, 63);
+  return s - v;
+}
+
+template <bool WRITE>
+__global__ __launch_bounds__(256) void gwalk_kernel(
+    const int4* __restrict__ cur, int n, const swh_gcell* __restrict__ cells,
+    const GWRec* __restrict__ rec, MacParams mac, int periodic,
+    double dimx, double dimy, double dimz, double r_cut_min, double r_cut_max, GWalkOut o) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const int4 it = cur[k];
-  if (it.z == GW_SELF) {  // runner_doself_recursive_grav (2386-2431)
-    const int c = it.x;
-    if (!act[c]) return;
-    const swh_gcell C = cells[c];
-    if (C.split) {
+  const int lane = threadIdx.x & 63;
+  if (__ballot(k < n) == 0ull) return;  // wave-uniform
+  int ga = GA_NONE, ci = -1, cj = -1, nn = 0, npp = 0, nmm = 0, ns = 0;
+  int trunc = 0, di = 0, dj = 0, split_i = 0;
+  if (k < n) {
+    const int4 it = cur[k];
+    ci = it.x;
+    cj = it.y;
+    if (it.z == GW_SELF) {  // runner_doself_recursive_grav (2386-2431)
+      const GWRec C = rec[ci];
+      if (C.flags & 2) {
+        if (C.flags & 1) {
+          int m = 0;
+          for (int j = 0; j < 8; j++) m += cells[ci].progeny[j] >= 0 ? 1 : 0;
+          ga = GA_SELF_SPLIT;
+          nn = m + m * (m - 1) / 2;
+          ns = m;
+        } else {
+          ga = GA_SELF_LEAF;
+          trunc = periodic && (2. * C.r_max > r_cut_min);
+          npp = 1;
+        }
+      }
+    } else if (it.z == GW_NOCACHE) {  // runner_dopair_grav_pp_no_cache (1440-1483)
+      const GWRec Ci = rec[ci];
+      if ((Ci.flags & 2) && Ci.count > 0 && rec[cj].count > 0) {
+        if (Ci.flags & 1) {
+          for (int j = 0; j < 8; j++) nn += cells[ci].progeny[j] >= 0 ? 1 : 0;
+          ga = GA_NC_SPLIT;
+        } else {
+          ga = GA_NC_LEAF;
+          trunc = periodic ? 1 : 0;
+          npp = 1;
+        }
+      }
+    } else {  // runner_dopair_recursive_grav (2208-2374)
+      const GWRec A = rec[ci];
+      const GWRec B = rec[cj];
+      di = (A.flags >> 1) & 1;
+      dj = (B.flags >> 1) & 1;
+      if (di || dj) {
+        double dx = A.com[0] - B.com[0], dy = A.com[1] - B.com[1], dz = A.com[2] - B.com[2];
+        if (periodic) {
+          dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
+          dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
+          dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
+        }
+        const double r2 = dx * dx + dy * dy + dz * dz;
+        const double r_lr_check = sqrt(r2) - (A.r_max + B.r_max);
+        const bool si = A.flags & 1, sj = B.flags & 1;
+        if (periodic && r_lr_check > r_cut_max) {
+          ga = GA_SKIP;
+        } else if (A.count <= 1 || B.count <= 1) {
+          ga = GA_PAIR_NC;
+          nn = 2;
+        } else if (m2l_accept(mac, rec_side(A), rec_side(B), (float)r2) &&
+                   m2l_accept(mac, rec_side(B), rec_side(A), (float)r2)) {
+          // runner_dopair_grav_mm (2050-2064): symmetric when both are active
+          ga = GA_MM;
+          nmm = di + dj;
+        } else if (!si && !sj) {
+          // runner_dopair_grav_pp(ci, cj, 1, 1): truncated iff periodic &&
+          // |CoM_i - CoM_j| + r_max_i + r_max_j > r_cut_min (float separations)
+          if (periodic) {
+            const float L[3] = {(float)dimx, (float)dimy, (float)dimz};
+            double d2 = 0.;
+            for (int q = 0; q < 3; q++) {
+              float dxf = (float)B.com[q] - (float)A.com[q];
+              dxf = dxf > 0.5f * L[q] ? dxf - L[q] : (dxf < -0.5f * L[q] ? dxf + L[q] : dxf);
+              d2 += (double)dxf * (double)dxf;
+            }
+            trunc = (sqrt(d2) + (double)(float)A.r_max + (double)(float)B.r_max) > r_cut_min;
+          }
+          ga = GA_PP;
+          npp = di + dj;
+        } else {
+          // split the larger cell (or the only split one)
+          split_i = A.r_max > B.r_max ? si : !sj;
+          const swh_gcell& S = split_i ? cells[ci] : cells[cj];
+          for (int j = 0; j < 8; j++) nn += S.progeny[j] >= 0 ? 1 : 0;
+          ga = GA_SPLIT;
+        }
+      }
+    }
+  }
+  const unsigned long long mine = (unsigned long long)nn | ((unsigned long long)npp << 16) |
+                                  ((unsigned long long)nmm << 32);
+  unsigned long long tot;
+  const unsigned long long ex = wave_excl_scan16x4(mine, &tot);
+  const int wave = k >> 6;
+  if (!WRITE) {
+    int sk = ga == GA_SKIP ? 1 : 0, nself = ns;
+    for (int d = 32; d > 0; d >>= 1) {
+      sk += __shfl_xor(sk, d);
+      nself += __shfl_xor(nself, d);
+    }
+    if (lane == 0) {
+      GWCnt c;
+      c.next = (unsigned int)(tot & 0xffffull);
+      c.pp = (unsigned int)((tot >> 16) & 0xffffull);
+      c.mm = (unsigned int)((tot >> 32) & 0xffffull);
+      c.skip = (unsigned int)sk;
+      c.self = (unsigned int)nself;
+      c.pad[0] = c.pad[1] = c.pad[2] = 0u;
+      o.wcnt[wave] = c;
+    }
+    return;
+  }
+  const GWCnt wb = o.wbase[wave];
+  unsigned int q = wb.next + (unsigned int)(ex & 0xffffull);
+  unsigned int p = wb.pp + (unsigned int)((ex >> 16) & 0xffffull);
+  unsigned int w = wb.mm + (unsigned int)((ex >> 32) & 0xffffull);
+  const int bits = o.bits;
+  auto pp = [&](int a, int b, int tr, int mpole) {
+    o.pp_key[p] = ((unsigned long long)(unsigned int)a << bits) | (unsigned int)b;
+    o.pp_val[p] = tr | (mpole << 1);
+    p++;
+  };
+  auto mm = [&](int t, int s, int sym) {
+    o.mm_key[w] = ((unsigned long long)(unsigned int)t << bits) | (unsigned int)s;
+    o.mm_val[w] = sym;
+    w++;
+  };
+  switch (ga) {
+    case GA_SELF_SPLIT: {
+      const swh_gcell& C = cells[ci];
       int ch[8], m = 0;
       for (int j = 0; j < 8; j++)
         if (C.progeny[j] >= 0) ch[m++] = C.progeny[j];
-      unsigned int q = atomicAdd(&o.ctr[0], (unsigned int)(m + m * (m - 1) / 2));
       for (int j = 0; j < m; j++) {
         o.next[q++] = make_int4(ch[j], -1, GW_SELF, 0);
         for (int l = j + 1; l < m; l++) o.next[q++] = make_int4(ch[j], ch[l], GW_PAIR, 0);
       }
-    } else {
-      gw_pp(o, c, c, periodic && (2. * mp[c].r_max > r_cut_min), 0);
+      break;
     }
-    return;
-  }
-  if (it.z == GW_NOCACHE) {  // runner_dopair_grav_pp_no_cache (1440-1483)
-    const int ci = it.x, cj = it.y;
-    if (!act[ci]) return;
-    const swh_gcell Ci = cells[ci];
-    if (Ci.count == 0 || cells[cj].count == 0) return;
-    if (Ci.split) {
-      int m = 0;
-      for (int j = 0; j < 8; j++) m += Ci.progeny[j] >= 0 ? 1 : 0;
-      unsigned int q = atomicAdd(&o.ctr[0], (unsigned int)m);
+    case GA_SELF_LEAF: pp(ci, ci, trunc, 0); break;
+    case GA_NC_SPLIT: {
+      const swh_gcell& Ci = cells[ci];
       for (int j = 0; j < 8; j++)
         if (Ci.progeny[j] >= 0) o.next[q++] = make_int4(Ci.progeny[j], cj, GW_NOCACHE, 0);
-    } else {
-      gw_pp(o, ci, cj, periodic ? 1 : 0, 0);
+      break;
     }
-    return;
-  }
-  // runner_dopair_recursive_grav (2208-2374)
-  const int ci = it.x, cj = it.y;
-  if (!(act[ci] || act[cj])) return;
-  const swh_multipole& A = mp[ci];
-  const swh_multipole& B = mp[cj];
-  double dx = A.CoM[0] - B.CoM[0], dy = A.CoM[1] - B.CoM[1], dz = A.CoM[2] - B.CoM[2];
-  if (periodic) {
-    dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
-    dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
-    dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
-  }
-  const double r2 = dx * dx + dy * dy + dz * dz;
-  const double r_lr_check = sqrt(r2) - (A.r_max + B.r_max);
-  if (periodic && r_lr_check > r_cut_max) {
-    atomicAdd(&o.ctr[3], 1u);
-    return;
-  }
-  const swh_gcell Ci = cells[ci], Cj = cells[cj];
-  if (Ci.count <= 1 || Cj.count <= 1) {
-    unsigned int q = atomicAdd(&o.ctr[0], 2u);
-    o.next[q] = make_int4(ci, cj, GW_NOCACHE, 0);
-    o.next[q + 1] = make_int4(cj, ci, GW_NOCACHE, 0);
-  } else if (m2l_accept(mac, m2l_side(A), m2l_side(B), (float)r2) &&
-             m2l_accept(mac, m2l_side(B), m2l_side(A), (float)r2)) {
-    // runner_dopair_grav_mm (2050-2064): symmetric when both are active
-    const bool di = act[ci], dj = act[cj];
-    if (di && dj) {
-      gw_mm(o, ci, cj, 1);
-      gw_mm(o, cj, ci, 1);
-    } else if (di) {
-      gw_mm(o, ci, cj, 0);
-    } else if (dj) {
-      gw_mm(o, cj, ci, 0);
-    }
-  } else if (!Ci.split && !Cj.split) {
-    // runner_dopair_grav_pp(ci, cj, 1, 1): truncated iff periodic &&
-    // |CoM_i - CoM_j| + r_max_i + r_max_j > r_cut_min (float separations)
-    int trunc = 0;
-    if (periodic) {
-      const float L[3] = {(float)dimx, (float)dimy, (float)dimz};
-      double d2 = 0.;
-      for (int q = 0; q < 3; q++) {
-        float dxf = (float)B.CoM[q] - (float)A.CoM[q];
-        dxf = dxf > 0.5f * L[q] ? dxf - L[q] : (dxf < -0.5f * L[q] ? dxf + L[q] : dxf);
-        d2 += (double)dxf * (double)dxf;
+    case GA_NC_LEAF: pp(ci, cj, trunc, 0); break;
+    case GA_PAIR_NC:
+      o.next[q] = make_int4(ci, cj, GW_NOCACHE, 0);
+      o.next[q + 1] = make_int4(cj, ci, GW_NOCACHE, 0);
+      break;
+    case GA_MM:
+      if (di && dj) {
+        mm(ci, cj, 1);
+        mm(cj, ci, 1);
+      } else if (di) {
+        mm(ci, cj, 0);
+      } else if (dj) {
+        mm(cj, ci, 0);
       }
-      trunc = (sqrt(d2) + (double)(float)A.r_max + (double)(float)B.r_max) > r_cut_min;
+      break;
+    case GA_PP:
+      if (di) pp(ci, cj, trunc, 1);
+      if (dj) pp(cj, ci, trunc, 1);
+      break;
+    case GA_SPLIT: {
+      const swh_gcell& S = split_i ? cells[ci] : cells[cj];
+      for (int j = 0; j < 8; j++) {
+        if (S.progeny[j] < 0) continue;
+        o.next[q++] = split_i ? make_int4(S.progeny[j], cj, GW_PAIR, 0)
+                              : make_int4(ci, S.progeny[j], GW_PAIR, 0);
+      }
+      break;
     }
-    if (act[ci]) gw_pp(o, ci, cj, trunc, 1);
-    if (act[cj]) gw_pp(o, cj, ci, trunc, 1);
-  } else {
-    // split the larger cell (or the only split one)
-    const bool split_i = A.r_max > B.r_max ? Ci.split : !Cj.split;
-    const swh_gcell& S = split_i ? Ci : Cj;
-    int m = 0;
-    for (int j = 0; j < 8; j++) m += S.progeny[j] >= 0 ? 1 : 0;
-    unsigned int q = atomicAdd(&o.ctr[0], (unsigned int)m);
-    for (int j = 0; j < 8; j++) {
-      if (S.progeny[j] < 0) continue;
-      o.next[q++] = split_i ? make_int4(S.progeny[j], cj, GW_PAIR, 0)
-                            : make_int4(ci, S.progeny[j], GW_PAIR, 0);
-    }
+    default: break;
   }
 }
 
+// CSR offsets from keys sorted by (cell << bits | other): off[c] = the first
+// entry of cell c (lower bound), c = 0..ncells.
+__global__ void gw_csr_kernel(const unsigned long long* __restrict__ key, int n, int bits,
+                              int ncells, int* __restrict__ off) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > ncells) return;
+  const unsigned long long v = (unsigned long long)(unsigned int)c << bits;
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (key[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  off[c] = lo;
+}
+
 __global__ void gw_unpack_pp(const unsigned long long* __restrict__ key, const int* __restrict__ val,
-                             int n, swh_leaf_pair* __restrict__ out) {
+                             int n, unsigned long long mask, swh_leaf_pair* __restrict__ out) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   swh_leaf_pair e;
-  e.j = (int)(unsigned int)(key[k] & 0xffffffffull);
+  e.j = (int)(key[k] & mask);
   e.truncated = val[k] & 1;
   e.allow_mpole = (val[k] >> 1) & 1;
   out[k] = e;
 }
 __global__ void gw_unpack_mm(const unsigned long long* __restrict__ key, const int* __restrict__ val,
-                             int n, int2* __restrict__ out) {
+                             int n, unsigned long long mask, int2* __restrict__ out) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
-  out[k] = make_int2((int)(unsigned int)(key[k] & 0xffffffffull), val[k]);
+  out[k] = make_int2((int)(key[k] & mask), val[k]);
 }
 
 // Grow a device buffer keeping its first `used` bytes.
@@ -1200,13 +1539,46 @@ static swh_status grow_keep(DevBuf& b, size_t need, size_t used, hipStream_t st)
   return SWH_OK;
 }
 
+static bool walk_debug() {
+  static const bool on = std::getenv("SWH_WALK_DEBUG") != nullptr;
+  return on;
+}
+
+// Sort one entry list by key (only the bits keys use) and build its CSR.
+static swh_status gw_sort_csr(swh_gspace* g, DevBuf& key, DevBuf& val, DevBuf& key2, DevBuf& val2,
+                              int n, int bits, int ncells, DevBuf& off, hipStream_t st) {
+  SWH_TRY(off.reserve(((size_t)ncells + 1) * sizeof(int32_t)));
+  if (n > 0) {
+    SWH_TRY(key2.reserve((size_t)n * 8));
+    SWH_TRY(val2.reserve((size_t)n * 4));
+    size_t tb = 0;
+    SWH_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.as<unsigned long long>(),
+                                               key2.as<unsigned long long>(), val.as<int>(),
+                                               val2.as<int>(), n, 0, 2 * bits, st));
+    SWH_TRY(g->wsort_tmp.reserve(tb));
+    tb = g->wsort_tmp.bytes;
+    SWH_HIP(hipcub::DeviceRadixSort::SortPairs(g->wsort_tmp.ptr, tb, key.as<unsigned long long>(),
+                                               key2.as<unsigned long long>(), val.as<int>(),
+                                               val2.as<int>(), n, 0, 2 * bits, st));
+  }
+  hipLaunchKernelGGL(gw_csr_kernel, dim3((ncells + 1 + 255) / 256), dim3(256), 0, st,
+                     key2.as<const unsigned long long>(), n, bits, ncells, off.as<int>());
+  SWH_HIP(hipGetLastError());
+  return SWH_OK;
+}
+
 // The walk on the device; fills g->pair_off / g->pairs (P-P CSR over i-cells)
-// and g->m2l_off / g->m2l_src (M-M CSR over targets).
+// and g->m2l_off / g->m2l_src (M-M CSR over targets). Each level reserves the
+// next frontier by task type: a split self task fans out to at most 8 + 28
+// tasks, a pair or no-cache task to at most 8.
 static swh_status device_walk(swh_gspace* g, const swh_grav_params* G, const int32_t* self_cells,
                               int32_t nself, const int32_t* pair_cells, int32_t npair,
                               int64_t* n_pp, int64_t* n_mm, int64_t* n_skip) {
   hipStream_t st = g->stream;
   const int ncells = (int)g->tree.size();
+  int bits = 1;
+  while ((1ll << bits) < (long long)ncells) bits++;  // <= 31: keys of 2 * bits <= 62 bits
+  const unsigned long long mask = (1ull << bits) - 1ull;
   const int64_t ntask = (int64_t)nself + npair;
   std::vector<int4> init((size_t)std::max<int64_t>(1, ntask));
   for (int k = 0; k < nself; k++) init[k] = make_int4(self_cells[k], -1, GW_SELF, 0);
@@ -1216,87 +1588,84 @@ static swh_status device_walk(swh_gspace* g, const swh_grav_params* G, const int
   if (ntask > 0)
     SWH_HIP(hipMemcpyAsync(g->wf0.ptr, init.data(), (size_t)ntask * sizeof(int4),
                            hipMemcpyHostToDevice, st));
-  SWH_TRY(g->wctr.reserve(4 * sizeof(unsigned int)));
-  SWH_TRY(g->pp_cnt.reserve(((size_t)ncells + 1) * sizeof(int)));
-  SWH_TRY(g->mm_cnt.reserve(((size_t)ncells + 1) * sizeof(int)));
-  SWH_HIP(hipMemsetAsync(g->wctr.ptr, 0, 4 * sizeof(unsigned int), st));
-  SWH_HIP(hipMemsetAsync(g->pp_cnt.ptr, 0, ((size_t)ncells + 1) * sizeof(int), st));
-  SWH_HIP(hipMemsetAsync(g->mm_cnt.ptr, 0, ((size_t)ncells + 1) * sizeof(int), st));
-  unsigned int* ctr = g->wctr.as<unsigned int>();
   const MacParams mac = mac_params(G);
-  int64_t n_cur = ntask;
-  unsigned int h[4] = {0, 0, 0, 0};
+  SWH_TRY(g->wrec.reserve((size_t)std::max(1, ncells) * sizeof(GWRec)));
+  hipLaunchKernelGGL(gw_rec_kernel, dim3((ncells + 255) / 256), dim3(256), 0, st,
+                     g->tree_d.as<const swh_gcell>(), g->mpoles.as<const swh_multipole>(),
+                     g->cell_act.as<const int8_t>(), ncells, g->wrec.as<GWRec>());
+  SWH_HIP(hipGetLastError());
+  int64_t n_cur = ntask, n_self_cur = nself;
+  GWCnt h{};  // running totals: P-P and M-M entries, skipped pairs
   DevBuf* cur = &g->wf0;
   DevBuf* nxt = &g->wf1;
   while (n_cur > 0) {
-    // room for the widest fan-out (a split self task: 8 + 28 sub-tasks) and
-    // two entries per task
-    SWH_TRY(nxt->reserve((size_t)n_cur * 36 * sizeof(int4)));
-    const size_t pp_need = (size_t)h[1] + 2 * (size_t)n_cur, mm_need = (size_t)h[2] + 2 * (size_t)n_cur;
-    SWH_TRY(grow_keep(g->pp_key, pp_need * 8, (size_t)h[1] * 8, st));
-    SWH_TRY(grow_keep(g->pp_val, pp_need * 4, (size_t)h[1] * 4, st));
-    SWH_TRY(grow_keep(g->mm_key, mm_need * 8, (size_t)h[2] * 8, st));
-    SWH_TRY(grow_keep(g->mm_val, mm_need * 4, (size_t)h[2] * 4, st));
-    SWH_HIP(hipMemsetAsync(ctr, 0, sizeof(unsigned int), st));
-    GWalkOut o{nxt->as<int4>(), ctr, g->pp_key.as<unsigned long long>(), g->pp_val.as<int>(),
-               g->pp_cnt.as<int>(), g->mm_key.as<unsigned long long>(), g->mm_val.as<int>(),
-               g->mm_cnt.as<int>()};
-    hipLaunchKernelGGL(gwalk_kernel, dim3((unsigned)((n_cur + 255) / 256)), dim3(256), 0, st,
-                       cur->as<const int4>(), (int)n_cur, g->tree_d.as<const swh_gcell>(),
-                       g->mpoles.as<const swh_multipole>(), g->cell_act.as<const int8_t>(), mac,
+    const size_t bound = (size_t)n_self_cur * 36 + (size_t)(n_cur - n_self_cur) * 8;
+    SWH_TRY(nxt->reserve(std::max<size_t>(1, bound) * sizeof(int4)));
+    const size_t pp_need = (size_t)h.pp + 2 * (size_t)n_cur, mm_need = (size_t)h.mm + 2 * (size_t)n_cur;
+    SWH_TRY(grow_keep(g->pp_key, pp_need * 8, (size_t)h.pp * 8, st));
+    SWH_TRY(grow_keep(g->pp_val, pp_need * 4, (size_t)h.pp * 4, st));
+    SWH_TRY(grow_keep(g->mm_key, mm_need * 8, (size_t)h.mm * 8, st));
+    SWH_TRY(grow_keep(g->mm_val, mm_need * 4, (size_t)h.mm * 4, st));
+    // count pass -> per-wave counts; their exclusive scan from the running
+    // totals (slot nw holds the new totals) -> write pass
+    const int nw = (int)((n_cur + 63) / 64);
+    SWH_TRY(g->wcnt.reserve(((size_t)nw + 1) * sizeof(GWCnt)));
+    SWH_TRY(g->wbase.reserve(((size_t)nw + 1) * sizeof(GWCnt)));
+    GWCnt* wcnt = g->wcnt.as<GWCnt>();
+    GWalkOut o{nxt->as<int4>(), wcnt, g->wbase.as<const GWCnt>(),
+               g->pp_key.as<unsigned long long>(), g->pp_val.as<int>(),
+               g->mm_key.as<unsigned long long>(), g->mm_val.as<int>(), bits};
+    const dim3 grid((unsigned)((n_cur + 255) / 256));
+    hipLaunchKernelGGL(gwalk_kernel<false>, grid, dim3(256), 0, st, cur->as<const int4>(),
+                       (int)n_cur, g->tree_d.as<const swh_gcell>(), g->wrec.as<const GWRec>(), mac,
                        G->periodic, (double)G->dim[0], (double)G->dim[1], (double)G->dim[2],
                        G->r_cut_min, G->r_cut_max, o);
     SWH_HIP(hipGetLastError());
-    SWH_HIP(hipMemcpyAsync(h, ctr, sizeof(h), hipMemcpyDeviceToHost, st));
+    GWCnt init = h;
+    init.next = 0u;
+    init.self = 0u;
+    SWH_HIP(hipMemsetAsync(wcnt + nw, 0, sizeof(GWCnt), st));
+    size_t tb = 0;
+    SWH_HIP(hipcub::DeviceScan::ExclusiveScan(nullptr, tb, wcnt, g->wbase.as<GWCnt>(), GWCntSum(),
+                                              init, nw + 1, st));
+    SWH_TRY(g->wsort_tmp.reserve(tb));
+    tb = g->wsort_tmp.bytes;
+    SWH_HIP(hipcub::DeviceScan::ExclusiveScan(g->wsort_tmp.ptr, tb, wcnt, g->wbase.as<GWCnt>(),
+                                              GWCntSum(), init, nw + 1, st));
+    hipLaunchKernelGGL(gwalk_kernel<true>, grid, dim3(256), 0, st, cur->as<const int4>(),
+                       (int)n_cur, g->tree_d.as<const swh_gcell>(), g->wrec.as<const GWRec>(), mac,
+                       G->periodic, (double)G->dim[0], (double)G->dim[1], (double)G->dim[2],
+                       G->r_cut_min, G->r_cut_max, o);
+    SWH_HIP(hipGetLastError());
+    SWH_HIP(hipMemcpyAsync(&h, g->wbase.as<GWCnt>() + nw, sizeof(GWCnt), hipMemcpyDeviceToHost, st));
     SWH_HIP(hipStreamSynchronize(st));
-    n_cur = h[0];
+    if (walk_debug())
+      std::fprintf(stderr, "[swh walk] frontier %lld -> %u (self %u), pp %u, mm %u, skipped %u\n",
+                   (long long)n_cur, h.next, h.self, h.pp, h.mm, h.skip);
+    n_cur = h.next;
+    n_self_cur = h.self;
     std::swap(cur, nxt);
   }
-  const int npp = (int)h[1], nmm = (int)h[2];
+  const int npp = (int)h.pp, nmm = (int)h.mm;
   *n_pp = npp;
   *n_mm = nmm;
-  *n_skip = h[3];
-  // CSR offsets: exclusive scans of the per-cell counts
-  SWH_TRY(g->pair_off.reserve(((size_t)ncells + 1) * sizeof(int32_t)));
-  SWH_TRY(g->m2l_off.reserve(((size_t)ncells + 1) * sizeof(int32_t)));
-  size_t tb = 0, tb2 = 0;
-  SWH_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, g->pp_cnt.as<int>(),
-                                           g->pair_off.as<int>(), ncells + 1, st));
-  SWH_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, g->pp_key.as<unsigned long long>(),
-                                             g->pp_key2.as<unsigned long long>(),
-                                             g->pp_val.as<int>(), g->pp_val2.as<int>(),
-                                             std::max(npp, nmm), 0, 64, st));
-  SWH_TRY(g->wsort_tmp.reserve(std::max(tb, tb2)));
-  SWH_HIP(hipcub::DeviceScan::ExclusiveSum(g->wsort_tmp.ptr, tb, g->pp_cnt.as<int>(),
-                                           g->pair_off.as<int>(), ncells + 1, st));
-  SWH_HIP(hipcub::DeviceScan::ExclusiveSum(g->wsort_tmp.ptr, tb, g->mm_cnt.as<int>(),
-                                           g->m2l_off.as<int>(), ncells + 1, st));
+  *n_skip = h.skip;
+  SWH_TRY(gw_sort_csr(g, g->pp_key, g->pp_val, g->pp_key2, g->pp_val2, npp, bits, ncells,
+                      g->pair_off, st));
+  SWH_TRY(gw_sort_csr(g, g->mm_key, g->mm_val, g->mm_key2, g->mm_val2, nmm, bits, ncells,
+                      g->m2l_off, st));
   SWH_TRY(g->pairs.reserve((size_t)std::max(1, npp) * sizeof(swh_leaf_pair)));
   SWH_TRY(g->m2l_src.reserve((size_t)std::max(1, nmm) * sizeof(int2)));
   if (npp > 0) {
-    SWH_TRY(g->pp_key2.reserve((size_t)npp * 8));
-    SWH_TRY(g->pp_val2.reserve((size_t)npp * 4));
-    size_t t = g->wsort_tmp.bytes;
-    SWH_HIP(hipcub::DeviceRadixSort::SortPairs(g->wsort_tmp.ptr, t, g->pp_key.as<unsigned long long>(),
-                                               g->pp_key2.as<unsigned long long>(),
-                                               g->pp_val.as<int>(), g->pp_val2.as<int>(), npp, 0, 64,
-                                               st));
     hipLaunchKernelGGL(gw_unpack_pp, dim3((npp + 255) / 256), dim3(256), 0, st,
                        g->pp_key2.as<const unsigned long long>(), g->pp_val2.as<const int>(), npp,
-                       g->pairs.as<swh_leaf_pair>());
+                       mask, g->pairs.as<swh_leaf_pair>());
     SWH_HIP(hipGetLastError());
   }
   if (nmm > 0) {
-    SWH_TRY(g->mm_key2.reserve((size_t)nmm * 8));
-    SWH_TRY(g->mm_val2.reserve((size_t)nmm * 4));
-    size_t t = g->wsort_tmp.bytes;
-    SWH_HIP(hipcub::DeviceRadixSort::SortPairs(g->wsort_tmp.ptr, t, g->mm_key.as<unsigned long long>(),
-                                               g->mm_key2.as<unsigned long long>(),
-                                               g->mm_val.as<int>(), g->mm_val2.as<int>(), nmm, 0, 64,
-                                               st));
     hipLaunchKernelGGL(gw_unpack_mm, dim3((nmm + 255) / 256), dim3(256), 0, st,
                        g->mm_key2.as<const unsigned long long>(), g->mm_val2.as<const int>(), nmm,
-                       g->m2l_src.as<int2>());
+                       mask, g->m2l_src.as<int2>());
     SWH_HIP(hipGetLastError());
   }
   g->npairs = npp;
@@ -1366,10 +1735,22 @@ swh_status swh_gspace_set_tree(swh_gspace* g, const swh_gcell* cells, int32_t nc
       if (depth[c] == d) l2l.push_back(make_int2(c, parent[c]));
     doff.push_back((int32_t)l2l.size());
   }
+  // the upward pass: split cells, deepest first (M2M reads finished progeny)
+  std::vector<int> m2m;
+  std::vector<int32_t> moff(1, 0);
+  for (int d = maxd; d >= 0; d--) {
+    for (int c = 0; c < ncells; c++)
+      if (depth[c] == d && cells[c].split) m2m.push_back(c);
+    moff.push_back((int32_t)m2m.size());
+  }
   std::vector<int> leaves;
   std::vector<swh_leaf> ranges(ncells);
+  std::vector<int> leaf_of((size_t)g->n, -1);  // gpart -> its leaf cell (L2P)
   for (int c = 0; c < ncells; c++) {
-    if (!cells[c].split) leaves.push_back(c);
+    if (!cells[c].split) {
+      leaves.push_back(c);
+      for (int k = cells[c].start; k < cells[c].start + cells[c].count; k++) leaf_of[k] = c;
+    }
     ranges[c] = swh_leaf{cells[c].start, cells[c].count};
   }
   // the cell table doubles as the P2P kernels' leaf table (pairs set later)
@@ -1381,6 +1762,14 @@ swh_status swh_gspace_set_tree(swh_gspace* g, const swh_gcell* cells, int32_t nc
   SWH_TRY(g->ftens.reserve((size_t)std::max(1, ncells) * SWH_MPOLE_TERMS * sizeof(double)));
   SWH_TRY(g->l2l_list.reserve(std::max<size_t>(1, l2l.size()) * sizeof(int2)));
   SWH_TRY(g->leaf_ids.reserve(std::max<size_t>(1, leaves.size()) * sizeof(int)));
+  SWH_TRY(g->leaf_of.reserve(std::max<size_t>(1, leaf_of.size()) * sizeof(int)));
+  SWH_TRY(g->m2m_list.reserve(std::max<size_t>(1, m2m.size()) * sizeof(int)));
+  if (!m2m.empty())
+    SWH_HIP(hipMemcpyAsync(g->m2m_list.ptr, m2m.data(), m2m.size() * sizeof(int),
+                           hipMemcpyHostToDevice, g->stream));
+  if (!leaf_of.empty())
+    SWH_HIP(hipMemcpyAsync(g->leaf_of.ptr, leaf_of.data(), leaf_of.size() * sizeof(int),
+                           hipMemcpyHostToDevice, g->stream));
   if (!l2l.empty())
     SWH_HIP(hipMemcpyAsync(g->l2l_list.ptr, l2l.data(), l2l.size() * sizeof(int2),
                            hipMemcpyHostToDevice, g->stream));
@@ -1389,6 +1778,7 @@ swh_status swh_gspace_set_tree(swh_gspace* g, const swh_gcell* cells, int32_t nc
                            hipMemcpyHostToDevice, g->stream));
   SWH_HIP(hipStreamSynchronize(g->stream));
   g->l2l_depth_off = doff;
+  g->m2m_depth_off = moff;
   g->nleaf_cells = (int32_t)leaves.size();
   int32_t ml = 0;
   for (int c : leaves) ml = std::max(ml, cells[c].count);
@@ -1425,8 +1815,26 @@ swh_status swh_grav_tree(swh_gspace* g, const swh_grav_params* G, const int32_t*
                      g->stream, g->layout, g->aos.as<const char>(), g->n, gsoa_of(g),
                      G->max_active_bin);
   SWH_HIP(hipGetLastError());
-  // multipoles (P2M per cell) and cell activity, to the host for the walk
-  SWH_TRY(swh_gspace_make_multipoles(g, nullptr));
+  // multipoles: P2M at the leaves, M2M up the tree (space_split.c:340-440)
+  hipEvent_t ev[6] = {};
+  if (stats) {
+    for (auto& e : ev) SWH_HIP(hipEventCreate(&e));
+    SWH_HIP(hipEventRecord(ev[0], g->stream));
+  }
+  SWH_TRY(g->mpoles.reserve((size_t)ncells * sizeof(swh_multipole)));
+  if (g->nleaf_cells > 0)
+    hipLaunchKernelGGL(p2m_kernel, dim3((g->nleaf_cells + kP2MWaves - 1) / kP2MWaves), dim3(64 * kP2MWaves), 0, g->stream,
+                       g->layout, g->aos.as<const char>(), g->leaves.as<const swh_leaf>(),
+                       g->leaf_ids.as<const int>(), g->nleaf_cells, g->mpoles.as<swh_multipole>());
+  for (size_t d = 0; d + 1 < g->m2m_depth_off.size(); d++) {
+    const int o0 = g->m2m_depth_off[d], o1 = g->m2m_depth_off[d + 1];
+    if (o1 > o0)
+      hipLaunchKernelGGL(m2m_kernel, dim3((o1 - o0 + 63) / 64), dim3(64), 0, g->stream,
+                         g->m2m_list.as<const int>() + o0, o1 - o0,
+                         g->tree_d.as<const swh_gcell>(), g->mpoles.as<swh_multipole>());
+  }
+  SWH_HIP(hipGetLastError());
+  if (stats) SWH_HIP(hipEventRecord(ev[1], g->stream));
   hipLaunchKernelGGL(cell_active_kernel, dim3(ncells), dim3(256), 0, g->stream,
                      g->leaves.as<const swh_leaf>(), g->active.as<const int8_t>(),
                      g->cell_act.as<int8_t>());
@@ -1516,25 +1924,27 @@ swh_status swh_grav_tree(swh_gspace* g, const swh_grav_params* G, const int32_t*
   }
 
   g->mpoles_valid = true;  // the same cell table: the multipoles stay
+  if (stats) SWH_HIP(hipEventRecord(ev[2], g->stream));
   // P2P + M2P
   SWH_TRY(g->counter.reserve(2 * sizeof(unsigned long long)));
   unsigned long long* ctr = g->counter.as<unsigned long long>();
   SWH_HIP(hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned long long), g->stream));
-  if (npp > 0) SWH_TRY(launch_pp(g, G, mac_params(G), ctr));
+  if (npp > 0) SWH_TRY(launch_pp(g, G, mac_params(G), ctr, stats ? ev[3] : nullptr));
+  if (stats) SWH_HIP(hipEventRecord(ev[4], g->stream));
   // M2L
   const bool f64 = g->ctx->precision == SWH_PRECISION_F64;
   SWH_HIP(hipMemsetAsync(g->ftens.ptr, 0, (size_t)ncells * SWH_MPOLE_TERMS * sizeof(double),
                          g->stream));
   if (nmm > 0) {
-    const dim3 mg((ncells + 63) / 64);
+    const dim3 mg((unsigned)(((int64_t)ncells * kM2LLanes + 255) / 256));
     if (f64)
-      hipLaunchKernelGGL((m2l_kernel<double>), mg, dim3(64), 0, g->stream,
+      hipLaunchKernelGGL((m2l_kernel<double>), mg, dim3(256), 0, g->stream,
                          g->mpoles.as<const swh_multipole>(), ncells, g->m2l_off.as<const int>(),
                          g->m2l_src.as<const int2>(), G->periodic, (double)G->dim[0],
                          (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv,
                          g->ftens.as<double>());
     else
-      hipLaunchKernelGGL((m2l_kernel<float>), mg, dim3(64), 0, g->stream,
+      hipLaunchKernelGGL((m2l_kernel<float>), mg, dim3(256), 0, g->stream,
                          g->mpoles.as<const swh_multipole>(), ncells, g->m2l_off.as<const int>(),
                          g->m2l_src.as<const int2>(), G->periodic, (double)G->dim[0],
                          (double)G->dim[1], (double)G->dim[2], (float)G->r_s_inv,
@@ -1556,20 +1966,19 @@ swh_status swh_grav_tree(swh_gspace* g, const swh_grav_params* G, const int32_t*
       SWH_HIP(hipGetLastError());
     }
     if (g->nleaf_cells > 0) {
-      const int lblk = g->tree_max_leaf <= 64 ? 64 : 256;  // one wave per small leaf
+      const dim3 pg((unsigned)((g->n + 255) / 256));
       if (f64)
-        hipLaunchKernelGGL((l2p_kernel<double>), dim3(g->nleaf_cells), dim3(lblk), 0, g->stream,
-                           g->leaves.as<const swh_leaf>(), g->leaf_ids.as<const int>(),
-                           g->mpoles.as<const swh_multipole>(), g->ftens.as<const double>(),
-                           gsoa_of(g));
+        hipLaunchKernelGGL((l2p_part_kernel<double>), pg, dim3(256), 0, g->stream, g->n,
+                           g->leaf_of.as<const int>(), g->mpoles.as<const swh_multipole>(),
+                           g->ftens.as<const double>(), gsoa_of(g));
       else
-        hipLaunchKernelGGL((l2p_kernel<float>), dim3(g->nleaf_cells), dim3(lblk), 0, g->stream,
-                           g->leaves.as<const swh_leaf>(), g->leaf_ids.as<const int>(),
-                           g->mpoles.as<const swh_multipole>(), g->ftens.as<const double>(),
-                           gsoa_of(g));
+        hipLaunchKernelGGL((l2p_part_kernel<float>), pg, dim3(256), 0, g->stream, g->n,
+                           g->leaf_of.as<const int>(), g->mpoles.as<const swh_multipole>(),
+                           g->ftens.as<const double>(), gsoa_of(g));
       SWH_HIP(hipGetLastError());
     }
   }
+  if (stats) SWH_HIP(hipEventRecord(ev[5], g->stream));
   unsigned long long h[2] = {0, 0};
   SWH_HIP(hipMemcpyAsync(h, ctr, sizeof(h), hipMemcpyDeviceToHost, g->stream));
   SWH_HIP(hipStreamSynchronize(g->stream));
@@ -1579,6 +1988,17 @@ swh_status swh_grav_tree(swh_gspace* g, const swh_grav_params* G, const int32_t*
     stats->n_m2l = nmm;
     stats->n_pp_tasks = npp;
     stats->n_skipped = skipped;
+    float* ms[5] = {&stats->ms_multipoles, &stats->ms_walk, &stats->ms_p2p, &stats->ms_m2p,
+                    &stats->ms_down};
+    for (int k = 0; k < 5; k++) {
+      *ms[k] = 0.f;
+      if (k == 3 && npp == 0) continue;  // no M2P launch: ev[3] never recorded
+      hipEvent_t a = ev[k], b = ev[k + 1];
+      if (k == 2 && npp > 0) b = ev[3];  // P2P ends where M2P starts
+      if (k == 2 && npp == 0) b = ev[4];
+      (void)hipEventElapsedTime(ms[k], a, b);
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
   }
   return SWH_OK;
 }

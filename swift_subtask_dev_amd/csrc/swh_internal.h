@@ -240,14 +240,17 @@ struct swh_gspace {
   swh::DevBuf m2l_off, m2l_src;  // CSR per target cell: int2 {source, symmetric}
   swh::DevBuf l2l_list;          // int2 {cell, parent}, grouped by depth
   std::vector<int32_t> l2l_depth_off;  // l2l_list range of each depth
+  swh::DevBuf m2m_list;          // int: split cells, deepest first (the upward M2M pass)
+  std::vector<int32_t> m2m_depth_off;  // m2m_list range of each depth
   swh::DevBuf leaf_ids;          // int: the unsplit cells
+  swh::DevBuf leaf_of;           // int per gpart: its unsplit cell (-1: none)
   int32_t nleaf_cells = 0;
   int32_t tree_max_leaf = 0;     // largest unsplit cell
   // device walk (swh_grav_tree): the cell table, two frontiers of tasks, the
   // emitted P-P / M-M entries (keys cell << 32 | other, flags) and their
   // sorted copies, per-cell counts
-  swh::DevBuf tree_d, wf0, wf1, wctr, pp_key, pp_val, pp_key2, pp_val2, pp_cnt;
-  swh::DevBuf mm_key, mm_val, mm_key2, mm_val2, mm_cnt, wsort_tmp;
+  swh::DevBuf tree_d, wf0, wf1, pp_key, pp_val, pp_key2, pp_val2;
+  swh::DevBuf mm_key, mm_val, mm_key2, mm_val2, wsort_tmp, wrec, wcnt, wbase;
   // PM mesh (swh_gspace_pm_mesh): density / potential mesh, its r2c
   // transform and the cached hipFFT plans of side mesh_N
   swh::DevBuf mesh_rho, mesh_frho;

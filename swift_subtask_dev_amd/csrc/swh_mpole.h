@@ -267,6 +267,27 @@ __host__ __device__ constexpr int mp_index(int a, int b, int c) {
 }
 __host__ __device__ constexpr int mp_order(int t) { return kMpA[t] + kMpB[t] + kMpC[t]; }
 
+// gravity_M2M (src/multipole.h:1278): M'_t += sum_{q <= t} M_q X_(t-q)(dx),
+// dx = the new centre - the old one, X as in xpowers, the zero dipole skipped.
+template <int t, int q>
+__device__ __forceinline__ void m2m_tq(const float* M, const double* X, double* Mt) {
+  if constexpr (q < SWH_MPOLE_TERMS) {
+    if constexpr ((q == 0 || q > 3) && kMpA[q] <= kMpA[t] && kMpB[q] <= kMpB[t] &&
+                  kMpC[q] <= kMpC[t]) {
+      constexpr int d = mp_index(kMpA[t] - kMpA[q], kMpB[t] - kMpB[q], kMpC[t] - kMpC[q]);
+      Mt[t] += (double)M[q] * X[d];
+    }
+    m2m_tq<t, q + 1>(M, X, Mt);
+  }
+}
+template <int t>
+__device__ __forceinline__ void m2m_t(const float* M, const double* X, double* Mt) {
+  if constexpr (t < SWH_MPOLE_TERMS) {
+    if constexpr (t == 0 || t > 3) m2m_tq<t, 0>(M, X, Mt);
+    m2m_t<t + 1>(M, X, Mt);
+  }
+}
+
 // D_m for the 35 multi-indices, |m| <= 4, from powers of r and the chain g
 template <typename T, int t>
 __device__ __forceinline__ void dtensors(const T* xp, const T* yp, const T* zp, const T* g,
@@ -366,9 +387,12 @@ __device__ __forceinline__ void l2p_t(const double* F, const T* X, T& pot, T& ax
   if constexpr (t < SWH_MPOLE_TERMS) {
     pot -= X[t] * (T)F[t];
     if constexpr (mp_order(t) <= 3) {
-      ax += X[t] * (T)F[mp_index(kMpA[t] + 1, kMpB[t], kMpC[t])];
-      ay += X[t] * (T)F[mp_index(kMpA[t], kMpB[t] + 1, kMpC[t])];
-      az += X[t] * (T)F[mp_index(kMpA[t], kMpB[t], kMpC[t] + 1)];
+      constexpr int ix = mp_index(kMpA[t] + 1, kMpB[t], kMpC[t]);
+      constexpr int iy = mp_index(kMpA[t], kMpB[t] + 1, kMpC[t]);
+      constexpr int iz = mp_index(kMpA[t], kMpB[t], kMpC[t] + 1);
+      ax += X[t] * (T)F[ix];
+      ay += X[t] * (T)F[iy];
+      az += X[t] * (T)F[iz];
     }
     l2p_t<T, t + 1>(F, X, pot, ax, ay, az);
   }

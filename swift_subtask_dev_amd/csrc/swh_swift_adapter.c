@@ -315,7 +315,12 @@ void runner_dopair_subset_branch_density(struct runner *r, struct cell *ci,
  * pairs (pid of ci, pjd of cj) that touch. Progeny k sits at offset
  * ((k >> 2) & 1, (k >> 1) & 1, k & 1) half-widths (space_split.c:233);
  * two progeny touch when every component of 2 d + off_j - off_i is in
- * [-1, 1]. Built at init instead of tabulated. */
+ * [-1, 1]. Built at init instead of tabulated: the SET of pairs per sid is
+ * the reference's (tests/test_dosub.py checks it against the table), their
+ * ORDER is (pid, pjd) ascending, not the table's. The order only decides in
+ * which order the leaf tasks of one DOSUB add into a particle's float sums,
+ * and inside a leaf pair the device kernels sum in their own order anyway,
+ * so the DOSUB parity tests compare with order-insensitive tolerances. */
 static const int swhs_sid_dir[13][3] = {{1, 1, 1},  {1, 1, 0},  {1, 1, -1}, {1, 0, 1},
                                         {1, 0, 0},  {1, 0, -1}, {1, -1, 1}, {1, -1, 0},
                                         {1, -1, -1}, {0, 1, 1}, {0, 1, 0},  {0, 1, -1},

@@ -262,18 +262,21 @@ def gravity_tree(gparts: np.ndarray, cdim: int, split_size: int = 64, box: float
     tkey, mort = tkey[order], mort[order]
     cells = []
 
-    def make(start, count, level):
+    def make(start, count, level, loc, width):
         idx = len(cells)
-        cells.append([start, count, 0, [-1] * 8])
+        cells.append([start, count, 0, [-1] * 8, loc, width])
         if count > split_size and level < max_depth:
             shift = np.uint64(3 * (20 - level))
             octant = ((mort[start:start + count] >> shift) & np.uint64(7)).astype(np.int64)
             bounds = np.searchsorted(octant, np.arange(9))  # sorted within the cell
             prog = [-1] * 8
-            for k in range(8):
+            hw = 0.5 * width
+            for k in range(8):  # octant bits: x (4), y (2), z (1)
                 c0, c1 = int(bounds[k]), int(bounds[k + 1])
                 if c1 > c0:
-                    prog[k] = make(start + c0, c1 - c0, level + 1)
+                    cl = (loc[0] + hw * ((k >> 2) & 1), loc[1] + hw * ((k >> 1) & 1),
+                          loc[2] + hw * (k & 1))
+                    prog[k] = make(start + c0, c1 - c0, level + 1, cl, hw)
             cells[idx][2] = 1
             cells[idx][3] = prog
         return idx
@@ -283,11 +286,11 @@ def gravity_tree(gparts: np.ndarray, cdim: int, split_size: int = 64, box: float
     tops = []
     for t in range(cdim ** 3):
         if counts[t] > 0:
-            tops.append(make(int(starts[t]), int(counts[t]), 0))
-    arr = np.zeros(len(cells), dtype=np.dtype([("start", "<i4"), ("count", "<i4"),
-                                               ("split", "<i4"), ("progeny", "<i4", 8)]))
-    for k, (st, ct, sp, pg) in enumerate(cells):
-        arr[k] = (st, ct, sp, pg)
+            tx, ty, tz = t // (cdim * cdim), (t // cdim) % cdim, t % cdim
+            tops.append(make(int(starts[t]), int(counts[t]), 0, (tx * w, ty * w, tz * w), w))
+    arr = np.zeros(len(cells), dtype=abi.GCELL_DTYPE)
+    for k, (st, ct, sp, pg, loc, width) in enumerate(cells):
+        arr[k] = (st, ct, sp, pg, loc, (width, width, width))
     return g, arr, np.asarray(tops, dtype=np.int32)
 
 

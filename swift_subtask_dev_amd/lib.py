@@ -450,7 +450,9 @@ class GravSpace:
         _check(self._lib.swh_grav_tree(self.handle, C.byref(G), _ptr(sc), len(sc), _ptr(pc),
                                        len(pc) // 2, C.byref(st)), "grav_tree")
         return {"n_pp": st.n_pp, "n_m2p": st.n_m2p, "n_m2l": st.n_m2l,
-                "n_pp_tasks": st.n_pp_tasks, "n_skipped": st.n_skipped}
+                "n_pp_tasks": st.n_pp_tasks, "n_skipped": st.n_skipped,
+                "ms": {"multipoles": st.ms_multipoles, "walk": st.ms_walk, "p2p": st.ms_p2p,
+                       "m2p": st.ms_m2p, "down": st.ms_down}}
 
     def field_tensors(self) -> np.ndarray:
         out = np.zeros((len(self._tree), abi.MPOLE_TERMS), dtype=np.float32)

@@ -72,6 +72,7 @@ def load(prec: str = "f32") -> C.CDLL:
                                     P(abi.Multipole), C.c_int, C.c_int, P(abi.GravParams),
                                     P(i64)])
     sig("grav_p2m", None, [vp, C.c_int, P(abi.Multipole)])
+    sig("grav_m2m", None, [vp, C.c_int, P(C.c_double), P(C.c_double), P(abi.Multipole)])
     sig("grav_tree", None, [vp, C.c_int, vp, C.c_int, vp, C.c_int, vp, C.c_int,
                             P(abi.GravParams), vp, vp])
     sig("pm_mesh", None, [vp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_float, vp])

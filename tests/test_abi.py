@@ -98,8 +98,9 @@ def test_params_struct_size():
     assert C.sizeof(abi.GravParams) == 72
     assert abi.GravParams.r_cut_max.offset == 64
     # swh_gcell: start, count, split, progeny[8]; swh_grav_tree_stats: 5 int64
-    assert C.sizeof(abi.GCell) == 44
-    assert C.sizeof(abi.GravTreeStats) == 40
+    assert C.sizeof(abi.GCell) == 96 == abi.GCELL_DTYPE.itemsize
+    assert abi.GCell.loc.offset == 48 and abi.GCell.width.offset == 72
+    assert C.sizeof(abi.GravTreeStats) == 64
     # swh_multipole: CoM, r_max, 35 terms, 5 powers, 2 floats
     assert C.sizeof(abi.Multipole) == 4 * 8 + 35 * 4 + 5 * 4 + 2 * 4
 

@@ -649,3 +649,47 @@ def test_grav_tree_walk_accounting():
     N = len(g)
     assert stats[2] == 0 and stats[1] == 0
     assert stats[0] == N * (N - 1)
+
+
+def test_m2m_equals_p2m_of_the_union():
+    """gravity_M2M (multipole.h:1278) shifts order-4 moments exactly: M2M of
+    the P2M of a cell's octants equals the P2M of the whole cell (CoM and
+    every term to the float storage of the children's moments); space_split's
+    r_max is an upper
+    bound of the exact one and never beyond the farthest corner."""
+    rng = np.random.Generator(np.random.PCG64(5))
+    g = abi.new_gparts(400)
+    g["x"] = rng.uniform(0.0, 1.0, (400, 3))
+    g["mass"] = rng.uniform(0.5, 2.0, 400)
+    g["epsilon"] = rng.uniform(0.01, 0.02, 400)
+    g["old_a_grav_norm"] = rng.uniform(1.0, 3.0, 400)
+    octant = ((g["x"][:, 0] >= 0.5) * 4 + (g["x"][:, 1] >= 0.5) * 2 + (g["x"][:, 2] >= 0.5))
+    order = np.argsort(octant, kind="stable")
+    g = abi.copy_parts(g[order])
+    octant = octant[order]
+    kids = []
+    for k in range(8):
+        sel = np.nonzero(octant == k)[0]
+        m = abi.Multipole()
+        O.fn("f64", "grav_p2m")(g[sel[0]:sel[-1] + 1].ctypes.data, len(sel), C.byref(m))
+        kids.append(m)
+    whole = abi.Multipole()
+    O.fn("f64", "grav_p2m")(g.ctypes.data, len(g), C.byref(whole))
+    arr = (C.POINTER(abi.Multipole) * 8)(*[C.pointer(m) for m in kids])
+    up = abi.Multipole()
+    loc = (C.c_double * 3)(0.0, 0.0, 0.0)
+    width = (C.c_double * 3)(1.0, 1.0, 1.0)
+    O.fn("f64", "grav_m2m")(arr, 8, loc, width, C.byref(up))
+    # the parent's CoM weights the children by their float M_000, as
+    # space_split does: exact to float rounding of the masses
+    assert np.allclose(list(up.CoM), list(whole.CoM), rtol=0, atol=1e-7)
+    Mw, Mu = np.array(list(whole.M)), np.array(list(up.M))
+    for o in range(5):
+        sel = [t for t, (a, b, c) in enumerate(abi.MPOLE_INDEX) if a + b + c == o]
+        scale = np.abs(Mw[sel]).max() or 1.0
+        assert np.abs(Mu[sel] - Mw[sel]).max() <= 1e-6 * scale, o  # float storage
+    assert whole.r_max <= up.r_max * (1 + 1e-12)
+    corner = np.sqrt(sum(max(c, 1 - c) ** 2 for c in whole.CoM))
+    assert up.r_max <= corner * (1 + 1e-12)
+    assert up.max_softening == max(m.max_softening for m in kids)
+    assert up.min_old_a_grav_norm == min(m.min_old_a_grav_norm for m in kids)

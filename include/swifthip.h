@@ -477,7 +477,7 @@ SWH_API swh_status swh_gspace_sync(swh_gspace *g);
  * them first); swh_gspace_download returns them. potential_out (nullable): the
  * N^3 potential mesh (row-major, z fastest), as mesh->potential_global. */
 typedef struct swh_pm_params {
-  int32_t N;                  /* gravity_props.mesh_size (2 to 1290) */
+  int32_t N;                  /* gravity_props.mesh_size (even, 2 to 1290; odd N refused, see swh_mesh.hip) */
   int32_t off_a_grav_mesh;    /* byte offsets in the gpart record: float[3] */
   int32_t off_potential_mesh; /* float */
   int32_t reserved;

@@ -182,13 +182,17 @@ using namespace swh;
 
 extern "C" {
 
+// N must be even here although mesh_gravity.c:1172 only bounds N <= 1290:
+// the odd-N 3D D2Z/Z2D plans of this image's hipFFT took the process down
+// (abort inside swh_gspace_pm_mesh, r03 GPU run of test_mesh.py with N = 15),
+// so odd meshes are refused with an error instead.
 swh_status swh_gspace_pm_mesh(swh_gspace* g, const swh_pm_params* M, double* potential_out) {
   if (!g || !M) return SWH_ERR_ARG;
   const GLayout& L = g->layout;
-  if (M->N < 2 || M->N > 1290 || !(M->box_size > 0.) || !(M->r_s > 0.) ||
+  if (M->N < 2 || M->N % 2 != 0 || M->N > 1290 || !(M->box_size > 0.) || !(M->r_s > 0.) ||
       M->off_a_grav_mesh < 0 || M->off_potential_mesh < 0 ||
       (g->n > 0 && (M->off_a_grav_mesh + 12 > L.stride || M->off_potential_mesh + 4 > L.stride))) {
-    set_error("pm_mesh: N must be in [2, 1290] (mesh_gravity.c:1172), box and r_s > 0, "
+    set_error("pm_mesh: N must be even in [2, 1290] (mesh_gravity.c:1172 bounds N; even: see swh_gspace_pm_mesh), box and r_s > 0, "
               "mesh fields inside the record");
     return SWH_ERR_ARG;
   }

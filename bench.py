@@ -587,23 +587,32 @@ def run_cosmo(args, ctx, rank, world, dist, torch):
     SWIFT step overlap); the line reports each alone and both together.
     The MAC is the geometric theta_cr = 0.7 one (SWH_COSMO_ADAPTIVE_MAC=1: the
     yml's adaptive MAC, whose |a| estimates the stand-in's units do not
-    reproduce: it accepts no M2L here). The recursive walk itself runs on the
-    host (swh_grav_tree): it dominates this step."""
-    import threading
-    from swift_subtask_dev_amd import abi, ics, lib
+    reproduce: it accepts no M2L here).
 
-    if world > 1:
-        raise SystemExit("--workload cosmo runs on one GPU (the driver's multi-GPU runs use sedov)")
+    With N ranks (one per GPU) the step is sharded: the gas by
+    the hydro block decomposition (decomp.HaloPlan: owned block + read-only
+    halo, swh_space_set_owned), the gravity by subtrees of the top cells
+    whose centres lie in the rank's block (decomp.gravity_owned_cells,
+    swh_gspace_set_owned_cells) with every gpart and the tree replicated
+    read-only, and the PM mesh computed by every rank on its replicated
+    gparts. The timed step needs no data-path collective: its loops read the
+    halo fields the untimed setup left (a full SWIFT step refreshes them
+    between phases, as the sedov workload does). value = interactions of all
+    ranks / the slowest rank's time."""
+    import threading
+    from swift_subtask_dev_amd import abi, decomp, ics, lib
+
     n = args.n if args.n != 128 else 64
+    box = (1.0, 1.0, 1.0)
     t0 = time.time()
     gas = ics.sedov_slabs(n, 1)
     gas["u"] = 1.0e-6 / (ics.GAMMA - 1.0)  # a cold uniform medium, no blast
-    P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
+    P = abi.default_hydro_params(box, True)
     P.max_active_bin = 1
     sp = lib.HydroSpace(ctx)
     sp.upload(gas)
     sp.rebuild(P)
-    sp.hydro_step(P)  # converged h, the force inputs
+    sp.hydro_step(P)  # converged h, the force inputs (whole box, untimed)
     sp.download(gas, abi.FIELDS_ALL)
     sp.close()
     # gparts: the gas + as many DM particles, softening 1/25 of the mean spacing
@@ -638,21 +647,33 @@ def run_cosmo(args, ctx, rank, world, dist, torch):
     G.use_advanced_MAC = int(os.environ.get("SWH_COSMO_ADAPTIVE_MAC", "0"))
     gs.upload(g)
     gs.set_tree(cells)
+    owned_cells = None
+    if world > 1:
+        owned_cells = decomp.gravity_owned_cells(cells, tops, rank, world, box)
+        gs.set_owned_cells(owned_cells)
     stats = gs.tree(G, tops, pairs)
     gs.pm_mesh(N_mesh, 1.0, r_s, 1.0)
 
     hs = lib.HydroSpace(ctx)
     hstream = torch.cuda.Stream()
     hs.set_stream(hstream.cuda_stream)
-    hs.upload(gas)
+    if world > 1:
+        reach = 1.01 * 1.825742 * float(gas["h"].max())  # 1.01 gamma h_max, as the sedov split
+        plan = decomp.HaloPlan(gas["x"], box, world, rank, reach)
+        local, n_owned = plan.local_set(gas), plan.n_owned
+    else:
+        local, n_owned = gas, len(gas)
+    hs.upload(local)
+    hs.set_owned(n_owned)
     hs.rebuild(P)
     hs.init_parts(P)
     n_density = hs.density(P)
     hs.reset_acceleration(P)
     n_force = hs.force(P)
     torch.cuda.synchronize()
-    log(f"[rank {rank}] cosmo setup {time.time() - t0:.1f}s: {n ** 3} gas + {n ** 3} DM gparts, "
-        f"{len(cells)} cells; gravity step {stats}; hydro {n_density} + {n_force}")
+    log(f"[rank {rank}] cosmo setup {time.time() - t0:.1f}s: {n_owned} of {n ** 3} gas + "
+        f"{2 * n ** 3} gparts ({int(owned_cells.sum()) if owned_cells is not None else len(cells)}"
+        f" of {len(cells)} cells owned); gravity step {stats}; hydro {n_density} + {n_force}")
 
     def hydro():
         hs.init_parts(P)
@@ -676,74 +697,93 @@ def run_cosmo(args, ctx, rank, world, dist, torch):
         for _ in range(args.warmup):
             fn()
         torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
         t = time.perf_counter()
         for _ in range(args.steps):
             fn()
         torch.cuda.synchronize()
-        return (time.perf_counter() - t) / args.steps
+        el = time.perf_counter() - t
+        if dist:
+            dist.barrier()
+            x = torch.tensor([el], dtype=torch.float64, device=RED_DEVICE)
+            dist.all_reduce(x, op=dist.ReduceOp.MAX)
+            el = x.item()
+        return el / args.steps
 
     t_h, t_g, t_b = timed(hydro), timed(gravity), timed(both)
-    total = float(n_density + n_force + stats["n_pp"])
-    out = {
-        "metric": "hydro (density+force) + gravity P2P interactions/s, SmallCosmoVolume stand-in",
-        "value": total / t_b, "unit": "interactions/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": t_b * 1e3, "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (64^3 perturbed-lattice gas + 64^3 uniform DM; SmallCosmoVolume ICs "
-                "unavailable offline)",
-        "config": {"workload": f"SmallCosmoVolume stand-in: {n}^3 gas + {n}^3 DM, hydro density + "
-                               "force loops || gravity tree (P2P, M2P, M2L, L2L, L2P) + PM mesh 64",
-                   "hydro_interactions_per_step": n_density + n_force,
-                   "gravity_tree_stats": stats, "cells": int(len(cells)),
-                   "softening": eps, "r_s": r_s},
-        "step_ms": {"hydro_alone": t_h * 1e3, "gravity_alone": t_g * 1e3,
-                    "overlapped": t_b * 1e3,
-                    "overlap_gain": (t_h + t_g) / t_b},
-        "roofline": None, "cpu_baseline": None,
-    }
+    mine = [float(n_density + n_force + stats["n_pp"]), float(n_density + n_force),
+            float(stats["n_pp"])]
+    tot = torch.tensor(mine, dtype=torch.float64, device=RED_DEVICE)
+    if dist:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    total, total_hydro, total_pp = tot.tolist()
     # roofline: the step's dominant kernel is the gravity P2P (its own HIP
     # events inside swh_grav_tree, on the gravity stream)
     st = gs.tree(G, tops, pairs)
     gs.sync()
-    out["gravity_phase_ms"] = st["ms"]
-    t_p2p = st["ms"]["p2p"] * 1e-3
-    if t_p2p > 0:
-        flops = st["n_pp"] * 28.0 / t_p2p
-        out["roofline"] = {"bound": "fp64-vector", "kernel": "p2p_kernel/p2p_small_kernel",
-                           "achieved": flops / 1e12, "peak": FP64_PEAK / 1e12,
-                           "unit": "TFLOP/s", "frac": flops / FP64_PEAK, "traffic": None,
-                           "flops_model": "28 flops per directed P2P interaction (the "
-                                          "truncated kernel's erfc/exp terms not counted)"}
-        tr = load_traffic("cosmo")
-        if tr:
-            out["roofline"]["traffic"] = tr.get("bytes_per_launch")
-            out["roofline"]["traffic_source"] = tr.get("source")
-    if not args.no_cpu_baseline:
-        try:
-            threads = cpu_share_threads()
-            G.use_advanced_MAC = 0
-            w = run_cpu_worker("cosmo", {"parts": np.ascontiguousarray(gas).view(np.uint8),
-                                         "gparts": np.ascontiguousarray(g).view(np.uint8),
-                                         "cells": np.ascontiguousarray(cells).view(np.uint8),
-                                         "tops": np.ascontiguousarray(tops, dtype=np.int32),
-                                         "pairs": np.ascontiguousarray(pairs, dtype=np.int32)
-                                         .reshape(-1),
-                                         "G": np.frombuffer(bytes(G), dtype=np.uint8)},
-                               {"cdim": 20}, threads)
-            n_cpu = n_density + n_force + w["tree_stats"][0]
-            out["cpu_baseline"] = {
-                "value": n_cpu / w["seconds_share"], "unit": "interactions/s",
-                "cores": threads, "kind": "port", "host": host_cpu_info(),
-                "pinning": "one thread per physical core, child process without torch",
-                "sample": f"one whole step: the float restatement's density + force loops over "
-                          f"a cdim-20 cell grid ({w['seconds_hydro']:.2f} s, OpenMP over cells) "
-                          f"and its gravity: tree walk (serial), P2P/M2P and M2L (OpenMP), "
-                          f"L2L/L2P (serial) ({w['seconds_gravity']:.2f} s); the PM mesh not included",
-                "tree_stats": w["tree_stats"]}
-            out["gpu_over_cpu"] = out["value"] / out["cpu_baseline"]["value"]
-        except Exception as e:  # report, never fake
-            log(f"cosmo cpu baseline failed: {e}")
-    print(json.dumps(out), flush=True)
+    if rank == 0:
+        out = {
+            "metric": "hydro (density+force) + gravity P2P interactions/s, SmallCosmoVolume stand-in",
+            "value": total / t_b, "unit": "interactions/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": t_b * 1e3, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (64^3 perturbed-lattice gas + 64^3 uniform DM; SmallCosmoVolume ICs "
+                    "unavailable offline)",
+            "config": {"workload": f"SmallCosmoVolume stand-in: {n}^3 gas + {n}^3 DM, hydro density + "
+                                   "force loops || gravity tree (P2P, M2P, M2L, L2L, L2P) + PM mesh 64",
+                       "parallelism": (f"{'x'.join(map(str, decomp.block_dims(world)))} blocks: gas "
+                                       "owned + halo, gravity subtrees owned, gparts replicated"
+                                       if world > 1 else "one GPU"),
+                       "hydro_interactions_per_step": int(total_hydro),
+                       "gravity_pp_per_step": int(total_pp),
+                       "gravity_tree_stats_rank0": stats, "cells": int(len(cells)),
+                       "softening": eps, "r_s": r_s},
+            "step_ms": {"hydro_alone": t_h * 1e3, "gravity_alone": t_g * 1e3,
+                        "overlapped": t_b * 1e3,
+                        "overlap_gain": (t_h + t_g) / t_b},
+            "gravity_phase_ms_rank0": st["ms"],
+            "roofline": None, "cpu_baseline": None,
+        }
+        t_p2p = st["ms"]["p2p"] * 1e-3
+        if t_p2p > 0:
+            flops = st["n_pp"] * 28.0 / t_p2p
+            out["roofline"] = {"bound": "fp64-vector", "kernel": "p2p_kernel/p2p_small_kernel",
+                               "achieved": flops / 1e12, "peak": FP64_PEAK / 1e12,
+                               "unit": "TFLOP/s", "frac": flops / FP64_PEAK, "traffic": None,
+                               "flops_model": "28 flops per directed P2P interaction (the "
+                                              "truncated kernel's erfc/exp terms not counted)"}
+            tr = load_traffic("cosmo") if world == 1 else None
+            if tr:
+                out["roofline"]["traffic"] = tr.get("bytes_per_launch")
+                out["roofline"]["traffic_source"] = tr.get("source")
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                threads = cpu_share_threads()
+                G.use_advanced_MAC = 0
+                w = run_cpu_worker("cosmo", {"parts": np.ascontiguousarray(gas).view(np.uint8),
+                                             "gparts": np.ascontiguousarray(g).view(np.uint8),
+                                             "cells": np.ascontiguousarray(cells).view(np.uint8),
+                                             "tops": np.ascontiguousarray(tops, dtype=np.int32),
+                                             "pairs": np.ascontiguousarray(pairs, dtype=np.int32)
+                                             .reshape(-1),
+                                             "G": np.frombuffer(bytes(G), dtype=np.uint8)},
+                                   {"cdim": 20}, threads)
+                n_cpu = n_density + n_force + w["tree_stats"][0]
+                out["cpu_baseline"] = {
+                    "value": n_cpu / w["seconds_share"], "unit": "interactions/s",
+                    "cores": threads, "kind": "port", "host": host_cpu_info(),
+                    "pinning": "one thread per physical core, child process without torch",
+                    "sample": f"one whole step: the float restatement's density + force loops over "
+                              f"a cdim-20 cell grid ({w['seconds_hydro']:.2f} s, OpenMP over cells) "
+                              f"and its gravity: tree walk (serial), P2P/M2P and M2L (OpenMP), "
+                              f"L2L/L2P (serial) ({w['seconds_gravity']:.2f} s); the PM mesh not "
+                              f"included",
+                    "tree_stats": w["tree_stats"]}
+                out["gpu_over_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+            except Exception as e:  # report, never fake
+                log(f"cosmo cpu baseline failed: {e}")
+        print(json.dumps(out), flush=True)
     hs.close()
     gs.close()
 

@@ -457,6 +457,18 @@ typedef struct swh_grav_tree_stats {
   int32_t reserved;
 } swh_grav_tree_stats;
 SWH_API swh_status swh_gspace_set_tree(swh_gspace *g, const swh_gcell *cells, int32_t ncells);
+/* Ownership for a step sharded over ranks (i-cells owned per GPU,
+ * every gpart and multipole replicated read-only): owned[c] != 0 for the
+ * cells whose gparts this rank computes. swh_grav_tree then runs only the
+ * tasks that can reach an owned cell and emits P-P / M-M entries only for
+ * owned targets; M-M symmetry and every acceptance decision still use the
+ * whole tree, so an owned gpart's result equals the single-domain one
+ * bit for bit, and the other gparts receive nothing from the tree (their
+ * accumulators are not meaningful on this rank). Ownership is whole
+ * subtrees: a cell must be owned exactly when its parent is (root cells
+ * choose). owned = NULL: every cell (the default, and after set_tree). */
+SWH_API swh_status swh_gspace_set_owned_cells(swh_gspace *g, const uint8_t *owned,
+                                              int32_t ncells);
 SWH_API swh_status swh_grav_tree(swh_gspace *g, const swh_grav_params *G,
                                  const int32_t *self_cells, int32_t nself,
                                  const int32_t *pair_cells, int32_t npair,

@@ -2859,6 +2859,7 @@ struct otree_walk {
   const struct oracle_gcell *cells;
   const struct oracle_multipole *mp;
   const char *act;
+  const unsigned char *own; /* NULL: every cell owned (the decomposition stand-in) */
   const struct oracle_grav_params *G;
   int *pp;      /* entries of 4 ints: i-cell, j-cell, truncated, allow_mpole */
   long long npp, cap_pp;
@@ -2932,8 +2933,14 @@ static int m2l_accept_o(const struct oracle_grav_params *G, const struct oracle_
 static void otw_self(struct otree_walk *w, int c);
 static void otw_pair(struct otree_walk *w, int ci, int cj);
 
+/* an entry for cell c: active, and owned by this rank when the step is
+ * sharded (runner_do*_grav run by the rank owning the i-cell) */
+static int otw_emits(const struct otree_walk *w, int c) {
+  return w->act[c] && (!w->own || w->own[c]);
+}
+
 static void otw_no_cache(struct otree_walk *w, int ci, int cj) {
-  if (!w->act[ci]) return;
+  if (!otw_emits(w, ci)) return;
   if (w->cells[ci].count == 0 || w->cells[cj].count == 0) return;
   if (w->cells[ci].split) {
     for (int k = 0; k < 8; k++)
@@ -2944,7 +2951,7 @@ static void otw_no_cache(struct otree_walk *w, int ci, int cj) {
 }
 
 static void otw_self(struct otree_walk *w, int c) {
-  if (!w->act[c]) return;
+  if (!otw_emits(w, c)) return;
   const struct oracle_gcell *C = &w->cells[c];
   if (C->split) {
     for (int j = 0; j < 8; j++) {
@@ -2960,7 +2967,7 @@ static void otw_self(struct otree_walk *w, int c) {
 
 static void otw_pair(struct otree_walk *w, int ci, int cj) {
   const struct oracle_grav_params *G = w->G;
-  if (!(w->act[ci] || w->act[cj])) return;
+  if (!(otw_emits(w, ci) || otw_emits(w, cj))) return;
   const struct oracle_multipole *A = &w->mp[ci], *B = &w->mp[cj];
   double d[3];
   for (int k = 0; k < 3; k++) {
@@ -2979,15 +2986,9 @@ static void otw_pair(struct otree_walk *w, int ci, int cj) {
     otw_no_cache(w, cj, ci);
   } else if (m2l_accept_o(G, A, B, (float)r2) && m2l_accept_o(G, B, A, (float)r2)) {
     /* runner_dopair_grav_mm: symmetric when both are active */
-    const int di = w->act[ci], dj = w->act[cj];
-    if (di && dj) {
-      otw_push_mm(w, ci, cj, 1);
-      otw_push_mm(w, cj, ci, 1);
-    } else if (di) {
-      otw_push_mm(w, ci, cj, 0);
-    } else if (dj) {
-      otw_push_mm(w, cj, ci, 0);
-    }
+    const int sym = w->act[ci] && w->act[cj];
+    if (otw_emits(w, ci)) otw_push_mm(w, ci, cj, sym);
+    if (otw_emits(w, cj)) otw_push_mm(w, cj, ci, sym);
   } else if (!Ci->split && !Cj->split) {
     /* runner_dopair_grav_pp(ci, cj, 1, 1) */
     int tr = 0;
@@ -3000,8 +3001,8 @@ static void otw_pair(struct otree_walk *w, int ci, int cj) {
       const double rr2 = dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2];
       tr = (sqrt(rr2) + (float)A->r_max + (float)B->r_max) > G->r_cut_min;
     }
-    if (w->act[ci]) otw_push_pp(w, ci, cj, tr, 1);
-    if (w->act[cj]) otw_push_pp(w, cj, ci, tr, 1);
+    if (otw_emits(w, ci)) otw_push_pp(w, ci, cj, tr, 1);
+    if (otw_emits(w, cj)) otw_push_pp(w, cj, ci, tr, 1);
   } else if (A->r_max > B->r_max) {
     if (Ci->split) {
       for (int k = 0; k < 8; k++)
@@ -3035,9 +3036,12 @@ static double xpow_o(const double dx[3], int t) {
 /* Field tensors of the whole walk: F (35 per cell, real) after the down
  * pass; stats = {n_pp, n_m2p, n_m2l, n_pp_tasks, n_skipped}. The gparts'
  * a_grav / potential receive P2P + M2P (grav_pp_leaves) and L2P. */
-API void PFX(grav_tree)(struct gpart *g, int n, const struct oracle_gcell *cells, int ncells,
-                        const int *self_cells, int nself, const int *pair_cells, int npair,
-                        const struct oracle_grav_params *G, long long *stats, float *ftens) {
+/* owned (NULL: every cell): the decomposition stand-in of
+ * swh_gspace_set_owned_cells -- entries only for owned targets */
+API void PFX(grav_tree_owned)(struct gpart *g, int n, const struct oracle_gcell *cells,
+                              int ncells, const int *self_cells, int nself, const int *pair_cells,
+                              int npair, const struct oracle_grav_params *G, long long *stats,
+                              float *ftens, const unsigned char *owned) {
   (void)n;
   struct oracle_multipole *mp =
       (struct oracle_multipole *)malloc(sizeof(struct oracle_multipole) * (size_t)ncells);
@@ -3084,6 +3088,7 @@ API void PFX(grav_tree)(struct gpart *g, int n, const struct oracle_gcell *cells
   w.cells = cells;
   w.mp = mp;
   w.act = act;
+  w.own = owned;
   w.G = G;
   for (int k = 0; k < nself; k++) otw_self(&w, self_cells[k]);
   for (int k = 0; k < npair; k++) otw_pair(&w, pair_cells[2 * k], pair_cells[2 * k + 1]);
@@ -3218,6 +3223,13 @@ API void PFX(grav_tree)(struct gpart *g, int n, const struct oracle_gcell *cells
   }
   free(F); free(moff); free(mord); free(depth); free(fill); free(pairs); free(off); free(leaves);
   free(w.pp); free(w.mm); free(parent); free(act); free(mp);
+}
+
+API void PFX(grav_tree)(struct gpart *g, int n, const struct oracle_gcell *cells, int ncells,
+                        const int *self_cells, int nself, const int *pair_cells, int npair,
+                        const struct oracle_grav_params *G, long long *stats, float *ftens) {
+  PFX(grav_tree_owned)(g, n, cells, ncells, self_cells, nself, pair_cells, npair, G, stats, ftens,
+                       NULL);
 }
 
 /* ======================================================================== */

@@ -746,7 +746,7 @@ swh_status swh_gspace_destroy(swh_gspace* g) {
                     &g->m2l_src,  &g->l2l_list, &g->leaf_ids, &g->leaf_of, &g->m2m_list, &g->tree_d, &g->wf0,
                     &g->wf1,      &g->pp_key,  &g->pp_val,  &g->pp_key2,
                     &g->pp_val2,  &g->mm_key,  &g->mm_val,  &g->mm_key2,
-                    &g->mm_val2,  &g->wsort_tmp, &g->wrec, &g->wcnt, &g->wbase};
+                    &g->mm_val2,  &g->wsort_tmp, &g->wrec, &g->wcnt, &g->wbase, &g->owned_d};
   for (DevBuf* b : bufs) b->release();
   mesh_release(g);
   (void)hipStreamDestroy(g->stream);
@@ -1083,6 +1083,7 @@ struct TreeWalk {
   const swh_gcell* cells;
   const swh_multipole* mp;
   const int8_t* act;
+  const uint8_t* own;  // null: every cell owned (swh_gspace_set_owned_cells)
   const swh_grav_params* G;
   MacParams mac;
   // the tasks' entries in walk order: {i-cell, P-P entry} and {target, {source,
@@ -1096,9 +1097,10 @@ struct TreeWalk {
     const double L = (double)G->dim[k];
     return d > 0.5 * L ? d - L : (d < -0.5 * L ? d + L : d);
   }
+  bool emits(int c) const { return act[c] && (!own || own[c]); }
   // runner_doself_recursive_grav (2386-2431)
   void self(int c) {
-    if (!act[c]) return;
+    if (!emits(c)) return;
     const swh_gcell& C = cells[c];
     if (C.split) {
       for (int j = 0; j < 8; j++) {
@@ -1118,7 +1120,7 @@ struct TreeWalk {
   }
   // runner_dopair_grav_pp_no_cache (1440-1483): ci's leaves <- all of cj
   void no_cache(int ci, int cj) {
-    if (!act[ci]) return;
+    if (!emits(ci)) return;
     if (cells[ci].count == 0 || cells[cj].count == 0) return;
     if (cells[ci].split) {
       for (int k = 0; k < 8; k++)
@@ -1132,16 +1134,11 @@ struct TreeWalk {
     }
   }
   // runner_dopair_grav_mm (2050-2064): symmetric when both are active
+  // (an entry only for an owned target; the symmetry from both activities)
   void mmpair(int ci, int cj) {
-    const bool di = act[ci], dj = act[cj];
-    if (di && dj) {
-      mm.emplace_back(ci, make_int2(cj, 1));
-      mm.emplace_back(cj, make_int2(ci, 1));
-    } else if (di) {
-      mm.emplace_back(ci, make_int2(cj, 0));
-    } else if (dj) {
-      mm.emplace_back(cj, make_int2(ci, 0));
-    }
+    const int sym = act[ci] && act[cj] ? 1 : 0;
+    if (emits(ci)) mm.emplace_back(ci, make_int2(cj, sym));
+    if (emits(cj)) mm.emplace_back(cj, make_int2(ci, sym));
   }
   // runner_dopair_grav_pp(ci, cj, symmetric = 1, allow_mpole = 1) (1202-1425):
   // truncated iff periodic && |CoM_i - CoM_j| + r_max_i + r_max_j > r_cut_min
@@ -1158,12 +1155,12 @@ struct TreeWalk {
       trunc = (std::sqrt(d2) + (double)(float)mp[ci].r_max + (double)(float)mp[cj].r_max) >
               G->r_cut_min;
     }
-    if (act[ci]) pp.emplace_back(ci, swh_leaf_pair{cj, trunc, 1});
-    if (act[cj]) pp.emplace_back(cj, swh_leaf_pair{ci, trunc, 1});
+    if (emits(ci)) pp.emplace_back(ci, swh_leaf_pair{cj, trunc, 1});
+    if (emits(cj)) pp.emplace_back(cj, swh_leaf_pair{ci, trunc, 1});
   }
   // runner_dopair_recursive_grav (2208-2374)
   void pair(int ci, int cj) {
-    if (!(act[ci] || act[cj])) return;
+    if (!(emits(ci) || emits(cj))) return;
     const swh_multipole& A = mp[ci];
     const swh_multipole& B = mp[cj];
     double dx = A.CoM[0] - B.CoM[0], dy = A.CoM[1] - B.CoM[1], dz = A.CoM[2] - B.CoM[2];
@@ -1256,14 +1253,15 @@ struct __align__(64) GWRec {
   double r_max;
   float max_soft, min_a, power[3];
   int count;
-  int flags;  // 1: split, 2: active
+  int flags;  // 1: split, 2: active, 4: owned
   int pad;
 };
 static_assert(sizeof(GWRec) == 64, "one cache line per cell");
 
 __global__ void gw_rec_kernel(const swh_gcell* __restrict__ cells,
                               const swh_multipole* __restrict__ mp,
-                              const int8_t* __restrict__ act, int n, GWRec* __restrict__ out) {
+                              const int8_t* __restrict__ act, const uint8_t* __restrict__ own,
+                              int n, GWRec* __restrict__ out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= n) return;
   GWRec r;
@@ -1273,7 +1271,7 @@ __global__ void gw_rec_kernel(const swh_gcell* __restrict__ cells,
   r.min_a = mp[c].min_old_a_grav_norm;
   for (int k = 0; k < 3; k++) r.power[k] = mp[c].power[k];
   r.count = cells[c].count;
-  r.flags = (cells[c].split ? 1 : 0) | (act[c] ? 2 : 0);
+  r.flags = (cells[c].split ? 1 : 0) | (act[c] ? 2 : 0) | ((!own || own[c]) ? 4 : 0);
   r.pad = 0;
   out[c] = r;
 }
@@ -1320,14 +1318,14 @@ __global__ __launch_bounds__(256) void gwalk_kernel(
   const int lane = threadIdx.x & 63;
   if (__ballot(k < n) == 0ull) return;  // wave-uniform
   int ga = GA_NONE, ci = -1, cj = -1, nn = 0, npp = 0, nmm = 0, ns = 0;
-  int trunc = 0, di = 0, dj = 0, split_i = 0;
+  int trunc = 0, di = 0, dj = 0, ei = 0, ej = 0, split_i = 0;
   if (k < n) {
     const int4 it = cur[k];
     ci = it.x;
     cj = it.y;
     if (it.z == GW_SELF) {  // runner_doself_recursive_grav (2386-2431)
       const GWRec C = rec[ci];
-      if (C.flags & 2) {
+      if ((C.flags & 6) == 6) {  // active and owned
         if (C.flags & 1) {
           int m = 0;
           for (int j = 0; j < 8; j++) m += cells[ci].progeny[j] >= 0 ? 1 : 0;
@@ -1342,7 +1340,7 @@ __global__ __launch_bounds__(256) void gwalk_kernel(
       }
     } else if (it.z == GW_NOCACHE) {  // runner_dopair_grav_pp_no_cache (1440-1483)
       const GWRec Ci = rec[ci];
-      if ((Ci.flags & 2) && Ci.count > 0 && rec[cj].count > 0) {
+      if ((Ci.flags & 6) == 6 && Ci.count > 0 && rec[cj].count > 0) {
         if (Ci.flags & 1) {
           for (int j = 0; j < 8; j++) nn += cells[ci].progeny[j] >= 0 ? 1 : 0;
           ga = GA_NC_SPLIT;
@@ -1357,7 +1355,9 @@ __global__ __launch_bounds__(256) void gwalk_kernel(
       const GWRec B = rec[cj];
       di = (A.flags >> 1) & 1;
       dj = (B.flags >> 1) & 1;
-      if (di || dj) {
+      ei = (A.flags & 6) == 6;  // an entry for ci / cj: active and owned
+      ej = (B.flags & 6) == 6;
+      if (ei || ej) {
         double dx = A.com[0] - B.com[0], dy = A.com[1] - B.com[1], dz = A.com[2] - B.com[2];
         if (periodic) {
           dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
@@ -1376,7 +1376,7 @@ __global__ __launch_bounds__(256) void gwalk_kernel(
                    m2l_accept(mac, rec_side(B), rec_side(A), (float)r2)) {
           // runner_dopair_grav_mm (2050-2064): symmetric when both are active
           ga = GA_MM;
-          nmm = di + dj;
+          nmm = ei + ej;
         } else if (!si && !sj) {
           // runner_dopair_grav_pp(ci, cj, 1, 1): truncated iff periodic &&
           // |CoM_i - CoM_j| + r_max_i + r_max_j > r_cut_min (float separations)
@@ -1391,7 +1391,7 @@ __global__ __launch_bounds__(256) void gwalk_kernel(
             trunc = (sqrt(d2) + (double)(float)A.r_max + (double)(float)B.r_max) > r_cut_min;
           }
           ga = GA_PP;
-          npp = di + dj;
+          npp = ei + ej;
         } else {
           // split the larger cell (or the only split one)
           split_i = A.r_max > B.r_max ? si : !sj;
@@ -1464,19 +1464,13 @@ __global__ __launch_bounds__(256) void gwalk_kernel(
       o.next[q] = make_int4(ci, cj, GW_NOCACHE, 0);
       o.next[q + 1] = make_int4(cj, ci, GW_NOCACHE, 0);
       break;
-    case GA_MM:
-      if (di && dj) {
-        mm(ci, cj, 1);
-        mm(cj, ci, 1);
-      } else if (di) {
-        mm(ci, cj, 0);
-      } else if (dj) {
-        mm(cj, ci, 0);
-      }
+    case GA_MM:  // symmetric when both are active, an entry per owned target
+      if (ei) mm(ci, cj, di & dj);
+      if (ej) mm(cj, ci, di & dj);
       break;
     case GA_PP:
-      if (di) pp(ci, cj, trunc, 1);
-      if (dj) pp(cj, ci, trunc, 1);
+      if (ei) pp(ci, cj, trunc, 1);
+      if (ej) pp(cj, ci, trunc, 1);
       break;
     case GA_SPLIT: {
       const swh_gcell& S = split_i ? cells[ci] : cells[cj];
@@ -1579,11 +1573,20 @@ static swh_status device_walk(swh_gspace* g, const swh_grav_params* G, const int
   int bits = 1;
   while ((1ll << bits) < (long long)ncells) bits++;  // <= 31: keys of 2 * bits <= 62 bits
   const unsigned long long mask = (1ull << bits) - 1ull;
-  const int64_t ntask = (int64_t)nself + npair;
-  std::vector<int4> init((size_t)std::max<int64_t>(1, ntask));
-  for (int k = 0; k < nself; k++) init[k] = make_int4(self_cells[k], -1, GW_SELF, 0);
+  // the tasks that can reach an owned cell (all of them without ownership)
+  const bool owns = !g->owned.empty();
+  auto own = [&](int c) { return !owns || g->owned[c] != 0; };
+  std::vector<int4> init;
+  init.reserve((size_t)nself + npair + 1);
+  int64_t nself_kept = 0;
+  for (int k = 0; k < nself; k++)
+    if (own(self_cells[k])) init.push_back(make_int4(self_cells[k], -1, GW_SELF, 0));
+  nself_kept = (int64_t)init.size();
   for (int k = 0; k < npair; k++)
-    init[nself + k] = make_int4(pair_cells[2 * k], pair_cells[2 * k + 1], GW_PAIR, 0);
+    if (own(pair_cells[2 * k]) || own(pair_cells[2 * k + 1]))
+      init.push_back(make_int4(pair_cells[2 * k], pair_cells[2 * k + 1], GW_PAIR, 0));
+  const int64_t ntask = (int64_t)init.size();
+  if (init.empty()) init.push_back(make_int4(0, 0, GW_PAIR, 0));
   SWH_TRY(g->wf0.reserve((size_t)std::max<int64_t>(1, ntask) * sizeof(int4)));
   if (ntask > 0)
     SWH_HIP(hipMemcpyAsync(g->wf0.ptr, init.data(), (size_t)ntask * sizeof(int4),
@@ -1592,9 +1595,10 @@ static swh_status device_walk(swh_gspace* g, const swh_grav_params* G, const int
   SWH_TRY(g->wrec.reserve((size_t)std::max(1, ncells) * sizeof(GWRec)));
   hipLaunchKernelGGL(gw_rec_kernel, dim3((ncells + 255) / 256), dim3(256), 0, st,
                      g->tree_d.as<const swh_gcell>(), g->mpoles.as<const swh_multipole>(),
-                     g->cell_act.as<const int8_t>(), ncells, g->wrec.as<GWRec>());
+                     g->cell_act.as<const int8_t>(),
+                     owns ? g->owned_d.as<const uint8_t>() : nullptr, ncells, g->wrec.as<GWRec>());
   SWH_HIP(hipGetLastError());
-  int64_t n_cur = ntask, n_self_cur = nself;
+  int64_t n_cur = ntask, n_self_cur = nself_kept;
   GWCnt h{};  // running totals: P-P and M-M entries, skipped pairs
   DevBuf* cur = &g->wf0;
   DevBuf* nxt = &g->wf1;
@@ -1758,6 +1762,8 @@ swh_status swh_gspace_set_tree(swh_gspace* g, const swh_gcell* cells, int32_t nc
   SWH_TRY(swh_gspace_set_leaves(g, ranges.data(), ncells, off.data(), nullptr, 0));
   SWH_HIP(hipSetDevice(g->ctx->device));
   g->tree.assign(cells, cells + ncells);
+  g->tree_parent = parent;
+  g->owned.clear();
   SWH_TRY(g->cell_act.reserve((size_t)std::max(1, ncells)));
   SWH_TRY(g->ftens.reserve((size_t)std::max(1, ncells) * SWH_MPOLE_TERMS * sizeof(double)));
   SWH_TRY(g->l2l_list.reserve(std::max<size_t>(1, l2l.size()) * sizeof(int2)));
@@ -1789,6 +1795,34 @@ swh_status swh_gspace_set_tree(swh_gspace* g, const swh_gcell* cells, int32_t nc
                            hipMemcpyHostToDevice, g->stream));
     SWH_HIP(hipStreamSynchronize(g->stream));
   }
+  return SWH_OK;
+}
+
+swh_status swh_gspace_set_owned_cells(swh_gspace* g, const uint8_t* owned, int32_t ncells) {
+  if (!g) return SWH_ERR_ARG;
+  if (!owned) {
+    g->owned.clear();
+    return SWH_OK;
+  }
+  if (ncells != (int32_t)g->tree.size()) {
+    set_error("set_owned_cells: %d cells, the tree has %zu (swh_gspace_set_tree first)", ncells,
+              g->tree.size());
+    return SWH_ERR_ARG;
+  }
+  for (int c = 0; c < ncells; c++) {
+    const int p = g->tree_parent[c];
+    if (p >= 0 && (owned[c] != 0) != (owned[p] != 0)) {
+      set_error("set_owned_cells: cell %d and its parent %d differ (own whole subtrees)", c, p);
+      return SWH_ERR_ARG;
+    }
+  }
+  SWH_HIP(hipSetDevice(g->ctx->device));
+  g->owned.assign(owned, owned + ncells);
+  for (auto& o : g->owned) o = o ? 1 : 0;
+  SWH_TRY(g->owned_d.reserve((size_t)std::max(1, ncells)));
+  SWH_HIP(hipMemcpyAsync(g->owned_d.ptr, g->owned.data(), (size_t)ncells, hipMemcpyHostToDevice,
+                         g->stream));
+  SWH_HIP(hipStreamSynchronize(g->stream));
   return SWH_OK;
 }
 
@@ -1866,6 +1900,7 @@ swh_status swh_grav_tree(swh_gspace* g, const swh_grav_params* G, const int32_t*
         w.cells = g->tree.data();
         w.mp = mp.data();
         w.act = act.data();
+        w.own = g->owned.empty() ? nullptr : g->owned.data();
         w.G = G;
         w.mac = mac;
         const int64_t t1 = std::min(ntask, (ch + 1) * kChunk);

@@ -246,6 +246,11 @@ struct swh_gspace {
   swh::DevBuf leaf_of;           // int per gpart: its unsplit cell (-1: none)
   int32_t nleaf_cells = 0;
   int32_t tree_max_leaf = 0;     // largest unsplit cell
+  std::vector<int32_t> tree_parent;  // -1 for a root
+  // ownership (swh_gspace_set_owned_cells): the walk emits P-P / M-M entries
+  // only for owned target cells (empty: every cell is owned)
+  std::vector<uint8_t> owned;
+  swh::DevBuf owned_d;
   // device walk (swh_grav_tree): the cell table, two frontiers of tasks, the
   // emitted P-P / M-M entries (keys cell << 32 | other, flags) and their
   // sorted copies, per-cell counts

@@ -247,3 +247,25 @@ def slab_local_set(parts: np.ndarray, rank: int, world: int, box_x: float, reach
     if halo_time_bin is not None:
         out["time_bin"][len(own_idx):] = halo_time_bin
     return out, len(own_idx)
+
+
+def gravity_owned_cells(cells: np.ndarray, tops, rank: int, world: int, box) -> np.ndarray:
+    """Tree-gravity ownership of one rank (swh_gspace_set_owned_cells): a top
+    cell belongs to the rank whose block holds its centre (the same block grid
+    as the hydro decomposition), and every cell to its top cell's owner
+    (whole subtrees). gparts and multipoles stay replicated on every rank
+    (i-cells owned, j-cells read-only), so no data moves while the
+    walk, P2P, M2P, M2L and the down pass run."""
+    dims = block_dims(world)
+    tops = np.asarray(tops, dtype=np.int64)
+    centre = np.asarray(cells["loc"][tops], dtype=np.float64) + 0.5 * np.asarray(
+        cells["width"][tops], dtype=np.float64)
+    own_top = block_of(centre, box, dims) == rank
+    owned = np.zeros(len(cells), dtype=np.uint8)
+    stack = [int(t) for t, o in zip(tops, own_top) if o]
+    while stack:
+        c = stack.pop()
+        owned[c] = 1
+        if cells["split"][c]:
+            stack.extend(int(p) for p in cells["progeny"][c] if p >= 0)
+    return owned

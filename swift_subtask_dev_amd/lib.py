@@ -41,7 +41,8 @@ HIP_SYMBOLS = [
     "swh_gspace_create",
     "swh_gspace_destroy", "swh_gspace_upload", "swh_gspace_set_leaves", "swh_grav_pp_batch",
     "swh_gspace_make_multipoles", "swh_space_upload_xparts", "swh_space_drift",
-    "swh_gspace_set_tree", "swh_grav_tree", "swh_gspace_field_tensors",
+    "swh_gspace_set_tree", "swh_gspace_set_owned_cells", "swh_grav_tree",
+    "swh_gspace_field_tensors",
     "swh_gspace_download", "swh_gspace_sync", "swh_gspace_pm_mesh",
 ]
 ADAPTER_SYMBOLS = [
@@ -130,6 +131,7 @@ def load() -> C.CDLL:
         "swh_grav_pp_batch": (C.c_int, [vp, P(abi.GravParams), P(i64), P(i64)]),
         "swh_gspace_make_multipoles": (C.c_int, [vp, vp]),
         "swh_gspace_set_tree": (C.c_int, [vp, vp, i32]),
+        "swh_gspace_set_owned_cells": (C.c_int, [vp, P(C.c_uint8), i32]),
         "swh_grav_tree": (C.c_int, [vp, P(abi.GravParams), vp, i32, vp, i32,
                                     P(abi.GravTreeStats)]),
         "swh_gspace_field_tensors": (C.c_int, [vp, vp]),
@@ -440,6 +442,18 @@ class GravSpace:
         assert cells.dtype.itemsize == C.sizeof(abi.GCell)
         self._tree = cells
         _check(self._lib.swh_gspace_set_tree(self.handle, _ptr(cells), len(cells)), "set_tree")
+
+    def set_owned_cells(self, owned):
+        """Per-cell ownership (uint8, whole subtrees; None: every cell) for a
+        step sharded over ranks (swh_gspace_set_owned_cells)."""
+        if owned is None:
+            _check(self._lib.swh_gspace_set_owned_cells(self.handle, None, 0), "set_owned_cells")
+            return
+        owned = np.ascontiguousarray(owned, dtype=np.uint8)
+        self._owned = owned
+        _check(self._lib.swh_gspace_set_owned_cells(
+            self.handle, owned.ctypes.data_as(C.POINTER(C.c_uint8)), len(owned)),
+            "set_owned_cells")
 
     def tree(self, G: abi.GravParams, self_cells, pair_cells) -> dict:
         """runner_doself_recursive_grav on self_cells, runner_dopair_recursive_grav

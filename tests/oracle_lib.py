@@ -75,6 +75,8 @@ def load(prec: str = "f32") -> C.CDLL:
     sig("grav_m2m", None, [vp, C.c_int, P(C.c_double), P(C.c_double), P(abi.Multipole)])
     sig("grav_tree", None, [vp, C.c_int, vp, C.c_int, vp, C.c_int, vp, C.c_int,
                             P(abi.GravParams), vp, vp])
+    sig("grav_tree_owned", None, [vp, C.c_int, vp, C.c_int, vp, C.c_int, vp, C.c_int,
+                                  P(abi.GravParams), vp, vp, vp])
     sig("pm_mesh", None, [vp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_float, vp])
     if prec == "f32":
         for n in ("iact_density", "iact_force", "iact_gradient"):

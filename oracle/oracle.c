@@ -2173,6 +2173,241 @@ API double orf_cellgrid_run(struct orf_cellgrid *g, struct runner *r, int loop,
   clock_gettime(CLOCK_MONOTONIC, &t1);
   return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
 }
+
+/* ------------------------------------------------------------------------ */
+/* CPU baseline on SWIFT's cell tree (clustered inputs): the top-level grid  */
+/* as above, each top cell split into octants while it holds more than      */
+/* splitsize particles (space_split, space_splitsize 400, space.h:49), every */
+/* cell sorted, and the tasks run through the DOSUB recursion              */
+/* (runner_doiact_functions_hydro.h:2524-2617 density, 2630-2720 force:     */
+/* recurse while cell_can_recurse_in_{self,pair}_hydro_task, cell.h:761-782, */
+/* over the touching progeny pairs of cell_split_pairs, cell.c:62; else the */
+/* DOSELF/DOPAIR branch). Scheduling as orf_cellgrid_run, so two threads    */
+/* never touch one top cell's subtree at once.                              */
+/* ------------------------------------------------------------------------ */
+struct orf_celltree {
+  int cdim;
+  struct cell *top;        /* cdim^3 top cells */
+  struct cell **blocks;    /* arena of progeny cells (stable addresses) */
+  int nblocks, used;       /* cells used in the last block */
+  long long ncells;
+  struct part *parts;      /* tree-ordered copy */
+  long long N;
+};
+#define ORF_ARENA 4096
+
+static struct cell *celltree_alloc(struct orf_celltree *t) {
+  if (t->nblocks == 0 || t->used == ORF_ARENA) {
+    t->blocks = (struct cell **)realloc(t->blocks, sizeof(struct cell *) * (size_t)(t->nblocks + 1));
+    t->blocks[t->nblocks++] = (struct cell *)calloc(ORF_ARENA, sizeof(struct cell));
+    t->used = 0;
+  }
+  t->ncells++;
+  return &t->blocks[t->nblocks - 1][t->used++];
+}
+
+static void celltree_hmax(struct cell *c) {
+  float hmax = 0.f;
+  for (int k = 0; k < c->hydro.count; k++)
+    if (c->hydro.parts[k].h > hmax) hmax = c->hydro.parts[k].h;
+  c->hydro.h_max = c->hydro.h_max_old = c->hydro.h_max_active = hmax;
+  c->hydro.ti_end_min = 8;
+  c->hydro.ti_old_part = 8;
+}
+
+/* space_split's octants: progeny k at ((k >> 2) & 1, (k >> 1) & 1, k & 1)
+ * half-widths from the cell's corner (space_split.c:233) */
+static void celltree_split(struct orf_celltree *t, struct cell *c, double box, int splitsize,
+                           int depth, struct part *tmp) {
+  if (c->hydro.count <= splitsize || depth >= 24) return;
+  const int n = c->hydro.count;
+  int cnt[9] = {0};
+  unsigned char *oct = (unsigned char *)malloc((size_t)n);
+  const double half[3] = {0.5 * c->width[0], 0.5 * c->width[1], 0.5 * c->width[2]};
+  for (int k = 0; k < n; k++) {
+    int o = 0;
+    for (int d = 0; d < 3; d++) {
+      const double xx = c->hydro.parts[k].x[d] - floor(c->hydro.parts[k].x[d] / box) * box;
+      o |= (xx >= c->loc[d] + half[d]) << (2 - d);
+    }
+    oct[k] = (unsigned char)o;
+    cnt[o + 1]++;
+  }
+  for (int o = 0; o < 8; o++) cnt[o + 1] += cnt[o];
+  int fill[8];
+  memcpy(fill, cnt, sizeof(fill));
+  for (int k = 0; k < n; k++) tmp[fill[oct[k]]++] = c->hydro.parts[k];
+  memcpy(c->hydro.parts, tmp, sizeof(struct part) * (size_t)n);
+  free(oct);
+  c->split = 1;
+  for (int o = 0; o < 8; o++) {
+    struct cell *p = celltree_alloc(t);
+    p->loc[0] = c->loc[0] + ((o >> 2) & 1) * half[0];
+    p->loc[1] = c->loc[1] + ((o >> 1) & 1) * half[1];
+    p->loc[2] = c->loc[2] + (o & 1) * half[2];
+    for (int d = 0; d < 3; d++) p->width[d] = half[d];
+    p->dmin = 0.5f * c->dmin;
+    p->parent = c;
+    p->hydro.parts = c->hydro.parts + cnt[o];
+    p->hydro.count = cnt[o + 1] - cnt[o];
+    celltree_hmax(p);
+    c->progeny[o] = p;
+    celltree_split(t, p, box, splitsize, depth + 1, tmp);
+  }
+}
+
+static void celltree_sort_all(struct cell *c) {
+  orf_cell_sort(c, 0x1FFF);
+  if (c->split)
+    for (int o = 0; o < 8; o++)
+      if (c->progeny[o]) celltree_sort_all(c->progeny[o]);
+}
+
+API struct orf_celltree *orf_celltree_new(const struct part *parts, long long N, double box,
+                                          int cdim, int splitsize) {
+  struct orf_celltree *t = (struct orf_celltree *)calloc(1, sizeof(*t));
+  struct orf_cellgrid *g = orf_cellgrid_new(parts, N, box, cdim);
+  /* take over the grid's top cells and particle copy; the top cells' sorts
+   * are rebuilt after the split reorders their particles */
+  const int nc = cdim * cdim * cdim;
+  for (int id = 0; id < nc; id++) orf_cell_free_sorts(&g->cells[id]);
+  t->cdim = cdim;
+  t->top = g->cells;
+  t->parts = g->parts;
+  t->N = N;
+  t->ncells = nc;
+  free(g);
+  struct part *tmp = (struct part *)malloc(sizeof(struct part) * (size_t)(N > 0 ? N : 1));
+  for (int id = 0; id < nc; id++) celltree_split(t, &t->top[id], box, splitsize, 0, tmp);
+  free(tmp);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int id = 0; id < nc; id++) celltree_sort_all(&t->top[id]);
+  return t;
+}
+
+static void celltree_free_sorts(struct cell *c) {
+  orf_cell_free_sorts(c);
+  if (c->split)
+    for (int o = 0; o < 8; o++)
+      if (c->progeny[o]) celltree_free_sorts(c->progeny[o]);
+}
+
+API void orf_celltree_free(struct orf_celltree *t) {
+  const int nc = t->cdim * t->cdim * t->cdim;
+  for (int id = 0; id < nc; id++) celltree_free_sorts(&t->top[id]);
+  for (int b = 0; b < t->nblocks; b++) free(t->blocks[b]);
+  free(t->blocks);
+  free(t->top);
+  free(t->parts);
+  free(t);
+}
+
+API long long orf_celltree_ncells(const struct orf_celltree *t) { return t->ncells; }
+API struct part *orf_celltree_parts(struct orf_celltree *t) { return t->parts; }
+
+/* cell_split_pairs (cell.c:62) as a set: the progeny pairs (pid of ci, pjd of
+ * cj) that touch across the face/edge/corner of direction sid */
+static int split_pairs_n[13], split_pairs_ij[13][16][2];
+static void split_pairs_make(void) {
+  for (int sid = 0; sid < 13; sid++) {
+    int n = 0;
+    for (int a = 0; a < 8; a++)
+      for (int b = 0; b < 8; b++) {
+        int ok = 1;
+        for (int k = 0; k < 3; k++) {
+          const int d = 2 * pair_dirs[sid][k] + ((b >> (2 - k)) & 1) - ((a >> (2 - k)) & 1);
+          if (d < -1 || d > 1) ok = 0;
+        }
+        if (ok) {
+          split_pairs_ij[sid][n][0] = a;
+          split_pairs_ij[sid][n][1] = b;
+          n++;
+        }
+      }
+    split_pairs_n[sid] = n;
+  }
+}
+
+static int can_recurse_pair(const struct cell *c) { /* cell.h:761-769 */
+  return c->split && (kernel_gamma * c->hydro.h_max_old + c->hydro.dx_max_part_old) < 0.5f * c->dmin;
+}
+static int can_recurse_self(const struct cell *c) { /* cell.h:778-782 */
+  return c->split && (kernel_gamma * c->hydro.h_max_old < 0.5f * c->dmin);
+}
+
+static void dosub_pair(struct runner *r, struct cell *ci, struct cell *cj, int loop) {
+  const struct engine *e = r->e;
+  if (!cell_is_active_hydro(ci, e) && !cell_is_active_hydro(cj, e)) return;
+  if (ci->hydro.count == 0 || cj->hydro.count == 0) return;
+  double shift[3];
+  const int sid = space_getsid(e->s, &ci, &cj, shift);
+  if (can_recurse_pair(ci) && can_recurse_pair(cj)) {
+    for (int k = 0; k < split_pairs_n[sid]; k++) {
+      struct cell *pi = ci->progeny[split_pairs_ij[sid][k][0]];
+      struct cell *pj = cj->progeny[split_pairs_ij[sid][k][1]];
+      if (pi && pj) dosub_pair(r, pi, pj, loop);
+    }
+  } else if (loop == LOOP_FORCE) {
+    orf_dopair2_branch(r, ci, cj);
+  } else {
+    orf_dopair1_branch(r, ci, cj, loop);
+  }
+}
+
+static void dosub_self(struct runner *r, struct cell *c, int loop) {
+  if (c->hydro.count == 0 || !cell_is_active_hydro(c, r->e)) return;
+  if (can_recurse_self(c)) {
+    for (int k = 0; k < 8; k++)
+      if (c->progeny[k]) {
+        dosub_self(r, c->progeny[k], loop);
+        for (int j = k + 1; j < 8; j++)
+          if (c->progeny[j]) dosub_pair(r, c->progeny[k], c->progeny[j], loop);
+      }
+  } else if (loop == LOOP_FORCE) {
+    orf_doself2_branch(r, c);
+  } else {
+    orf_doself1_branch(r, c, loop);
+  }
+}
+
+/* The density (loop 0) or force (loop 2) pass over the tree with `nthreads`
+ * threads; returns elapsed wall seconds. */
+API double orf_celltree_run(struct orf_celltree *t, struct runner *r, int loop, int nthreads) {
+  if (!split_pairs_n[12]) split_pairs_make();
+  const int cdim = t->cdim;
+  const int nc = cdim * cdim * cdim;
+  struct timespec t0, t1;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+  (void)nthreads;
+#endif
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+#pragma omp parallel
+  {
+#pragma omp for schedule(dynamic, 1)
+    for (int id = 0; id < nc; id++) dosub_self(r, &t->top[id], loop);
+    for (int d = 0; d < 13; d++) {
+      for (int par = 0; par < 8; par++) {
+        const int px = par & 1, py = (par >> 1) & 1, pz = (par >> 2) & 1;
+        const int h = cdim / 2;
+#pragma omp for schedule(dynamic, 1)
+        for (int q = 0; q < h * h * h; q++) {
+          const int cx = 2 * (q / (h * h)) + px;
+          const int cy = 2 * ((q / h) % h) + py;
+          const int cz = 2 * (q % h) + pz;
+          const int nx = (cx + pair_dirs[d][0] + cdim) % cdim;
+          const int ny = (cy + pair_dirs[d][1] + cdim) % cdim;
+          const int nz = (cz + pair_dirs[d][2] + cdim) % cdim;
+          dosub_pair(r, &t->top[(cx * cdim + cy) * cdim + cz],
+                     &t->top[(nx * cdim + ny) * cdim + nz], loop);
+        }
+      }
+    }
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+}
 #endif /* ORACLE_F32 */
 
 /* ======================================================================== */

@@ -104,6 +104,11 @@ def load(prec: str = "f32") -> C.CDLL:
         sig("cellgrid_free", None, [vp])
         sig("cellgrid_parts", vp, [vp])
         sig("cellgrid_run", C.c_double, [vp, vp, C.c_int, C.c_int])
+        sig("celltree_new", vp, [vp, i64, C.c_double, C.c_int, C.c_int])
+        sig("celltree_free", None, [vp])
+        sig("celltree_parts", vp, [vp])
+        sig("celltree_ncells", i64, [vp])
+        sig("celltree_run", C.c_double, [vp, vp, C.c_int, C.c_int])
     lib.pfx = pfx
     _libs[prec] = lib
     return lib

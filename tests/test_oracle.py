@@ -693,3 +693,62 @@ def test_m2m_equals_p2m_of_the_union():
     assert up.r_max <= corner * (1 + 1e-12)
     assert up.max_softening == max(m.max_softening for m in kids)
     assert up.min_old_a_grav_norm == min(m.min_old_a_grav_norm for m in kids)
+
+
+def test_celltree_dosub_matches_f64_on_clustered_box():
+    """The clustered config's CPU baseline (oracle celltree: top grid split to
+    <= splitsize, DOSUB recursion, runner_doiact_functions_hydro.h:2524-2720)
+    computes the f64 box loops' density and force: the float port to float
+    rounding, with h converged by the f64 ghost (clumps 10x denser)."""
+    from swift_subtask_dev_amd import abi, ics
+
+    parts = ics.clustered_box(14, n_clumps=3, per_clump=1200, seed=3)
+    P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
+    P.max_active_bin = 1
+    f64 = lambda n: O.fn("f64", n)  # noqa: E731
+    N = len(parts)
+    O.fn("f32", "init_parts")(parts.ctypes.data, N, C.byref(P))
+    f64("box_density")(parts.ctypes.data, N, C.byref(P), None)
+    nfail = C.c_longlong(0)
+    f64("box_ghost")(parts.ctypes.data, N, C.byref(P), C.byref(nfail))
+    assert parts["h"].max() > 5 * parts["h"].min()
+    parts["laplace_u"] = 0
+    f64("box_gradient")(parts.ctypes.data, N, C.byref(P), None)
+    f64("box_extra_ghost")(parts.ctypes.data, N, C.byref(P))
+    # reference: the f64 loops on the prepared state
+    dref, fref = parts.copy(), parts.copy()
+    O.fn("f32", "init_parts")(dref.ctypes.data, N, C.byref(P))
+    f64("box_density")(dref.ctypes.data, N, C.byref(P), None)
+    f64("box_force")(fref.ctypes.data, N, C.byref(P), None)
+    eb = abi.EngineBundle(dim=(1.0, 1.0, 1.0), periodic=True, params=P, max_active_bin=1)
+    H = 1.825742 * float(parts["h"].max())
+    cdim = int(1.0 / (H * 1.0001))
+    cdim -= cdim % 2
+    assert cdim >= 4
+    f32 = lambda n: O.fn("f32", n)  # noqa: E731
+
+    def tree_run(src, loop, split):
+        t = f32("celltree_new")(src.ctypes.data, N, 1.0, cdim, split)
+        try:
+            assert f32("celltree_ncells")(t) > cdim ** 3  # the clumps split
+            f32("celltree_run")(t, C.addressof(eb.runner), loop, 4)
+            buf = np.ctypeslib.as_array(C.cast(f32("celltree_parts")(t), C.POINTER(C.c_uint8)),
+                                        shape=(N * abi.PART_DTYPE.itemsize,))
+            out = buf.view(abi.PART_DTYPE).copy()
+        finally:
+            f32("celltree_free")(t)
+        return out[np.argsort(out["id"])]
+
+    dsrc = parts.copy()
+    O.fn("f32", "init_parts")(dsrc.ctypes.data, N, C.byref(P))
+    dr, fr = dref[np.argsort(dref["id"])], fref[np.argsort(fref["id"])]
+    for split in (400, 64):
+        d = tree_run(dsrc, 0, split)
+        for k in ("rho", "wcount", "div_v"):
+            scale = np.abs(dr[k]).max()
+            assert np.abs(d[k] - dr[k]).max() < 1e-5 * scale, (split, k)
+        f = tree_run(parts, 2, split)
+        assert np.array_equal(f["min_ngb_time_bin"], fr["min_ngb_time_bin"])
+        for k in ("a_hydro", "u_dt", "h_dt"):
+            scale = np.abs(fr[k]).max()
+            assert np.abs(f[k] - fr[k]).max() < 2e-4 * scale, (split, k)

@@ -146,6 +146,15 @@ __device__ __forceinline__ void list_flush(const ListDev& ld, LDS& L, int& nq, i
   wave_sync();
 }
 
+// Pad the staged region [nst, next multiple of kListBlk * 4) with candidates
+// that never hit (the consume blocks then need no bound test).
+template <class LDS>
+__device__ __forceinline__ void list_pad(LDS& L, int nst) {
+  const int lane = threadIdx.x & 63;
+  const int end = min((nst + kListBlk * 4 - 1) / (kListBlk * 4) * (kListBlk * 4), kListRegion);
+  if (nst + lane < end) L.cand[nst + lane] = make_float4(3e30f, 3e30f, 3e30f, -1.f);
+}
+
 // Phase A over the staged region [0, nst) for the list criterion, then flush.
 template <int LPI, bool WRAP, class LDS>
 __device__ __forceinline__ void list_consume(const GridDev& g, const ListDev& ld,
@@ -176,16 +185,27 @@ __device__ __forceinline__ void list_consume(const GridDev& g, const ListDev& ld
       float r2 = dx * dx;
       r2 = fmaf(dy, dy, r2);
       r2 = fmaf(dz, dz, r2);
-      hit[kk] = act & (c0 + kk * LPI < nst) & (r2 < fmaxf(thr_i, cv[kk].w));
+      // slots past nst hold far-away padding (list_build), which never hits
+      hit[kk] = act & ((r2 < thr_i) | (r2 < cv[kk].w));
       cnt += hit[kk] ? 1 : 0;
     }
     // this lane's first position in i's list: i's count + earlier sub-lanes' hits
-    int inc = cnt;
-    for (int o = 1; o < LPI; o <<= 1) {
-      const int tt = __shfl_up(inc, o, LPI);
-      if (s >= o) inc += tt;
+    int inc, tot;
+    if constexpr (LPI == 4) {  // quad scan by DPP quad permutes (no LDS round trip)
+      inc = cnt;
+      int tt = __builtin_amdgcn_mov_dpp(inc, 0x90, 0xF, 0xF, false);  // quad_perm [0,0,1,2]
+      inc += s >= 1 ? tt : 0;
+      tt = __builtin_amdgcn_mov_dpp(inc, 0x40, 0xF, 0xF, false);  // quad_perm [0,0,0,1]
+      inc += s >= 2 ? tt : 0;
+      tot = __builtin_amdgcn_mov_dpp(inc, 0xFF, 0xF, 0xF, false);  // quad_perm [3,3,3,3]
+    } else {
+      inc = cnt;
+      for (int o = 1; o < LPI; o <<= 1) {
+        const int tt = __shfl_up(inc, o, LPI);
+        if (s >= o) inc += tt;
+      }
+      tot = __shfl(inc, LPI - 1, LPI);
     }
-    const int tot = __shfl(inc, LPI - 1, LPI);
     int pos = il * LDS::kStride + nq + inc - cnt;
 #pragma unroll
     for (int kk = 0; kk < kListBlk; kk++) {
@@ -225,14 +245,16 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
   if (act) pi = a.pos[i];
   const double Ri = act ? pi.w * (double)kGamma * skin1 : 0.;
   // group box and reach (wave-uniform)
-  const double Rg = uni_d(wave_max_d(Ri));
+  // (the four lanes of an i hold the same values: quad-uniform reductions)
+  static_assert(LPI == 4, "quad_group_* reductions assume four lanes per i");
+  const double Rg = uni_d(quad_group_max_d(Ri));
   double lo[3], hi[3];
-  lo[0] = uni_d(wave_min_d(act ? pi.x : 1e300));
-  lo[1] = uni_d(wave_min_d(act ? pi.y : 1e300));
-  lo[2] = uni_d(wave_min_d(act ? pi.z : 1e300));
-  hi[0] = uni_d(wave_max_d(act ? pi.x : -1e300));
-  hi[1] = uni_d(wave_max_d(act ? pi.y : -1e300));
-  hi[2] = uni_d(wave_max_d(act ? pi.z : -1e300));
+  lo[0] = uni_d(quad_group_min_d(act ? pi.x : 1e300));
+  lo[1] = uni_d(quad_group_min_d(act ? pi.y : 1e300));
+  lo[2] = uni_d(quad_group_min_d(act ? pi.z : 1e300));
+  hi[0] = uni_d(quad_group_max_d(act ? pi.x : -1e300));
+  hi[1] = uni_d(quad_group_max_d(act ? pi.y : -1e300));
+  hi[2] = uni_d(quad_group_max_d(act ? pi.z : -1e300));
   TileStats ts;
   const int gbase = gid * kListSlots;
   int nq = 0, wr = 0;
@@ -339,6 +361,7 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
       wave_sync();
       for (int base = 0; base < total; base += 64 * kStageU) {
         if (nst > kListRegion - 64 * kStageU) {  // no room for this pass: consume the region
+          list_pad(L, nst);
           wave_sync();
           if (diag != 1) {
             if (wrap)
@@ -355,17 +378,27 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
         float4 q[kStageU];
         float4 off[kStageU];
         bool val[kStageU];
+        // largest cell k with pre[k] <= qq (pre is non-decreasing, pre[0] = 0):
+        // the kStageU searches step together, so each step is one LDS round
+        // trip for all of them
+        int kc[kStageU];
+#pragma unroll
+        for (int u = 0; u < kStageU; u++) kc[u] = 0;
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1) {
+          int pv[kStageU];
+#pragma unroll
+          for (int u = 0; u < kStageU; u++) pv[u] = L.cell_pre[kc[u] + st];
+#pragma unroll
+          for (int u = 0; u < kStageU; u++)
+            if (pv[u] <= base + 64 * u + lane) kc[u] += st;
+        }
 #pragma unroll
         for (int u = 0; u < kStageU; u++) {
           const int qq = base + 64 * u + lane;
           val[u] = qq < total;
-          // largest cell k with pre[k] <= qq (pre is non-decreasing, pre[0] = 0)
-          int k = 0;
-#pragma unroll
-          for (int st = 32; st > 0; st >>= 1)
-            if (L.cell_pre[k + st] <= qq) k += st;
-          jj[u] = val[u] ? L.cell_j0[k] + qq : 0;
-          off[u] = L.cell_off[k];
+          jj[u] = val[u] ? L.cell_j0[kc[u]] + qq : 0;
+          off[u] = L.cell_off[kc[u]];
         }
 #pragma unroll
         for (int u = 0; u < kStageU; u++)
@@ -402,6 +435,7 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
       }
       wave_sync();  // the next batch rewrites the cell table
     }
+    list_pad(L, nst);
     wave_sync();
     if (diag != 1 && nst > 0) {
       if (wrap)

@@ -63,6 +63,37 @@ __device__ __forceinline__ double wave_max_d(double v) {
   for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
   return v;
 }
+// Wave-uniform max / min of a double that is equal within each quad of
+// lanes (the list build's four lanes per i): two DPP mirrors combine the
+// quads of each 16-lane row, four readlanes the rows -- no LDS round trip
+// (__shfl_xor is a ds_bpermute).
+__device__ __forceinline__ double dpp_d(double v, int ctrl_is_mirror) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  int l2, h2;
+  if (ctrl_is_mirror) {
+    l2 = __builtin_amdgcn_mov_dpp(lo, 0x140, 0xF, 0xF, false);  // row_mirror
+    h2 = __builtin_amdgcn_mov_dpp(hi, 0x140, 0xF, 0xF, false);
+  } else {
+    l2 = __builtin_amdgcn_mov_dpp(lo, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    h2 = __builtin_amdgcn_mov_dpp(hi, 0x141, 0xF, 0xF, false);
+  }
+  return __hiloint2double(h2, l2);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+__device__ __forceinline__ double quad_group_max_d(double v) {
+  v = fmax(v, dpp_d(v, 0));
+  v = fmax(v, dpp_d(v, 1));
+  return fmax(fmax(readlane_d(v, 0), readlane_d(v, 16)), fmax(readlane_d(v, 32), readlane_d(v, 48)));
+}
+__device__ __forceinline__ double quad_group_min_d(double v) {
+  v = fmin(v, dpp_d(v, 0));
+  v = fmin(v, dpp_d(v, 1));
+  return fmin(fmin(readlane_d(v, 0), readlane_d(v, 16)), fmin(readlane_d(v, 32), readlane_d(v, 48)));
+}
+
 __device__ __forceinline__ int wave_max_i(int v) {
   for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
   return v;

@@ -375,7 +375,7 @@ typedef struct swh_space_info {
   double cell_width[3];
   double h_max;     /* max gamma*h at rebuild */
   int64_t loop_stats[4]; /* last counted search (tile loop or list build): candidates loaded,
-                            staged, phase-A wave steps, phase-B / flush wave steps */
+                            staged, test wave steps, list-flush lane steps */
   int64_t list_entries;  /* last counted list build: total entries */
   int32_t list_overflow; /* last counted list build: particles over list_capacity */
   int32_t list_valid;    /* the step's pair lists are current */

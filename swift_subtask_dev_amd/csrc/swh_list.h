@@ -131,14 +131,22 @@ template <int LPI, class LDS>
 __device__ __forceinline__ void list_flush(const ListDev& ld, LDS& L, int& nq, int& wr, int il,
                                            int s, int gbase, TileStats& ts) {
   wave_sync();  // list entries were written by the other lanes of i
-  const int nmax = uni_i(wave_max_i(nq));
-  ts.bsteps += (unsigned int)((nmax + LPI - 1) / LPI);
+  ts.bsteps += (unsigned int)(nq > s ? (nq - s + LPI - 1) / LPI : 0);  // this lane's entries
   const unsigned short* list = &L.hits[il * LDS::kStride];
   int* col = ld.nbr + list_col(gbase + il, ld.K);
   if (ld.diag != 2) {
-    for (int t = s; t < nq; t += LPI) {
-      const int k = wr + t;
-      if (k < ld.K) col[list_off(k)] = L.candj[list[t]];
+    // four entries per lane per step: their slot and index reads are
+    // independent, so a step costs two LDS round trips, not eight
+    const int nk = min(nq, ld.K - wr);  // entries past K are not stored
+    for (int t = s; t < nk; t += 4 * LPI) {
+      int sl[4], jv[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) sl[q] = t + q * LPI < nk ? list[t + q * LPI] : 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) jv[q] = L.candj[sl[q]];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (t + q * LPI < nk) col[list_off(wr + t + q * LPI)] = jv[q];
     }
   }
   wr += nq;
@@ -454,18 +462,19 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
   }
   if (counter) {
     unsigned long long v = (unsigned long long)((act && s == 0) ? wr : 0);
-    unsigned long long ld_ = ts.loaded, sg = ts.staged;
+    unsigned long long ld_ = ts.loaded, sg = ts.staged, fl = ts.bsteps;
     for (int o = 32; o > 0; o >>= 1) {
       v += __shfl_xor(v, o);
       ld_ += __shfl_xor(ld_, o);
       sg += __shfl_xor(sg, o);
+      fl += __shfl_xor(fl, o);
     }
     if (lane == 0) {
       atomicAdd(counter + 3, v);  // list entries
       atomicAdd(counter + 4, ld_);
       atomicAdd(counter + 5, sg);
       atomicAdd(counter + 6, (unsigned long long)ts.asteps);
-      atomicAdd(counter + 7, (unsigned long long)ts.bsteps);
+      atomicAdd(counter + 7, fl);  // lane flush steps
     }
   }
   BuildSlot b;

@@ -35,7 +35,7 @@ constexpr double kUnitRound = 5.9604644775390625e-8;   // u = 2^-24
 constexpr float kThrSlack = 1.f + 8.f * 5.9604645e-8f;  // (1 + 8u)
 
 // Work counters of a counted launch (swh_space_info.loop_stats): candidates
-// loaded, candidates staged, test wave steps and list-flush wave steps.
+// loaded, candidates staged, test wave steps and list-flush lane steps.
 struct TileStats {
   unsigned int loaded = 0, staged = 0, asteps = 0, bsteps = 0;
 };

@@ -97,7 +97,10 @@ struct ListLds {
   static constexpr int kICap = SWH_LIST_ICAP;           // LDS hits per i before a flush
   static_assert(kICap >= kListBlk * LPI, "one consume block must fit i's LDS hits");
   static constexpr int kStride = kICap + 2;  // odd dword stride: lists start on different banks
-  float4 cand[kListRegion];  // x, y, z relative to the box centre; w = inflated R_j^2
+  // staged candidates (SoA, so a lane's run of candidates reads as float4s and
+  // pairs of them feed the packed fp32 tests): x, y, z relative to the box
+  // centre, w = inflated R_j^2
+  float cx[kListRegion], cy[kListRegion], cz[kListRegion], cw[kListRegion];
   int candj[kListRegion];
   unsigned short hits[GS * kStride + 64];  // [i slot][entry] region slots; + per-lane dummies
   int cell_pre[64];     // staging batch: prefix sum of the cells' counts
@@ -160,7 +163,12 @@ template <class LDS>
 __device__ __forceinline__ void list_pad(LDS& L, int nst) {
   const int lane = threadIdx.x & 63;
   const int end = min((nst + kListBlk * 4 - 1) / (kListBlk * 4) * (kListBlk * 4), kListRegion);
-  if (nst + lane < end) L.cand[nst + lane] = make_float4(3e30f, 3e30f, 3e30f, -1.f);
+  if (nst + lane < end) {
+    L.cx[nst + lane] = 3e30f;
+    L.cy[nst + lane] = 3e30f;
+    L.cz[nst + lane] = 3e30f;
+    L.cw[nst + lane] = -1.f;
+  }
 }
 
 // Phase A over the staged region [0, nst) for the list criterion, then flush.
@@ -176,26 +184,44 @@ __device__ __forceinline__ void list_consume(const GridDev& g, const ListDev& ld
   const float bx = (float)g.dim[0], by = (float)g.dim[1], bz = (float)g.dim[2];
   for (int b = 0; b < nblk; b++) {
     if (__any(nq > LDS::kICap - kListBlk * LPI)) list_flush<LPI>(ld, L, nq, wr, il, s, gbase, ts);
-    const int c0 = b * kListBlk * LPI + s;
-    float4 cv[kListBlk];
+    // lane s of i tests the contiguous run c0 .. c0 + kListBlk - 1 (its hits
+    // come out in candidate order), two candidates per packed fp32 op
+    const int c0 = (b * LPI + s) * kListBlk;
+    static_assert(kListBlk == 8, "two float4 reads per coordinate");
+    float4 qx[2], qy[2], qz[2], qw[2];
 #pragma unroll
-    for (int kk = 0; kk < kListBlk; kk++) cv[kk] = L.cand[min(c0 + kk * LPI, kListRegion - 1)];
+    for (int h = 0; h < 2; h++) {
+      qx[h] = *reinterpret_cast<const float4*>(&L.cx[c0 + 4 * h]);
+      qy[h] = *reinterpret_cast<const float4*>(&L.cy[c0 + 4 * h]);
+      qz[h] = *reinterpret_cast<const float4*>(&L.cz[c0 + 4 * h]);
+      qw[h] = *reinterpret_cast<const float4*>(&L.cw[c0 + 4 * h]);
+    }
     bool hit[kListBlk];
     int cnt = 0;
+    const f32x2 xi2 = {xi, xi}, yi2 = {yi, yi}, zi2 = {zi, zi};
 #pragma unroll
-    for (int kk = 0; kk < kListBlk; kk++) {
-      float dx = xi - cv[kk].x, dy = yi - cv[kk].y, dz = zi - cv[kk].z;
+    for (int p = 0; p < kListBlk / 2; p++) {
+      const float4& X = qx[p >> 1];
+      const float4& Y = qy[p >> 1];
+      const float4& Z = qz[p >> 1];
+      const float4& W = qw[p >> 1];
+      const bool hi2 = p & 1;
+      f32x2 dx = xi2 - (hi2 ? f32x2{X.z, X.w} : f32x2{X.x, X.y});
+      f32x2 dy = yi2 - (hi2 ? f32x2{Y.z, Y.w} : f32x2{Y.x, Y.y});
+      f32x2 dz = zi2 - (hi2 ? f32x2{Z.z, Z.w} : f32x2{Z.x, Z.y});
+      const f32x2 w2 = hi2 ? f32x2{W.z, W.w} : f32x2{W.x, W.y};
       if (WRAP) {
-        if (c.full[0]) dx = wrap_nearest_f(dx, bx);
-        if (c.full[1]) dy = wrap_nearest_f(dy, by);
-        if (c.full[2]) dz = wrap_nearest_f(dz, bz);
+        if (c.full[0]) dx = f32x2{wrap_nearest_sel(dx.x, bx), wrap_nearest_sel(dx.y, bx)};
+        if (c.full[1]) dy = f32x2{wrap_nearest_sel(dy.x, by), wrap_nearest_sel(dy.y, by)};
+        if (c.full[2]) dz = f32x2{wrap_nearest_sel(dz.x, bz), wrap_nearest_sel(dz.y, bz)};
       }
-      float r2 = dx * dx;
-      r2 = fmaf(dy, dy, r2);
-      r2 = fmaf(dz, dz, r2);
-      // slots past nst hold far-away padding (list_build), which never hits
-      hit[kk] = act & ((r2 < thr_i) | (r2 < cv[kk].w));
-      cnt += hit[kk] ? 1 : 0;
+      f32x2 r2 = dx * dx;
+      r2 = __builtin_elementwise_fma(dy, dy, r2);
+      r2 = __builtin_elementwise_fma(dz, dz, r2);
+      // slots past nst hold far-away padding (list_pad), which never hits
+      hit[2 * p] = act & ((r2.x < thr_i) | (r2.x < w2.x));
+      hit[2 * p + 1] = act & ((r2.y < thr_i) | (r2.y < w2.y));
+      cnt += (hit[2 * p] ? 1 : 0) + (hit[2 * p + 1] ? 1 : 0);
     }
     // this lane's first position in i's list: i's count + earlier sub-lanes' hits
     int inc, tot;
@@ -217,7 +243,7 @@ __device__ __forceinline__ void list_consume(const GridDev& g, const ListDev& ld
     int pos = il * LDS::kStride + nq + inc - cnt;
 #pragma unroll
     for (int kk = 0; kk < kListBlk; kk++) {
-      L.hits[hit[kk] ? pos : dummy] = (unsigned short)(c0 + kk * LPI);
+      L.hits[hit[kk] ? pos : dummy] = (unsigned short)(c0 + kk);
       pos += hit[kk] ? 1 : 0;
     }
     nq += tot;
@@ -356,12 +382,8 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
           if (gx * gx + gy * gy + gz * gz > Rc * Rc * (1. + 1e-6)) cnt = 0;
         }
       }
-      int inc = cnt;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int tt = __shfl_up(inc, o);
-        if (lane >= o) inc += tt;
-      }
-      const int total = uni_i(__shfl(inc, 63));
+      const int inc = wave_incl_scan(cnt);
+      const int total = __builtin_amdgcn_readlane(inc, 63);
       wave_sync();
       L.cell_pre[lane] = inc - cnt;  // cells past ncells: pre = total (never found)
       L.cell_j0[lane] = j0 - (inc - cnt);
@@ -433,7 +455,10 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
           const unsigned long long m = __ballot(keep);
           if (keep) {
             const int slot = nst + __popcll(m & ((1ull << lane) - 1ull));
-            L.cand[slot] = cf;
+            L.cx[slot] = cf.x;
+            L.cy[slot] = cf.y;
+            L.cz[slot] = cf.z;
+            L.cw[slot] = cf.w;
             L.candj[slot] = jj[u];
           }
           nst += __popcll(m);

@@ -44,6 +44,15 @@ __device__ __forceinline__ float wrap_nearest_f(float d, float box) {
   return d > 0.5f * box ? d - box : (d < -0.5f * box ? d + box : d);
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));  // packed fp32 (v_pk_*)
+
+// The same nearest image by selects (no divergent branch).
+__device__ __forceinline__ float wrap_nearest_sel(float d, float box) {
+  const float hb = 0.5f * box;
+  d = d > hb ? d - box : d;
+  return d < -hb ? d + box : d;
+}
+
 __device__ __forceinline__ int uni_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ float uni_f(float v) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
@@ -92,6 +101,18 @@ __device__ __forceinline__ double quad_group_min_d(double v) {
   v = fmin(v, dpp_d(v, 0));
   v = fmin(v, dpp_d(v, 1));
   return fmin(fmin(readlane_d(v, 0), readlane_d(v, 16)), fmin(readlane_d(v, 32), readlane_d(v, 48)));
+}
+
+// Inclusive prefix sum over the 64 lanes by DPP (GFX9 row shifts within
+// each 16-lane row, then row_bcast:15 / row_bcast:31 across rows).
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return v;
 }
 
 __device__ __forceinline__ int wave_max_i(int v) {

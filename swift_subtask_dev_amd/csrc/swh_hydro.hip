@@ -144,7 +144,7 @@ void list_build_kernel(GridDev g, SoA a, ListDev ld,
 #define SWH_WALK_WPE 0
 #endif
 #ifndef SWH_WALK_WPE_DENS
-#define SWH_WALK_WPE_DENS SWH_WALK_WPE
+#define SWH_WALK_WPE_DENS 4
 #endif
 template <int LOOP, typename T>
 __global__ __launch_bounds__(256)
@@ -157,6 +157,21 @@ void walk_kernel(GridDev g, SoA a, ListDev ld, int i0, int n,
                                                    unsigned long long* counter,
                                                    int* __restrict__ ncount) {
   list_walk<LOOP, T, kWalkLpi>(g, a, ld, i0, n, max_active_bin, a2H, hmax_bits, counter, ncount);
+}
+
+// The density walk held to 4 waves/SIMD (its four entries in flight per lane
+// want 132 VGPRs, i.e. 3 waves; at <= 128 it runs 1.157 -> 1.10 ms per loop
+// at 128^3; the force walk already fits 128 and does not gain).
+template <typename T>
+__global__ __launch_bounds__(256)
+#if SWH_WALK_WPE_DENS > 0
+__attribute__((amdgpu_waves_per_eu(SWH_WALK_WPE_DENS)))
+#endif
+void density_walk_kernel(GridDev g, SoA a, ListDev ld, int i0, int n, int max_active_bin, T a2H,
+                         const unsigned int* __restrict__ hmax_bits, unsigned long long* counter,
+                         int* __restrict__ ncount) {
+  list_walk<LOOP_DENSITY, T, kWalkLpi>(g, a, ld, i0, n, max_active_bin, a2H, hmax_bits, counter,
+                                       ncount);
 }
 
 // The list's overflow particles (more than K hits: a large H in a dense
@@ -628,6 +643,7 @@ static ListDev list_dev(swh_space* s) {
   d.base = s->nbr_base.as<int>();
   d.reach = s->nbr_reach.as<float>();
   d.K = s->list_K;
+  d.KS = (s->list_K + 15) & ~15;
   d.skin1 = 1.f + s->list_skin_cur;
   d.rwrap_bits = rwrap_slot(s);
   d.ovf = s->nbr_ovf.as<int>();
@@ -646,7 +662,8 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
                               float skin, const unsigned int* run_if = nullptr) {
   const int K = s->tuning.list_capacity > 0 ? s->tuning.list_capacity : 128;
   s->list_skin_cur = skin;
-  SWH_TRY(s->nbr.reserve((size_t)std::max(1, s->ngroups) * K * kListSlots * sizeof(int)));
+  SWH_TRY(s->nbr.reserve((size_t)std::max(1, s->ngroups) * ((K + 15) & ~15) * kListSlots *
+                         sizeof(int)));
   if (K % 4 != 0) {
     set_error("list_capacity must be a multiple of 4");
     return SWH_ERR_ARG;
@@ -723,9 +740,14 @@ static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int
                        search_slot(s), max_active_bin, a2H, hmax_slot(s), ctr, ncount);
     return;
   }
-  hipLaunchKernelGGL((walk_kernel<LOOP, T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
-                     s->stream, gd, soa_of(s), ld, 0, nitems, max_active_bin, a2H, hmax_slot(s),
-                     ctr, ncount);
+  if (LOOP == LOOP_DENSITY && sizeof(T) == 8)  // (the fp32 walk would spill)
+    hipLaunchKernelGGL((density_walk_kernel<T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
+                       s->stream, gd, soa_of(s), ld, 0, nitems, max_active_bin, a2H,
+                       hmax_slot(s), ctr, ncount);
+  else
+    hipLaunchKernelGGL((walk_kernel<LOOP, T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
+                       s->stream, gd, soa_of(s), ld, 0, nitems, max_active_bin, a2H,
+                       hmax_slot(s), ctr, ncount);
   hipLaunchKernelGGL((overflow_kernel<LOOP, T>), dim3(64), dim3(block), 0, s->stream, gd,
                      soa_of(s), ld, ld.ovf, ld.ovf_n, max_active_bin, a2H, hmax_slot(s), ctr,
                      ncount);

@@ -49,12 +49,20 @@ constexpr int kListLpiBuild = 4;  // lanes per i in the list build
 constexpr int kListRegion = SWH_LIST_REGION;  // staged candidates per region of the build
 constexpr int kListBlk = 8;  // candidates per lane per test block of the build
 
-// First entry of a listed particle (`base` = group * kListSlots + slot) and
-// the offset of its entry k (module layout comment).
-__device__ __forceinline__ size_t list_col(int base, int K) {
-  return (size_t)(base >> 4) * (size_t)(kListSlots * K) + (size_t)((base & 15) * 4);
+// Layout of a group's lists: 16 slots x KS entries (KS = K rounded up to 16).
+// Entry k of slot sl is the m-th entry (m = k / 4) of walk lane s = k % 4 of
+// that slot; lane l = 4 sl + s keeps its entries 4w .. 4w + 3 in one 16-byte
+// word of window w (256 ints: one word per lane), so a walk lane reads four
+// indices with one load.
+__device__ __forceinline__ size_t list_lane(int base, int KS) {  // base = group * 16 + slot
+  return (size_t)(base >> 4) * (size_t)(kListSlots * KS) + (size_t)((base & 15) * 16);
 }
-__device__ __forceinline__ size_t list_off(int k) { return (size_t)((k >> 2) * 64 + (k & 3)); }
+__device__ __forceinline__ size_t list_off4(int s, int m) {
+  return (size_t)((m >> 2) * 256 + s * 4 + (m & 3));
+}
+__device__ __forceinline__ size_t list_at(int base, int KS, int k) {
+  return list_lane(base, KS) + list_off4(k & 3, k >> 2);
+}
 
 struct ListDev {
   int* nbr;      // entries: sorted j indices
@@ -63,6 +71,7 @@ struct ListDev {
   float* reach;  // per particle: R = gamma h (1 + skin) at build (0: not listed)
   const float4* posf;  // per particle: x, y, z relative to its grid cell's corner, h
   int K;
+  int KS;        // entries per slot in memory (K rounded up to 16)
   float skin1;   // 1 + skin
   const unsigned int* rwrap_bits;  // max R at build (float bits): particles farther than
                                    // this from every face need no periodic wrap
@@ -136,7 +145,7 @@ __device__ __forceinline__ void list_flush(const ListDev& ld, LDS& L, int& nq, i
   wave_sync();  // list entries were written by the other lanes of i
   ts.bsteps += (unsigned int)(nq > s ? (nq - s + LPI - 1) / LPI : 0);  // this lane's entries
   const unsigned short* list = &L.hits[il * LDS::kStride];
-  int* col = ld.nbr + list_col(gbase + il, ld.K);
+
   if (ld.diag != 2) {
     // four entries per lane per step: their slot and index reads are
     // independent, so a step costs two LDS round trips, not eight
@@ -149,7 +158,7 @@ __device__ __forceinline__ void list_flush(const ListDev& ld, LDS& L, int& nq, i
       for (int q = 0; q < 4; q++) jv[q] = L.candj[sl[q]];
 #pragma unroll
       for (int q = 0; q < 4; q++)
-        if (t + q * LPI < nk) col[list_off(wr + t + q * LPI)] = jv[q];
+        if (t + q * LPI < nk) ld.nbr[list_at(gbase + il, ld.KS, wr + t + q * LPI)] = jv[q];
     }
   }
   wr += nq;
@@ -517,49 +526,19 @@ __device__ __forceinline__ bool near_face(const GridDev& g, const double4& p, do
          (p.z > g.dim[2] - R);
 }
 
-// Walk entries s, s+LPI, ... of i's list (nl entries from list base lb):
-// indices are loaded four entries ahead, the particle data of the next entry
-// before this entry's math, so each lane keeps several independent loads in
-// flight (the list itself streams from HBM).
+// Walk entries s, s+LPI, ... of i's list (nl entries from list base lb),
+// four at a time: one 16-byte load gives a window's four indices (the next
+// window's is loaded ahead), then the four entries' particle data are loaded
+// together (only lanes that have them issue loads) and evaluated.
 template <int LPI, bool WRAP, typename T, class S>
 __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, const ListDev& ld,
                                              const double4& pi, int nl, int lb, int s, S& st) {
-  const int* __restrict__ col = ld.nbr + (nl > 0 ? list_col(lb, ld.K) : 0);
+  static_assert(LPI == 4, "the list layout gives each of four lanes per i its own windows");
   const int nme = nl > s ? (nl - s + LPI - 1) / LPI : 0;  // this lane's entries
-  auto idx = [&](int m) { return m < nme ? col[list_off(s + m * LPI)] : -1; };
-  // profiling only (diag 4): every entry loads the lane's first j's data, so
-  // the gathers hit one line while the arithmetic stays the same
-  const int jfix = ld.diag == 4 ? idx(0) : 0;
-  auto dj = [&](int j) { return ld.diag == 4 ? jfix : j; };
-  if constexpr (S::kPay > 1) {
-    // heavy j records (gradient, force): the index two entries ahead, the
-    // record loaded at its entry -- prefetching the record one entry ahead
-    // held 21 more VGPRs (force 148: 3 waves/SIMD); without it the force walk
-    // fits 4 waves/SIMD and runs 4.5% faster (1.042 -> 0.996 ms at 128^3)
-    int jn = idx(0), jn2 = idx(1);
-    for (int k = 0; k < nme; k++) {
-      const int j = jn;
-      jn = jn2;
-      jn2 = idx(k + 2);
-      const double4 pj = a.pos[dj(j)];
-      const JRec<S::kPay> rj = S::load_j(a, dj(j));
-      double dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
-      if (WRAP) {
-        dx = wrap_nearest(dx, g.dim[0]);
-        dy = wrap_nearest(dy, g.dim[1]);
-        dz = wrap_nearest(dz, g.dim[2]);
-      }
-      const T tdx = (T)dx, tdy = (T)dy, tdz = (T)dz;
-      const T r2 = tdx * tdx + tdy * tdy + tdz * tdz;
-      if (st.accept(j, pj, r2)) st.interact_staged(rj.p, rj.meta, pj, tdx, tdy, tdz, r2);
-    }
-    return;
-  }
+  const int nw = (nme + 3) >> 2;
+  if (nw == 0) return;
+  const int* __restrict__ lanep = ld.nbr + list_lane(lb, ld.KS) + s * 4;
   auto step = [&](int j, const double4& pj, const JRec<S::kPay>& rj) {
-    if (ld.diag == 3) {  // profiling only: the loads without the math
-      st.n += (pj.x + (double)rj.p[0].x > 1e300) ? 1 : 0;
-      return;
-    }
     double dx = pi.x - pj.x, dy = pi.y - pj.y, dz = pi.z - pj.z;
     if (WRAP) {
       dx = wrap_nearest(dx, g.dim[0]);
@@ -570,40 +549,44 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
     const T r2 = tdx * tdx + tdy * tdy + tdz * tdz;
     if (st.accept(j, pj, r2)) st.interact_staged(rj.p, rj.meta, pj, tdx, tdy, tdz, r2);
   };
-  // light j records (density): a software pipeline over three register
-  // slots, entry e in slot e % 3. A slot's particle data are loaded three
-  // entries before its math and its list index three entries before that.
-  // Every load is unconditional (indices past the list are clamped to its
-  // last entry), and each slot is refilled in place after its math, so the
-  // compiler emits no copy of an in-flight load. A rotating ring with
-  // conditional loads made it wait for every load it had just issued (the ISA
-  // showed s_waitcnt vmcnt(0) ahead of each entry's math), so the prefetch
-  // bought nothing.
-  if (nme <= 0) return;
-  const int last = nme - 1;
-  auto idx_c = [&](int m) { return col[list_off(s + min(m, last) * LPI)]; };
-  int x0 = idx_c(0), x1 = idx_c(1), x2 = idx_c(2);
-  int j0 = x0, j1 = x1, j2 = x2;
-  double4 p0 = a.pos[dj(j0)], p1 = a.pos[dj(j1)], p2 = a.pos[dj(j2)];
-  JRec<S::kPay> r0 = S::load_j(a, dj(j0)), r1 = S::load_j(a, dj(j1)), r2 = S::load_j(a, dj(j2));
-  x0 = idx_c(3);
-  x1 = idx_c(4);
-  x2 = idx_c(5);
-#define SWH_WALK_SLOT(K, E)                 \
-  {                                         \
-    if ((E) >= nme) break;                  \
-    step(j##K, p##K, r##K);                 \
-    j##K = x##K;                            \
-    p##K = a.pos[dj(j##K)];                 \
-    r##K = S::load_j(a, dj(j##K));          \
-    x##K = idx_c((E) + 6);                  \
+  int4 wv = *reinterpret_cast<const int4*>(lanep);
+  if constexpr (S::kPay > 1) {
+    // heavy records (gradient, force): one entry at a time, its record loaded
+    // at its entry (one record live: 4 waves/SIMD)
+    int4 cur = wv;
+#pragma unroll 1
+    for (int m = 0; m < nme; m++) {
+      const int q = m & 3;
+      if (q == 0) {
+        cur = wv;
+        if (m + 4 < nme) wv = *reinterpret_cast<const int4*>(lanep + ((m >> 2) + 1) * 256);
+      }
+      const int j = q == 0 ? cur.x : q == 1 ? cur.y : q == 2 ? cur.z : cur.w;
+      const double4 pj = a.pos[j];
+      const JRec<S::kPay> rj = S::load_j(a, j);
+      step(j, pj, rj);
+    }
+    return;
   }
-  for (int m = 0; m < nme; m += 3) {
-    SWH_WALK_SLOT(0, m)
-    SWH_WALK_SLOT(1, m + 1)
-    SWH_WALK_SLOT(2, m + 2)
+  for (int w = 0; w < nw; w++) {
+    const int jv[4] = {wv.x, wv.y, wv.z, wv.w};
+    if (w + 1 < nw) wv = *reinterpret_cast<const int4*>(lanep + (w + 1) * 256);
+    const int mrem = nme - 4 * w;  // entries of this window (>= 1)
+    {
+      double4 pj[4];
+      JRec<S::kPay> rj[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        if (q < mrem) {
+          pj[q] = a.pos[jv[q]];
+          rj[q] = S::load_j(a, jv[q]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (q < mrem) step(jv[q], pj[q], rj[q]);
+    }
   }
-#undef SWH_WALK_SLOT
 }
 
 // One loop over every active, listed particle: LPI lanes per i, 256/LPI

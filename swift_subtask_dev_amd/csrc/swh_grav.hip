@@ -727,7 +727,17 @@ swh_status swh_gspace_create(swh_context* ctx, swh_gspace** out) {
   SWH_HIP(hipSetDevice(ctx->device));
   auto* g = new swh_gspace();
   g->ctx = ctx;
-  const hipError_t e = hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking);
+  // The gravity step is a chain of small, dependent launches (the walk's
+  // levels, the P2P / M2P / M2L / down passes): its stream takes the highest
+  // priority, so a concurrent hydro loop (SWIFT runs both in one step) fills
+  // the CUs the chain leaves idle instead of delaying it. SWH_GRAV_STREAM_PRIORITY=0:
+  // default priority.
+  int least = 0, greatest = 0;
+  const char* pe = std::getenv("SWH_GRAV_STREAM_PRIORITY");
+  const bool high = !(pe && pe[0] == '0');
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e == hipSuccess)
+    e = hipStreamCreateWithPriority(&g->stream, hipStreamNonBlocking, high ? greatest : least);
   if (e != hipSuccess) {
     delete g;
     return SWH_ERR_HIP;

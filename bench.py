@@ -403,8 +403,10 @@ def step_breakdown(sp, P, stream, torch, local, reps=3):
 def steady_state(sp, P, stream, torch, local, n_owned, args, skin=None, steps=None):
     """K steps of drift + density + force on the device-resident box with the
     pair lists kept while valid (swh_tuning.list_keep). Drift velocities:
-    random, |v| ~ 1, dt so that the fastest particle moves `disp` h per step
-    (a Courant-limited subsonic flow moves < 0.05 h per step); the space is
+    random, |v| ~ 1, dt so that the fastest particle moves `disp` h_min per step
+    (a Courant-limited subsonic flow moves < 0.05 h per step; with the smallest
+    h, h_dt dt / h stays small for every particle, as SWIFT's time bins keep it,
+    so the predicted h of a clustered box stays finite); the space is
     re-binned every `rebin` steps (dx bound > half a cell). The K steps run
     twice from the same state: counted (exact interactions per step), then
     timed without counting; the list builds the device ran are reported."""
@@ -417,7 +419,7 @@ def steady_state(sp, P, stream, torch, local, n_owned, args, skin=None, steps=No
     xp = abi.new_xparts(n)
     xp["v_full"] = rng.normal(0.0, 0.577, (n, 3)).astype(np.float32)
     vmax = float(np.sqrt((xp["v_full"].astype(np.float64) ** 2).sum(axis=1)).max())
-    h = float(np.median(local["h"]))
+    h = float(np.min(local["h"][:n_owned]))
     dt = disp * h / vmax
     D = abi.DriftParams(dt, 0.0, 0.0, 0.0, 0.0)
     sp.set_tuning(args.cell_factor, args.loop_variant, args.group_size, args.cell_scale, 0,
@@ -1109,7 +1111,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "list_build_kernel + walk_kernel<DENSITY,double>",
+                "kernel": "list_build_kernel + density_walk_kernel<double>",
                 "achieved": achieved / 1e9,
                 "peak": HBM_PEAK / 1e9,
                 "unit": "GB/s",

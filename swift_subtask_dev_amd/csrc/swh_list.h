@@ -290,14 +290,15 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
   // group box and reach (wave-uniform)
   // (the four lanes of an i hold the same values: quad-uniform reductions)
   static_assert(LPI == 4, "quad_group_* reductions assume four lanes per i");
-  const double Rg = uni_d(quad_group_max_d(Ri));
+  // (readlane results: already wave-uniform)
+  const double Rg = quad_group_max_d(Ri);
   double lo[3], hi[3];
-  lo[0] = uni_d(quad_group_min_d(act ? pi.x : 1e300));
-  lo[1] = uni_d(quad_group_min_d(act ? pi.y : 1e300));
-  lo[2] = uni_d(quad_group_min_d(act ? pi.z : 1e300));
-  hi[0] = uni_d(quad_group_max_d(act ? pi.x : -1e300));
-  hi[1] = uni_d(quad_group_max_d(act ? pi.y : -1e300));
-  hi[2] = uni_d(quad_group_max_d(act ? pi.z : -1e300));
+  lo[0] = quad_group_min_d(act ? pi.x : 1e300);
+  lo[1] = quad_group_min_d(act ? pi.y : 1e300);
+  lo[2] = quad_group_min_d(act ? pi.z : 1e300);
+  hi[0] = quad_group_max_d(act ? pi.x : -1e300);
+  hi[1] = quad_group_max_d(act ? pi.y : -1e300);
+  hi[2] = quad_group_max_d(act ? pi.z : -1e300);
   TileStats ts;
   const int gbase = gid * kListSlots;
   int nq = 0, wr = 0;

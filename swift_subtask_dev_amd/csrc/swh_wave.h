@@ -92,15 +92,21 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
                           __builtin_amdgcn_readlane(__double2loint(v), l));
 }
+// (compare + select, not fmax/fmin: those canonicalize both operands first,
+// three v_max_f64 per call; the inputs here are finite coordinates and reaches)
+__device__ __forceinline__ double sel_max_d(double a, double b) { return b > a ? b : a; }
+__device__ __forceinline__ double sel_min_d(double a, double b) { return b < a ? b : a; }
 __device__ __forceinline__ double quad_group_max_d(double v) {
-  v = fmax(v, dpp_d(v, 0));
-  v = fmax(v, dpp_d(v, 1));
-  return fmax(fmax(readlane_d(v, 0), readlane_d(v, 16)), fmax(readlane_d(v, 32), readlane_d(v, 48)));
+  v = sel_max_d(v, dpp_d(v, 0));
+  v = sel_max_d(v, dpp_d(v, 1));
+  return sel_max_d(sel_max_d(readlane_d(v, 0), readlane_d(v, 16)),
+                   sel_max_d(readlane_d(v, 32), readlane_d(v, 48)));
 }
 __device__ __forceinline__ double quad_group_min_d(double v) {
-  v = fmin(v, dpp_d(v, 0));
-  v = fmin(v, dpp_d(v, 1));
-  return fmin(fmin(readlane_d(v, 0), readlane_d(v, 16)), fmin(readlane_d(v, 32), readlane_d(v, 48)));
+  v = sel_min_d(v, dpp_d(v, 0));
+  v = sel_min_d(v, dpp_d(v, 1));
+  return sel_min_d(sel_min_d(readlane_d(v, 0), readlane_d(v, 16)),
+                   sel_min_d(readlane_d(v, 32), readlane_d(v, 48)));
 }
 
 // Inclusive prefix sum over the 64 lanes by DPP (GFX9 row shifts within

@@ -255,17 +255,22 @@ __global__ void gpack_kernel(GLayout L, char* __restrict__ aos, int64_t n, GSoA 
 // runner_iact_grav_pp_full / _truncated (gravity_iact.h:47-135) for one
 // pair, fp64: h2 = max(eps_i^2, eps_j^2), h_inv = min(1/eps_i, 1/eps_j).
 template <bool TRUNC>
-__device__ __forceinline__ void p2p_pair(double dx, double dy, double dz, double h2,
-                                         double h_inv, double mass, double r_s_inv,
+__device__ __forceinline__ void p2p_pair(double dx, double dy, double dz, double e2i, double e2j,
+                                         double hvi, double hvj, double mass, double r_s_inv,
                                          double& ax, double& ay, double& az, double& pot) {
+  // The pair's softening is the larger of the two (h2 = max(eps_i^2, eps_j^2),
+  // h_inv = min(1/eps_i, 1/eps_j)); r2 >= h2 is tested as two compares and
+  // h_inv formed only for softened pairs -- fmax/fmin of doubles canonicalize
+  // both operands (three v_max_f64 each), a quarter of the pair's fp64 work.
   const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
   const double r_inv = rsqrt1_f64(r2 + (double)FLT_MIN);
   double f_ij, pot_ij;
-  if (r2 >= h2) {
+  if ((r2 >= e2i) & (r2 >= e2j)) {
     const double mr = mass * r_inv;
     f_ij = mr * (r_inv * r_inv);
     pot_ij = -mr;
   } else {
+    const double h_inv = hvj < hvi ? hvj : hvi;
     const double ui = r2 * r_inv * h_inv;
     const double mh = mass * h_inv;
     f_ij = mh * (h_inv * h_inv) * grav_force_eval(ui);
@@ -310,7 +315,7 @@ __device__ __forceinline__ void p2p_tile(const double* sx, const double* sy, con
       }
       double mass = act[k] ? mj : 0.;
       if (SELF) mass = t == self_local[k] ? 0. : mass;  // j == i: no term
-      p2p_pair<TRUNC>(dx, dy, dz, fmax(hi2[k], e2j), fmin(hv[k], hvj), mass, r_s_inv, ax[k],
+      p2p_pair<TRUNC>(dx, dy, dz, hi2[k], e2j, hv[k], hvj, mass, r_s_inv, ax[k],
                       ay[k], az[k], pot[k]);
     }
   }
@@ -509,10 +514,10 @@ __global__ __launch_bounds__(64) void p2p_small_kernel(
         }
         const double mass = (actp && t != self_local) ? (double)sm[t] : 0.;
         if (pr.truncated)
-          p2p_pair<true>(dx, dy, dz, fmax(hi2, se2[t]), fmin(hv, sh[t]), mass, r_s_inv, ax, ay,
+          p2p_pair<true>(dx, dy, dz, hi2, se2[t], hv, sh[t], mass, r_s_inv, ax, ay,
                          az, pot);
         else
-          p2p_pair<false>(dx, dy, dz, fmax(hi2, se2[t]), fmin(hv, sh[t]), mass, r_s_inv, ax, ay,
+          p2p_pair<false>(dx, dy, dz, hi2, se2[t], hv, sh[t], mass, r_s_inv, ax, ay,
                           az, pot);
       }
     }

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SWH_ABI_VERSION 7
+#define SWH_ABI_VERSION 8
 
 #if defined(__GNUC__)
 #define SWH_API __attribute__((visibility("default")))
@@ -61,7 +61,8 @@ typedef enum swh_status {
   SWH_ERR_NOT_CONVERGED = 5, /* "Smoothing length failed to converge" */
   SWH_ERR_NO_DEVICE = 6,     /* no usable gfx950 device */
   SWH_ERR_OOM = 7,           /* device allocation failed */
-  SWH_ERR_STATE = 8          /* call out of order (e.g. loop before rebuild) */
+  SWH_ERR_STATE = 8,         /* call out of order (e.g. loop before rebuild) */
+  SWH_BUSY = 9               /* swh_*_query: queued work still running (not an error) */
 } swh_status;
 
 typedef enum swh_precision { SWH_PRECISION_F64 = 0, SWH_PRECISION_F32 = 1 } swh_precision;
@@ -339,6 +340,13 @@ SWH_API swh_status swh_space_drift(swh_space *s, const swh_drift_params *D,
 
 /* Wait for all queued work on the space's stream. */
 SWH_API swh_status swh_space_sync(swh_space *s);
+/* Without waiting: SWH_OK when all queued work on the space's stream has
+ * finished, SWH_BUSY while it runs. The batch calls only enqueue (with NULL
+ * counters nothing waits), so a scheduler can start a phase as one task and
+ * let its CPU runners take other tasks, polling this where SWIFT's dependent
+ * task (e.g. the ghost after the density loop, engine_maketasks.c:2313-2316
+ * ghost_in/ghost_out) would become ready. */
+SWH_API swh_status swh_space_query(swh_space *s);
 
 /* Kernel-tuning knobs of the batch loops (bench/diagnostics). */
 typedef struct swh_tuning {
@@ -477,6 +485,8 @@ SWH_API swh_status swh_grav_tree(swh_gspace *g, const swh_grav_params *G,
  * grav_tensor's F order = swh_multipole::M's), after the down pass. */
 SWH_API swh_status swh_gspace_field_tensors(swh_gspace *g, float *out);
 SWH_API swh_status swh_gspace_sync(swh_gspace *g);
+/* Without waiting: SWH_OK when the gspace's stream is idle, SWH_BUSY otherwise. */
+SWH_API swh_status swh_gspace_query(swh_gspace *g);
 
 /* PM mesh gravity: pm_mesh_compute_potential's
  * non-distributed path, compute_potential_global (src/mesh_gravity.c:844-1041)

@@ -132,6 +132,7 @@ const char* swh_status_string(swh_status s) {
     case SWH_ERR_NO_DEVICE: return "no usable gfx950 device";
     case SWH_ERR_OOM: return "device out of memory";
     case SWH_ERR_STATE: return "call out of order";
+    case SWH_BUSY: return "busy (queued work still running)";
   }
   return "unknown";
 }

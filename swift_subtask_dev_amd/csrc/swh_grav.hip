@@ -966,6 +966,14 @@ swh_status swh_gspace_sync(swh_gspace* g) {
   return SWH_OK;
 }
 
+swh_status swh_gspace_query(swh_gspace* g) {
+  if (!g) return SWH_ERR_ARG;
+  const hipError_t e = hipStreamQuery(g->stream);
+  if (e == hipErrorNotReady) return SWH_BUSY;
+  SWH_HIP(e);
+  return SWH_OK;
+}
+
 }  // extern "C"
 
 // ===========================================================================

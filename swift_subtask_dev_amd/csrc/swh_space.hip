@@ -849,6 +849,14 @@ swh_status swh_space_sync(swh_space* s) {
   return SWH_OK;
 }
 
+swh_status swh_space_query(swh_space* s) {
+  if (!s) return SWH_ERR_ARG;
+  const hipError_t e = hipStreamQuery(s->stream);
+  if (e == hipErrorNotReady) return SWH_BUSY;
+  SWH_HIP(e);
+  return SWH_OK;
+}
+
 swh_status swh_space_upload_parts(swh_space* s, const void* parts, int64_t count,
                                   const swh_part_layout* PL, int on_device) {
   if (!s || (count > 0 && !parts) || count < 0 || count > INT32_MAX / 2 || !PL)

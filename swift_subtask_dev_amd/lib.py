@@ -36,14 +36,14 @@ HIP_SYMBOLS = [
     "swh_space_download_parts", "swh_space_count", "swh_space_rebuild", "swh_space_init_parts",
     "swh_space_reset_acceleration",
     "swh_density_loop", "swh_ghost", "swh_gradient_loop", "swh_extra_ghost", "swh_force_loop",
-    "swh_end_force", "swh_space_sync", "swh_space_set_tuning", "swh_space_get_info",
+    "swh_end_force", "swh_space_sync", "swh_space_query", "swh_space_set_tuning", "swh_space_get_info",
     "swh_space_set_owned", "swh_space_pack_halo", "swh_space_unpack_halo",
     "swh_gspace_create",
     "swh_gspace_destroy", "swh_gspace_upload", "swh_gspace_set_leaves", "swh_grav_pp_batch",
     "swh_gspace_make_multipoles", "swh_space_upload_xparts", "swh_space_drift",
     "swh_gspace_set_tree", "swh_gspace_set_owned_cells", "swh_grav_tree",
     "swh_gspace_field_tensors",
-    "swh_gspace_download", "swh_gspace_sync", "swh_gspace_pm_mesh",
+    "swh_gspace_download", "swh_gspace_sync", "swh_gspace_query", "swh_gspace_pm_mesh",
 ]
 ADAPTER_SYMBOLS = [
     "swifthip_swift_init", "swifthip_swift_finalize", "swifthip_swift_last_error",
@@ -69,6 +69,9 @@ class SwhError(RuntimeError):
 _lib = None
 _adapter = None
 
+
+
+SWH_BUSY = 9  # swh_*_query: queued work still running
 
 def load() -> C.CDLL:
     """Load libswifthip.so (raises if it was not built)."""
@@ -117,6 +120,7 @@ def load() -> C.CDLL:
         "swh_force_loop": (C.c_int, [vp, P(abi.HydroParams), P(i64)]),
         "swh_end_force": (C.c_int, [vp, P(abi.HydroParams)]),
         "swh_space_sync": (C.c_int, [vp]),
+        "swh_space_query": (C.c_int, [vp]),
         "swh_space_set_owned": (C.c_int, [vp, i64]),
         "swh_space_pack_halo": (C.c_int, [vp, vp, i32, vp]),
         "swh_space_unpack_halo": (C.c_int, [vp, vp, i32, vp, C.c_int]),
@@ -137,6 +141,7 @@ def load() -> C.CDLL:
         "swh_gspace_field_tensors": (C.c_int, [vp, vp]),
         "swh_gspace_download": (C.c_int, [vp, vp, P(abi.GPartLayout), C.c_int]),
         "swh_gspace_sync": (C.c_int, [vp]),
+        "swh_gspace_query": (C.c_int, [vp]),
         "swh_gspace_pm_mesh": (C.c_int, [vp, P(abi.PMParams), vp]),
     }
     for name, (res, args) in sigs.items():
@@ -348,6 +353,14 @@ class HydroSpace:
     def sync(self):
         _check(self._lib.swh_space_sync(self.handle), "sync")
 
+    def done(self) -> bool:
+        """swh_space_query: True once the queued work has finished (no wait)."""
+        r = self._lib.swh_space_query(self.handle)
+        if r == SWH_BUSY:
+            return False
+        _check(r, "query")
+        return True
+
     def upload_xparts(self, xparts: np.ndarray):
         """struct xpart array (abi.XPART_DTYPE), same order/count as the parts."""
         XL = abi.XPartLayout(abi.XPART_DTYPE.itemsize, abi.XPART_DTYPE.fields["v_full"][1],
@@ -479,6 +492,14 @@ class GravSpace:
 
     def sync(self):
         _check(self._lib.swh_gspace_sync(self.handle), "gspace_sync")
+
+    def done(self) -> bool:
+        """swh_gspace_query: True once the queued work has finished (no wait)."""
+        r = self._lib.swh_gspace_query(self.handle)
+        if r == SWH_BUSY:
+            return False
+        _check(r, "gspace_query")
+        return True
 
     def pm_mesh(self, N: int, box_size: float, r_s: float, const_G: float = 1.0,
                 want_potential: bool = False):

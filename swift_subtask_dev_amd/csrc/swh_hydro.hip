@@ -649,6 +649,7 @@ static ListDev list_dev(swh_space* s) {
   d.ovf = s->nbr_ovf.as<int>();
   d.posf = s->posf.as<const float4>();
   d.diag = s->tuning.diag_mode;
+  d.gbox = s->gbox.as<const GroupBox>();
   d.ovf_n = ovf_slot(s);
   // per-cell reach pruning only pays on an adaptive (clustered) grid
   d.cell_R = s->grid.adaptive ? s->cell_hreach.as<const float>() : nullptr;
@@ -692,10 +693,15 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
   hipLaunchKernelGGL(list_prep_kernel, dim3(1), dim3(64), 0, s->stream, hmax_slot(s),
                      kGamma * ld.skin1, (float)s->grid.dx, rwrap_slot(s), rwrap_base_slot(s),
                      ovf_slot(s), run_if, nbuild_slot(s));
+  SWH_TRY(s->gbox.reserve((size_t)std::max(1, s->ngroups) * sizeof(GroupBox)));
+  ListDev ldb = list_dev(s);
+  hipLaunchKernelGGL(group_box_kernel, dim3((s->ngroups + 255) / 256), dim3(256), 0, s->stream,
+                     soa_of(s), s->groups.as<const int2>(), s->ngroups, P->max_active_bin,
+                     (double)ld.skin1, s->gbox.as<GroupBox>(), run_if);
   hipLaunchKernelGGL(list_build_kernel, dim3(s->ngroups), dim3(64), 0, s->stream, grid_dev(s),
-                     soa_of(s), ld, s->groups.as<const int2>(), 0, s->ngroups, P->max_active_bin,
-                     hmax_slot(s), count ? counter_slot(s) : nullptr, s->tuning.diag_mode,
-                     run_if);
+                     soa_of(s), ldb, s->groups.as<const int2>(), 0, s->ngroups,
+                     P->max_active_bin, hmax_slot(s), count ? counter_slot(s) : nullptr,
+                     s->tuning.diag_mode, run_if);
   SWH_HIP(hipGetLastError());
   s->list_valid = true;
   s->list_check = false;

@@ -64,6 +64,14 @@ __device__ __forceinline__ size_t list_at(int base, int KS, int k) {
   return list_lane(base, KS) + list_off4(k & 3, k >> 2);
 }
 
+// Per i-group box of the list build (group_box_kernel): the active
+// particles' bounding box and the largest R = gamma h (1 + skin); Rg = 0: no
+// active particle. One thread per group computes it, so the build's waves
+// read it with scalar loads instead of reducing across lanes.
+struct GroupBox {
+  double lo[3], hi[3], Rg, pad;
+};
+
 struct ListDev {
   int* nbr;      // entries: sorted j indices
   int* cnt;      // per particle: entries found (> K: overflow, searched instead)
@@ -80,7 +88,34 @@ struct ListDev {
   const float* cell_R;  // per linear grid cell: max R of its particles (cell_reach_kernel);
                         // null on a uniform grid (no per-cell pruning)
   int diag;      // profiling only: 2 = the build writes no entries
+  const GroupBox* gbox;  // per group (group_box_kernel), read by the build
 };
+
+__global__ void group_box_kernel(SoA a, const int2* __restrict__ groups, int ngroups,
+                                 int max_active_bin, double gs1, GroupBox* __restrict__ out,
+                                 const unsigned int* run_if) {
+  const int gidx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gidx >= ngroups || (run_if && *run_if == 0u)) return;
+  const int2 gr = groups[gidx];
+  GroupBox b;
+  b.lo[0] = b.lo[1] = b.lo[2] = 1e300;
+  b.hi[0] = b.hi[1] = b.hi[2] = -1e300;
+  b.Rg = 0.;
+  b.pad = 0.;
+  for (int i = gr.x; i < gr.x + gr.y; i++) {
+    if (!active_part(a, i, max_active_bin)) continue;
+    const double4 p = a.pos[i];
+    b.lo[0] = p.x < b.lo[0] ? p.x : b.lo[0];
+    b.lo[1] = p.y < b.lo[1] ? p.y : b.lo[1];
+    b.lo[2] = p.z < b.lo[2] ? p.z : b.lo[2];
+    b.hi[0] = p.x > b.hi[0] ? p.x : b.hi[0];
+    b.hi[1] = p.y > b.hi[1] ? p.y : b.hi[1];
+    b.hi[2] = p.z > b.hi[2] ? p.z : b.hi[2];
+    const double R = p.w * (double)kGamma * gs1;
+    b.Rg = R > b.Rg ? R : b.Rg;
+  }
+  out[gidx] = b;
+}
 
 // Per-cell maximum R = gamma h (1 + skin): the list build skips a cell whose
 // box lies farther than max(R_group, R_cell) from the group box (SWIFT's
@@ -288,17 +323,10 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
   if (act) pi = a.pos[i];
   const double Ri = act ? pi.w * (double)kGamma * skin1 : 0.;
   // group box and reach (wave-uniform)
-  // (the four lanes of an i hold the same values: quad-uniform reductions)
-  static_assert(LPI == 4, "quad_group_* reductions assume four lanes per i");
-  // (readlane results: already wave-uniform)
-  const double Rg = quad_group_max_d(Ri);
-  double lo[3], hi[3];
-  lo[0] = quad_group_min_d(act ? pi.x : 1e300);
-  lo[1] = quad_group_min_d(act ? pi.y : 1e300);
-  lo[2] = quad_group_min_d(act ? pi.z : 1e300);
-  hi[0] = quad_group_max_d(act ? pi.x : -1e300);
-  hi[1] = quad_group_max_d(act ? pi.y : -1e300);
-  hi[2] = quad_group_max_d(act ? pi.z : -1e300);
+  const GroupBox gb = ld.gbox[gid < ngroups ? gid : 0];
+  const double Rg = gid < ngroups ? gb.Rg : 0.;
+  const double lo[3] = {gb.lo[0], gb.lo[1], gb.lo[2]};
+  const double hi[3] = {gb.hi[0], gb.hi[1], gb.hi[2]};
   TileStats ts;
   const int gbase = gid * kListSlots;
   int nq = 0, wr = 0;

@@ -481,9 +481,31 @@ SWH_API swh_status swh_grav_tree(swh_gspace *g, const swh_grav_params *G,
                                  const int32_t *self_cells, int32_t nself,
                                  const int32_t *pair_cells, int32_t npair,
                                  swh_grav_tree_stats *stats);
+/* The same tasks with flags: SWH_TREE_NO_DOWN leaves out the down pass, so
+ * the field tensors hold each cell's M2L sums (runner_doself/dopair_
+ * recursive_grav only accumulate into c->grav.multipole->pot; SWIFT's
+ * runner_do_grav_down task pushes them down later: swh_gspace_grav_down). */
+#define SWH_TREE_NO_DOWN 1
+SWH_API swh_status swh_grav_tree_tasks(swh_gspace *g, const swh_grav_params *G,
+                                       const int32_t *self_cells, int32_t nself,
+                                       const int32_t *pair_cells, int32_t npair, int32_t flags,
+                                       swh_grav_tree_stats *stats);
 /* Field tensors of the last swh_grav_tree (35 floats per cell, struct
  * grav_tensor's F order = swh_multipole::M's), after the down pass. */
 SWH_API swh_status swh_gspace_field_tensors(swh_gspace *g, float *out);
+/* The tree cells' multipoles (after swh_grav_tree, or as given). */
+SWH_API swh_status swh_gspace_multipoles(swh_gspace *g, swh_multipole *out);
+/* Use the caller's multipoles for the cells of the current tree (SWIFT's
+ * c->grav.multipole, drifted by its own tasks) instead of building them from
+ * the gparts; valid until the next swh_gspace_set_tree. */
+SWH_API swh_status swh_gspace_set_multipoles(swh_gspace *g, const swh_multipole *in);
+/* runner_do_grav_down (runner_doiact_grav.c:65-164) over the current tree:
+ * fields = each cell's field tensor (35 floats per cell, as
+ * swh_gspace_field_tensors); L2L into the progeny depth by depth, L2P into the
+ * active gparts of the leaves; swh_gspace_download adds the accelerations and
+ * potentials, swh_gspace_field_tensors returns the pushed-down tensors. */
+SWH_API swh_status swh_gspace_grav_down(swh_gspace *g, const swh_grav_params *G,
+                                        const float *fields);
 SWH_API swh_status swh_gspace_sync(swh_gspace *g);
 /* Without waiting: SWH_OK when the gspace's stream is idle, SWH_BUSY otherwise. */
 SWH_API swh_status swh_gspace_query(swh_gspace *g);

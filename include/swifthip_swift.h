@@ -16,6 +16,9 @@
  *   runner_dosub_subset_density         src/runner_doiact_hydro.h:172-191 -> DOSUB_*
  *   runner_doself_grav_pp               src/runner_doiact_grav.h:41     (runner_doiact_grav.c:1788)
  *   runner_dopair_grav_pp               src/runner_doiact_grav.h:44-50  (runner_doiact_grav.c:1202)
+ *   runner_doself_recursive_grav,       src/runner_doiact_grav.h:33-37  (runner_doiact_grav.c:2386,
+ *   runner_dopair_recursive_grav,                                        2208, 65)
+ *   runner_do_grav_down                 src/runner_doiact_grav.h:28
  *
  * Inside a SWIFT build these are compiled against SWIFT's headers and linked
  * instead of the CPU template instances; in this repo they are
@@ -87,6 +90,11 @@ SWHS_API void runner_dosub_subset_density(struct runner *r, struct cell *ci,
                                           struct part *parts, int *ind, int count,
                                           struct cell *cj, int gettimer);
 SWHS_API void runner_doself_grav_pp(struct runner *r, struct cell *c);
+/* the recursive gravity tasks and the down pass (src/runner_doiact_grav.h:28-37) */
+SWHS_API void runner_doself_recursive_grav(struct runner *r, struct cell *c, int gettimer);
+SWHS_API void runner_dopair_recursive_grav(struct runner *r, struct cell *ci, struct cell *cj,
+                                           int gettimer);
+SWHS_API void runner_do_grav_down(struct runner *r, struct cell *c, int timer);
 SWHS_API void runner_dopair_grav_pp(struct runner *r, struct cell *ci, struct cell *cj,
                                     const int symmetric, const int allow_mpole);
 

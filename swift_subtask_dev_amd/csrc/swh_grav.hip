@@ -1708,6 +1708,7 @@ extern "C" {
 
 swh_status swh_gspace_set_tree(swh_gspace* g, const swh_gcell* cells, int32_t ncells) {
   if (!g || ncells < 0 || (ncells > 0 && !cells)) return SWH_ERR_ARG;
+  g->mpoles_given = false;
   std::vector<int> parent(ncells, -1);
   for (int c = 0; c < ncells; c++) {
     const swh_gcell& C = cells[c];
@@ -1849,9 +1850,72 @@ swh_status swh_gspace_set_owned_cells(swh_gspace* g, const uint8_t* owned, int32
   return SWH_OK;
 }
 
+// The multipoles of the tree's cells: P2M at the leaves, M2M up the tree
+// (space_split.c:340-440), unless the caller gave them.
+static swh_status tree_multipoles(swh_gspace* g) {
+  const int ncells = (int)g->tree.size();
+  SWH_TRY(g->mpoles.reserve((size_t)ncells * sizeof(swh_multipole)));
+  if (g->mpoles_given) return SWH_OK;
+  if (g->nleaf_cells > 0)
+    hipLaunchKernelGGL(p2m_kernel, dim3((g->nleaf_cells + kP2MWaves - 1) / kP2MWaves), dim3(64 * kP2MWaves), 0, g->stream,
+                       g->layout, g->aos.as<const char>(), g->leaves.as<const swh_leaf>(),
+                       g->leaf_ids.as<const int>(), g->nleaf_cells, g->mpoles.as<swh_multipole>());
+  for (size_t d = 0; d + 1 < g->m2m_depth_off.size(); d++) {
+    const int o0 = g->m2m_depth_off[d], o1 = g->m2m_depth_off[d + 1];
+    if (o1 > o0)
+      hipLaunchKernelGGL(m2m_kernel, dim3((o1 - o0 + 63) / 64), dim3(64), 0, g->stream,
+                         g->m2m_list.as<const int>() + o0, o1 - o0,
+                         g->tree_d.as<const swh_gcell>(), g->mpoles.as<swh_multipole>());
+  }
+  SWH_HIP(hipGetLastError());
+  return SWH_OK;
+}
+
+// The down pass (runner_do_grav_down, runner_doiact_grav.c:65-164): L2L from
+// every cell into its progeny, depth by depth, then L2P at the leaves. A cell
+// whose tensor received nothing holds zeros, so pushing it changes nothing,
+// as the reference's `interacted` test skips it.
+static swh_status tree_down(swh_gspace* g) {
+  const bool f64 = g->ctx->precision == SWH_PRECISION_F64;
+  for (size_t d = 0; d + 1 < g->l2l_depth_off.size(); d++) {
+    const int o0 = g->l2l_depth_off[d], o1 = g->l2l_depth_off[d + 1];
+    if (o1 <= o0) continue;
+    const int2* lst = g->l2l_list.as<const int2>() + o0;
+    if (f64)
+      hipLaunchKernelGGL((l2l_kernel<double>), dim3((o1 - o0 + 63) / 64), dim3(64), 0,
+                         g->stream, lst, o1 - o0, g->mpoles.as<const swh_multipole>(),
+                         g->ftens.as<double>());
+    else
+      hipLaunchKernelGGL((l2l_kernel<float>), dim3((o1 - o0 + 63) / 64), dim3(64), 0,
+                         g->stream, lst, o1 - o0, g->mpoles.as<const swh_multipole>(),
+                         g->ftens.as<double>());
+    SWH_HIP(hipGetLastError());
+  }
+  if (g->nleaf_cells > 0) {
+    const dim3 pg((unsigned)((g->n + 255) / 256));
+    if (f64)
+      hipLaunchKernelGGL((l2p_part_kernel<double>), pg, dim3(256), 0, g->stream, g->n,
+                         g->leaf_of.as<const int>(), g->mpoles.as<const swh_multipole>(),
+                         g->ftens.as<const double>(), gsoa_of(g));
+    else
+      hipLaunchKernelGGL((l2p_part_kernel<float>), pg, dim3(256), 0, g->stream, g->n,
+                         g->leaf_of.as<const int>(), g->mpoles.as<const swh_multipole>(),
+                         g->ftens.as<const double>(), gsoa_of(g));
+    SWH_HIP(hipGetLastError());
+  }
+  return SWH_OK;
+}
+
 swh_status swh_grav_tree(swh_gspace* g, const swh_grav_params* G, const int32_t* self_cells,
                          int32_t nself, const int32_t* pair_cells, int32_t npair,
                          swh_grav_tree_stats* stats) {
+  return swh_grav_tree_tasks(g, G, self_cells, nself, pair_cells, npair, 0, stats);
+}
+
+swh_status swh_grav_tree_tasks(swh_gspace* g, const swh_grav_params* G,
+                               const int32_t* self_cells, int32_t nself,
+                               const int32_t* pair_cells, int32_t npair, int32_t flags,
+                               swh_grav_tree_stats* stats) {
   if (!g || !G || nself < 0 || npair < 0 || (nself > 0 && !self_cells) ||
       (npair > 0 && !pair_cells))
     return SWH_ERR_ARG;
@@ -1878,19 +1942,7 @@ swh_status swh_grav_tree(swh_gspace* g, const swh_grav_params* G, const int32_t*
     for (auto& e : ev) SWH_HIP(hipEventCreate(&e));
     SWH_HIP(hipEventRecord(ev[0], g->stream));
   }
-  SWH_TRY(g->mpoles.reserve((size_t)ncells * sizeof(swh_multipole)));
-  if (g->nleaf_cells > 0)
-    hipLaunchKernelGGL(p2m_kernel, dim3((g->nleaf_cells + kP2MWaves - 1) / kP2MWaves), dim3(64 * kP2MWaves), 0, g->stream,
-                       g->layout, g->aos.as<const char>(), g->leaves.as<const swh_leaf>(),
-                       g->leaf_ids.as<const int>(), g->nleaf_cells, g->mpoles.as<swh_multipole>());
-  for (size_t d = 0; d + 1 < g->m2m_depth_off.size(); d++) {
-    const int o0 = g->m2m_depth_off[d], o1 = g->m2m_depth_off[d + 1];
-    if (o1 > o0)
-      hipLaunchKernelGGL(m2m_kernel, dim3((o1 - o0 + 63) / 64), dim3(64), 0, g->stream,
-                         g->m2m_list.as<const int>() + o0, o1 - o0,
-                         g->tree_d.as<const swh_gcell>(), g->mpoles.as<swh_multipole>());
-  }
-  SWH_HIP(hipGetLastError());
+  SWH_TRY(tree_multipoles(g));
   if (stats) SWH_HIP(hipEventRecord(ev[1], g->stream));
   hipLaunchKernelGGL(cell_active_kernel, dim3(ncells), dim3(256), 0, g->stream,
                      g->leaves.as<const swh_leaf>(), g->active.as<const int8_t>(),
@@ -2008,33 +2060,9 @@ swh_status swh_grav_tree(swh_gspace* g, const swh_grav_params* G, const int32_t*
                          (double)G->dim[1], (double)G->dim[2], (float)G->r_s_inv,
                          g->ftens.as<double>());
     SWH_HIP(hipGetLastError());
-    // down pass: L2L depth by depth, then L2P at the leaves
-    for (size_t d = 0; d + 1 < g->l2l_depth_off.size(); d++) {
-      const int o0 = g->l2l_depth_off[d], o1 = g->l2l_depth_off[d + 1];
-      if (o1 <= o0) continue;
-      const int2* lst = g->l2l_list.as<const int2>() + o0;
-      if (f64)
-        hipLaunchKernelGGL((l2l_kernel<double>), dim3((o1 - o0 + 63) / 64), dim3(64), 0,
-                           g->stream, lst, o1 - o0, g->mpoles.as<const swh_multipole>(),
-                           g->ftens.as<double>());
-      else
-        hipLaunchKernelGGL((l2l_kernel<float>), dim3((o1 - o0 + 63) / 64), dim3(64), 0,
-                           g->stream, lst, o1 - o0, g->mpoles.as<const swh_multipole>(),
-                           g->ftens.as<double>());
-      SWH_HIP(hipGetLastError());
-    }
-    if (g->nleaf_cells > 0) {
-      const dim3 pg((unsigned)((g->n + 255) / 256));
-      if (f64)
-        hipLaunchKernelGGL((l2p_part_kernel<double>), pg, dim3(256), 0, g->stream, g->n,
-                           g->leaf_of.as<const int>(), g->mpoles.as<const swh_multipole>(),
-                           g->ftens.as<const double>(), gsoa_of(g));
-      else
-        hipLaunchKernelGGL((l2p_part_kernel<float>), pg, dim3(256), 0, g->stream, g->n,
-                           g->leaf_of.as<const int>(), g->mpoles.as<const swh_multipole>(),
-                           g->ftens.as<const double>(), gsoa_of(g));
-      SWH_HIP(hipGetLastError());
-    }
+    // down pass: L2L depth by depth, then L2P at the leaves (SWH_TREE_NO_DOWN:
+    // the caller runs it later, swh_gspace_grav_down, as SWIFT's grav_down task)
+    if (!(flags & SWH_TREE_NO_DOWN)) SWH_TRY(tree_down(g));
   }
   if (stats) SWH_HIP(hipEventRecord(ev[5], g->stream));
   unsigned long long h[2] = {0, 0};
@@ -2058,6 +2086,61 @@ swh_status swh_grav_tree(swh_gspace* g, const swh_grav_params* G, const int32_t*
     }
     for (auto& e : ev) (void)hipEventDestroy(e);
   }
+  return SWH_OK;
+}
+
+swh_status swh_gspace_multipoles(swh_gspace* g, swh_multipole* out) {
+  if (!g || !out) return SWH_ERR_ARG;
+  const size_t n = g->tree.size();
+  if (n == 0) return SWH_OK;
+  if (!g->mpoles_valid && !g->mpoles_given) {
+    set_error("swh_gspace_multipoles: no tree multipoles yet (run swh_grav_tree)");
+    return SWH_ERR_STATE;
+  }
+  SWH_HIP(hipSetDevice(g->ctx->device));
+  SWH_HIP(hipMemcpyAsync(out, g->mpoles.ptr, n * sizeof(swh_multipole), hipMemcpyDeviceToHost,
+                         g->stream));
+  SWH_HIP(hipStreamSynchronize(g->stream));
+  return SWH_OK;
+}
+
+swh_status swh_gspace_set_multipoles(swh_gspace* g, const swh_multipole* in) {
+  if (!g || !in) return SWH_ERR_ARG;
+  const size_t n = g->tree.size();
+  if (n == 0) {
+    set_error("swh_gspace_set_tree must precede swh_gspace_set_multipoles");
+    return SWH_ERR_STATE;
+  }
+  SWH_HIP(hipSetDevice(g->ctx->device));
+  SWH_TRY(g->mpoles.reserve(n * sizeof(swh_multipole)));
+  SWH_HIP(hipMemcpyAsync(g->mpoles.ptr, in, n * sizeof(swh_multipole), hipMemcpyHostToDevice,
+                         g->stream));
+  SWH_HIP(hipStreamSynchronize(g->stream));
+  g->mpoles_given = true;
+  return SWH_OK;
+}
+
+swh_status swh_gspace_grav_down(swh_gspace* g, const swh_grav_params* G, const float* fields) {
+  if (!g || !G || !fields) return SWH_ERR_ARG;
+  const int ncells = (int)g->tree.size();
+  if (g->n == 0 || ncells == 0) {
+    set_error("swh_gspace_set_tree must precede swh_gspace_grav_down");
+    return ncells == 0 ? SWH_ERR_STATE : SWH_OK;
+  }
+  SWH_HIP(hipSetDevice(g->ctx->device));
+  // activity and the accumulators (swh_gspace_download adds them)
+  hipLaunchKernelGGL(gunpack_kernel, dim3((int)((g->n + 255) / 256)), dim3(256), 0, g->stream,
+                     g->layout, g->aos.as<const char>(), g->n, gsoa_of(g), G->max_active_bin);
+  SWH_HIP(hipGetLastError());
+  SWH_TRY(tree_multipoles(g));
+  const size_t nt = (size_t)ncells * SWH_MPOLE_TERMS;
+  std::vector<double> f(nt);
+  for (size_t k = 0; k < nt; k++) f[k] = (double)fields[k];
+  SWH_TRY(g->ftens.reserve(nt * sizeof(double)));
+  SWH_HIP(hipMemcpyAsync(g->ftens.ptr, f.data(), nt * sizeof(double), hipMemcpyHostToDevice,
+                         g->stream));
+  SWH_TRY(tree_down(g));
+  SWH_HIP(hipStreamSynchronize(g->stream));  // f goes out of scope
   return SWH_OK;
 }
 

@@ -229,6 +229,7 @@ struct swh_gspace {
   swh::DevBuf oagn;    // float old_a_grav_norm (the adaptive MAC's estimate)
   swh::DevBuf mpoles;  // swh_multipole[nleaves] (swh_gspace_make_multipoles)
   bool mpoles_valid = false;
+  bool mpoles_given = false;  // swh_gspace_set_multipoles: the tree uses the caller's
   bool any_mpole = false;  // some pair has allow_mpole
   swh::DevBuf leaves, pair_off, pairs;
   int32_t nleaves = 0, npairs = 0;

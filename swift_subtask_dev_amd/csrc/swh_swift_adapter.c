@@ -12,6 +12,7 @@
 #include <math.h>
 #include <stddef.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "swifthip.h"
@@ -591,4 +592,237 @@ void runner_dopair_grav_pp(struct runner *r, struct cell *ci, struct cell *cj,
     vj.multipole = &mj;
   }
   report(swh_grav_pair_pp(swhs_ctx, &vi, &vj, symmetric, allow_mpole, &swhs_glayout, &G));
+}
+
+
+/* ------------------------------------------------------------------------ */
+/* Tree gravity per task: runner_doself_recursive_grav /                     */
+/* runner_dopair_recursive_grav (runner_doiact_grav.c:2386, 2208) and        */
+/* runner_do_grav_down (65-164). The task's cell tree(s) are flattened into  */
+/* libswifthip's swh_gcell table with SWIFT's own multipoles                 */
+/* (swh_gspace_set_multipoles); the library makes the recursion's decisions  */
+/* on the device (r_cut_max skip, P-P of <= 1-particle cells, M-M under      */
+/* gravity_M2L_accept_symmetric, leaf P-P with M2P, split the larger cell)   */
+/* and returns the P-P accelerations and the M2L field tensors, which are    */
+/* added into c->grav.multipole->pot as the reference's M-M interactions do  */
+/* (the down pass is its own task, as in SWIFT).                             */
+/* ------------------------------------------------------------------------ */
+
+struct swhs_tree {
+  swh_gcell *cells;
+  struct cell **cptr;
+  int n, cap;
+};
+
+static int swhs_tree_add(struct swhs_tree *t, struct cell *c, const struct gpart *base,
+                         int offset) {
+  if (t->n == t->cap) {
+    t->cap = t->cap ? 2 * t->cap : 64;
+    t->cells = (swh_gcell *)realloc(t->cells, (size_t)t->cap * sizeof(swh_gcell));
+    t->cptr = (struct cell **)realloc(t->cptr, (size_t)t->cap * sizeof(struct cell *));
+  }
+  const int id = t->n++;
+  swh_gcell *g = &t->cells[id];
+  memset(g, 0, sizeof(*g));
+  g->start = offset + (int)(c->grav.parts - base);
+  g->count = c->grav.count;
+  g->split = c->split;
+  for (int k = 0; k < 3; k++) {
+    g->loc[k] = c->loc[k];
+    g->width[k] = c->width[k];
+  }
+  t->cptr[id] = c;
+  for (int k = 0; k < 8; k++) {
+    t->cells[id].progeny[k] = -1;
+    if (c->split && c->progeny[k] && c->progeny[k]->grav.count > 0) {
+      const int p = swhs_tree_add(t, c->progeny[k], base, offset);
+      t->cells[id].progeny[k] = p;
+    }
+  }
+  return id;
+}
+
+static void swhs_tree_free(struct swhs_tree *t) {
+  free(t->cells);
+  free(t->cptr);
+}
+
+/* struct grav_tensor <-> the library's 35 floats (swh_multipole::M order) */
+static void tensor_to(const struct grav_tensor *p, float *f) {
+  const float v[SWH_MPOLE_TERMS] = {
+      p->F_000, p->F_100, p->F_010, p->F_001, p->F_200, p->F_020, p->F_002, p->F_110, p->F_101,
+      p->F_011, p->F_300, p->F_030, p->F_003, p->F_210, p->F_201, p->F_120, p->F_021, p->F_102,
+      p->F_012, p->F_111, p->F_400, p->F_040, p->F_004, p->F_310, p->F_301, p->F_130, p->F_031,
+      p->F_103, p->F_013, p->F_220, p->F_202, p->F_022, p->F_211, p->F_121, p->F_112};
+  memcpy(f, v, sizeof(v));
+}
+static void tensor_from(struct grav_tensor *p, const float *f, int add) {
+  float *d[SWH_MPOLE_TERMS] = {
+      &p->F_000, &p->F_100, &p->F_010, &p->F_001, &p->F_200, &p->F_020, &p->F_002, &p->F_110,
+      &p->F_101, &p->F_011, &p->F_300, &p->F_030, &p->F_003, &p->F_210, &p->F_201, &p->F_120,
+      &p->F_021, &p->F_102, &p->F_012, &p->F_111, &p->F_400, &p->F_040, &p->F_004, &p->F_310,
+      &p->F_301, &p->F_130, &p->F_031, &p->F_103, &p->F_013, &p->F_220, &p->F_202, &p->F_022,
+      &p->F_211, &p->F_121, &p->F_112};
+  for (int k = 0; k < SWH_MPOLE_TERMS; k++) *d[k] = add ? *d[k] + f[k] : f[k];
+}
+
+/* Upload the task's gparts (roots' slices, concatenated in a staging copy)
+ * with its tree and SWIFT's multipoles. */
+static swh_status swhs_gspace_for(swh_gspace **gs, struct swhs_tree *t, struct cell **roots,
+                                  const int *offs, int nroots, char **stage, int total) {
+  const size_t st = (size_t)swhs_glayout.stride;
+  *stage = (char *)malloc((size_t)total * st);
+  for (int r = 0; r < nroots; r++)
+    memcpy(*stage + (size_t)offs[r] * st, roots[r]->grav.parts, (size_t)roots[r]->grav.count * st);
+  swh_status s = swh_gspace_create(swhs_ctx, gs);
+  if (s != SWH_OK) return s;
+  s = swh_gspace_upload(*gs, *stage, total, &swhs_glayout, 0);
+  if (s == SWH_OK) s = swh_gspace_set_tree(*gs, t->cells, t->n);
+  if (s == SWH_OK) {
+    swh_multipole *mp = (swh_multipole *)calloc((size_t)t->n, sizeof(swh_multipole));
+    for (int c = 0; c < t->n; c++) multipole_of(t->cptr[c]->grav.multipole, &mp[c]);
+    s = swh_gspace_set_multipoles(*gs, mp);
+    free(mp);
+  }
+  return s;
+}
+
+/* After the tasks: the gparts of the local roots get their results back
+ * (swh_gspace_download adds them to the staging copy), the local cells'
+ * field tensors receive their M2L sums. */
+static swh_status swhs_gspace_finish(swh_gspace *gs, struct swhs_tree *t, struct cell **roots,
+                                     const int *offs, int nroots, char *stage,
+                                     const struct engine *e, int tensors_add) {
+  swh_status s = swh_gspace_download(gs, stage, &swhs_glayout, 0);
+  const size_t st = (size_t)swhs_glayout.stride;
+  if (s == SWH_OK)
+    for (int r = 0; r < nroots; r++)
+      if (roots[r]->nodeID == e->nodeID)
+        memcpy(roots[r]->grav.parts, stage + (size_t)offs[r] * st,
+               (size_t)roots[r]->grav.count * st);
+  if (s == SWH_OK) {
+    float *f = (float *)malloc((size_t)t->n * SWH_MPOLE_TERMS * sizeof(float));
+    s = swh_gspace_field_tensors(gs, f);
+    for (int c = 0; s == SWH_OK && c < t->n; c++) {
+      struct cell *cc = t->cptr[c];
+      if (cc->nodeID != e->nodeID || !cc->grav.multipole) continue;
+      const float *fc = f + (size_t)c * SWH_MPOLE_TERMS;
+      if (tensors_add) {
+        int any = 0;
+        for (int k = 0; k < SWH_MPOLE_TERMS; k++) any |= fc[k] != 0.f;
+        if (!any) continue; /* no M-M interaction reached this cell */
+        tensor_from(&cc->grav.multipole->pot, fc, 1);
+        cc->grav.multipole->pot.interacted = 1;
+      } else if (c > 0 && cell_is_active_gravity(cc, e)) {
+        /* grav_down: the progeny tensors with their parents' pushed in
+         * (gravity_field_tensors_add marks them interacted) */
+        tensor_from(&cc->grav.multipole->pot, fc, 0);
+        int any = 0;
+        for (int k = 0; k < SWH_MPOLE_TERMS; k++) any |= fc[k] != 0.f;
+        if (any) cc->grav.multipole->pot.interacted = 1;
+      }
+    }
+    free(f);
+  }
+  swh_gspace_destroy(gs);
+  free(stage);
+  return s;
+}
+
+/* runner_doself_recursive_grav (runner_doiact_grav.c:2386-2431) */
+void runner_doself_recursive_grav(struct runner *r, struct cell *c, int gettimer) {
+  (void)gettimer;
+  const struct engine *e = r->e;
+  if (!swhs_ctx) SWH_ADAPTER_ERROR("swifthip_swift_init() was not called");
+  if (c->grav.count == 0) SWH_ADAPTER_ERROR("Doing self gravity on an empty cell !");
+  if (!cell_is_active_gravity(c, e)) return;
+  if (!c->grav.multipole) SWH_ADAPTER_ERROR("self gravity without cell multipoles");
+  swh_grav_params G;
+  grav_params_of(e, &G);
+  struct swhs_tree t = {0};
+  swhs_tree_add(&t, c, c->grav.parts, 0);
+  swh_gspace *gs = NULL;
+  char *stage = NULL;
+  const int off = 0;
+  swh_status s = swhs_gspace_for(&gs, &t, &c, &off, 1, &stage, c->grav.count);
+  const int32_t self = 0;
+  if (s == SWH_OK) s = swh_grav_tree_tasks(gs, &G, &self, 1, NULL, 0, SWH_TREE_NO_DOWN, NULL);
+  if (gs) {
+    const swh_status s2 = swhs_gspace_finish(gs, &t, &c, &off, 1, stage, e, 1);
+    if (s == SWH_OK) s = s2;
+  } else {
+    free(stage);
+  }
+  swhs_tree_free(&t);
+  report(s);
+}
+
+/* runner_dopair_recursive_grav (runner_doiact_grav.c:2208-2370) */
+void runner_dopair_recursive_grav(struct runner *r, struct cell *ci, struct cell *cj,
+                                  int gettimer) {
+  (void)gettimer;
+  const struct engine *e = r->e;
+  if (!swhs_ctx) SWH_ADAPTER_ERROR("swifthip_swift_init() was not called");
+  if (!((cell_is_active_gravity(ci, e) && ci->nodeID == e->nodeID) ||
+        (cell_is_active_gravity(cj, e) && cj->nodeID == e->nodeID)))
+    return;
+  if (ci->grav.count == 0 || cj->grav.count == 0)
+    SWH_ADAPTER_ERROR("Doing pair gravity on an empty cell !");
+  if (ci == cj) SWH_ADAPTER_ERROR("Pair interaction between a cell and itself.");
+  if (!ci->grav.multipole || !cj->grav.multipole)
+    SWH_ADAPTER_ERROR("pair gravity without cell multipoles");
+  swh_grav_params G;
+  grav_params_of(e, &G);
+  struct cell *roots[2] = {ci, cj};
+  const int offs[2] = {0, ci->grav.count};
+  struct swhs_tree t = {0};
+  const int32_t pair[2] = {swhs_tree_add(&t, ci, ci->grav.parts, 0),
+                           swhs_tree_add(&t, cj, cj->grav.parts, ci->grav.count)};
+  swh_gspace *gs = NULL;
+  char *stage = NULL;
+  swh_status s = swhs_gspace_for(&gs, &t, roots, offs, 2, &stage, ci->grav.count + cj->grav.count);
+  if (s == SWH_OK) s = swh_grav_tree_tasks(gs, &G, NULL, 0, pair, 1, SWH_TREE_NO_DOWN, NULL);
+  if (gs) {
+    const swh_status s2 = swhs_gspace_finish(gs, &t, roots, offs, 2, stage, e, 1);
+    if (s == SWH_OK) s = s2;
+  } else {
+    free(stage);
+  }
+  swhs_tree_free(&t);
+  report(s);
+}
+
+/* runner_do_grav_down (runner_doiact_grav.c:65-164) */
+void runner_do_grav_down(struct runner *r, struct cell *c, int timer) {
+  (void)timer;
+  const struct engine *e = r->e;
+  if (!swhs_ctx) SWH_ADAPTER_ERROR("swifthip_swift_init() was not called");
+  if (!c->grav.multipole) SWH_ADAPTER_ERROR("grav_down without cell multipoles");
+  if (c->grav.count == 0) return;
+  swh_grav_params G;
+  grav_params_of(e, &G);
+  struct swhs_tree t = {0};
+  swhs_tree_add(&t, c, c->grav.parts, 0);
+  swh_gspace *gs = NULL;
+  char *stage = NULL;
+  const int off = 0;
+  swh_status s = swhs_gspace_for(&gs, &t, &c, &off, 1, &stage, c->grav.count);
+  if (s == SWH_OK) {
+    /* the cells' tensors; those that received nothing (interacted == 0) push
+     * nothing, as the reference's test skips them */
+    float *f = (float *)calloc((size_t)t.n * SWH_MPOLE_TERMS, sizeof(float));
+    for (int k = 0; k < t.n; k++)
+      if (t.cptr[k]->grav.multipole && t.cptr[k]->grav.multipole->pot.interacted)
+        tensor_to(&t.cptr[k]->grav.multipole->pot, f + (size_t)k * SWH_MPOLE_TERMS);
+    s = swh_gspace_grav_down(gs, &G, f);
+    free(f);
+  }
+  if (gs) {
+    const swh_status s2 = swhs_gspace_finish(gs, &t, &c, &off, 1, stage, e, 0);
+    if (s == SWH_OK) s = s2;
+  } else {
+    free(stage);
+  }
+  swhs_tree_free(&t);
+  report(s);
 }

@@ -42,7 +42,8 @@ HIP_SYMBOLS = [
     "swh_gspace_destroy", "swh_gspace_upload", "swh_gspace_set_leaves", "swh_grav_pp_batch",
     "swh_gspace_make_multipoles", "swh_space_upload_xparts", "swh_space_drift",
     "swh_gspace_set_tree", "swh_gspace_set_owned_cells", "swh_grav_tree",
-    "swh_gspace_field_tensors",
+    "swh_grav_tree_tasks", "swh_gspace_field_tensors", "swh_gspace_multipoles",
+    "swh_gspace_set_multipoles", "swh_gspace_grav_down",
     "swh_gspace_download", "swh_gspace_sync", "swh_gspace_query", "swh_gspace_pm_mesh",
 ]
 ADAPTER_SYMBOLS = [
@@ -53,6 +54,7 @@ ADAPTER_SYMBOLS = [
     "runner_dopair1_branch_gradient", "runner_doself2_branch_force",
     "runner_dopair2_branch_force", "runner_doself_subset_branch_density",
     "runner_dopair_subset_branch_density", "runner_doself_grav_pp", "runner_dopair_grav_pp",
+    "runner_doself_recursive_grav", "runner_dopair_recursive_grav", "runner_do_grav_down",
     "runner_dosub_self1_density", "runner_dosub_pair1_density", "runner_dosub_self1_gradient",
     "runner_dosub_pair1_gradient", "runner_dosub_self2_force", "runner_dosub_pair2_force",
     "runner_dosub_subset_density", "swifthip_swift_part_layout", "swifthip_swift_gpart_layout",
@@ -139,6 +141,11 @@ def load() -> C.CDLL:
         "swh_grav_tree": (C.c_int, [vp, P(abi.GravParams), vp, i32, vp, i32,
                                     P(abi.GravTreeStats)]),
         "swh_gspace_field_tensors": (C.c_int, [vp, vp]),
+        "swh_grav_tree_tasks": (C.c_int, [vp, P(abi.GravParams), vp, i32, vp, i32, i32,
+                                          P(abi.GravTreeStats)]),
+        "swh_gspace_multipoles": (C.c_int, [vp, vp]),
+        "swh_gspace_set_multipoles": (C.c_int, [vp, vp]),
+        "swh_gspace_grav_down": (C.c_int, [vp, P(abi.GravParams), vp]),
         "swh_gspace_download": (C.c_int, [vp, vp, P(abi.GPartLayout), C.c_int]),
         "swh_gspace_sync": (C.c_int, [vp]),
         "swh_gspace_query": (C.c_int, [vp]),
@@ -182,6 +189,11 @@ def load_adapter() -> C.CDLL:
     ad.runner_dopair_subset_branch_density.restype = None
     ad.runner_dopair_grav_pp.argtypes = [vp, vp, vp, C.c_int, C.c_int]
     ad.runner_dopair_grav_pp.restype = None
+    for n in ("runner_doself_recursive_grav", "runner_do_grav_down"):
+        getattr(ad, n).argtypes = [vp, vp, C.c_int]
+        getattr(ad, n).restype = None
+    ad.runner_dopair_recursive_grav.argtypes = [vp, vp, vp, C.c_int]
+    ad.runner_dopair_recursive_grav.restype = None
     _adapter = ad
     return ad
 
@@ -480,6 +492,12 @@ class GravSpace:
                 "n_pp_tasks": st.n_pp_tasks, "n_skipped": st.n_skipped,
                 "ms": {"multipoles": st.ms_multipoles, "walk": st.ms_walk, "p2p": st.ms_p2p,
                        "m2p": st.ms_m2p, "down": st.ms_down}}
+
+    def multipoles(self):
+        """The tree cells' multipoles (abi.Multipole array)."""
+        out = (abi.Multipole * len(self._tree))()
+        _check(self._lib.swh_gspace_multipoles(self.handle, out), "multipoles")
+        return out
 
     def field_tensors(self) -> np.ndarray:
         out = np.zeros((len(self._tree), abi.MPOLE_TERMS), dtype=np.float32)

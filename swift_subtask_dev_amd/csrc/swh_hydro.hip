@@ -19,10 +19,18 @@
 
 namespace swh {
 
-__device__ __forceinline__ void count_add(int n, unsigned long long* counter) {
-  unsigned long long v = (unsigned long long)n;
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  if ((threadIdx.x & 63) == 0 && v) atomicAdd(counter, v);
+// Sum the counter stripes (counter_stripe) into the counter slots and clear
+// them: one block of kCounterStripes threads, thread t owning stripe t.
+__global__ __launch_bounds__(kCounterStripes) void stripe_reduce_kernel(
+    unsigned long long* __restrict__ stripes, unsigned long long* __restrict__ out) {
+  const int t = threadIdx.x;
+  for (int k = 0; k < 8; k++) {
+    if (k == 1 || k == 2) continue;  // slots 1-2 hold other state (swh_hydro.hip counter map)
+    unsigned long long v = stripes[t * 8 + k];
+    stripes[t * 8 + k] = 0ull;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((t & 63) == 0 && v) atomicAdd(out + k, v);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -86,33 +94,38 @@ __global__ void zero_u32_kernel(unsigned int* __restrict__ p, int64_t n,
 // largest displacement since the build, r_now >= r_build - 2D, so a pair it
 // lacks can enter r < max(H_i, H_j) only if some particle has H_now + 2D >
 // R_build. Pass 1: D (float bits) from the displacement record.
-__global__ void list_disp_kernel(const float4* __restrict__ xdiff, const float4* __restrict__ xd0,
-                                 const int8_t* __restrict__ tb, int64_t n,
-                                 unsigned int* __restrict__ disp_bits) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void list_disp_kernel(const float4* __restrict__ xdiff,
+                                                        const float4* __restrict__ xd0,
+                                                        const int8_t* __restrict__ tb, int64_t n,
+                                                        unsigned int* __restrict__ disp_bits) {
+  __shared__ float sm[4];
   float d = 0.f;
-  if (i < n && tb[i] != kTimeBinInhibited) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (tb[i] == kTimeBinInhibited) continue;
     const float4 a = xdiff[i], b = xd0[i];
     const float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
-    d = sqrtf(dx * dx + dy * dy + dz * dz) * (1.f + 1e-5f);
+    d = fmaxf(d, sqrtf(dx * dx + dy * dy + dz * dz) * (1.f + 1e-5f));
   }
-  for (int o = 32; o > 0; o >>= 1) d = fmaxf(d, __shfl_xor(d, o));
-  if ((threadIdx.x & 63) == 0 && d > 0.f) atomicMax(disp_bits, __float_as_uint(d));
+  block_max_bits(disp_bits, d, sm);
 }
 
 // Pass 2: stale if an active particle is unlisted, or any listed particle's
 // H_now + 2D exceeds its build reach.
-__global__ void list_check_kernel(SoA a, ListDev ld, int64_t n, int max_active_bin,
-                                  const unsigned int* __restrict__ disp_bits,
-                                  unsigned int* __restrict__ stale) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool bad = false;
-  if (i < n && active_part(a, i, max_active_bin)) {
-    const double D = (double)__uint_as_float(*disp_bits);
+__global__ __launch_bounds__(256) void list_check_kernel(SoA a, ListDev ld, int64_t n,
+                                                         int max_active_bin,
+                                                         const unsigned int* __restrict__ disp_bits,
+                                                         unsigned int* __restrict__ stale) {
+  __shared__ float sm[4];
+  const double D = (double)__uint_as_float(*disp_bits);
+  float bad = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (!active_part(a, i, max_active_bin)) continue;
     const double H = a.pos[i].w * (double)kGamma;
-    bad = ld.base[i] < 0 || H + 2. * D > (double)ld.reach[i];
+    if (ld.base[i] < 0 || H + 2. * D > (double)ld.reach[i]) bad = 1.f;
   }
-  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(stale, 1u);
+  block_max_bits(stale, bad, sm);  // 1.0f's bits: nonzero = stale
 }
 
 // Kept lists: the wrap radius follows the displacement bound dx of the drifts.
@@ -241,7 +254,7 @@ __global__ __launch_bounds__(256) void overflow_kernel(GridDev g, SoA a, ListDev
     if (lane == 0) {
       st.store(a, i);
       if (ncount) ncount[i] = st.n;
-      if (counter) atomicAdd(counter, (unsigned long long)st.n);
+      if (counter) atomicAdd(counter_stripe(counter), (unsigned long long)st.n);
     }
   }
 }
@@ -298,7 +311,7 @@ __global__ __launch_bounds__(256) void walk_subset_kernel(GridDev g, SoA a, List
   if (counter) {
     unsigned long long v = (unsigned long long)((act && s == 0) ? st.n : 0);
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(counter, v);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(counter_stripe(counter), v);
   }
 }
 
@@ -500,11 +513,8 @@ __global__ __launch_bounds__(1024) void ghost_kernel(
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   const bool any_stale = __any(stale);
   if ((threadIdx.x & 63) == 0) {
-    if (m > 0.f && __float_as_uint(m) > __hip_atomic_load(hmax_bits, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT))
-      atomicMax(hmax_bits, __float_as_uint(m));
-    if (any_stale && __hip_atomic_load(list_stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-      atomicOr(list_stale, 1u);
+    if (m > 0.f) atomic_max_bits_if(hmax_bits, __float_as_uint(m));
+    if (any_stale) atomic_flag_if(list_stale);
   }
 }
 
@@ -615,6 +625,17 @@ static unsigned long long* counter_slot(swh_space* s) {
   return s->counters.as<unsigned long long>();  // slot 0: interactions
 }
 static unsigned int* hmax_slot(swh_space* s) { return s->counters.as<unsigned int>() + 2; }
+// The stripes the counted kernels add into (kCounterStripes x 8 u64, zero
+// between counted loops: stripe_reduce_kernel clears them).
+static swh_status stripes_slot(swh_space* s, unsigned long long** out) {
+  if (!s->ctr_stripes.ptr) {
+    const size_t b = (size_t)kCounterStripes * 8 * sizeof(unsigned long long);
+    SWH_TRY(s->ctr_stripes.reserve(b));
+    SWH_HIP(hipMemsetAsync(s->ctr_stripes.ptr, 0, b, s->stream));
+  }
+  *out = s->ctr_stripes.as<unsigned long long>();
+  return SWH_OK;
+}
 
 // Counter slots (s->counters, 128 bytes): u64[0] interactions, u32[2] max h
 // (float bits), u32[4..5] ghost list counts, u64[3] list entries, u64[4..7]
@@ -662,6 +683,8 @@ static ListDev list_dev(swh_space* s) {
 static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool count,
                               float skin, const unsigned int* run_if = nullptr) {
   const int K = s->tuning.list_capacity > 0 ? s->tuning.list_capacity : 128;
+  unsigned long long* stripes = nullptr;
+  if (count) SWH_TRY(stripes_slot(s, &stripes));
   s->list_skin_cur = skin;
   SWH_TRY(s->nbr.reserve((size_t)std::max(1, s->ngroups) * ((K + 15) & ~15) * kListSlots *
                          sizeof(int)));
@@ -700,7 +723,7 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
                      (double)ld.skin1, s->gbox.as<GroupBox>(), run_if);
   hipLaunchKernelGGL(list_build_kernel, dim3(s->ngroups), dim3(64), 0, s->stream, grid_dev(s),
                      soa_of(s), ldb, s->groups.as<const int2>(), 0, s->ngroups,
-                     P->max_active_bin, hmax_slot(s), count ? counter_slot(s) : nullptr,
+                     P->max_active_bin, hmax_slot(s), count ? stripes : nullptr,
                      s->tuning.diag_mode, run_if);
   SWH_HIP(hipGetLastError());
   s->list_valid = true;
@@ -715,10 +738,10 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
 static swh_status check_kept_lists(swh_space* s, const swh_hydro_params* P, bool count) {
   const int nb = (int)((s->n + 255) / 256);
   SWH_HIP(hipMemsetAsync(keep_stale_slot(s), 0, 2 * sizeof(unsigned int), s->stream));
-  hipLaunchKernelGGL(list_disp_kernel, dim3(nb), dim3(256), 0, s->stream,
+  hipLaunchKernelGGL(list_disp_kernel, dim3(std::min(nb, kReduceBlocks)), dim3(256), 0, s->stream,
                      s->xdiff.as<const float4>(), s->list_xd0.as<const float4>(),
                      s->tb.as<const int8_t>(), s->n, disp_slot(s));
-  hipLaunchKernelGGL(list_check_kernel, dim3(nb), dim3(256), 0, s->stream, soa_of(s), list_dev(s),
+  hipLaunchKernelGGL(list_check_kernel, dim3(std::min(nb, kReduceBlocks)), dim3(256), 0, s->stream, soa_of(s), list_dev(s),
                      s->n, P->max_active_bin, disp_slot(s), keep_stale_slot(s));
   hipLaunchKernelGGL(list_rwrap_kernel, dim3(1), dim3(64), 0, s->stream, rwrap_slot(s),
                      rwrap_base_slot(s), (float)s->grid.dx);
@@ -786,7 +809,8 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const int
   }
   const GridDev gd = grid_dev(s);
   const double a2H = P->a * P->a * P->H;
-  unsigned long long* ctr = count ? counter_slot(s) : nullptr;
+  unsigned long long* ctr = nullptr;
+  if (count) SWH_TRY(stripes_slot(s, &ctr));
   int* ncount = count ? s->ncount.as<int>() : nullptr;
   if (s->ctx->precision == SWH_PRECISION_F64)
     launch_typed<LOOP, double>(s, gd, subset, nitems, P->max_active_bin, a2H, ctr, ncount);
@@ -816,6 +840,11 @@ static swh_status run_loop(swh_space* s, const swh_hydro_params* P, int64_t* n_o
   const bool rebuilds = (LOOP == LOOP_DENSITY && !(keep && fresh)) || !fresh;
   SWH_TRY(launch_loop<LOOP>(s, P, nullptr, (int)s->n, n_out != nullptr));
   if (n_out) {
+    unsigned long long* stripes = nullptr;
+    SWH_TRY(stripes_slot(s, &stripes));
+    hipLaunchKernelGGL(stripe_reduce_kernel, dim3(1), dim3(kCounterStripes), 0, s->stream,
+                       stripes, ctr);
+    SWH_HIP(hipGetLastError());
     unsigned long long h[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     SWH_HIP(hipMemcpyAsync(h, ctr, sizeof(h), hipMemcpyDeviceToHost, s->stream));
     SWH_HIP(hipStreamSynchronize(s->stream));

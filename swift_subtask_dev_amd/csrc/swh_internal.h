@@ -210,6 +210,7 @@ struct swh_space {
   int32_t list_overflow = 0;  // last counted build: particles over capacity
   // scratch
   swh::DevBuf keys, keys2, idx, idx2, sort_tmp, scan_tmp, counters;
+  swh::DevBuf ctr_stripes;  // counted launches' per-block counter stripes (swh_hydro.hip)
   swh::DevBuf tmp_soa;     // staging for permutation gathers
   swh::DevBuf ghost_left, ghost_right, ghost_list, ghost_list2, ghost_search;
   swh::HostBuf hstage;

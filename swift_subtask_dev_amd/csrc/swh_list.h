@@ -533,11 +533,12 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
       fl += __shfl_xor(fl, o);
     }
     if (lane == 0) {
-      atomicAdd(counter + 3, v);  // list entries
-      atomicAdd(counter + 4, ld_);
-      atomicAdd(counter + 5, sg);
-      atomicAdd(counter + 6, (unsigned long long)ts.asteps);
-      atomicAdd(counter + 7, fl);  // lane flush steps
+      unsigned long long* cs = counter_stripe(counter);
+      atomicAdd(cs + 3, v);  // list entries
+      atomicAdd(cs + 4, ld_);
+      atomicAdd(cs + 5, sg);
+      atomicAdd(cs + 6, (unsigned long long)ts.asteps);
+      atomicAdd(cs + 7, fl);  // lane flush steps
     }
   }
   BuildSlot b;
@@ -657,7 +658,7 @@ __device__ __forceinline__ void list_walk(const GridDev& g, SoA& a, const ListDe
   if (counter) {
     unsigned long long v = (unsigned long long)((act && s == 0) ? st.n : 0);
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(counter, v);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(counter_stripe(counter), v);
   }
 }
 

@@ -17,6 +17,7 @@
 #include "swh_internal.h"
 #include "swh_physics.h"
 #include "swh_space.h"
+#include "swh_wave.h"
 
 namespace swh {
 
@@ -380,7 +381,7 @@ __global__ void halo_unpack_kernel(SoA a, const int* __restrict__ idx, int n,
   const float4 r0 = in[2 * t], r1 = in[2 * t + 1];
   if (mask & SWH_HALO_H) {
     a.pos[s].w = (double)r0.x;
-    atomicMax(hmax_bits, __float_as_uint(r0.x));
+    atomic_max_bits_if(hmax_bits, __float_as_uint(r0.x));
   }
   float4 th = a.th[s];
   if (mask & SWH_HALO_RHO) th.y = r0.y;
@@ -439,15 +440,16 @@ struct DriftParams {
 // arithmetic, positions in double. dx_bits / h_bits: running maxima of the
 // displacement since the rebuild and of h (float bits, positive).
 // max |v_full| over the xparts (float bits; |v| >= 0 orders as its bits)
-__global__ void vmax_kernel(const float4* __restrict__ vfull, int64_t n, unsigned int* vbits) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void vmax_kernel(const float4* __restrict__ vfull, int64_t n,
+                                                   unsigned int* vbits) {
+  __shared__ float sm[4];
   float v = 0.f;
-  if (s < n) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x) {
     const float4 q = vfull[s];
-    v = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z);
+    v = fmaxf(v, sqrtf(q.x * q.x + q.y * q.y + q.z * q.z));
   }
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  if ((threadIdx.x & 63) == 0 && v > 0.f) atomicMax(vbits, __float_as_uint(v));
+  block_max_bits(vbits, v, sm);
 }
 
 // xparts / gpart flags (caller order) -> sorted order
@@ -463,13 +465,15 @@ __global__ void xsort_kernel(const int* __restrict__ perm, const float4* __restr
   hasg_s[s] = hasg[c];
 }
 
-__global__ void drift_kernel(SoA a, const float4* __restrict__ vfull,
+__global__ __launch_bounds__(256) void drift_kernel(SoA a, const float4* __restrict__ vfull,
                              const float4* __restrict__ agrav, const int8_t* __restrict__ hasg,
                              float4* __restrict__ xdiff, int64_t n, DriftParams D,
                              unsigned int* dx_bits, unsigned int* h_bits) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float sm[2][4];
   float dmax = 0.f, hm = 0.f;
-  if (s < n && a.tb[s] != kTimeBinInhibited) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    if (a.tb[s] == kTimeBinInhibited) continue;
     const int c = (int)s;  // vfull / agrav / hasg in sorted order (xsort_kernel)
     const float4 vf = vfull[c];
     double4 p = a.pos[s];
@@ -517,17 +521,11 @@ __global__ void drift_kernel(SoA a, const float4* __restrict__ vfull,
     xd.y -= (float)((double)vf.y * D.dt_drift);
     xd.z -= (float)((double)vf.z * D.dt_drift);
     xdiff[s] = xd;
-    dmax = sqrtf(xd.x * xd.x + xd.y * xd.y + xd.z * xd.z);
-    hm = h;
+    dmax = fmaxf(dmax, sqrtf(xd.x * xd.x + xd.y * xd.y + xd.z * xd.z));
+    hm = fmaxf(hm, h);
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    dmax = fmaxf(dmax, __shfl_xor(dmax, o));
-    hm = fmaxf(hm, __shfl_xor(hm, o));
-  }
-  if ((threadIdx.x & 63) == 0) {
-    atomicMax(dx_bits, __float_as_uint(dmax));
-    atomicMax(h_bits, __float_as_uint(hm));
-  }
+  block_max_bits(dx_bits, dmax, sm[0]);
+  block_max_bits(h_bits, hm, sm[1]);
 }
 
 // cell_start[c] = first sorted index with key >= c (c in [0, ncell]).
@@ -547,7 +545,7 @@ __global__ void hmax_kernel(const double4* __restrict__ pos, const int8_t* __res
        i += (int64_t)gridDim.x * blockDim.x)
     if (tb[i] != kTimeBinInhibited) m = fmaxf(m, (float)pos[i].w);
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0) atomicMax(out_bits, __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) atomic_max_bits_if(out_bits, __float_as_uint(m));
 }
 
 
@@ -688,7 +686,7 @@ swh_status swh_space_destroy(swh_space* s) {
                     &s->seg_off, &s->keys, &s->keys2, &s->idx, &s->idx2, &s->sort_tmp,
                     &s->scan_tmp, &s->counters, &s->tmp_soa, &s->ghost_left,
                     &s->ghost_right, &s->ghost_list, &s->ghost_list2, &s->ghost_search,
-                    &s->nbr, &s->nbr_cnt, &s->nbr_base, &s->nbr_reach, &s->nbr_ovf, &s->posf, &s->gbox,
+                    &s->nbr, &s->nbr_cnt, &s->nbr_base, &s->nbr_reach, &s->nbr_ovf, &s->posf, &s->gbox, &s->ctr_stripes,
                     &s->iperm, &s->vfull_s, &s->agrav_s, &s->hasg_s, &s->list_xd0};
   for (DevBuf* b : bufs) b->release();
   s->hstage.release();
@@ -782,7 +780,7 @@ swh_status swh_space_upload_xparts(swh_space* s, const void* xparts, int64_t cou
   }
   unsigned int* vbits = s->counters.as<unsigned int>() + 21;
   SWH_HIP(hipMemsetAsync(vbits, 0, sizeof(unsigned int), s->stream));
-  hipLaunchKernelGGL(vmax_kernel, dim3((int)((count + 255) / 256)), dim3(256), 0, s->stream,
+  hipLaunchKernelGGL(vmax_kernel, dim3((int)std::min<int64_t>((count + 255) / 256, kReduceBlocks)), dim3(256), 0, s->stream,
                      s->vfull_c.as<const float4>(), count, vbits);
   SWH_HIP(hipGetLastError());
   unsigned int vb = 0;
@@ -823,7 +821,7 @@ swh_status swh_space_drift(swh_space* s, const swh_drift_params* D, const swh_hy
                        s->vfull_s.as<float4>(), s->agrav_s.as<float4>(), s->hasg_s.as<int8_t>());
     s->xsorted_valid = true;
   }
-  hipLaunchKernelGGL(drift_kernel, dim3((int)((s->n + 255) / 256)), dim3(256), 0, st, soa_of(s),
+  hipLaunchKernelGGL(drift_kernel, dim3((int)std::min<int64_t>((s->n + 255) / 256, 4 * kReduceBlocks)), dim3(256), 0, st, soa_of(s),
                      s->vfull_s.as<const float4>(), s->agrav_s.as<const float4>(),
                      s->hasg_s.as<const int8_t>(), s->xdiff.as<float4>(), s->n, dp, dx_bits,
                      ctr + 2);

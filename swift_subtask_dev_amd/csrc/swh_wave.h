@@ -9,6 +9,37 @@
 
 namespace swh {
 
+// Counted launches add their per-wave counts into kCounterStripes stripes of
+// 8 counters (a block's stripe by its index), summed afterwards by
+// stripe_reduce_kernel: with one address for every wave's atomics the adds
+// serialise at the L2 (~10 ns each: a 1M-wave launch spent 11 ms on them).
+// Max / flag updates on one word from every wave: issue the atomic only when
+// it changes the word (a relaxed load first; the atomics would serialise).
+__device__ __forceinline__ void atomic_max_bits_if(unsigned int* p, unsigned int v) {
+  if (v > __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(p, v);
+}
+__device__ __forceinline__ void atomic_flag_if(unsigned int* p) {
+  if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) atomicOr(p, 1u);
+}
+// Max of v over a 256-thread block (every thread must call it), then one
+// conditional atomic per block on p (float bits, v >= 0). sm: 4 floats of LDS.
+__device__ __forceinline__ void block_max_bits(unsigned int* p, float v, float* sm) {
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float m = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+    if (m > 0.f) atomic_max_bits_if(p, __float_as_uint(m));
+  }
+}
+// Grid of the max / flag reductions: grid-stride loops over this many blocks
+// keep the atomics on one word to a few thousand per launch.
+constexpr int kReduceBlocks = 1024;
+constexpr int kCounterStripes = 256;
+__device__ __forceinline__ unsigned long long* counter_stripe(unsigned long long* c) {
+  return c + (size_t)(blockIdx.x & (kCounterStripes - 1)) * 8;
+}
+
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();

@@ -538,14 +538,14 @@ __global__ void cell_start_kernel(const uint32_t* __restrict__ keys, int64_t n, 
   for (int64_t c = prev + 1; c <= cur; c++) start[c] = (int)i;
 }
 
-__global__ void hmax_kernel(const double4* __restrict__ pos, const int8_t* __restrict__ tb,
+__global__ __launch_bounds__(256) void hmax_kernel(const double4* __restrict__ pos, const int8_t* __restrict__ tb,
                             int64_t n, unsigned int* out_bits) {
+  __shared__ float sm[4];
   float m = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     if (tb[i] != kTimeBinInhibited) m = fmaxf(m, (float)pos[i].w);
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0) atomic_max_bits_if(out_bits, __float_as_uint(m));
+  block_max_bits(out_bits, m, sm);
 }
 
 

@@ -40,10 +40,6 @@ constexpr int kGravBlock = 256;
 #define SWH_GRAV_IPER 2
 #endif
 constexpr int kIPer = SWH_GRAV_IPER;  // i-particles per thread per pass
-#ifndef SWH_P2P_SKIP
-#define SWH_P2P_SKIP 1
-#endif
-constexpr bool kP2PSkip = SWH_P2P_SKIP;  // skip i-slots empty in the whole wave
 
 struct GSoA {
   double4* pos;  // x, y, z, epsilon
@@ -303,15 +299,14 @@ __device__ __forceinline__ void p2p_tile(const double* sx, const double* sy, con
                                          const double* se2, const double* sh, const float* sm,
                                          int nt, const int* self_local, const double* xi,
                                          const double* yi, const double* zi, const double* hi2,
-                                         const double* hv, const bool* act, const bool* kw,
-                                         double dimx, double dimy, double dimz, double r_s_inv,
-                                         double* ax, double* ay, double* az, double* pot) {
+                                         const double* hv, const bool* act, double dimx,
+                                         double dimy, double dimz, double r_s_inv, double* ax,
+                                         double* ay, double* az, double* pot) {
   for (int t = 0; t < nt; t++) {
     const double xj = sx[t], yj = sy[t], zj = sz[t], e2j = se2[t], hvj = sh[t];
     const double mj = (double)sm[t];
 #pragma unroll
     for (int k = 0; k < IPER; k++) {
-      if (kP2PSkip && !kw[k]) continue;  // wave-uniform: no lane of this wave has an i in slot k
       double dx = xj - xi[k], dy = yj - yi[k], dz = zj - zi[k];
       if (PERIODIC) {
         dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
@@ -394,12 +389,6 @@ __global__ __launch_bounds__(BLK) void p2p_kernel(
 #pragma unroll
         for (int k = 0; k < IPER; k++) actp[k] = act[k];
       }
-      // slots k without an i in any lane of the wave skip their pair work, so the
-      // SIMD's cycles go to the other resident blocks (a 391-gpart leaf fills
-      // 391 of the 512 slots; the last wave's second slot is empty)
-      bool kw[IPER];
-#pragma unroll
-      for (int k = 0; k < IPER; k++) kw[k] = __any(actp[k]);
       for (int jbase = 0; jbase < J.count; jbase += BLK) {
         const int nt = min(BLK, J.count - jbase);
         __syncthreads();
@@ -424,8 +413,8 @@ __global__ __launch_bounds__(BLK) void p2p_kernel(
             nint += (unsigned long long)(nt - ((self_local[k] >= 0 && self_local[k] < nt) ? 1 : 0));
         }
 #define SWH_P2P_TILE(TR, PE, SE)                                                             \
-  p2p_tile<TR, PE, SE, IPER>(sx, sy, sz, se2, sh, sm, nt, self_local, xi, yi, zi, hi2, hv, actp, kw, \
-                       dimx, dimy, dimz, r_s_inv, ax, ay, az, pot)
+  p2p_tile<TR, PE, SE, IPER>(sx, sy, sz, se2, sh, sm, nt, self_local, xi, yi, zi, hi2, hv, actp, dimx, \
+                       dimy, dimz, r_s_inv, ax, ay, az, pot)
         if (self) {
           if (pr.truncated) {
             if (periodic) SWH_P2P_TILE(true, true, true);

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SWH_ABI_VERSION 8
+#define SWH_ABI_VERSION 9
 
 #if defined(__GNUC__)
 #define SWH_API __attribute__((visibility("default")))
@@ -188,6 +188,11 @@ SWH_API const char *swh_status_string(swh_status s);
 /* Last error text of the calling thread (empty string if none). */
 SWH_API const char *swh_last_error(void);
 SWH_API int swh_abi_version(void);
+/* The SPH kernel this library was built for ("cubic-spline" or
+ * "wendland-c2"): SWIFT selects it at configure time (--with-kernel,
+ * configure.ac:2107-2137, kernel_hydro.h:45-147); one library per kernel
+ * (libswifthip.so / libswifthip_wc2.so), the same ABI. (ABI v9) */
+SWH_API const char *swh_kernel_name(void);
 
 /* ================================================================== */
 /* (1) Per-task entry points                                          */

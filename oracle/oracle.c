@@ -8,7 +8,8 @@
  * and bench.py's cpu_baseline leg may load this library; the product
  * (swift_subtask_dev_amd) never links or calls it.
  *
- * Compiled twice (oracle/Makefile):
+ * Compiled twice per SPH kernel (oracle/Makefile; cubic spline, and Wendland C2
+ * with -DORACLE_WENDLAND_C2 into liboracle_wc2_{f32,f64}.so):
  *   ORACLE_F32 -> liboracle_f32.so, symbols orf_*: float arithmetic with the
  *      reference's exact operation order, operating in place on the 160-byte
  *      struct part (include/swift_compat.h). This is the faithful restatement.
@@ -63,15 +64,24 @@ static inline real rmax(real a, real b) { return a > b ? a : b; }
 static inline real rmin(real a, real b) { return a < b ? a : b; }
 
 /* ======================================================================== */
-/* Constants — restated from src/kernel_hydro.h:45-64,195-241 (cubic spline,
- * 3D), src/dimension.h:40-43, src/adiabatic_index.h:43-44,
+/* Constants — restated from src/kernel_hydro.h:45-64,121-147,195-241 (3D),
+ * src/dimension.h:40-43, src/adiabatic_index.h:43-44,
  * src/hydro/SPHENIX/hydro_parameters.h:53. Same C expressions, so the float
- * values are bit-identical to the reference macros.                         */
+ * values are bit-identical to the reference macros. The kernel is a
+ * compile-time choice as in SWIFT (configure --with-kernel): cubic spline by
+ * default, Wendland C2 with -DORACLE_WENDLAND_C2 (liboracle_wc2_*.so).       */
 /* ======================================================================== */
+#if defined(ORACLE_WENDLAND_C2)
+#define kernel_degree 5
+#define kernel_ivals 1
+#define kernel_gamma ((float)(1.936492))
+#define kernel_constant ((float)(21. * M_1_PI / 2.))
+#else
 #define kernel_degree 3
 #define kernel_ivals 2
 #define kernel_gamma ((float)(1.825742))
 #define kernel_constant ((float)(16. * M_1_PI))
+#endif
 #define kernel_gamma_inv ((float)(1. / kernel_gamma))
 #define kernel_gamma2 ((float)(kernel_gamma * kernel_gamma))
 #define kernel_gamma_dim ((float)(kernel_gamma * kernel_gamma * kernel_gamma))
@@ -80,8 +90,13 @@ static inline real rmin(real a, real b) { return a < b ? a : b; }
 #define kernel_gamma_inv_dim_plus_one \
   ((float)(1. / (kernel_gamma * kernel_gamma * kernel_gamma * kernel_gamma)))
 #define kernel_ivals_f ((float)(kernel_ivals))
+#if defined(ORACLE_WENDLAND_C2)
+static const float kernel_coeffs[(kernel_degree + 1) * (kernel_ivals + 1)] = {
+    4.f, -15.f, 20.f, -10.f, 0.f, 1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#else
 static const float kernel_coeffs[(kernel_degree + 1) * (kernel_ivals + 1)] = {
     3.f, -3.f, 0.f, 0.5f, -1.f, 3.f, -3.f, 1.f, 0.f, 0.f, 0.f, 0.f};
+#endif
 #define kernel_root \
   ((float)(kernel_coeffs[kernel_degree]) * kernel_constant * kernel_gamma_inv_dim)
 #define hydro_dimension 3.f

@@ -4,6 +4,7 @@
 #include <cstddef>
 
 #include "swh_internal.h"
+#include "swh_physics.h"
 #include "swift_compat.h"
 
 namespace swh {
@@ -118,6 +119,8 @@ void swh_context::unlease(swh::TaskWorker* w) { w->busy.unlock(); }
 extern "C" {
 
 int swh_abi_version(void) { return SWH_ABI_VERSION; }
+
+const char* swh_kernel_name(void) { return SWH_KERNEL_NAME; }
 
 const char* swh_last_error(void) { return swh::g_err; }
 

@@ -110,19 +110,29 @@ __global__ __launch_bounds__(256) void list_disp_kernel(const float4* __restrict
   block_max_bits(disp_bits, d, sm);
 }
 
-// Pass 2: stale if an active particle is unlisted, or any listed particle's
-// H_now + 2D exceeds its build reach.
+// Pass 2: stale if an active particle is unlisted, or the H_now + 2D of ANY
+// particle in a cell (active or not) exceeds its build reach. The j side of
+// the list criterion used R_j of every candidate, and the drift grows h of
+// inactive particles too (drift_part's h_dt term), so an inactive j whose H
+// outgrew R_j - 2D would lose force pairs r < H_j (DOPAIR2's max(H_i, H_j)).
+// Every candidate's build h is the w of its staging copy (posf, rewritten by
+// every build): R_j,build >= fl(h) gamma (1 + skin), taken 1e-6 low for the
+// float product the build rounded.
 __global__ __launch_bounds__(256) void list_check_kernel(SoA a, ListDev ld, int64_t n,
                                                          int max_active_bin,
+                                                         const int* __restrict__ pcell,
                                                          const unsigned int* __restrict__ disp_bits,
                                                          unsigned int* __restrict__ stale) {
   __shared__ float sm[4];
   const double D = (double)__uint_as_float(*disp_bits);
+  const double gs1 = (double)kGamma * (double)ld.skin1 * (1. - 1e-6);
   float bad = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    if (!active_part(a, i, max_active_bin)) continue;
+    if (a.tb[i] == kTimeBinInhibited || pcell[i] < 0) continue;
     const double H = a.pos[i].w * (double)kGamma;
+    if (H + 2. * D > (double)ld.posf[i].w * gs1) bad = 1.f;
+    if (!active_part(a, i, max_active_bin)) continue;
     if (ld.base[i] < 0 || H + 2. * D > (double)ld.reach[i]) bad = 1.f;
   }
   block_max_bits(stale, bad, sm);  // 1.0f's bits: nonzero = stale
@@ -742,7 +752,8 @@ static swh_status check_kept_lists(swh_space* s, const swh_hydro_params* P, bool
                      s->xdiff.as<const float4>(), s->list_xd0.as<const float4>(),
                      s->tb.as<const int8_t>(), s->n, disp_slot(s));
   hipLaunchKernelGGL(list_check_kernel, dim3(std::min(nb, kReduceBlocks)), dim3(256), 0, s->stream, soa_of(s), list_dev(s),
-                     s->n, P->max_active_bin, disp_slot(s), keep_stale_slot(s));
+                     s->n, P->max_active_bin, s->pcell.as<const int>(), disp_slot(s),
+                     keep_stale_slot(s));
   hipLaunchKernelGGL(list_rwrap_kernel, dim3(1), dim3(64), 0, s->stream, rwrap_slot(s),
                      rwrap_base_slot(s), (float)s->grid.dx);
   SWH_HIP(hipGetLastError());

@@ -1,10 +1,11 @@
-// swh_physics.h — device-side SPHENIX / cubic-spline / Wendland-C2 physics,
+// swh_physics.h — device-side SPHENIX physics with the cubic-spline or
+// Wendland-C2 SPH kernel (build-time choice), and Wendland-C2 gravity softening,
 // templated on the arithmetic type T (double = the fp64 path, float = the
 // reference's own precision). Constants are the reference's float values
 // (same expressions as the macros they cite), promoted to T.
 //
 // References (/root/reference/src):
-//   kernel_hydro.h:45-64,195-284   cubic spline, kernel_deval
+//   kernel_hydro.h:45-64,121-147,195-284   cubic spline, Wendland C2, kernel_deval
 //   hydro/SPHENIX/hydro_iact.h     runner_iact_nonsym_{density,gradient,force}
 //   hydro/SPHENIX/hydro.h          end_density / prepare_gradient / prepare_force ...
 //   kernel_gravity.h:48-100, kernel_long_gravity.h:204-262, gravity/MultiSoftening/gravity_iact.h
@@ -16,15 +17,29 @@
 
 namespace swh {
 
-// --- constants: cubic spline, 3D, gamma = 5/3 -----------------------------
+// --- constants: the SPH kernel (3D), gamma = 5/3 ---------------------------
+// The kernel is a build-time choice, as SWIFT's configure --with-kernel
+// (configure.ac:2107-2137): cubic spline (default, libswifthip.so) or
+// Wendland C2 (-DSWH_KERNEL_WENDLAND_C2, libswifthip_wc2.so).
 constexpr double kPi = 3.14159265358979323846;
+#if defined(SWH_KERNEL_WENDLAND_C2)
+// kernel_hydro.h:121-147: degree 5, one branch, W(x) = (1-x)^4 (1+4x)
+constexpr float kGamma = (float)(1.936492);
+constexpr float kConstant = (float)(21. * (1. / kPi) / 2.);
+constexpr float kKernelW0 = 1.f;  // kernel_coeffs[kernel_degree]
+#define SWH_KERNEL_NAME "wendland-c2"
+#else
+// kernel_hydro.h:45-64: degree 3, two branches
 constexpr float kGamma = (float)(1.825742);
+constexpr float kConstant = (float)(16. * (1. / kPi));
+constexpr float kKernelW0 = 0.5f;  // kernel_coeffs[kernel_degree]
+#define SWH_KERNEL_NAME "cubic-spline"
+#endif
 constexpr float kGammaInv = (float)(1. / kGamma);
 constexpr float kGamma2 = kGamma * kGamma;
-constexpr float kConstant = (float)(16. * (1. / kPi));
 constexpr float kGammaInvDim = (float)(1. / (kGamma * kGamma * kGamma));
 constexpr float kGammaInvDimPlusOne = (float)(1. / (kGamma * kGamma * kGamma * kGamma));
-constexpr float kRoot = 0.5f * kConstant * kGammaInvDim;  // W(0)
+constexpr float kRoot = kKernelW0 * kConstant * kGammaInvDim;  // W(0), kernel_root
 constexpr float kDim = 3.f;
 constexpr float kDimInv = 0.3333333333f;
 constexpr float kHydroGamma = 1.66666666666666667f;
@@ -94,12 +109,51 @@ __device__ __forceinline__ void r_and_inv<float>(float r2, float& r, float& r_in
   r_inv = r > 0.f ? 1.f / r : 0.f;
 }
 
-// kernel_deval (kernel_hydro.h:257-284). Branch 0: u/H < 1/2, branch 1: < 1,
-// branch 2 (outside support): all-zero coefficients. Coefficients are picked
-// with selects instead of a table load.
+// kernel_deval (kernel_hydro.h:257-284): W(u), dW/du from the kernel's
+// coefficient table by Horner, the branch index (int)(x * kernel_ivals)
+// clamped to kernel_ivals (an all-zero row: outside the support).
 template <typename T>
 __device__ __forceinline__ void kernel_deval(T u, T& W, T& dW_dx);
 
+#if defined(SWH_KERNEL_WENDLAND_C2)
+// fp64: (1-x)^4 (1+4x) and its derivative -20 x (1-x)^3 in closed form
+// (equal to the table's Horner form on [0,1), zero beyond).
+template <>
+__device__ __forceinline__ void kernel_deval<double>(double u, double& W, double& dW_dx) {
+  const double x = u * (double)kGammaInv;
+  const double t = fmax(1. - x, 0.);
+  const double t2 = t * t;
+  const double t3 = t2 * t;
+  W = t3 * t * fma(4., x, 1.) * ((double)kConstant * (double)kGammaInvDim);
+  dW_dx = -20. * x * t3 * ((double)kConstant * (double)kGammaInvDimPlusOne);
+}
+
+// float: the reference's Horner evaluation of {4, -15, 20, -10, 0, 1} on
+// branch 0 and the zero row beyond (kernel_hydro.h:143-146).
+template <>
+__device__ __forceinline__ void kernel_deval<float>(float u, float& W, float& dW_dx) {
+  using T = float;
+  const T x = u * (T)kGammaInv;
+  const int temp = (int)(x * (T)1);
+  const bool in = (temp > 1 ? 1 : temp) == 0;
+  const T c0 = in ? (T)4 : (T)0, c1 = in ? (T)-15 : (T)0, c2 = in ? (T)20 : (T)0;
+  const T c3 = in ? (T)-10 : (T)0, c4 = (T)0, c5 = in ? (T)1 : (T)0;
+  T w = c0 * x + c1;
+  T dw = c0;
+  dw = dw * x + w;
+  w = x * w + c2;
+  dw = dw * x + w;
+  w = x * w + c3;
+  dw = dw * x + w;
+  w = x * w + c4;
+  dw = dw * x + w;
+  w = x * w + c5;
+  w = tmax(w, (T)0);
+  dw = tmin(dw, (T)0);
+  W = w * (T)kConstant * (T)kGammaInvDim;
+  dW_dx = dw * (T)kConstant * (T)kGammaInvDimPlusOne;
+}
+#else
 // fp64: the same piecewise cubic in closed form, w = (1-x)^3_+ - 4 (1/2-x)^3_+
 // (equal to the table's Horner forms on [0,1/2) and [1/2,1), zero beyond),
 // without the index selects.
@@ -113,6 +167,8 @@ __device__ __forceinline__ void kernel_deval<double>(double u, double& W, double
   dW_dx = fma(12., q2, -3. * t2) * ((double)kConstant * (double)kGammaInvDimPlusOne);
 }
 
+// float: branch 0: u/H < 1/2, branch 1: < 1, branch 2 (outside support):
+// all-zero coefficients, picked with selects instead of a table load.
 template <>
 __device__ __forceinline__ void kernel_deval<float>(float u, float& W, float& dW_dx) {
   using T = float;
@@ -134,6 +190,7 @@ __device__ __forceinline__ void kernel_deval<float>(float u, float& W, float& dW
   W = w * (T)kConstant * (T)kGammaInvDim;
   dW_dx = dw * (T)kConstant * (T)kGammaInvDimPlusOne;
 }
+#endif
 
 // ---------------------------------------------------------------------------
 // Accumulators of one i-particle for each loop (registers for the duration of

@@ -31,7 +31,11 @@ static swh_context *swhs_ctx = NULL;
 static swh_part_layout swhs_layout;
 static swh_gpart_layout swhs_glayout;
 
+#if defined(SWH_KERNEL_WENDLAND_C2)
+#define kernel_gamma ((float)(1.936492)) /* src/kernel_hydro.h:137 */
+#else
 #define kernel_gamma ((float)(1.825742)) /* src/kernel_hydro.h:51 */
+#endif
 #define space_maxreldx 0.1f              /* src/space.h:66 */
 
 /* src/sort_part.h:59-92 */

@@ -18,6 +18,10 @@ PKG = Path(__file__).resolve().parent
 # SWH_LIB_PATH: developer override (occupancy experiments, tools/build_variant.sh)
 LIB_PATH = Path(os.environ.get("SWH_LIB_PATH", str(PKG / "libswifthip.so")))
 ADAPTER_PATH = PKG / "libswifthip_swift.so"
+# The SPH kernel is a build-time choice, as SWIFT's configure --with-kernel
+# (configure.ac:2107-2137): one library per kernel, the same C ABI.
+KERNEL_LIBS = {"cubic-spline": LIB_PATH, "wendland-c2": PKG / "libswifthip_wc2.so"}
+ADAPTER_LIBS = {"cubic-spline": ADAPTER_PATH, "wendland-c2": PKG / "libswifthip_swift_wc2.so"}
 
 STATUS = {
     0: "ok", 1: "invalid argument", 2: "HIP runtime error", 3: "Interacting unsorted cells.",
@@ -29,6 +33,7 @@ STATUS = {
 HIP_SYMBOLS = [
     "swh_part_layout_sphenix", "swh_gpart_layout_multisoftening", "swh_init", "swh_finalize",
     "swh_set_precision", "swh_status_string", "swh_last_error", "swh_abi_version",
+    "swh_kernel_name",
     "swh_doself_density", "swh_dopair_density", "swh_doself_gradient", "swh_dopair_gradient",
     "swh_doself_force", "swh_dopair_force", "swh_doself_subset_density",
     "swh_dopair_subset_density", "swh_grav_self_pp", "swh_grav_pair_pp", "swh_space_create",
@@ -68,23 +73,27 @@ class SwhError(RuntimeError):
         super().__init__(f"{where}: {STATUS.get(status, status)} {detail}".strip())
 
 
-_lib = None
-_adapter = None
+_libs: dict = {}
+_adapters: dict = {}
 
 
 
 SWH_BUSY = 9  # swh_*_query: queued work still running
 
-def load() -> C.CDLL:
-    """Load libswifthip.so (raises if it was not built)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not LIB_PATH.exists():
+def load(kernel: str = "cubic-spline") -> C.CDLL:
+    """Load the libswifthip built for `kernel` (raises if it was not built).
+    The default cubic-spline library is loaded RTLD_GLOBAL (the adapter links
+    it); other kernels' libraries are private to their handle."""
+    if kernel in _libs:
+        return _libs[kernel]
+    if kernel not in KERNEL_LIBS:
+        raise ValueError(f"unknown SPH kernel {kernel!r}: {sorted(KERNEL_LIBS)}")
+    path = KERNEL_LIBS[kernel]
+    if not path.exists():
         raise ImportError(
-            f"{LIB_PATH} is missing: build it with `python -m swift_subtask_dev_amd.build` "
+            f"{path} is missing: build it with `python -m swift_subtask_dev_amd.build` "
             "(the HIP library is the only implementation of this path)")
-    lib = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
+    lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL if kernel == "cubic-spline" else C.RTLD_LOCAL)
     vp, i32, i64, dp = C.c_void_p, C.c_int32, C.c_int64, C.c_double
     P = C.POINTER
     sigs = {
@@ -96,6 +105,7 @@ def load() -> C.CDLL:
         "swh_status_string": (C.c_char_p, [C.c_int]),
         "swh_last_error": (C.c_char_p, []),
         "swh_abi_version": (C.c_int, []),
+        "swh_kernel_name": (C.c_char_p, []),
         "swh_doself_density": (C.c_int, [vp, P(abi.CellView), P(abi.PartLayout), P(abi.HydroParams)]),
         "swh_doself_gradient": (C.c_int, [vp, P(abi.CellView), P(abi.PartLayout), P(abi.HydroParams)]),
         "swh_doself_force": (C.c_int, [vp, P(abi.CellView), P(abi.PartLayout), P(abi.HydroParams)]),
@@ -155,18 +165,21 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
+    got = lib.swh_kernel_name().decode()
+    if got != kernel:
+        raise ImportError(f"{path} was built for the {got} kernel, not {kernel}")
+    _libs[kernel] = lib
     return lib
 
 
-def load_adapter() -> C.CDLL:
-    global _adapter
-    if _adapter is not None:
-        return _adapter
-    load()
-    if not ADAPTER_PATH.exists():
-        raise ImportError(f"{ADAPTER_PATH} is missing: run the build")
-    ad = C.CDLL(str(ADAPTER_PATH))
+def load_adapter(kernel: str = "cubic-spline") -> C.CDLL:
+    if kernel in _adapters:
+        return _adapters[kernel]
+    load(kernel)
+    path = ADAPTER_LIBS[kernel]
+    if not path.exists():
+        raise ImportError(f"{path} is missing: run the build")
+    ad = C.CDLL(str(path))
     vp, P = C.c_void_p, C.POINTER
     ad.swifthip_swift_init.restype = C.c_int
     ad.swifthip_swift_init.argtypes = [C.c_int, C.c_int]
@@ -194,13 +207,13 @@ def load_adapter() -> C.CDLL:
         getattr(ad, n).restype = None
     ad.runner_dopair_recursive_grav.argtypes = [vp, vp, vp, C.c_int]
     ad.runner_dopair_recursive_grav.restype = None
-    _adapter = ad
+    _adapters[kernel] = ad
     return ad
 
 
-def _check(status: int, where: str) -> None:
+def _check(status: int, where: str, lib: C.CDLL | None = None) -> None:
     if status != 0:
-        detail = (load().swh_last_error() or b"").decode(errors="replace")
+        detail = ((lib or load()).swh_last_error() or b"").decode(errors="replace")
         raise SwhError(status, where, detail)
 
 
@@ -223,11 +236,12 @@ def _ptr(a: np.ndarray) -> int:
 class Context:
     """One swh_context (device + per-task streams)."""
 
-    def __init__(self, device: int = 0, precision: str = "f64"):
-        lib = load()
+    def __init__(self, device: int = 0, precision: str = "f64", kernel: str = "cubic-spline"):
+        lib = load(kernel)
+        self.kernel = kernel
         self._lib = lib
         h = C.c_void_p()
-        _check(lib.swh_init(C.byref(h), device), "swh_init")
+        _check(lib.swh_init(C.byref(h), device), "swh_init", self._lib)
         self.handle = h
         self.set_precision(precision)
         self.L = part_layout()
@@ -235,7 +249,7 @@ class Context:
 
     def set_precision(self, precision: str) -> None:
         _check(self._lib.swh_set_precision(self.handle, 0 if precision == "f64" else 1),
-               "swh_set_precision")
+               "swh_set_precision", self._lib)
         self.precision = precision
 
     def close(self) -> None:
@@ -263,14 +277,14 @@ class Context:
     def doself(self, loop: str, view: abi.CellView, P: abi.HydroParams) -> None:
         fn = {"density": self._lib.swh_doself_density, "gradient": self._lib.swh_doself_gradient,
               "force": self._lib.swh_doself_force}[loop]
-        _check(fn(self.handle, C.byref(view), C.byref(self.L), C.byref(P)), f"doself_{loop}")
+        _check(fn(self.handle, C.byref(view), C.byref(self.L), C.byref(P)), f"doself_{loop}", self._lib)
 
     def dopair(self, loop: str, vi, vj, shift, P) -> None:
         fn = {"density": self._lib.swh_dopair_density, "gradient": self._lib.swh_dopair_gradient,
               "force": self._lib.swh_dopair_force}[loop]
         sh = (C.c_double * 3)(*shift)
         _check(fn(self.handle, C.byref(vi), C.byref(vj), sh, C.byref(self.L), C.byref(P)),
-               f"dopair_{loop}")
+               f"dopair_{loop}", self._lib)
 
 
 class HydroSpace:
@@ -280,7 +294,7 @@ class HydroSpace:
         self.ctx = ctx
         self._lib = ctx._lib
         h = C.c_void_p()
-        _check(self._lib.swh_space_create(ctx.handle, C.byref(h)), "swh_space_create")
+        _check(self._lib.swh_space_create(ctx.handle, C.byref(h)), "swh_space_create", self._lib)
         self.handle = h
 
     def close(self):
@@ -298,11 +312,11 @@ class HydroSpace:
                    diag_mode=0, list_capacity=0, list_skin=0.0, list_keep=0):
         t = abi.Tuning(cell_factor, loop_variant, group_size, cell_scale, diag_mode,
                        list_capacity, list_skin, list_keep)
-        _check(self._lib.swh_space_set_tuning(self.handle, C.byref(t)), "set_tuning")
+        _check(self._lib.swh_space_set_tuning(self.handle, C.byref(t)), "set_tuning", self._lib)
 
     def info(self) -> dict:
         i = abi.SpaceInfo()
-        _check(self._lib.swh_space_get_info(self.handle, C.byref(i)), "get_info")
+        _check(self._lib.swh_space_get_info(self.handle, C.byref(i)), "get_info", self._lib)
         return {"cdim": list(i.cdim), "ncell": i.ncell, "ngroups": i.ngroups,
                 "cell_width": list(i.cell_width), "h_max": i.h_max,
                 "loop_stats": list(i.loop_stats), "list_entries": i.list_entries,
@@ -313,32 +327,32 @@ class HydroSpace:
         """parts: numpy PART_DTYPE array (host) or a device pointer (int) with count."""
         if on_device:
             _check(self._lib.swh_space_upload_parts(self.handle, C.c_void_p(parts), count,
-                                                    C.byref(self.ctx.L), 1), "upload")
+                                                    C.byref(self.ctx.L), 1), "upload", self._lib)
         else:
             _check(self._lib.swh_space_upload_parts(self.handle, _ptr(parts), len(parts),
-                                                    C.byref(self.ctx.L), 0), "upload")
+                                                    C.byref(self.ctx.L), 0), "upload", self._lib)
 
     def download(self, parts: np.ndarray, fields=abi.FIELDS_ALL):
         _check(self._lib.swh_space_download_parts(self.handle, _ptr(parts), C.byref(self.ctx.L),
-                                                  fields, 0), "download")
+                                                  fields, 0), "download", self._lib)
 
     def rebuild(self, P, min_cell_width=0.0):
-        _check(self._lib.swh_space_rebuild(self.handle, C.byref(P), min_cell_width), "rebuild")
+        _check(self._lib.swh_space_rebuild(self.handle, C.byref(P), min_cell_width), "rebuild", self._lib)
 
     def init_parts(self, P):
-        _check(self._lib.swh_space_init_parts(self.handle, C.byref(P)), "init_parts")
+        _check(self._lib.swh_space_init_parts(self.handle, C.byref(P)), "init_parts", self._lib)
 
     def reset_acceleration(self, P):
         _check(self._lib.swh_space_reset_acceleration(self.handle, C.byref(P)),
-               "reset_acceleration")
+               "reset_acceleration", self._lib)
 
     def set_stream(self, stream_ptr: int):
         """Bind a HIP stream (e.g. torch.cuda.current_stream().cuda_stream)."""
-        _check(self._lib.swh_space_set_stream(self.handle, C.c_void_p(stream_ptr)), "set_stream")
+        _check(self._lib.swh_space_set_stream(self.handle, C.c_void_p(stream_ptr)), "set_stream", self._lib)
 
     def _loop(self, fn, P, count):
         n = C.c_int64(0)
-        _check(fn(self.handle, C.byref(P), C.byref(n) if count else None), fn.__name__)
+        _check(fn(self.handle, C.byref(P), C.byref(n) if count else None), fn.__name__, self._lib)
         return n.value if count else None
 
     def density(self, P, count=True):
@@ -353,24 +367,24 @@ class HydroSpace:
     def ghost(self, P):
         it = C.c_int32(0)
         nu = C.c_int64(0)
-        _check(self._lib.swh_ghost(self.handle, C.byref(P), C.byref(it), C.byref(nu)), "ghost")
+        _check(self._lib.swh_ghost(self.handle, C.byref(P), C.byref(it), C.byref(nu)), "ghost", self._lib)
         return it.value, nu.value
 
     def extra_ghost(self, P):
-        _check(self._lib.swh_extra_ghost(self.handle, C.byref(P)), "extra_ghost")
+        _check(self._lib.swh_extra_ghost(self.handle, C.byref(P)), "extra_ghost", self._lib)
 
     def end_force(self, P):
-        _check(self._lib.swh_end_force(self.handle, C.byref(P)), "end_force")
+        _check(self._lib.swh_end_force(self.handle, C.byref(P)), "end_force", self._lib)
 
     def sync(self):
-        _check(self._lib.swh_space_sync(self.handle), "sync")
+        _check(self._lib.swh_space_sync(self.handle), "sync", self._lib)
 
     def done(self) -> bool:
         """swh_space_query: True once the queued work has finished (no wait)."""
         r = self._lib.swh_space_query(self.handle)
         if r == SWH_BUSY:
             return False
-        _check(r, "query")
+        _check(r, "query", self._lib)
         return True
 
     def upload_xparts(self, xparts: np.ndarray):
@@ -378,23 +392,23 @@ class HydroSpace:
         XL = abi.XPartLayout(abi.XPART_DTYPE.itemsize, abi.XPART_DTYPE.fields["v_full"][1],
                              abi.XPART_DTYPE.fields["a_grav"][1])
         _check(self._lib.swh_space_upload_xparts(self.handle, _ptr(xparts), len(xparts),
-                                                 C.byref(XL), 0), "upload_xparts")
+                                                 C.byref(XL), 0), "upload_xparts", self._lib)
 
     def drift(self, D: abi.DriftParams, P: abi.HydroParams):
-        _check(self._lib.swh_space_drift(self.handle, C.byref(D), C.byref(P)), "drift")
+        _check(self._lib.swh_space_drift(self.handle, C.byref(D), C.byref(P)), "drift", self._lib)
 
     def set_owned(self, n_owned: int):
         """Caller indices >= n_owned become read-only halo (foreign) particles."""
-        _check(self._lib.swh_space_set_owned(self.handle, n_owned), "set_owned")
+        _check(self._lib.swh_space_set_owned(self.handle, n_owned), "set_owned", self._lib)
 
     def pack_halo(self, idx_ptr: int, n: int, out_ptr: int):
         """Device pointers: int32 caller indices -> n * 8 float halo records."""
         _check(self._lib.swh_space_pack_halo(self.handle, C.c_void_p(idx_ptr), n,
-                                             C.c_void_p(out_ptr)), "pack_halo")
+                                             C.c_void_p(out_ptr)), "pack_halo", self._lib)
 
     def unpack_halo(self, idx_ptr: int, n: int, in_ptr: int, fields: int = 31):
         _check(self._lib.swh_space_unpack_halo(self.handle, C.c_void_p(idx_ptr), n,
-                                               C.c_void_p(in_ptr), fields), "unpack_halo")
+                                               C.c_void_p(in_ptr), fields), "unpack_halo", self._lib)
 
     def hydro_step(self, P):
         """The full SPHENIX hydro chain of one step:
@@ -416,7 +430,7 @@ class GravSpace:
         self.ctx = ctx
         self._lib = ctx._lib
         h = C.c_void_p()
-        _check(self._lib.swh_gspace_create(ctx.handle, C.byref(h)), "swh_gspace_create")
+        _check(self._lib.swh_gspace_create(ctx.handle, C.byref(h)), "swh_gspace_create", self._lib)
         self.handle = h
 
     def close(self):
@@ -432,7 +446,7 @@ class GravSpace:
 
     def upload(self, gparts: np.ndarray):
         _check(self._lib.swh_gspace_upload(self.handle, _ptr(gparts), len(gparts),
-                                           C.byref(self.ctx.GL), 0), "gspace_upload")
+                                           C.byref(self.ctx.GL), 0), "gspace_upload", self._lib)
 
     def set_leaves(self, leaves: np.ndarray, pair_offset: np.ndarray, pairs: np.ndarray):
         leaves = np.ascontiguousarray(leaves, dtype=abi.LEAF_DTYPE)
@@ -442,13 +456,13 @@ class GravSpace:
         _check(self._lib.swh_gspace_set_leaves(
             self.handle, _ptr(leaves), len(leaves),
             pair_offset.ctypes.data_as(C.POINTER(C.c_int32)), _ptr(pairs), len(pairs)),
-            "set_leaves")
+            "set_leaves", self._lib)
 
     def make_multipoles(self, want=False):
         """Leaf multipoles on the device (P2M); want=True returns a host copy
         (ctypes array of abi.Multipole)."""
         out = (abi.Multipole * max(1, len(self._keep[0])))() if want else None
-        _check(self._lib.swh_gspace_make_multipoles(self.handle, out), "make_multipoles")
+        _check(self._lib.swh_gspace_make_multipoles(self.handle, out), "make_multipoles", self._lib)
         return out
 
     def pp(self, G: abi.GravParams, count=True, m2p=False):
@@ -456,7 +470,7 @@ class GravSpace:
         m2p=True returns (P2P interactions, M2P evaluations)."""
         n, m = C.c_int64(0), C.c_int64(0)
         _check(self._lib.swh_grav_pp_batch(self.handle, C.byref(G), C.byref(n) if count else None,
-                                           C.byref(m) if m2p else None), "grav_pp_batch")
+                                           C.byref(m) if m2p else None), "grav_pp_batch", self._lib)
         if m2p:
             return n.value, m.value
         return n.value if count else None
@@ -466,19 +480,19 @@ class GravSpace:
         cells = np.ascontiguousarray(cells)
         assert cells.dtype.itemsize == C.sizeof(abi.GCell)
         self._tree = cells
-        _check(self._lib.swh_gspace_set_tree(self.handle, _ptr(cells), len(cells)), "set_tree")
+        _check(self._lib.swh_gspace_set_tree(self.handle, _ptr(cells), len(cells)), "set_tree", self._lib)
 
     def set_owned_cells(self, owned):
         """Per-cell ownership (uint8, whole subtrees; None: every cell) for a
         step sharded over ranks (swh_gspace_set_owned_cells)."""
         if owned is None:
-            _check(self._lib.swh_gspace_set_owned_cells(self.handle, None, 0), "set_owned_cells")
+            _check(self._lib.swh_gspace_set_owned_cells(self.handle, None, 0), "set_owned_cells", self._lib)
             return
         owned = np.ascontiguousarray(owned, dtype=np.uint8)
         self._owned = owned
         _check(self._lib.swh_gspace_set_owned_cells(
             self.handle, owned.ctypes.data_as(C.POINTER(C.c_uint8)), len(owned)),
-            "set_owned_cells")
+            "set_owned_cells", self._lib)
 
     def tree(self, G: abi.GravParams, self_cells, pair_cells) -> dict:
         """runner_doself_recursive_grav on self_cells, runner_dopair_recursive_grav
@@ -487,7 +501,7 @@ class GravSpace:
         pc = np.ascontiguousarray(pair_cells, dtype=np.int32).reshape(-1)
         st = abi.GravTreeStats()
         _check(self._lib.swh_grav_tree(self.handle, C.byref(G), _ptr(sc), len(sc), _ptr(pc),
-                                       len(pc) // 2, C.byref(st)), "grav_tree")
+                                       len(pc) // 2, C.byref(st)), "grav_tree", self._lib)
         return {"n_pp": st.n_pp, "n_m2p": st.n_m2p, "n_m2l": st.n_m2l,
                 "n_pp_tasks": st.n_pp_tasks, "n_skipped": st.n_skipped,
                 "ms": {"multipoles": st.ms_multipoles, "walk": st.ms_walk, "p2p": st.ms_p2p,
@@ -496,27 +510,27 @@ class GravSpace:
     def multipoles(self):
         """The tree cells' multipoles (abi.Multipole array)."""
         out = (abi.Multipole * len(self._tree))()
-        _check(self._lib.swh_gspace_multipoles(self.handle, out), "multipoles")
+        _check(self._lib.swh_gspace_multipoles(self.handle, out), "multipoles", self._lib)
         return out
 
     def field_tensors(self) -> np.ndarray:
         out = np.zeros((len(self._tree), abi.MPOLE_TERMS), dtype=np.float32)
-        _check(self._lib.swh_gspace_field_tensors(self.handle, _ptr(out)), "field_tensors")
+        _check(self._lib.swh_gspace_field_tensors(self.handle, _ptr(out)), "field_tensors", self._lib)
         return out
 
     def download(self, gparts: np.ndarray):
         _check(self._lib.swh_gspace_download(self.handle, _ptr(gparts), C.byref(self.ctx.GL), 0),
-               "gspace_download")
+               "gspace_download", self._lib)
 
     def sync(self):
-        _check(self._lib.swh_gspace_sync(self.handle), "gspace_sync")
+        _check(self._lib.swh_gspace_sync(self.handle), "gspace_sync", self._lib)
 
     def done(self) -> bool:
         """swh_gspace_query: True once the queued work has finished (no wait)."""
         r = self._lib.swh_gspace_query(self.handle)
         if r == SWH_BUSY:
             return False
-        _check(r, "gspace_query")
+        _check(r, "gspace_query", self._lib)
         return True
 
     def pm_mesh(self, N: int, box_size: float, r_s: float, const_G: float = 1.0,
@@ -528,5 +542,5 @@ class GravSpace:
                          box_size, r_s, const_G)
         pot = np.zeros((N, N, N), dtype=np.float64) if want_potential else None
         _check(self._lib.swh_gspace_pm_mesh(self.handle, C.byref(M),
-                                            _ptr(pot) if pot is not None else None), "pm_mesh")
+                                            _ptr(pot) if pot is not None else None), "pm_mesh", self._lib)
         return pot

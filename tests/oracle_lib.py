@@ -16,6 +16,9 @@ REPO = Path(__file__).resolve().parents[1]
 ORACLE_DIR = REPO / "oracle"
 F32 = ORACLE_DIR / "_build" / "liboracle_f32.so"
 F64 = ORACLE_DIR / "_build" / "liboracle_f64.so"
+# the Wendland C2 SPH kernel builds (oracle/Makefile, -DORACLE_WENDLAND_C2)
+WC2 = {"f32": ORACLE_DIR / "_build" / "liboracle_wc2_f32.so",
+       "f64": ORACLE_DIR / "_build" / "liboracle_wc2_f64.so"}
 
 _libs = {}
 
@@ -34,10 +37,16 @@ class OracleGravParams(abi.GravParams):
     pass
 
 
-def load(prec: str = "f32") -> C.CDLL:
-    if prec in _libs:
-        return _libs[prec]
-    path = F32 if prec == "f32" else F64
+def load(prec: str = "f32", kernel: str = "cubic-spline") -> C.CDLL:
+    key = (prec, kernel)
+    if key in _libs:
+        return _libs[key]
+    if kernel == "cubic-spline":
+        path = F32 if prec == "f32" else F64
+    elif kernel == "wendland-c2":
+        path = WC2[prec]
+    else:
+        raise ValueError(kernel)
     if not _libs:
         build()  # incremental make: picks up oracle.c edits
     lib = C.CDLL(str(path))
@@ -110,12 +119,12 @@ def load(prec: str = "f32") -> C.CDLL:
         sig("celltree_ncells", i64, [vp])
         sig("celltree_run", C.c_double, [vp, vp, C.c_int, C.c_int])
     lib.pfx = pfx
-    _libs[prec] = lib
+    _libs[key] = lib
     return lib
 
 
-def fn(prec: str, name: str):
-    lib = load(prec)
+def fn(prec: str, name: str, kernel: str = "cubic-spline"):
+    lib = load(prec, kernel)
     return getattr(lib, lib.pfx + name)
 
 

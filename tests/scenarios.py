@@ -60,11 +60,11 @@ def density_columns(sub: np.ndarray, end: bool = True) -> np.ndarray:
         sub["wcount"], sub["wcount_dh"], sub["div_v"], sub["rot_v"]])
 
 
-def end_calculation(sub: np.ndarray, P):
+def end_calculation(sub: np.ndarray, P, kernel="cubic-spline"):
     """test27cells.c end_calculation: hydro_end_density, then wcount *= h^3 *
     kernel_norm (via the oracle's restated hydro_end_density)."""
-    f = O.fn("f32", "part_end_density")
-    norm = O.load("f32").orf_kernel_norm()
+    f = O.fn("f32", "part_end_density", kernel)
+    norm = O.load("f32", kernel).orf_kernel_norm()
     for i in range(len(sub)):
         f(sub[i:i + 1].ctypes.data, C.byref(P))
     h = sub["h"].astype(np.float32)
@@ -72,7 +72,7 @@ def end_calculation(sub: np.ndarray, P):
 
 
 def run27(parts, bounds, locs, backend: str, P, engine=None, main=13, loops="density",
-          subset=False):
+          subset=False, kernel="cubic-spline"):
     """Density loop of test27cells.c:566-582 on the main cell: 26 pairs +
     self. backend: 'sorted' (oracle restatement of DOPAIR1/DOSELF1), 'brute'
     (tools.c pairs_all_density/self_all_density), 'adapter' (GPU through the
@@ -84,22 +84,22 @@ def run27(parts, bounds, locs, backend: str, P, engine=None, main=13, loops="den
     r = eb.runner_ptr
     ncell = len(bounds)
     if backend == "sorted":
-        pair = O.fn("f32", "dopair1_branch")
-        slf = O.fn("f32", "doself1_branch")
+        pair = O.fn("f32", "dopair1_branch", kernel)
+        slf = O.fn("f32", "doself1_branch", kernel)
         for j in range(ncell):
             if j != main:
                 assert pair(C.addressof(eb.runner), cs.ptr(main), cs.ptr(j), 0) == 0
         assert slf(C.addressof(eb.runner), cs.ptr(main), 0) == 0
     elif backend == "brute":
-        pair = O.fn("f32", "pairs_all_density")
-        slf = O.fn("f32", "self_all_density")
+        pair = O.fn("f32", "pairs_all_density", kernel)
+        slf = O.fn("f32", "self_all_density", kernel)
         for j in range(ncell):
             if j != main:
                 pair(C.addressof(eb.runner), cs.ptr(main), cs.ptr(j))
         slf(C.addressof(eb.runner), cs.ptr(main))
     elif backend == "adapter":
         from swift_subtask_dev_amd import lib as L
-        ad = L.load_adapter()
+        ad = L.load_adapter(kernel)
         ad.swifthip_swift_clear_error()
         if subset:
             s, e = bounds[main]

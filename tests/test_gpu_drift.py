@@ -312,3 +312,56 @@ def test_kept_lists_across_drifts_vs_f64(gpu_ctx, disp, expect_rebuilds):
         assert builds >= 2, builds
     else:
         assert builds == 1, builds  # built at the first force loop, then kept
+
+
+def test_kept_lists_follow_inactive_h_growth_vs_f64(gpu_ctx):
+    """Kept lists must cover the j side of DOPAIR2's r < max(H_i, H_j) for
+    inactive j too: the drift grows h of every particle (drift_part's h_dt
+    term, src/drift.h), active or not. Mixed time bins (bin 2 inactive at
+    max_active_bin 1), no list skin, no displacement (v_full = 0, so D = 0),
+    and only the inactive particles' h grows (w1 = 0.1 per drift). A check
+    that looks at active particles alone keeps the lists and loses the pairs
+    H_j,build < r < H_j,now; the force loop after the drift must match the
+    fp64 oracle's count, a_hydro, u_dt, h_dt and min_ngb_time_bin."""
+    from swift_subtask_dev_amd import lib
+    parts, P = _stepped_state(gpu_ctx, n=14, seed=14)
+    N = len(parts)
+    rng = np.random.Generator(np.random.PCG64(17))
+    inactive = rng.uniform(size=N) < 0.4
+    parts["time_bin"] = np.where(inactive, 2, 1).astype(np.int8)
+    P.max_active_bin = 1
+    dt = 1e-3
+    parts["h_dt"] = np.where(inactive, 0.1 * parts["h"] / dt, 0.0).astype(np.float32)
+    xp = abi.new_xparts(N)  # v_full = 0, a_grav = 0: nothing moves
+    D = abi.DriftParams(dt, 0.0, 0.0, 0.0, 0.0)
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.set_tuning(1, 0, 0, list_skin=0.0, list_keep=1)
+    sp.upload(abi.copy_parts(parts))
+    sp.rebuild(P)
+    sp.upload_xparts(xp)
+    sp.reset_acceleration(P)
+    sp.force(P)  # builds the lists at the pre-drift h
+    b0 = sp.info()["list_builds"]
+    sp.drift(D, P)
+    assert sp.info()["dx_max"] < 1e-9  # nothing moved (1e-12: the bound's floor)
+    sp.reset_acceleration(P)
+    nf = sp.force(P)
+    gf = abi.copy_parts(parts)
+    sp.download(gf, abi.FIELDS_FORCE | abi.FIELDS_DRIFT)
+    builds = sp.info()["list_builds"] - b0
+    sp.close()
+    o, _ = _oracle_drift(parts, xp, D)
+    grown = gf["h"][inactive] / parts["h"][inactive]
+    assert np.all(grown > 1.09), grown.min()
+    of = abi.copy_parts(o)
+    of["a_hydro"] = 0
+    of["u_dt"] = 0
+    of["h_dt"] = 0
+    of["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
+    no = O.fn("f64", "box_force")(of.ctypes.data, len(of), C.byref(P), None)
+    assert nf == no
+    assert builds == 1, builds  # the device check found the kept lists stale
+    act = ~inactive
+    for f in ("a_hydro", "u_dt", "h_dt"):
+        assert_close(gf[f][act], of[f][act], 5e-5, 1e-4, f)
+    assert np.array_equal(gf["min_ngb_time_bin"][act], of["min_ngb_time_bin"][act])

@@ -42,6 +42,58 @@ def test_kernel_deval_properties(oracle32):
     assert abs(W.value - oracle32.orf_kernel_root()) < 1e-7
 
 
+def test_wendland_c2_kernel_pinned_to_reference_definition():
+    """The Wendland C2 oracle builds (liboracle_wc2_*.so) against the
+    reference's own kernel definition: theory/SPH/Kernels/kernel_definitions
+    .tex:143-151 (C = 21/(2 pi), gamma = H/h = 1.936492, Psi(u) = 4u^5 - 15u^4
+    + 20u^3 - 10u^2 + 1) and kernels.py:89,155,222 (the same constants and
+    polynomial, f(u > 1) = 0); W(u) = C Psi(u/gamma) / gamma^3 and dW/du its
+    derivative (kernel_hydro.h:257-284 scaling). Also: W integrates to 1 over
+    the support sphere (a normalised SPH kernel), W(0) = kernel_root, and the
+    sorted test27cells loops agree with brute force as for the cubic spline."""
+    g = 1.936492
+    Cn = 21.0 / (2.0 * np.pi)
+    o32 = O.load("f32", "wendland-c2")
+    o64 = O.load("f64", "wendland-c2")
+    assert o32.orf_kernel_gamma() == np.float32(g)
+    assert abs(o32.orf_kernel_root() - Cn / g ** 3) < 1e-6 * Cn / g ** 3
+    u = np.linspace(0.0, 1.2 * g, 4001)
+    x = u / g
+    psi = np.where(x > 1.0, 0.0, 4 * x**5 - 15 * x**4 + 20 * x**3 - 10 * x**2 + 1)
+    dpsi = np.where(x > 1.0, 0.0, 20 * x**4 - 60 * x**3 + 60 * x**2 - 20 * x)
+    W_ref, dW_ref = Cn * psi / g**3, Cn * dpsi / g**4
+    W32, dW32 = C.c_float(), C.c_float()
+    W64, dW64 = C.c_double(), C.c_double()
+    for k in range(len(u)):
+        o32.orf_kernel_deval(u[k], C.byref(W32), C.byref(dW32))
+        o64.ord_kernel_deval(u[k], C.byref(W64), C.byref(dW64))
+        assert abs(W32.value - W_ref[k]) <= 2e-6 * W_ref[0]
+        assert abs(dW32.value - dW_ref[k]) <= 2e-6 * np.abs(dW_ref).max()
+        assert abs(W64.value - W_ref[k]) <= 1e-6 * W_ref[0]  # float constants
+        assert abs(dW64.value - dW_ref[k]) <= 1e-6 * np.abs(dW_ref).max()
+    # normalisation: 4 pi int_0^H W r^2 dr = 1 (h = 1)
+    r = np.linspace(0.0, g, 200001)
+    Wr = np.array([(o64.ord_kernel_deval(v, C.byref(W64), C.byref(dW64)), W64.value)[1]
+                   for v in r[::100]])
+    integral = 4 * np.pi * np.trapezoid(Wr * r[::100] ** 2, r[::100])
+    assert abs(integral - 1.0) < 1e-5, integral
+    # the same sorted-vs-brute identity as the cubic spline's test27cells
+    P = abi.default_hydro_params((3.0, 3.0, 3.0), True)
+    parts, bounds, locs = S.cells_grid(3, 6, vel="divergent", h_pert=1.1, pert=0.1, seed=0)
+    a, b = parts.copy(), parts.copy()
+    S.zero_density_fields(a)
+    S.zero_density_fields(b)
+    S.run27(a, bounds, locs, "sorted", P, kernel="wendland-c2")
+    S.run27(b, bounds, locs, "brute", P, kernel="wendland-c2")
+    s, e = bounds[13]
+    ma, mb = a[s:e].copy(), b[s:e].copy()
+    S.end_calculation(ma, P, "wendland-c2")
+    S.end_calculation(mb, P, "wendland-c2")
+    names, at, rt, lt = load_tolerance("tolerance_27_perturbed_h.dat")
+    errs = compare_columns(S.density_columns(mb), S.density_columns(ma), at, rt, lt, names)
+    assert not errs, "\n".join(errs)
+
+
 CASES27 = [
     # (vel, h_pert, pert, tolerance file) — test27cells.sh.in + Perturbed.sh.in
     ("zero", 0.0, 0.0, "tolerance_27_normal.dat"),

@@ -1088,13 +1088,31 @@ API void PFX(init_parts)(struct part *parts, long long N,
 /* "subset reruns" of runner_ghost.c:1503-1546 become box_loop(subset).     */
 /* Returns the number of iterations; *n_failed = particles not converged.   */
 /* ------------------------------------------------------------------------ */
+/* The reference keeps struct part in float: between the ghost's passes the
+ * density sums and h live in float fields (runner_ghost.c reads p->rho,
+ * p->density.wcount, ... and writes p->h). The f64 build keeps its arithmetic
+ * in double but rounds those stored values to float at the same points, so a
+ * particle whose Newton step lands within float rounding of h_tolerance
+ * takes the reference's storage path (identities in the f32 build). */
+static inline real fstore(real x) { return (real)(float)x; }
+static void store_density_sums(opart *p) {
+  p->rho = fstore(p->rho);
+  p->density.wcount = fstore(p->density.wcount);
+  p->density.wcount_dh = fstore(p->density.wcount_dh);
+  p->density.rho_dh = fstore(p->density.rho_dh);
+  p->viscosity.div_v = fstore(p->viscosity.div_v);
+  for (int k = 0; k < 3; k++) p->density.rot_v[k] = fstore(p->density.rot_v[k]);
+}
+
 API int PFX(box_ghost)(struct part *parts, long long N,
                        const struct oracle_params *P, long long *n_failed) {
   opart *o = to_oparts(parts, N, PHASE_DENSITY);
   const real eps = (real)P->h_tolerance;
   const real hydro_h_max = (real)P->h_max, hydro_h_min = (real)P->h_min;
-  const real eta = (real)P->eta_neighbours;
-  const real hydro_eta_dim = pow_dimension(eta);
+  /* runner_ghost.c:1103-1105: eps and hydro_eta_dim are floats (the f64
+   * build keeps the reference's float constants, like the kernel's) */
+  const float eta_f = P->eta_neighbours;
+  const real hydro_eta_dim = (real)(eta_f * eta_f * eta_f);
   int *pid = (int *)malloc(sizeof(int) * (size_t)(N > 0 ? N : 1));
   real *left = (real *)malloc(sizeof(real) * (size_t)(N > 0 ? N : 1));
   real *right = (real *)malloc(sizeof(real) * (size_t)(N > 0 ? N : 1));
@@ -1156,10 +1174,10 @@ API int PFX(box_ghost)(struct part *parts, long long N,
 #ifdef ORACLE_F32
           p->h = cbrtf(0.5f * (pow_dimension(left[i]) + pow_dimension(right[i])));
 #else
-          p->h = cbrt(0.5 * (pow_dimension(left[i]) + pow_dimension(right[i])));
+          p->h = fstore(cbrt(0.5 * (pow_dimension(left[i]) + pow_dimension(right[i]))));
 #endif
         } else {
-          p->h = h_new;
+          p->h = fstore(h_new);
         }
         if (p->h < hydro_h_max && p->h > hydro_h_min) {
           pid[redo] = pid[i];
@@ -1180,7 +1198,10 @@ API int PFX(box_ghost)(struct part *parts, long long N,
       hydro_reset_gradient(p);
     }
     count = redo;
-    if (count > 0) box_loop(o, N, P, LOOP_DENSITY, pid, count, NULL);
+    if (count > 0) {
+      box_loop(o, N, P, LOOP_DENSITY, pid, count, NULL);
+      for (long long i = 0; i < count; i++) store_density_sums(&o[pid[i]]);
+    }
   }
   if (n_failed) *n_failed = count;
   free(pid);

@@ -299,3 +299,93 @@ def top_level_pairs(tops: np.ndarray) -> np.ndarray:
     n = len(tops)
     i, j = np.triu_indices(n, k=1)
     return np.stack([tops[i], tops[j]], axis=1).astype(np.int32)
+
+
+# examples/SmallCosmoVolume/SmallCosmoVolume_hydro/small_cosmo_volume.yml:
+# WMAP9 (Omega_cdm 0.2305, Omega_b 0.0455, Omega_lambda 0.724, h 0.703),
+# a_begin 0.019607843 (z = 50), a 64^3 box of 142.248 Mpc (100 Mpc/h; the
+# yml's softening 0.0889 Mpc = 1/25 of the 2.2226 Mpc mean separation),
+# initial_temperature 7075 K. Internal units of the stand-in: length = the box,
+# velocity = km/s, G = 1 (so masses are G M); H0 = 70.3 km/s/Mpc x 142.248
+# Mpc = 1e4 km/s per box length.
+SCV_OMEGA_CDM, SCV_OMEGA_B, SCV_OMEGA_L = 0.2305, 0.0455, 0.724
+SCV_H0 = 1.0e4
+SCV_A_BEGIN = 0.019607843
+SCV_T_INIT = 7075.0
+
+
+def small_cosmo_volume(n: int = 64, seed: int = 50, disp_rms: float = 0.2,
+                       spectral_index: float = -1.5):
+    """SmallCosmoVolume stand-in (BASELINE config 5): a DM-only Zel'dovich
+    field turned into DM + gas pairs the way SWIFT's generate_gas_in_ics does
+    (space_generate_gas, src/space.c:1747-1935).
+
+    DM: an n^3 lattice displaced by a Gaussian random Zel'dovich field
+    (displacement psi = grad of the potential of a density field with power
+    P(k) ~ k^spectral_index, i.e. psi_k ~ i k delta_k / k^2, rms |psi| =
+    disp_rms of the mean separation: ~0.2 at z = 50 for this box), velocity
+    the linear growing mode v = a^2 H f psi (SWIFT's internal a^2 dx/dt; f = 1
+    in matter domination). Each DM particle then splits (space.c:1883-1904):
+    d = mean separation, the DM keeps mass (1 - Omega_b/Omega_m) and moves by
+    +0.5 d Omega_b/Omega_m along the diagonal, the gas gets Omega_b/Omega_m of
+    the mass and moves by -0.5 d (1 - Omega_b/Omega_m), h = d, the gas velocity
+    is its gpart's. Total mass = the critical density's Omega_m share, 3 H0^2
+    Omega_m / (8 pi) in G = 1 units; u = the comoving internal energy of
+    7075 K gas (mu = 1.22), u_phys a^2 (SWIFT's a^(3(gamma-1)) factor).
+
+    Returns (gas struct-part records, gpart records: the n^3 DM first, then
+    the n^3 gas gparts, softening d / 25)."""
+    rng = _rng(seed)
+    N = n ** 3
+    d = 1.0 / n
+    k1 = np.fft.fftfreq(n, d=d) * 2.0 * np.pi
+    kz1 = np.fft.rfftfreq(n, d=d) * 2.0 * np.pi
+    kx, ky, kz = np.meshgrid(k1, k1, kz1, indexing="ij")
+    k2 = kx * kx + ky * ky + kz * kz
+    k2[0, 0, 0] = 1.0
+    amp = np.sqrt(k2 ** (0.5 * spectral_index))
+    amp[0, 0, 0] = 0.0
+    noise = np.fft.rfftn(rng.standard_normal((n, n, n)))
+    delta_k = noise * amp
+    psi = np.empty((n, n, n, 3))
+    for c, kc in enumerate((kx, ky, kz)):
+        psi[..., c] = np.fft.irfftn(1j * kc * delta_k / k2, s=(n, n, n))
+    psi = psi.reshape(N, 3)
+    psi *= disp_rms * d / np.sqrt((psi ** 2).sum(axis=1).mean())
+    g1 = (np.arange(n) + 0.5) * d
+    qx, qy, qz = np.meshgrid(g1, g1, g1, indexing="ij")
+    x = np.stack([qx.ravel(), qy.ravel(), qz.ravel()], axis=1) + psi
+    a = SCV_A_BEGIN
+    om = SCV_OMEGA_CDM + SCV_OMEGA_B
+    H = SCV_H0 * np.sqrt(om / a ** 3 + SCV_OMEGA_L)
+    v = a * a * H * psi
+    m_tot = 3.0 * SCV_H0 ** 2 * om / (8.0 * np.pi)
+    ratio = SCV_OMEGA_B / om
+    m = m_tot / N
+    shift_dm, shift_gas = 0.5 * d * ratio, 0.5 * d * (1.0 - ratio)
+    eps = d / 25.0
+    gp = abi.new_gparts(2 * N)
+    gp["id_or_neg_offset"][:N] = 2 * np.arange(1, N + 1)
+    gp["id_or_neg_offset"][N:] = -np.arange(N)  # linked to gas part j (space.c:1880)
+    gp["x"][:N] = np.mod(x + shift_dm, 1.0)
+    gp["x"][N:] = np.mod(x - shift_gas, 1.0)
+    gp["v_full"][:N] = v
+    gp["v_full"][N:] = v
+    gp["mass"][:N] = m * (1.0 - ratio)
+    gp["mass"][N:] = m * ratio
+    gp["epsilon"] = eps
+    gp["time_bin"] = 1
+    gp["type"][:N] = 1
+    gp["type"][N:] = 0
+    gas = abi.new_parts(N)
+    gas["id"] = 2 * np.arange(1, N + 1) + 1
+    gas["x"] = gp["x"][N:]
+    gas["v"] = v.astype(np.float32)
+    gas["mass"] = m * ratio
+    gas["h"] = d
+    k_B, m_p, mu = 1.380649e-16, 1.67262192e-24, 1.22
+    u_phys = SCV_T_INIT * k_B / (mu * m_p * (GAMMA - 1.0)) / 1e10  # (km/s)^2
+    gas["u"] = u_phys * a * a
+    gas["time_bin"] = 1
+    gas["visc_alpha"] = 0.1
+    return gas, gp

@@ -82,8 +82,10 @@ SWH_BUSY = 9  # swh_*_query: queued work still running
 
 def load(kernel: str = "cubic-spline") -> C.CDLL:
     """Load the libswifthip built for `kernel` (raises if it was not built).
-    The default cubic-spline library is loaded RTLD_GLOBAL (the adapter links
-    it); other kernels' libraries are private to their handle."""
+    Every kernel's library is private to its handle (RTLD_LOCAL): the
+    libraries export the same swh_* names, and a global one would capture the
+    other adapter's calls (global scope is searched before a library's own
+    dependencies)."""
     if kernel in _libs:
         return _libs[kernel]
     if kernel not in KERNEL_LIBS:
@@ -93,7 +95,7 @@ def load(kernel: str = "cubic-spline") -> C.CDLL:
         raise ImportError(
             f"{path} is missing: build it with `python -m swift_subtask_dev_amd.build` "
             "(the HIP library is the only implementation of this path)")
-    lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL if kernel == "cubic-spline" else C.RTLD_LOCAL)
+    lib = C.CDLL(str(path), mode=C.RTLD_LOCAL)
     vp, i32, i64, dp = C.c_void_p, C.c_int32, C.c_int64, C.c_double
     P = C.POINTER
     sigs = {

@@ -319,9 +319,10 @@ def test_kept_lists_follow_inactive_h_growth_vs_f64(gpu_ctx):
     inactive j too: the drift grows h of every particle (drift_part's h_dt
     term, src/drift.h), active or not. Mixed time bins (bin 2 inactive at
     max_active_bin 1), no list skin, no displacement (v_full = 0, so D = 0),
-    and only the inactive particles' h grows (w1 = 0.1 per drift). A check
-    that looks at active particles alone keeps the lists and loses the pairs
-    H_j,build < r < H_j,now; the force loop after the drift must match the
+    the inactive particles' h grows by w1 = 0.1 (the active ones move by
+    their own force-loop h_dt only). A check that looks at active particles
+    alone keeps the lists and loses the pairs H_j,build < r < H_j,now. Both
+    sides run force -> drift -> force; the second force loop must match the
     fp64 oracle's count, a_hydro, u_dt, h_dt and min_ngb_time_bin."""
     from swift_subtask_dev_amd import lib
     parts, P = _stepped_state(gpu_ctx, n=14, seed=14)
@@ -350,14 +351,21 @@ def test_kept_lists_follow_inactive_h_growth_vs_f64(gpu_ctx):
     sp.download(gf, abi.FIELDS_FORCE | abi.FIELDS_DRIFT)
     builds = sp.info()["list_builds"] - b0
     sp.close()
-    o, _ = _oracle_drift(parts, xp, D)
+
+    def reset_force(p):
+        p["a_hydro"] = 0
+        p["u_dt"] = 0
+        p["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
+        p["h_dt"] = np.where(p["time_bin"] <= P.max_active_bin, 0.0, p["h_dt"])
+
+    o = abi.copy_parts(parts)
+    reset_force(o)
+    O.fn("f64", "box_force")(o.ctypes.data, N, C.byref(P), None)  # the active h_dt
+    o, _ = _oracle_drift(o, xp, D)
     grown = gf["h"][inactive] / parts["h"][inactive]
     assert np.all(grown > 1.09), grown.min()
     of = abi.copy_parts(o)
-    of["a_hydro"] = 0
-    of["u_dt"] = 0
-    of["h_dt"] = 0
-    of["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
+    reset_force(of)
     no = O.fn("f64", "box_force")(of.ctypes.data, len(of), C.byref(P), None)
     assert nf == no
     assert builds == 1, builds  # the device check found the kept lists stale

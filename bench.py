@@ -46,6 +46,7 @@ HBM_PEAK = 8.0e12       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_PEAK = 78.6e12     # MI355X fp64 vector
 S_IN_DENSITY, S_OUT_DENSITY = 45, 32   # SURVEY 8d algorithmic bytes per particle
 S_IN_FORCE, S_OUT_FORCE = 77, 21
+KERNEL_GAMMA = 1.825742  # H/h of the cubic spline (kernel_hydro.h:52): libswifthip.so's kernel
 FLOPS_DENSITY, FLOPS_FORCE = 65, 146   # SURVEY 8d flops per directed interaction
 
 
@@ -167,10 +168,11 @@ def cpu_worker_main(kind, path, meta):
         out["seconds_share"] = statistics.median(times)
         out["interactions"] = int(n)
     elif kind == "cosmo":
+        from swift_subtask_dev_amd import cosmo
         parts = z["parts"].view(abi.PART_DTYPE).reshape(-1)
-        P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
-        P.max_active_bin = 1
-        eb = abi.EngineBundle(dim=(1.0, 1.0, 1.0), periodic=True, params=P, max_active_bin=1)
+        _, P = cosmo.small_cosmo_volume_params()  # the GPU step's engine scalars
+        eb = abi.EngineBundle(dim=(1.0, 1.0, 1.0), periodic=True, params=P,
+                              max_active_bin=int(P.max_active_bin))
         new, run, free = (O.fn("f32", n) for n in ("cellgrid_new", "cellgrid_run",
                                                     "cellgrid_free"))
         gd = new(parts.ctypes.data, len(parts), 1.0, meta["cdim"])
@@ -608,75 +610,73 @@ def run_grav(args, ctx, rank, world, dist, torch):
 
 
 def run_cosmo(args, ctx, rank, world, dist, torch):
-    """BASELINE config 5 stand-in (SmallCosmoVolume hydro + self-gravity,
-    small_cosmo_volume.yml: 64^3 gas + 64^3 DM, softening 1/25 of the mean
-    separation, PM mesh 64, a_smooth 1.25, r_cut_max 4.5 r_s, adaptive MAC
-    epsilon_fmm 0.001, theta_cr 0.7, cell_split_size 50), in box units.
-    One step = the hydro density + force loops on the gas (the headline's
-    loops) and the gravity of every gpart: the recursive gravity tasks over
-    the cell tree (P2P, M2P, M2L, L2L, L2P) plus the PM mesh. Hydro and gravity
-    run on two streams from two host threads (the two task families of a
-    SWIFT step overlap); the line reports each alone and both together.
-    The MAC is the geometric theta_cr = 0.7 one (SWH_COSMO_ADAPTIVE_MAC=1: the
-    yml's adaptive MAC, whose |a| estimates the stand-in's units do not
-    reproduce: it accepts no M2L here).
+    """BASELINE config 5 stand-in: SmallCosmoVolume hydro + self-gravity
+    (small_cosmo_volume.yml), its first step. ics.small_cosmo_volume(64): a
+    Zel'dovich 64^3 DM field split into DM + gas as space_generate_gas does
+    (src/space.c:1747-1935), box units of 142.248 Mpc, km/s, G = 1; WMAP9
+    cosmology at a = 0.0198 (cosmo.small_cosmo_volume_params: the hydro loops
+    take a, H, a^2 H and the gamma = 5/3 scale-factor powers); softening 1/25
+    of the mean separation, PM mesh 64, a_smooth 1.25, r_cut_max 4.5 r_s,
+    theta_cr 0.7, cell_split_size 50, and the yml's MAC: adaptive with
+    epsilon_fmm 0.001 (gravity_M2L_accept, src/multipole_accept.h:81-170),
+    fed |a_tree + a_mesh / G| of an untimed geometric-MAC step as SWIFT's
+    gravity_end_force records old_a_grav_norm
+    (src/gravity/MultiSoftening/gravity.h:244-253). SWH_COSMO_MAC=geometric
+    times the theta_cr-only walk instead.
 
-    With N ranks (one per GPU) the step is sharded: the gas by
-    the hydro block decomposition (decomp.HaloPlan: owned block + read-only
-    halo, swh_space_set_owned), the gravity by subtrees of the top cells
-    whose centres lie in the rank's block (decomp.gravity_owned_cells,
-    swh_gspace_set_owned_cells) with every gpart and the tree replicated
-    read-only, and the PM mesh computed by every rank on its replicated
-    gparts. The timed step needs no data-path collective: its loops read the
-    halo fields the untimed setup left (a full SWIFT step refreshes them
-    between phases, as the sedov workload does). value = interactions of all
-    ranks / the slowest rank's time."""
+    One step = the hydro density + force loops on the gas and the gravity of
+    every gpart: the recursive gravity tasks over the cell tree (P2P, M2P,
+    M2L, L2L, L2P) plus the PM mesh. Hydro is queued on its own stream, then
+    the gravity chain runs on the high-priority gravity stream (the two task
+    families of a SWIFT step overlap); the line reports each alone and both.
+
+    With N ranks (one per GPU) the step is sharded: the gas by the
+    hydro block decomposition (decomp.HaloPlan: owned block + read-only halo,
+    swh_space_set_owned) with the halo's rho refreshed point-to-point between
+    density and force (decomp.DeviceHalo, as the sedov step), the gravity by
+    subtrees of the top cells whose centres lie in the rank's block
+    (decomp.gravity_owned_cells, swh_gspace_set_owned_cells) with every gpart
+    and the tree replicated read-only, and the PM mesh computed by every rank
+    on its replicated gparts. value = interactions of all ranks / the slowest
+    rank's time."""
     import threading
-    from swift_subtask_dev_amd import abi, decomp, ics, lib
+    from swift_subtask_dev_amd import abi, cosmo, decomp, ics, lib
 
     n = args.n if args.n != 128 else 64
     box = (1.0, 1.0, 1.0)
     t0 = time.time()
-    gas = ics.sedov_slabs(n, 1)
-    gas["u"] = 1.0e-6 / (ics.GAMMA - 1.0)  # a cold uniform medium, no blast
-    P = abi.default_hydro_params(box, True)
-    P.max_active_bin = 1
+    gas, gp = ics.small_cosmo_volume(n)
+    cm, P = cosmo.small_cosmo_volume_params()
+    gas["time_bin"] = cosmo.SCV_FIRST_BIN
     sp = lib.HydroSpace(ctx)
     sp.upload(gas)
     sp.rebuild(P)
-    sp.hydro_step(P)  # converged h, the force inputs (whole box, untimed)
+    chain = sp.hydro_step(P)  # converged h, the force inputs (whole box, untimed)
     sp.download(gas, abi.FIELDS_ALL)
     sp.close()
-    # gparts: the gas + as many DM particles, softening 1/25 of the mean spacing
     eps = 1.0 / (25.0 * n)
-    dm = ics.uniform_gravity_box(n, epsilon=eps, seed=65)
-    gp = abi.new_gparts(2 * n ** 3)
-    gp[: n ** 3] = dm
-    gp["x"][n ** 3:] = gas["x"]
-    gp["mass"][n ** 3:] = gas["mass"]
-    gp["mass"] *= 0.5
-    gp["epsilon"] = eps
-    gp["time_bin"] = 1
-    gp["type"][n ** 3:] = 0
     N_mesh = 64
     r_s = 1.25 / N_mesh
+    mac = os.environ.get("SWH_COSMO_MAC", "adaptive")
     G = abi.GravParams(1, (C.c_float * 3)(1, 1, 1), 1.0 / r_s, 0.1 * r_s, abi.NUM_TIME_BINS)
     G.theta_crit = 0.7
     G.adaptive_tolerance = 1e-3
-    G.use_advanced_MAC = int(os.environ.get("SWH_COSMO_ADAPTIVE_MAC", "0"))
     G.r_cut_max = 4.5 * r_s
     g, cells, tops = ics.gravity_tree(gp, 8, split_size=50)
     pairs = ics.top_level_pairs(tops)
     gs = lib.GravSpace(ctx)
-    # one untimed step gives the adaptive MAC its |a| estimate (old_a_grav_norm)
+    # an untimed geometric-MAC step gives the adaptive MAC its |a| estimate:
+    # old_a_grav_norm = |a_tree + a_mesh / G| (gravity.h:244-253), G = 1
     gs.upload(g)
     gs.set_tree(cells)
-    g0 = abi.copy_parts(g)
     G.use_advanced_MAC = 0
     gs.tree(G, tops, pairs)
+    gs.pm_mesh(N_mesh, 1.0, r_s, 1.0)
+    g0 = abi.copy_parts(g)
     gs.download(g0)
-    g["old_a_grav_norm"] = np.linalg.norm(g0["a_grav"].astype(np.float64), axis=1)
-    G.use_advanced_MAC = int(os.environ.get("SWH_COSMO_ADAPTIVE_MAC", "0"))
+    g["old_a_grav_norm"] = np.linalg.norm(g0["a_grav"].astype(np.float64)
+                                          + g0["a_grav_mesh"].astype(np.float64), axis=1)
+    G.use_advanced_MAC = 1 if mac == "adaptive" else 0
     gs.upload(g)
     gs.set_tree(cells)
     owned_cells = None
@@ -689,8 +689,9 @@ def run_cosmo(args, ctx, rank, world, dist, torch):
     hs = lib.HydroSpace(ctx)
     hstream = torch.cuda.Stream()
     hs.set_stream(hstream.cuda_stream)
+    plan = None
     if world > 1:
-        reach = 1.01 * 1.825742 * float(gas["h"].max())  # 1.01 gamma h_max, as the sedov split
+        reach = 1.01 * KERNEL_GAMMA * float(gas["h"].max())  # 1.01 gamma h_max, as the sedov split
         plan = decomp.HaloPlan(gas["x"], box, world, rank, reach)
         local, n_owned = plan.local_set(gas), plan.n_owned
     else:
@@ -698,6 +699,7 @@ def run_cosmo(args, ctx, rank, world, dist, torch):
     hs.upload(local)
     hs.set_owned(n_owned)
     hs.rebuild(P)
+    exchanger = decomp.DeviceHalo(plan, hs, dist, torch, hstream) if plan else None
     hs.init_parts(P)
     n_density = hs.density(P)
     hs.reset_acceleration(P)
@@ -705,25 +707,25 @@ def run_cosmo(args, ctx, rank, world, dist, torch):
     torch.cuda.synchronize()
     log(f"[rank {rank}] cosmo setup {time.time() - t0:.1f}s: {n_owned} of {n ** 3} gas + "
         f"{2 * n ** 3} gparts ({int(owned_cells.sum()) if owned_cells is not None else len(cells)}"
-        f" of {len(cells)} cells owned); gravity step {stats}; hydro {n_density} + {n_force}")
+        f" of {len(cells)} cells owned); a = {P.a:.5f}, H = {P.H:.4g}; chain {chain}; "
+        f"gravity step ({mac} MAC) {stats}; hydro {n_density} + {n_force}")
 
-    def hydro():
+    def hydro_async():
         hs.init_parts(P)
         hs.density(P, count=False)
+        if exchanger:  # the force loop reads the neighbours' new rho
+            exchanger.refresh(abi.HALO_RHO)
         hs.reset_acceleration(P)
         hs.force(P, count=False)
+
+    def hydro():
+        hydro_async()
         hs.sync()
 
     def gravity():
         gs.tree(G, tops, pairs)  # the device accumulators restart at every walk
         gs.pm_mesh(N_mesh, 1.0, r_s, 1.0)
         gs.sync()
-
-    def hydro_async():
-        hs.init_parts(P)
-        hs.density(P, count=False)
-        hs.reset_acceleration(P)
-        hs.force(P, count=False)
 
     overlap = os.environ.get("SWH_COSMO_OVERLAP", "async")
 
@@ -776,13 +778,23 @@ def run_cosmo(args, ctx, rank, world, dist, torch):
             "value": total / t_b, "unit": "interactions/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": t_b * 1e3, "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (64^3 perturbed-lattice gas + 64^3 uniform DM; SmallCosmoVolume ICs "
-                    "unavailable offline)",
-            "config": {"workload": f"SmallCosmoVolume stand-in: {n}^3 gas + {n}^3 DM, hydro density + "
-                                   "force loops || gravity tree (P2P, M2P, M2L, L2L, L2P) + PM mesh 64",
+            "data": "synthetic (Zel'dovich 64^3 DM field split into DM + gas as space_generate_gas, "
+                    "z = 50; SmallCosmoVolume ICs unavailable offline)",
+            "config": {"workload": f"SmallCosmoVolume stand-in: {n}^3 gas + {n}^3 DM, first step "
+                                   f"(a = {P.a:.5f}): hydro density + force loops || gravity tree "
+                                   f"(P2P, M2P, M2L, L2L, L2P; {mac} MAC) + PM mesh 64",
                        "parallelism": (f"{'x'.join(map(str, decomp.block_dims(world)))} blocks: gas "
-                                       "owned + halo, gravity subtrees owned, gparts replicated"
+                                       "owned + halo (rho refreshed between density and force), "
+                                       "gravity subtrees owned, gparts replicated"
                                        if world > 1 else "one GPU"),
+                       "world_size": world,
+                       "backend": (dist.get_backend() if dist else None),
+                       "device": torch.cuda.current_device(),
+                       "cosmology": {"a": P.a, "H": P.H, "Omega_cdm": ics.SCV_OMEGA_CDM,
+                                     "Omega_b": ics.SCV_OMEGA_B, "Omega_lambda": ics.SCV_OMEGA_L,
+                                     "units": "box (142.248 Mpc), km/s, G = 1"},
+                       "mac": {"kind": mac, "theta_crit": 0.7, "epsilon_fmm": 1e-3,
+                               "old_a_grav_norm": "|a_tree + a_mesh/G| of an untimed geometric step"},
                        "hydro_interactions_per_step": int(total_hydro),
                        "gravity_pp_per_step": int(total_pp),
                        "gravity_tree_stats_rank0": stats, "cells": int(len(cells)),
@@ -808,7 +820,6 @@ def run_cosmo(args, ctx, rank, world, dist, torch):
         if world == 1 and not args.no_cpu_baseline:
             try:
                 threads = cpu_share_threads()
-                G.use_advanced_MAC = 0
                 w = run_cpu_worker("cosmo", {"parts": np.ascontiguousarray(gas).view(np.uint8),
                                              "gparts": np.ascontiguousarray(g).view(np.uint8),
                                              "cells": np.ascontiguousarray(cells).view(np.uint8),
@@ -822,10 +833,12 @@ def run_cosmo(args, ctx, rank, world, dist, torch):
                     "value": n_cpu / w["seconds_share"], "unit": "interactions/s",
                     "cores": threads, "kind": "port", "host": host_cpu_info(),
                     "pinning": "one thread per physical core, child process without torch",
-                    "sample": f"one whole step: the float restatement's density + force loops over "
-                              f"a cdim-20 cell grid ({w['seconds_hydro']:.2f} s, OpenMP over cells) "
-                              f"and its gravity: tree walk (serial), P2P/M2P and M2L (OpenMP), "
-                              f"L2L/L2P (serial) ({w['seconds_gravity']:.2f} s); the PM mesh not "
+                    "sample": f"one whole step, the same inputs and MAC: the float restatement's "
+                              f"density + force loops over a cdim-20 cell grid "
+                              f"({w['seconds_hydro']:.2f} s, OpenMP over cells) and its gravity "
+                              f"({w['seconds_gravity']:.2f} s): the recursive task walk serial "
+                              f"(the reference runs it inside its threaded tasks), P2P/M2P and "
+                              f"M2L OpenMP over target cells, L2L/L2P serial; the PM mesh not "
                               f"included",
                     "tree_stats": w["tree_stats"]}
                 out["gpu_over_cpu"] = out["value"] / out["cpu_baseline"]["value"]
@@ -960,7 +973,7 @@ def main():
     if eagle:  # converged h: re-bin on the final smoothing lengths
         log(f"[rank {rank}] eagle stand-in: {len(parts)} parts, h {parts['h'].min():.3g}.."
             f"{parts['h'].max():.3g}, chain ghost iterations {chain['ghost_iterations']}")
-    hmax = float(parts["h"].max()) * 1.825742
+    hmax = float(parts["h"].max()) * KERNEL_GAMMA
 
     if strong:
         # one box, world blocks (2x2x2 at 8 GPUs); halo = everything within
@@ -1151,7 +1164,7 @@ def main():
             # space_splitsize 400 and the DOSUB recursion
             try:
                 threads = cpu_share_threads()
-                Hmax = 1.825742 * float(local["h"].max())
+                Hmax = KERNEL_GAMMA * float(local["h"].max())
                 cdim = max(4, int(float(P.dim[0]) / (Hmax * 1.0001)))
                 cdim -= cdim % 2
                 w = run_cpu_worker("hydro_tree", {"parts": np.ascontiguousarray(local).view(np.uint8)},

@@ -395,6 +395,9 @@ typedef struct swh_space_info {
   double dx_max;         /* largest displacement since the last rebuild (drift) */
   int64_t list_builds;   /* pair-list builds run on the device since the space was created */
 } swh_space_info;
+/* Note: get_info WAITS for the space's stream (it reads the device's
+ * list-build counter, info->list_builds); in the enqueue-then-poll model
+ * (swh_space_query) call it only after the queued phases are done. */
 SWH_API swh_status swh_space_get_info(const swh_space *s, swh_space_info *info);
 
 /* Batch P2P gravity over leaf cells of a device-resident gpart set. Leaves

@@ -152,3 +152,22 @@ def cosmological_params(cosmo: Cosmology, ti_current: int, dim=(1.0, 1.0, 1.0),
     P.time_base = cosmo.time_base
     P.set_dt_alpha_bins(dt_alpha_table(cosmo, ti_current))
     return P
+
+
+# BASELINE config 5: the SmallCosmoVolume run's first step (small_cosmo_volume.yml)
+SCV_FIRST_BIN = 47          # dt_max = 1e-2 in log a -> 2^48 ticks of time_base: bin 47
+SCV_TI_CURRENT = 1 << 48    # the end of that first step (every bin <= 47 ends here)
+
+
+def small_cosmo_volume_params(max_active_bin: int = SCV_FIRST_BIN) -> tuple:
+    """(Cosmology, swh_hydro_params) of the SmallCosmoVolume stand-in's first
+    step (ics.small_cosmo_volume): WMAP9 (Omega_cdm 0.2305, Omega_b 0.0455,
+    Omega_lambda 0.724), H0 = 1e4 km/s per box length (70.3 km/s/Mpc x
+    142.248 Mpc), a_begin = 1/51, a_end = 1; dt_max = 1e-2 in log a is
+    2^48 ticks (time_base = ln(51) / 2^57), i.e. time bin 47, and the step
+    ends at ti_current = 2^48 (a = 0.01976)."""
+    from . import ics
+    cm = Cosmology(Omega_cdm=ics.SCV_OMEGA_CDM, Omega_b=ics.SCV_OMEGA_B,
+                   Omega_lambda=ics.SCV_OMEGA_L, H0=ics.SCV_H0, a_begin=ics.SCV_A_BEGIN, a_end=1.0)
+    P = cosmological_params(cm, SCV_TI_CURRENT, max_active_bin=max_active_bin)
+    return cm, P

@@ -1718,6 +1718,14 @@ swh_status swh_gspace_set_tree(swh_gspace* g, const swh_gcell* cells, int32_t nc
       return SWH_ERR_ARG;
     }
     if (C.split) {
+      // m2m_kernel bounds r_max by the CoM's distance to the farthest
+      // corner of [loc, loc + width] (space_split.c:419-433): a split cell
+      // needs real geometry, and its progeny must lie inside it
+      if (!(C.width[0] > 0. && C.width[1] > 0. && C.width[2] > 0.)) {
+        set_error("cell %d is split but its width (%g, %g, %g) is not positive", c, C.width[0],
+                  C.width[1], C.width[2]);
+        return SWH_ERR_ARG;
+      }
       int64_t sum = 0;
       for (int k = 0; k < 8; k++) {
         const int p = C.progeny[k];
@@ -1730,6 +1738,13 @@ swh_status swh_gspace_set_tree(swh_gspace* g, const swh_gcell* cells, int32_t nc
         if (P.start < C.start || P.start + P.count > C.start + C.count) {
           set_error("cell %d: progeny %d outside its range", c, p);
           return SWH_ERR_ARG;
+        }
+        for (int a = 0; a < 3; a++) {
+          const double tol = 1e-12 * C.width[a];
+          if (P.loc[a] < C.loc[a] - tol || P.loc[a] + P.width[a] > C.loc[a] + C.width[a] + tol) {
+            set_error("cell %d: progeny %d box outside the cell's box (axis %d)", c, p, a);
+            return SWH_ERR_ARG;
+          }
         }
         parent[p] = c;
         sum += P.count;
@@ -1937,9 +1952,17 @@ swh_status swh_grav_tree_tasks(swh_gspace* g, const swh_grav_params* G,
                      G->max_active_bin);
   SWH_HIP(hipGetLastError());
   // multipoles: P2M at the leaves, M2M up the tree (space_split.c:340-440)
-  hipEvent_t ev[6] = {};
+  // the phase events, destroyed on every exit path (SWH_TRY / SWH_HIP return early)
+  struct Events {
+    hipEvent_t e[6] = {};
+    ~Events() {
+      for (auto& x : e)
+        if (x) (void)hipEventDestroy(x);
+    }
+  } evs;
+  hipEvent_t* ev = evs.e;
   if (stats) {
-    for (auto& e : ev) SWH_HIP(hipEventCreate(&e));
+    for (int k = 0; k < 6; k++) SWH_HIP(hipEventCreate(&ev[k]));
     SWH_HIP(hipEventRecord(ev[0], g->stream));
   }
   SWH_TRY(tree_multipoles(g));
@@ -2084,7 +2107,6 @@ swh_status swh_grav_tree_tasks(swh_gspace* g, const swh_grav_params* G,
       if (k == 2 && npp == 0) b = ev[4];
       (void)hipEventElapsedTime(ms[k], a, b);
     }
-    for (auto& e : ev) (void)hipEventDestroy(e);
   }
   return SWH_OK;
 }

@@ -10,6 +10,7 @@
  */
 #include <float.h>
 #include <math.h>
+#include <pthread.h>
 #include <stddef.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -112,7 +113,29 @@ int swifthip_swift_set_precision(int precision) {
              : -1;
 }
 
+/* One persistent gspace and staging buffer per runner thread: the recursive
+ * gravity tasks (runner_do{self,pair}_recursive_grav, runner_do_grav_down)
+ * reuse its device buffers and stream instead of creating and destroying a
+ * gspace per task -- SWIFT runs thousands of these tasks per step. The
+ * registry lets swifthip_swift_finalize destroy them all; a thread whose
+ * gspace belongs to a finalized context (older generation) makes a new one.
+ * Past SWHS_MAX_GSPACES threads a task falls back to a gspace of its own. */
+#define SWHS_MAX_GSPACES 1024
+static __thread swh_gspace *swhs_tls_gs = NULL;
+static __thread unsigned swhs_tls_gen = 0;
+static __thread char *swhs_tls_stage = NULL;
+static __thread size_t swhs_tls_stage_cap = 0;
+static unsigned swhs_ctx_gen = 1;
+static pthread_mutex_t swhs_reg_lock = PTHREAD_MUTEX_INITIALIZER;
+static swh_gspace *swhs_reg[SWHS_MAX_GSPACES];
+static int swhs_nreg = 0;
+
 void swifthip_swift_finalize(void) {
+  pthread_mutex_lock(&swhs_reg_lock);
+  for (int k = 0; k < swhs_nreg; k++) swh_gspace_destroy(swhs_reg[k]);
+  swhs_nreg = 0;
+  swhs_ctx_gen++;
+  pthread_mutex_unlock(&swhs_reg_lock);
   if (swhs_ctx) swh_finalize(swhs_ctx);
   swhs_ctx = NULL;
 }
@@ -675,11 +698,31 @@ static void tensor_from(struct grav_tensor *p, const float *f, int add) {
 static swh_status swhs_gspace_for(swh_gspace **gs, struct swhs_tree *t, struct cell **roots,
                                   const int *offs, int nroots, char **stage, int total) {
   const size_t st = (size_t)swhs_glayout.stride;
-  *stage = (char *)malloc((size_t)total * st);
+  const size_t need = (size_t)(total > 0 ? total : 1) * st;
+  if (need > swhs_tls_stage_cap) {
+    char *b = (char *)realloc(swhs_tls_stage, need);
+    if (!b) return SWH_ERR_OOM;
+    swhs_tls_stage = b;
+    swhs_tls_stage_cap = need;
+  }
+  *stage = swhs_tls_stage;
   for (int r = 0; r < nroots; r++)
     memcpy(*stage + (size_t)offs[r] * st, roots[r]->grav.parts, (size_t)roots[r]->grav.count * st);
-  swh_status s = swh_gspace_create(swhs_ctx, gs);
-  if (s != SWH_OK) return s;
+  swh_status s = SWH_OK;
+  if (swhs_tls_gs && swhs_tls_gen == swhs_ctx_gen) {
+    *gs = swhs_tls_gs;
+  } else {
+    swhs_tls_gs = NULL;
+    s = swh_gspace_create(swhs_ctx, gs);
+    if (s != SWH_OK) return s;
+    pthread_mutex_lock(&swhs_reg_lock);
+    if (swhs_nreg < SWHS_MAX_GSPACES) {
+      swhs_reg[swhs_nreg++] = *gs;
+      swhs_tls_gs = *gs;
+      swhs_tls_gen = swhs_ctx_gen;
+    }
+    pthread_mutex_unlock(&swhs_reg_lock);
+  }
   s = swh_gspace_upload(*gs, *stage, total, &swhs_glayout, 0);
   if (s == SWH_OK) s = swh_gspace_set_tree(*gs, t->cells, t->n);
   if (s == SWH_OK) {
@@ -728,8 +771,8 @@ static swh_status swhs_gspace_finish(swh_gspace *gs, struct swhs_tree *t, struct
     }
     free(f);
   }
-  swh_gspace_destroy(gs);
-  free(stage);
+  (void)stage;                            /* the thread's staging buffer, kept */
+  if (gs != swhs_tls_gs) swh_gspace_destroy(gs);  /* unregistered: a task's own */
   return s;
 }
 
@@ -754,8 +797,6 @@ void runner_doself_recursive_grav(struct runner *r, struct cell *c, int gettimer
   if (gs) {
     const swh_status s2 = swhs_gspace_finish(gs, &t, &c, &off, 1, stage, e, 1);
     if (s == SWH_OK) s = s2;
-  } else {
-    free(stage);
   }
   swhs_tree_free(&t);
   report(s);
@@ -789,8 +830,6 @@ void runner_dopair_recursive_grav(struct runner *r, struct cell *ci, struct cell
   if (gs) {
     const swh_status s2 = swhs_gspace_finish(gs, &t, roots, offs, 2, stage, e, 1);
     if (s == SWH_OK) s = s2;
-  } else {
-    free(stage);
   }
   swhs_tree_free(&t);
   report(s);
@@ -824,8 +863,6 @@ void runner_do_grav_down(struct runner *r, struct cell *c, int timer) {
   if (gs) {
     const swh_status s2 = swhs_gspace_finish(gs, &t, &c, &off, 1, stage, e, 0);
     if (s == SWH_OK) s = s2;
-  } else {
-    free(stage);
   }
   swhs_tree_free(&t);
   report(s);

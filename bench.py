@@ -199,14 +199,37 @@ def cpu_worker_main(kind, path, meta):
     print(json.dumps(out), flush=True)
 
 
+def cgroup_cpu_quota():
+    """The CPU bandwidth limit of this job's cgroup (v2 cpu.max, or v1
+    cfs_quota_us / cfs_period_us): CPUs' worth of time, or None if unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(parts, P, n_density, n_force, runs=3, threads=None):
     """The oracle's float restatement of DOSELF1/DOPAIR1 + DOSELF2/DOPAIR2
-    (sorted pseudo-Verlet loops) over a cdim=20 periodic cell grid, timed on
-    this job's CPU share, one pinned thread per physical core (kind "port";
-    the reference's own build is unavailable), and on one pinned thread. The
-    full host (every physical core) is projected from the per-thread rate the
-    share run reaches: the pool gives one GPU's job 16 CPUs, so a run on all
-    of the host's cores is not ours to start."""
+    (sorted pseudo-Verlet loops) over a cdim=20 periodic cell grid (kind
+    "port"; the reference's own build is unavailable), timed on pinned
+    threads, one per physical core (OMP_PLACES=cores):
+
+      * `value`: this job's CPU share (16 threads per GPU on the pool's boxes),
+        median of `runs` after a warm-up, and one pinned thread;
+      * `full_host`: as many pinned threads as the host has physical cores and
+        the job's cgroup CPU quota allows (both recorded), measured -- the
+        north_star's "host cores of the same box";
+      * `calibration`: the port runs at 0.72x the reference build's rate on
+        one thread and 1.09x on eight (profiles/cpu_calibration.json, SURVEY 6
+        recipe in the build container), so `reference_equivalent` divides
+        the port's rates by the factor of its thread regime."""
     threads = threads or cpu_share_threads()
     w = run_cpu_worker("hydro", {"parts": np.ascontiguousarray(parts).view(np.uint8)},
                        {"dim": list(P.dim), "max_active_bin": int(P.max_active_bin),
@@ -215,12 +238,18 @@ def cpu_baseline(parts, P, n_density, n_force, runs=3, threads=None):
     n = n_density + n_force
     host = host_cpu_info()
     phys = host.get("physical_cores") or threads
+    quota = cgroup_cpu_quota()
+    host["cgroup_cpu_quota"] = quota
     eff = (n / t / threads) / (n / t1)  # per-thread efficiency of the share run
     calib = None
     cpath = ROOT / "profiles" / "cpu_calibration.json"
     if cpath.exists():
         calib = json.loads(cpath.read_text())
-    return {
+    f1 = f8 = None
+    if calib:
+        f1 = calib["threads"]["1"]["port_over_reference"]
+        f8 = calib["threads"]["8"]["port_over_reference"]
+    out = {
         "value": n / t,
         "unit": "interactions/s",
         "cores": threads,
@@ -235,12 +264,42 @@ def cpu_baseline(parts, P, n_density, n_force, runs=3, threads=None):
                   f"{t1:.3f} s per step",
         "seconds_per_step": t,
         "single_core": {"value": n / t1, "seconds_per_step": t1},
+        "reference_equivalent": ({"value": n / t / f8, "single_core": n / t1 / f1,
+                                  "basis": f"port rates / {f8:.3f} (multi-thread) and / "
+                                           f"{f1:.3f} (one thread): the reference build's rate "
+                                           "on the calibration recipe"} if calib else None),
         "full_host_projected": {
             "value": n / t1 * phys * eff, "cores": phys,
             "basis": f"one-thread rate x {phys} physical cores x the {eff:.3f} per-thread "
-                     f"efficiency of the {threads}-thread run (projected, not measured: a "
-                     "1-GPU job here gets a 16-CPU share)"},
+                     f"efficiency of the {threads}-thread run"},
     }
+    # every physical core the job may use, measured
+    allowed = phys if quota is None else min(phys, max(1, int(quota)))
+    try:
+        aff = len(os.sched_getaffinity(0))
+        allowed = min(allowed, aff)
+    except AttributeError:
+        pass
+    if allowed > threads:
+        try:
+            wf = run_cpu_worker("hydro", {"parts": np.ascontiguousarray(parts).view(np.uint8)},
+                                {"dim": list(P.dim), "max_active_bin": int(P.max_active_bin),
+                                 "cdim": 20, "runs": 1}, allowed)
+            out["full_host"] = {"value": n / wf["seconds_share"], "cores": allowed,
+                                "seconds_per_step": wf["seconds_share"],
+                                "limit": f"min({phys} physical cores, cgroup quota {quota}, "
+                                         f"affinity)",
+                                "sample": "the same box and loops, 1 run after 1 warm-up"}
+            if calib:
+                out["full_host"]["reference_equivalent"] = n / wf["seconds_share"] / f8
+        except Exception as e:  # report, never fake
+            out["full_host"] = {"error": str(e)[-300:], "cores": allowed}
+    else:
+        out["full_host"] = {"value": None, "cores": allowed,
+                            "limit": f"the job may use {allowed} cores (cgroup quota {quota}, "
+                                     f"{phys} physical): the share run above is the full host "
+                                     "available to it"}
+    return out
 
 
 def host_cpu_info():
@@ -1197,6 +1256,9 @@ def main():
                                              "pinned threads, one GPU's CPU share")
                 out["gpu_over_cpu_full_host_projected"] = (
                     out["value"] / out["cpu_baseline"]["full_host_projected"]["value"])
+                fh = out["cpu_baseline"].get("full_host") or {}
+                if fh.get("value"):
+                    out["gpu_over_cpu_full_host_measured"] = out["value"] / fh["value"]
             except Exception as e:  # report, never fake
                 log(f"cpu baseline failed: {e}")
             try:

@@ -3513,8 +3513,8 @@ API void PFX(grav_tree)(struct gpart *g, int n, const struct oracle_gcell *cells
 /* + the const_G scaling of mesh_to_gpart_CIC_mapper (428-470). All double, */
 /* as the reference, in both oracle builds. FFTW (third-party, not under    */
 /* /root/reference) computes the unnormalised DFT; this restates it with a  */
-/* plain radix-2 complex transform over the full N^3 spectrum (N a power of */
-/* two), applying the Green function to every k (the factor is even in each*/
+/* plain radix-2 complex transform over the full N^3 spectrum (a plain DFT */
+/* for other N, e.g. odd meshes), applying the Green function to every k (the factor is even in each*/
 /* component, so the spectrum stays Hermitian and the real part is the c2r */
 /* result).                                                                 */
 /* ======================================================================== */
@@ -3523,6 +3523,25 @@ static int pm_id(int i, int j, int k, int N) { /* row_major_id_periodic (row_maj
 }
 
 static void pm_fft_line(double *re, double *im, int n, int sign) {
+  if (n & (n - 1)) { /* not a power of two (odd meshes): the plain O(n^2) DFT */
+    double *tr = malloc(n * sizeof(double)), *ti = malloc(n * sizeof(double));
+    for (int k = 0; k < n; k++) {
+      double sr = 0., si = 0.;
+      for (int t = 0; t < n; t++) {
+        const double ang = sign * 2. * M_PI * (double)(((long long)k * t) % n) / n;
+        const double c = cos(ang), sn = sin(ang);
+        sr += re[t] * c - im[t] * sn;
+        si += re[t] * sn + im[t] * c;
+      }
+      tr[k] = sr;
+      ti[k] = si;
+    }
+    memcpy(re, tr, n * sizeof(double));
+    memcpy(im, ti, n * sizeof(double));
+    free(tr);
+    free(ti);
+    return;
+  }
   for (int i = 1, j = 0; i < n; i++) {
     int bit = n >> 1;
     for (; j & bit; bit >>= 1) j ^= bit;

@@ -25,6 +25,8 @@
 
 #include <cfloat>
 
+#include <cstdio>
+#include <cstdlib>
 #include "swh_internal.h"
 #include "swh_physics.h"
 
@@ -182,17 +184,17 @@ using namespace swh;
 
 extern "C" {
 
-// N must be even here although mesh_gravity.c:1172 only bounds N <= 1290:
-// the odd-N 3D D2Z/Z2D plans of this image's hipFFT took the process down
-// (abort inside swh_gspace_pm_mesh, r03 GPU run of test_mesh.py with N = 15),
-// so odd meshes are refused with an error instead.
+// N in [2, 1290] (mesh_gravity.c:1172), even or odd. The plans are made with
+// hipfftCreate + hipfftMakePlan3d, which report each plan's work area, so a
+// failing plan is an error return, never a crash (SWH_PM_DEBUG=1 prints the
+// work sizes).
 swh_status swh_gspace_pm_mesh(swh_gspace* g, const swh_pm_params* M, double* potential_out) {
   if (!g || !M) return SWH_ERR_ARG;
   const GLayout& L = g->layout;
-  if (M->N < 2 || M->N % 2 != 0 || M->N > 1290 || !(M->box_size > 0.) || !(M->r_s > 0.) ||
+  if (M->N < 2 || M->N > 1290 || !(M->box_size > 0.) || !(M->r_s > 0.) ||
       M->off_a_grav_mesh < 0 || M->off_potential_mesh < 0 ||
       (g->n > 0 && (M->off_a_grav_mesh + 12 > L.stride || M->off_potential_mesh + 4 > L.stride))) {
-    set_error("pm_mesh: N must be even in [2, 1290] (mesh_gravity.c:1172 bounds N; even: see swh_gspace_pm_mesh), box and r_s > 0, "
+    set_error("pm_mesh: N must be in [2, 1290] (mesh_gravity.c:1172), box and r_s > 0, "
               "mesh fields inside the record");
     return SWH_ERR_ARG;
   }
@@ -207,10 +209,19 @@ swh_status swh_gspace_pm_mesh(swh_gspace* g, const swh_pm_params* M, double* pot
       hipfftDestroy((hipfftHandle)g->mesh_inv);
       g->mesh_plans_valid = false;
     }
-    hipfftHandle f, b;
-    if (hipfftPlan3d(&f, N, N, N, HIPFFT_D2Z) != HIPFFT_SUCCESS ||
-        hipfftPlan3d(&b, N, N, N, HIPFFT_Z2D) != HIPFFT_SUCCESS) {
-      set_error("hipfftPlan3d failed for N = %d", N);
+    hipfftHandle f = nullptr, b = nullptr;
+    size_t wf = 0, wb = 0;
+    hipfftResult rf = hipfftCreate(&f);
+    if (rf == HIPFFT_SUCCESS) rf = hipfftMakePlan3d(f, N, N, N, HIPFFT_D2Z, &wf);
+    hipfftResult rb = rf == HIPFFT_SUCCESS ? hipfftCreate(&b) : rf;
+    if (rb == HIPFFT_SUCCESS) rb = hipfftMakePlan3d(b, N, N, N, HIPFFT_Z2D, &wb);
+    if (std::getenv("SWH_PM_DEBUG"))
+      std::fprintf(stderr, "swh_gspace_pm_mesh: N = %d D2Z plan %d work %zu B, Z2D plan %d work %zu B\n",
+                   N, (int)rf, wf, (int)rb, wb);
+    if (rf != HIPFFT_SUCCESS || rb != HIPFFT_SUCCESS) {
+      if (f) hipfftDestroy(f);
+      if (b) hipfftDestroy(b);
+      set_error("hipfftMakePlan3d failed for N = %d (D2Z %d, Z2D %d)", N, (int)rf, (int)rb);
       return SWH_ERR_HIP;
     }
     g->mesh_fwd = (void*)f;

@@ -128,6 +128,57 @@ def test_oracle_pm_momentum_and_potential_shape():
     assert np.allclose(pot1[c, c + 2, c], pot1[c, c, c - 2], rtol=1e-10)
 
 
+def _numpy_pm(g, N, box, r_s, G=1.0):
+    """The PM potential mesh with numpy's FFT (an independent transform):
+    CIC_set (mesh_gravity.c:103-125), the Green function with the CIC
+    deconvolution (519-638), the inverse c2r transform."""
+    x = np.mod(g["x"].astype(np.float64), box)
+    fac = N / box
+    m = g["mass"].astype(np.float64)
+    live = g["time_bin"] != INHIBITED
+    rho = np.zeros((N, N, N))
+    i = np.minimum((fac * x).astype(np.int64), N - 1)
+    d = fac * x - i
+    for a in (0, 1):
+        for b in (0, 1):
+            for c in (0, 1):
+                w = ((d[:, 0] if a else 1 - d[:, 0]) * (d[:, 1] if b else 1 - d[:, 1]) *
+                     (d[:, 2] if c else 1 - d[:, 2]))
+                np.add.at(rho, ((i[live, 0] + a) % N, (i[live, 1] + b) % N, (i[live, 2] + c) % N),
+                          (m * w)[live])
+    f = np.fft.rfftn(rho)
+    k1 = np.fft.fftfreq(N, 1.0 / N)
+    kz1 = np.arange(N // 2 + 1, dtype=np.float64)
+    kx, ky, kz = np.meshgrid(k1, k1, kz1, indexing="ij")
+    k2 = kx ** 2 + ky ** 2 + kz ** 2
+    k2[0, 0, 0] = 1.0
+    kf = np.pi / N
+
+    def sinc_inv(kk):
+        out = np.ones_like(kk)
+        nz = kk != 0
+        out[nz] = (kf * kk[nz]) / np.sin(kf * kk[nz])
+        return out
+
+    u = np.sqrt(k2 * 4 * np.pi ** 2 * r_s ** 2 / box ** 2)
+    W = (np.pi / 2 * u) / np.sinh(np.pi / 2 * u)
+    green = -1.0 / (np.pi * box) * W / k2 * (sinc_inv(kx) * sinc_inv(ky) * sinc_inv(kz)) ** 4
+    green[0, 0, 0] = 0.0
+    return np.fft.irfftn(f * green, s=(N, N, N), axes=(0, 1, 2)) * N ** 3
+
+
+@pytest.mark.parametrize("N", [15, 16, 9])
+def test_oracle_pm_matches_numpy_fft(N):
+    """Pins the oracle's transforms (radix-2 for powers of two, the plain DFT
+    otherwise, odd meshes included) against numpy's FFT on the same pipeline:
+    the potential meshes agree to 1e-10 of their maximum."""
+    g = ics.uniform_gravity_box(8, seed=13)
+    g["time_bin"][:3] = INHIBITED
+    po = oracle_pm(g.copy(), N, 1.0, 1.25 / N)
+    pn = _numpy_pm(g, N, 1.0, 1.25 / N)
+    assert np.abs(po - pn).max() < 1e-10 * np.abs(pn).max()
+
+
 def test_oracle_pm_skips_inhibited():
     N = 16
     g = ics.uniform_gravity_box(6, seed=9)
@@ -150,7 +201,7 @@ def _gpu_pm(ctx, g, N, box, r_s, G=1.0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N", [16, 32])
+@pytest.mark.parametrize("N", [15, 16, 32])
 def test_gpu_pm_vs_oracle(gpu_ctx, N):
     g = ics.uniform_gravity_box(14, seed=7)
     g["x"][:5] += 1.0   # a few gparts drifted past the periodic faces (box_wrap)
@@ -187,7 +238,7 @@ def test_gpu_pm_bad_args(gpu_ctx):
     g = ics.uniform_gravity_box(4)
     gs = lib.GravSpace(gpu_ctx)
     gs.upload(g)
-    for N in (0, 1, 15, 1291):  # odd N refused: see swh_gspace_pm_mesh
+    for N in (0, 1, 1291):  # mesh_gravity.c:1172 bounds N to [2, 1290]
         with pytest.raises(RuntimeError):
             gs.pm_mesh(N, 1.0, 0.1)
     with pytest.raises(RuntimeError):

@@ -711,7 +711,9 @@ static ListDev list_dev(swh_space* s) {
   d.ovf_n = ovf_slot(s);
   // per-cell reach pruning only pays on an adaptive (clustered) grid
   d.cell_R = s->grid.adaptive ? s->cell_hreach.as<const float>() : nullptr;
-  const bool gw = s->tuning.diag_mode == 8 && s->gw_u.ptr;
+  // group walks: diag_mode 8, with the default list capacity (16 x K hit
+  // positions per group fit the walk's LDS, GwHits::kHCap)
+  const bool gw = s->tuning.diag_mode == 8 && s->gw_u.ptr && s->list_K * kListSlots <= GwHits::kHCap;
   d.U = gw ? s->gw_u.as<int>() : nullptr;
   d.ucnt = gw ? s->gw_ucnt.as<int>() : nullptr;
   d.h16 = gw ? s->gw_h16.as<unsigned short>() : nullptr;
@@ -743,7 +745,7 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
   SWH_TRY(s->posf.reserve((size_t)s->n * sizeof(float4)));
   SWH_TRY(s->list_xd0.reserve((size_t)s->n * sizeof(float4)));
   SWH_TRY(s->cell_hreach.reserve((size_t)std::max(1, s->grid.ncell) * sizeof(float)));
-  if (s->tuning.diag_mode == 8) {  // group walks: the U format too
+  if (s->tuning.diag_mode == 8 && K * kListSlots <= GwHits::kHCap) {  // group walks: the U format too
     const size_t ng = (size_t)std::max(1, s->ngroups);
     SWH_TRY(s->gw_u.reserve(ng * kGwUCap * sizeof(int)));
     SWH_TRY(s->gw_ucnt.reserve(ng * sizeof(int)));

@@ -715,18 +715,28 @@ __device__ __forceinline__ void list_walk(const GridDev& g, SoA& a, const ListDe
 // ---------------------------------------------------------------------------
 // U records staged in LDS at a time, per loop (the force record is 81 bytes)
 #ifndef SWH_GW_CAP
-#define SWH_GW_CAP 256
+#define SWH_GW_CAP 192
 #endif
 #ifndef SWH_GW_CAP_FORCE
 #define SWH_GW_CAP_FORCE 128
 #endif
 
 // The loops' j records in LDS (SoA) and the lane partials of the final
-// combine (a union: the combine runs after the walk).
+// combine (a union: the combine runs after the walk); every group walk also
+// keeps its i's hit positions in LDS (loaded once, so an entry costs no
+// global-memory round trip).
+#ifndef SWH_GW_HCAP
+#define SWH_GW_HCAP 2048
+#endif
+struct GwHits {
+  static constexpr int kHCap = SWH_GW_HCAP;  // hit positions of a group (16 slots x K)
+  unsigned short hpos[kHCap];
+  int hoff[kListSlots + 1];  // slot il's positions: hpos[hoff[il] .. hoff[il] + nl)
+};
 template <int LOOP>
 struct GwLds;
 template <>
-struct GwLds<LOOP_DENSITY> {
+struct GwLds<LOOP_DENSITY> : GwHits {
   static constexpr int kCap = SWH_GW_CAP;
   static constexpr int kAcc = 8;
   union {
@@ -739,8 +749,8 @@ struct GwLds<LOOP_DENSITY> {
   int j[kCap];
 };
 template <>
-struct GwLds<LOOP_GRADIENT> {
-  static constexpr int kCap = SWH_GW_CAP;
+struct GwLds<LOOP_GRADIENT> : GwHits {
+  static constexpr int kCap = SWH_GW_CAP_FORCE;
   static constexpr int kAcc = 3;
   union {
     struct {
@@ -752,7 +762,7 @@ struct GwLds<LOOP_GRADIENT> {
   int j[kCap];
 };
 template <>
-struct GwLds<LOOP_FORCE> {
+struct GwLds<LOOP_FORCE> : GwHits {
   static constexpr int kCap = SWH_GW_CAP_FORCE;
   static constexpr int kAcc = 6;
   union {
@@ -837,10 +847,10 @@ __device__ __forceinline__ void gw_walk(const GridDev& g, const SoA& a, const Li
   constexpr int CAP = GwLds<LOOP>::kCap;
   const int lane = threadIdx.x & 63;
   const int s = lane % lpi;
-  const unsigned short* __restrict__ hl = ld.h16 + (size_t)(gid * kListSlots + il) * ld.K;
   const int* __restrict__ U = ld.U + (size_t)gid * ld.UC;
+  const unsigned short* hp = L.hpos + (act ? L.hoff[il] : 0);
   int m = s;
-  int pos = (act && m < nl) ? hl[m] : 0x7fffffff;
+  int pos = (act && m < nl) ? hp[m] : 0x7fffffff;
   for (int c0 = 0; c0 < nU; c0 += CAP) {
     const int cn = min(CAP, nU - c0);
     wave_sync();  // the previous chunk's readers are done
@@ -849,7 +859,7 @@ __device__ __forceinline__ void gw_walk(const GridDev& g, const SoA& a, const Li
     const int cend = c0 + cn;
     while (pos < cend) {
       m += lpi;
-      const int next = m < nl ? hl[m] : 0x7fffffff;
+      const int next = m < nl ? hp[m] : 0x7fffffff;
       gw_entry<LOOP, T, WRAP>(g, pi, L, pos - c0, st);
       pos = next;
     }
@@ -922,6 +932,18 @@ __device__ __forceinline__ void gw_loop(const GridDev& g, SoA& a, const ListDev 
     pi = a.pos[i];
   } else {
     nl = 0;
+  }
+  // the group's hit positions into LDS: slot il's nl entries at hoff[il]
+  {
+    const int cnt = (act && s == 0) ? nl : 0;  // one count per slot
+    const int inc = wave_incl_scan(cnt);
+    if (act && s == 0) L.hoff[il] = inc - cnt;
+    wave_sync();  // (16 slots x K <= kHCap: group walks run with K <= 128 only)
+    if (act) {
+      const unsigned short* __restrict__ hl = ld.h16 + (size_t)(gid * kListSlots + il) * ld.K;
+      unsigned short* dst = L.hpos + L.hoff[il];
+      for (int e = s; e < nl; e += lpi) dst[e] = hl[e];
+    }
   }
   // (every lane of an i starts from load_i's values: the sums at zero, the
   // max / min reductions at i's own v_sig, alpha_max and limiter bin, which

@@ -805,7 +805,7 @@ def test_group_walks_vs_f64(gpu_ctx, case):
         parts = ics.sedov_box(7, velocity="rotating", seed=4)
     else:
         parts = evolving_box(n=16, seed=61)
-        P = abi.default_hydro_params(time_base=2e-3, max_active_bin=2)
+        P = abi.default_hydro_params(time_base=2e-3, max_active_bin=3)
     sp = lib.HydroSpace(gpu_ctx)
     sp.set_tuning(1, 0, 0, diag_mode=8)
     g = abi.copy_parts(parts)

@@ -59,13 +59,12 @@ __device__ __forceinline__ unsigned int rwrap_of(float base, float dx) {
 __global__ void list_prep_kernel(const unsigned int* hmax_bits, float gs1, float dx,
                                  unsigned int* rwrap, unsigned int* rwrap_base,
                                  unsigned int* ovf_n, const unsigned int* run_if,
-                                 unsigned int* nbuilds, unsigned int* govf_n) {
+                                 unsigned int* nbuilds) {
   if (threadIdx.x == 0 && !skip_build(run_if)) {
     const float base = __uint_as_float(*hmax_bits) * gs1 * (1.f + 1e-4f) + 1e-30f;
     *rwrap_base = __float_as_uint(base);
     *rwrap = rwrap_of(base, dx);
     *ovf_n = 0u;
-    *govf_n = 0u;
     *nbuilds += 1u;
   }
 }
@@ -196,30 +195,6 @@ void density_walk_kernel(GridDev g, SoA a, ListDev ld, int i0, int n, int max_ac
                          int* __restrict__ ncount) {
   list_walk<LOOP_DENSITY, T, kWalkLpi>(g, a, ld, i0, n, max_active_bin, a2H, hmax_bits, counter,
                                        ncount);
-}
-
-// Group walks of the loops (swh_list.h gw_loop): one wave per i-group, the
-// group's staged candidates in LDS.
-template <int LOOP, typename T>
-__global__ __launch_bounds__(64) void gw_kernel(GridDev g, SoA a, ListDev ld,
-                                                const int2* __restrict__ groups, int ngroups,
-                                                int max_active_bin, T a2H,
-                                                const unsigned int* __restrict__ hmax_bits,
-                                                unsigned long long* counter,
-                                                int* __restrict__ ncount) {
-  __shared__ GwLds<LOOP> L;
-  gw_loop<LOOP, T>(g, a, ld, groups, ngroups, max_active_bin, a2H, hmax_bits, counter, ncount,
-                   L);
-}
-
-template <int LOOP, typename T>
-__global__ __launch_bounds__(64) void gw_overflow_kernel(GridDev g, SoA a, ListDev ld,
-                                                         const int2* __restrict__ groups,
-                                                         int max_active_bin, T a2H,
-                                                         const unsigned int* __restrict__ hmax_bits,
-                                                         unsigned long long* counter,
-                                                         int* __restrict__ ncount) {
-  gw_overflow_walk<LOOP, T>(g, a, ld, groups, max_active_bin, a2H, hmax_bits, counter, ncount);
 }
 
 // The list's overflow particles (more than K hits: a large H in a dense
@@ -685,13 +660,11 @@ static unsigned int* search_slot(swh_space* s) { return s->counters.as<unsigned 
 // (u32[19]: the drift's displacement, u32[21]: max |v_full|, swh_space.hip)
 // u32[24]: kept lists found stale by the device check; u32[25]: displacement
 // since the list build (float bits); u32[26]: list builds run on the device;
-// u32[27]: the wrap radius's R_max part; u32[28]: groups whose U did not fit (group walks)
+// u32[27]: the wrap radius's R_max part
 static unsigned int* keep_stale_slot(swh_space* s) { return s->counters.as<unsigned int>() + 24; }
 static unsigned int* disp_slot(swh_space* s) { return s->counters.as<unsigned int>() + 25; }
 static unsigned int* nbuild_slot(swh_space* s) { return s->counters.as<unsigned int>() + 26; }
 static unsigned int* rwrap_base_slot(swh_space* s) { return s->counters.as<unsigned int>() + 27; }
-
-constexpr int kGwUCap = 512;  // staged candidates recorded per group (group walks)
 
 static ListDev list_dev(swh_space* s) {
   // skin of the lists in use (the ghost may rebuild them with a wider one)
@@ -711,15 +684,6 @@ static ListDev list_dev(swh_space* s) {
   d.ovf_n = ovf_slot(s);
   // per-cell reach pruning only pays on an adaptive (clustered) grid
   d.cell_R = s->grid.adaptive ? s->cell_hreach.as<const float>() : nullptr;
-  // group walks: diag_mode 8, with the default list capacity (16 x K hit
-  // positions per group fit the walk's LDS, GwHits::kHCap)
-  const bool gw = s->tuning.diag_mode == 8 && s->gw_u.ptr && s->list_K * kListSlots <= GwHits::kHCap;
-  d.U = gw ? s->gw_u.as<int>() : nullptr;
-  d.ucnt = gw ? s->gw_ucnt.as<int>() : nullptr;
-  d.h16 = gw ? s->gw_h16.as<unsigned short>() : nullptr;
-  d.UC = kGwUCap;
-  d.govf = gw ? s->gw_govf.as<int>() : nullptr;
-  d.govf_n = s->counters.as<unsigned int>() + 28;
   return d;
 }
 
@@ -745,13 +709,6 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
   SWH_TRY(s->posf.reserve((size_t)s->n * sizeof(float4)));
   SWH_TRY(s->list_xd0.reserve((size_t)s->n * sizeof(float4)));
   SWH_TRY(s->cell_hreach.reserve((size_t)std::max(1, s->grid.ncell) * sizeof(float)));
-  if (s->tuning.diag_mode == 8 && K * kListSlots <= GwHits::kHCap) {  // group walks: the U format too
-    const size_t ng = (size_t)std::max(1, s->ngroups);
-    SWH_TRY(s->gw_u.reserve(ng * kGwUCap * sizeof(int)));
-    SWH_TRY(s->gw_ucnt.reserve(ng * sizeof(int)));
-    SWH_TRY(s->gw_h16.reserve(ng * kListSlots * (size_t)K * sizeof(unsigned short)));
-    SWH_TRY(s->gw_govf.reserve(ng * sizeof(int)));
-  }
   s->list_K = K;
   const ListDev ld = list_dev(s);
   if (ld.cell_R) {
@@ -768,7 +725,7 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
                      s->list_xd0.as<float4>(), run_if);
   hipLaunchKernelGGL(list_prep_kernel, dim3(1), dim3(64), 0, s->stream, hmax_slot(s),
                      kGamma * ld.skin1, (float)s->grid.dx, rwrap_slot(s), rwrap_base_slot(s),
-                     ovf_slot(s), run_if, nbuild_slot(s), s->counters.as<unsigned int>() + 28);
+                     ovf_slot(s), run_if, nbuild_slot(s));
   SWH_TRY(s->gbox.reserve((size_t)std::max(1, s->ngroups) * sizeof(GroupBox)));
   ListDev ldb = list_dev(s);
   hipLaunchKernelGGL(group_box_kernel, dim3((s->ngroups + 255) / 256), dim3(256), 0, s->stream,
@@ -823,15 +780,7 @@ static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int
                        search_slot(s), max_active_bin, a2H, hmax_slot(s), ctr, ncount);
     return;
   }
-  if (ld.U) {  // group walk (+ the groups whose U did not fit)
-    hipLaunchKernelGGL((gw_kernel<LOOP, T>), dim3(s->ngroups), dim3(64), 0, s->stream, gd,
-                       soa_of(s), ld, s->groups.as<const int2>(), s->ngroups, max_active_bin,
-                       a2H, hmax_slot(s), ctr, ncount);
-    hipLaunchKernelGGL((gw_overflow_kernel<LOOP, T>), dim3(256), dim3(64), 0, s->stream, gd,
-                       soa_of(s), ld, s->groups.as<const int2>(), max_active_bin, a2H,
-                       hmax_slot(s), ctr, ncount);
-  }
-  else if (LOOP == LOOP_DENSITY && sizeof(T) == 8)  // (the fp32 walk would spill)
+  if (LOOP == LOOP_DENSITY && sizeof(T) == 8)  // (the fp32 walk would spill)
     hipLaunchKernelGGL((density_walk_kernel<T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
                        s->stream, gd, soa_of(s), ld, 0, nitems, max_active_bin, a2H,
                        hmax_slot(s), ctr, ncount);
@@ -866,7 +815,7 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const int
       SWH_TRY(check_kept_lists(s, P, count));
     }
     if (s->tuning.diag_mode != 0 && s->tuning.diag_mode != 3 && s->tuning.diag_mode != 4 &&
-        s->tuning.diag_mode != 7 && s->tuning.diag_mode != 8)
+        s->tuning.diag_mode != 7)
       return SWH_OK;
   }
   const GridDev gd = grid_dev(s);

@@ -199,7 +199,6 @@ struct swh_space {
   // the step's pair lists (swh_list.h): valid from a density loop until the
   // next upload / rebuild / tuning change, or a ghost that grows an H past its R
   swh::DevBuf nbr, nbr_cnt, nbr_base, nbr_reach, nbr_ovf;
-  swh::DevBuf gw_u, gw_ucnt, gw_h16, gw_govf;  // group-walk format of the lists (swh_list.h)
   swh::DevBuf posf;  // float4: position relative to its grid cell's corner, h
   swh::DevBuf gbox;  // GroupBox per i-group: the list build's group boxes
   swh::DevBuf list_xd0;  // float4: the displacement record (xdiff) at the list build

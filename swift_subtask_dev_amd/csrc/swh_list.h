@@ -89,16 +89,6 @@ struct ListDev {
                         // null on a uniform grid (no per-cell pruning)
   int diag;      // profiling only: 2 = the build writes no entries
   const GroupBox* gbox;  // per group (group_box_kernel), read by the build
-  // group-walk format (null: not written): per group, the candidates the
-  // build staged, in staging order (U, UC per group; ucnt = how many, > UC:
-  // the group's U did not fit), and per i-slot its hits as 16-bit positions
-  // in its group's U (K per slot, in candidate order)
-  int* U;
-  int* ucnt;
-  unsigned short* h16;
-  int UC;
-  int* govf;             // groups whose U did not fit (their count in *govf_n)
-  unsigned int* govf_n;
 };
 
 __global__ void group_box_kernel(SoA a, const int2* __restrict__ groups, int ngroups,
@@ -186,7 +176,7 @@ __device__ __forceinline__ float4 cell_local(const GridDev& g, const double4& p,
 // Copy i's pending LDS hits to its global list (the LPI lanes of i split them).
 template <int LPI, class LDS>
 __device__ __forceinline__ void list_flush(const ListDev& ld, LDS& L, int& nq, int& wr, int il,
-                                           int s, int gbase, TileStats& ts, int ust) {
+                                           int s, int gbase, TileStats& ts) {
   wave_sync();  // list entries were written by the other lanes of i
   ts.bsteps += (unsigned int)(nq > s ? (nq - s + LPI - 1) / LPI : 0);  // this lane's entries
   const unsigned short* list = &L.hits[il * LDS::kStride];
@@ -204,12 +194,6 @@ __device__ __forceinline__ void list_flush(const ListDev& ld, LDS& L, int& nq, i
 #pragma unroll
       for (int q = 0; q < 4; q++)
         if (t + q * LPI < nk) ld.nbr[list_at(gbase + il, ld.KS, wr + t + q * LPI)] = jv[q];
-      if (ld.h16) {  // the same entries as positions in the group's U
-        unsigned short* hl = ld.h16 + (size_t)(gbase + il) * ld.K + wr;
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-          if (t + q * LPI < nk) hl[t + q * LPI] = (unsigned short)(ust + sl[q]);
-      }
     }
   }
   wr += nq;
@@ -236,16 +220,14 @@ template <int LPI, bool WRAP, class LDS>
 __device__ __forceinline__ void list_consume(const GridDev& g, const ListDev& ld,
                                              const CellRange& c, float xi, float yi, float zi,
                                              float thr_i, bool act, int nst, LDS& L, int& nq,
-                                             int& wr, int il, int s, int gbase, TileStats& ts,
-                                             int ust) {
+                                             int& wr, int il, int s, int gbase, TileStats& ts) {
   constexpr int GS = 64 / LPI;
   const int dummy = GS * LDS::kStride + il * LPI + s;
   const int nblk = (nst + kListBlk * LPI - 1) / (kListBlk * LPI);
   ts.asteps += (unsigned int)(nblk * kListBlk);
   const float bx = (float)g.dim[0], by = (float)g.dim[1], bz = (float)g.dim[2];
   for (int b = 0; b < nblk; b++) {
-    if (__any(nq > LDS::kICap - kListBlk * LPI))
-      list_flush<LPI>(ld, L, nq, wr, il, s, gbase, ts, ust);
+    if (__any(nq > LDS::kICap - kListBlk * LPI)) list_flush<LPI>(ld, L, nq, wr, il, s, gbase, ts);
     // lane s of i tests the contiguous run c0 .. c0 + kListBlk - 1 (its hits
     // come out in candidate order), two candidates per packed fp32 op
     const int c0 = (b * LPI + s) * kListBlk;
@@ -310,21 +292,7 @@ __device__ __forceinline__ void list_consume(const GridDev& g, const ListDev& ld
     }
     nq += tot;
   }
-  list_flush<LPI>(ld, L, nq, wr, il, s, gbase, ts, ust);
-}
-
-// Append the consumed region's candidates [0, nst) to the group's U (the
-// 16-bit positions its hits were flushed with start at ust).
-template <class LDS>
-__device__ __forceinline__ void list_record_u(const ListDev& ld, LDS& L, int gid, int& ust,
-                                              int nst) {
-  if (ld.U) {
-    const int lane = threadIdx.x & 63;
-    int* u = ld.U + (size_t)gid * ld.UC;
-    for (int k = lane; k < nst; k += 64)
-      if (ust + k < ld.UC) u[ust + k] = L.candj[k];
-  }
-  ust += nst;
+  list_flush<LPI>(ld, L, nq, wr, il, s, gbase, ts);
 }
 
 // What a build wave knows about its i-slot when the group's lists are done
@@ -362,7 +330,6 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
   TileStats ts;
   const int gbase = gid * kListSlots;
   int nq = 0, wr = 0;
-  int ust = 0;  // candidates of this group staged (and recorded in U) so far
   if (Rg > 0.) {
     const double Rmax = (double)__uint_as_float(*hmax_bits) * (double)kGamma * skin1;
     // r < max(R_i, R_j); cells are enumerated out to reach + dx (drift)
@@ -467,12 +434,11 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
           if (diag != 1) {
             if (wrap)
               list_consume<LPI, true>(g, ld, c, xi, yi, zi, thr_i, act, nst, L, nq, wr, il, s,
-                                      gbase, ts, ust);
+                                      gbase, ts);
             else
               list_consume<LPI, false>(g, ld, c, xi, yi, zi, thr_i, act, nst, L, nq, wr, il, s,
-                                       gbase, ts, ust);
+                                       gbase, ts);
           }
-          list_record_u(ld, L, gid, ust, nst);
           nst = 0;
           wave_sync();
         }
@@ -545,16 +511,11 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
     if (diag != 1 && nst > 0) {
       if (wrap)
         list_consume<LPI, true>(g, ld, c, xi, yi, zi, thr_i, act, nst, L, nq, wr, il, s, gbase,
-                                ts, ust);
+                                ts);
       else
         list_consume<LPI, false>(g, ld, c, xi, yi, zi, thr_i, act, nst, L, nq, wr, il, s, gbase,
-                                 ts, ust);
+                                 ts);
     }
-    if (nst > 0) list_record_u(ld, L, gid, ust, nst);
-  }
-  if (ld.ucnt && gid < ngroups && lane == 0) {
-    ld.ucnt[gid] = ust;
-    if (ust > ld.UC) ld.govf[atomicAdd(ld.govf_n, 1u)] = gid;
   }
   if (i >= 0 && s == 0) {
     ld.cnt[i] = act ? wr : 0;
@@ -698,332 +659,6 @@ __device__ __forceinline__ void list_walk(const GridDev& g, SoA& a, const ListDe
     unsigned long long v = (unsigned long long)((act && s == 0) ? st.n : 0);
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(counter_stripe(counter), v);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Group walks: one wave per i-group over the group's staged candidates U.
-// A list walk gathers each entry's j record from HBM/L2 -- a j in ~48 lists
-// is fetched ~48 times, and the walks are bound by the texture addresser
-// (TA_BUSY 60-66%). A group walk stages the group's U records into LDS once
-// (each cell's candidates are a contiguous run of the sorted arrays) and
-// every i reads its j's from LDS through its 16-bit positions; the group's
-// i's share the wave's 64 lanes (64 / n_i lanes each, so a 10-particle
-// group keeps 60 lanes busy), and the lanes of an i combine their partial
-// sums through LDS. Groups whose U exceeds the recorded capacity walk their
-// 32-bit lists as the list walk does.
-// ---------------------------------------------------------------------------
-// U records staged in LDS at a time, per loop (the force record is 81 bytes)
-#ifndef SWH_GW_CAP
-#define SWH_GW_CAP 192
-#endif
-#ifndef SWH_GW_CAP_FORCE
-#define SWH_GW_CAP_FORCE 128
-#endif
-
-// The loops' j records in LDS (SoA) and the lane partials of the final
-// combine (a union: the combine runs after the walk); every group walk also
-// keeps its i's hit positions in LDS (loaded once, so an entry costs no
-// global-memory round trip).
-#ifndef SWH_GW_HCAP
-#define SWH_GW_HCAP 2048
-#endif
-struct GwHits {
-  static constexpr int kHCap = SWH_GW_HCAP;  // hit positions of a group (16 slots x K)
-  unsigned short hpos[kHCap];
-  int hoff[kListSlots + 1];  // slot il's positions: hpos[hoff[il] .. hoff[il] + nl)
-};
-template <int LOOP>
-struct GwLds;
-template <>
-struct GwLds<LOOP_DENSITY> : GwHits {
-  static constexpr int kCap = SWH_GW_CAP;
-  static constexpr int kAcc = 8;
-  union {
-    struct {
-      double x[kCap], y[kCap], z[kCap];
-      float4 p0[kCap];  // v, m
-    } st;
-    double red[kAcc][64];
-  };
-  int j[kCap];
-};
-template <>
-struct GwLds<LOOP_GRADIENT> : GwHits {
-  static constexpr int kCap = SWH_GW_CAP_FORCE;
-  static constexpr int kAcc = 3;
-  union {
-    struct {
-      double x[kCap], y[kCap], z[kCap];
-      float4 p0[kCap], p1[kCap];  // v, m; u, rho, c, alpha_visc
-    } st;
-    double red[kAcc][64];
-  };
-  int j[kCap];
-};
-template <>
-struct GwLds<LOOP_FORCE> : GwHits {
-  static constexpr int kCap = SWH_GW_CAP_FORCE;
-  static constexpr int kAcc = 6;
-  union {
-    struct {
-      double x[kCap], y[kCap], z[kCap];
-      float4 p0[kCap], p1[kCap], p2[kCap];  // v, m; u, rho, P, c; f, balsara, alphas
-      float h[kCap];
-      int8_t tb[kCap];
-    } st;
-    double red[kAcc][64];
-  };
-  int j[kCap];
-};
-
-// Stage U records [c0, c0 + cn) of the group into LDS slots [0, cn).
-template <int LOOP>
-__device__ __forceinline__ void gw_stage(const SoA& a, const int* __restrict__ U, int c0, int cn,
-                                         GwLds<LOOP>& L) {
-  constexpr int R = GwLds<LOOP>::kCap / 64;
-  const int lane = threadIdx.x & 63;
-  int jv[R];
-#pragma unroll
-  for (int u = 0; u < R; u++) {
-    const int k = lane + 64 * u;
-    jv[u] = k < cn ? U[c0 + k] : -1;
-  }
-#pragma unroll
-  for (int u = 0; u < R; u++) {
-    const int k = lane + 64 * u;
-    if (jv[u] < 0) continue;
-    const int j = jv[u];
-    const double4 p = a.pos[j];
-    L.st.x[k] = p.x;
-    L.st.y[k] = p.y;
-    L.st.z[k] = p.z;
-    L.st.p0[k] = a.vm[j];
-    if constexpr (LOOP == LOOP_GRADIENT) {
-      const float4 t = a.th[j];
-      L.st.p1[k] = make_float4(t.x, t.y, t.w, a.fc[j].z);
-    }
-    if constexpr (LOOP == LOOP_FORCE) {
-      L.st.p1[k] = a.th[j];
-      L.st.p2[k] = a.fc[j];
-      L.st.h[k] = (float)p.w;
-      L.st.tb[k] = a.tb[j];
-    }
-    L.j[k] = j;
-  }
-}
-
-// One entry: the record in LDS slot k.
-template <int LOOP, typename T, bool WRAP>
-__device__ __forceinline__ void gw_entry(const GridDev& g, const double4& pi, GwLds<LOOP>& L,
-                                         int k, LoopState<LOOP, T>& st) {
-  double dx = pi.x - L.st.x[k], dy = pi.y - L.st.y[k], dz = pi.z - L.st.z[k];
-  if (WRAP) {
-    dx = wrap_nearest(dx, g.dim[0]);
-    dy = wrap_nearest(dy, g.dim[1]);
-    dz = wrap_nearest(dz, g.dim[2]);
-  }
-  const T tdx = (T)dx, tdy = (T)dy, tdz = (T)dz;
-  const T r2 = tdx * tdx + tdy * tdy + tdz * tdz;
-  double4 pj = make_double4(0., 0., 0., 0.);
-  int meta = 0;
-  float4 p[LoopState<LOOP, T>::kPay];
-  p[0] = L.st.p0[k];
-  if constexpr (LOOP == LOOP_GRADIENT) p[1] = L.st.p1[k];
-  if constexpr (LOOP == LOOP_FORCE) {
-    pj.w = (double)L.st.h[k];
-    p[1] = L.st.p1[k];
-    p[2] = L.st.p2[k];
-    meta = L.st.tb[k];
-  }
-  if (st.accept(L.j[k], pj, r2)) st.interact_staged(p, meta, pj, tdx, tdy, tdz, r2);
-}
-
-template <int LOOP, typename T, bool WRAP>
-__device__ __forceinline__ void gw_walk(const GridDev& g, const SoA& a, const ListDev& ld,
-                                        GwLds<LOOP>& L, int gid, int nU, int lpi, bool act,
-                                        const double4& pi, int nl, int il,
-                                        LoopState<LOOP, T>& st) {
-  constexpr int CAP = GwLds<LOOP>::kCap;
-  const int lane = threadIdx.x & 63;
-  const int s = lane % lpi;
-  const int* __restrict__ U = ld.U + (size_t)gid * ld.UC;
-  const unsigned short* hp = L.hpos + (act ? L.hoff[il] : 0);
-  int m = s;
-  int pos = (act && m < nl) ? hp[m] : 0x7fffffff;
-  for (int c0 = 0; c0 < nU; c0 += CAP) {
-    const int cn = min(CAP, nU - c0);
-    wave_sync();  // the previous chunk's readers are done
-    gw_stage<LOOP>(a, U, c0, cn, L);
-    wave_sync();
-    const int cend = c0 + cn;
-    while (pos < cend) {
-      m += lpi;
-      const int next = m < nl ? hp[m] : 0x7fffffff;
-      gw_entry<LOOP, T, WRAP>(g, pi, L, pos - c0, st);
-      pos = next;
-    }
-  }
-}
-
-// The loops' accumulators <-> doubles, and how the lpi partials combine.
-template <typename T>
-__device__ __forceinline__ void gw_put(const LoopState<LOOP_DENSITY, T>& st, double* v) {
-  v[0] = st.A.rho; v[1] = st.A.rho_dh; v[2] = st.A.wcount; v[3] = st.A.wcount_dh;
-  v[4] = st.A.div_v; v[5] = st.A.rot_x; v[6] = st.A.rot_y; v[7] = st.A.rot_z;
-}
-template <typename T>
-__device__ __forceinline__ void gw_add(LoopState<LOOP_DENSITY, T>& st, const double* v) {
-  st.A.rho += (T)v[0]; st.A.rho_dh += (T)v[1]; st.A.wcount += (T)v[2];
-  st.A.wcount_dh += (T)v[3]; st.A.div_v += (T)v[4]; st.A.rot_x += (T)v[5];
-  st.A.rot_y += (T)v[6]; st.A.rot_z += (T)v[7];
-}
-template <typename T>
-__device__ __forceinline__ void gw_put(const LoopState<LOOP_GRADIENT, T>& st, double* v) {
-  v[0] = st.A.v_sig; v[1] = st.A.laplace_u; v[2] = st.A.alpha_visc_max_ngb;
-}
-template <typename T>
-__device__ __forceinline__ void gw_add(LoopState<LOOP_GRADIENT, T>& st, const double* v) {
-  st.A.v_sig = tmax(st.A.v_sig, (T)v[0]);
-  st.A.laplace_u += (T)v[1];
-  st.A.alpha_visc_max_ngb = tmax(st.A.alpha_visc_max_ngb, (T)v[2]);
-}
-template <typename T>
-__device__ __forceinline__ void gw_put(const LoopState<LOOP_FORCE, T>& st, double* v) {
-  v[0] = st.A.ax; v[1] = st.A.ay; v[2] = st.A.az; v[3] = st.A.u_dt; v[4] = st.A.h_dt;
-  v[5] = (double)st.A.min_ngb_time_bin;
-}
-template <typename T>
-__device__ __forceinline__ void gw_add(LoopState<LOOP_FORCE, T>& st, const double* v) {
-  st.A.ax += (T)v[0]; st.A.ay += (T)v[1]; st.A.az += (T)v[2];
-  st.A.u_dt += (T)v[3]; st.A.h_dt += (T)v[4];
-  st.A.min_ngb_time_bin = min(st.A.min_ngb_time_bin, (int)v[5]);
-}
-
-// One loop over the active listed particles of every group (one wave each).
-template <int LOOP, typename T>
-__device__ __forceinline__ void gw_loop(const GridDev& g, SoA& a, const ListDev ld,
-                                        const int2* __restrict__ groups, int ngroups,
-                                        int max_active_bin, T a2H,
-                                        const unsigned int* __restrict__ hmax_bits,
-                                        unsigned long long* counter, int* __restrict__ ncount,
-                                        GwLds<LOOP>& L) {
-  constexpr int NA = GwLds<LOOP>::kAcc;
-  const int lane = threadIdx.x & 63;
-  const int gid = xcd_block_id();
-  if (gid >= ngroups) return;
-  const int2 gr = groups[gid];
-  const int nU = ld.ucnt[gid];
-  if (nU > ld.UC || gr.y <= 0) return;  // U did not fit: gw_overflow_walk
-  const int lpi = 64 / gr.y;
-  const int il = lane / lpi, s = lane % lpi;
-  const int i = il < gr.y ? gr.x + il : -1;
-  bool act = i >= 0 && active_part(a, i, max_active_bin);
-  int nl = 0;
-  if (act) {
-    nl = ld.cnt[i];
-    if (nl > ld.K || ld.base[i] < 0) act = false;  // overflow: the search walks it
-  }
-  LoopState<LOOP, T> st;
-  st.n = 0;
-  double4 pi = make_double4(0., 0., 0., 0.);
-  if (act) {
-    st.load_i(a, i, a2H, hmax_bits);
-    pi = a.pos[i];
-  } else {
-    nl = 0;
-  }
-  // the group's hit positions into LDS: slot il's nl entries at hoff[il]
-  {
-    const int cnt = (act && s == 0) ? nl : 0;  // one count per slot
-    const int inc = wave_incl_scan(cnt);
-    if (act && s == 0) L.hoff[il] = inc - cnt;
-    wave_sync();  // (16 slots x K <= kHCap: group walks run with K <= 128 only)
-    if (act) {
-      const unsigned short* __restrict__ hl = ld.h16 + (size_t)(gid * kListSlots + il) * ld.K;
-      unsigned short* dst = L.hpos + L.hoff[il];
-      for (int e = s; e < nl; e += lpi) dst[e] = hl[e];
-    }
-  }
-  // (every lane of an i starts from load_i's values: the sums at zero, the
-  // max / min reductions at i's own v_sig, alpha_max and limiter bin, which
-  // combine idempotently)
-  const double rwrap = (double)__uint_as_float(*ld.rwrap_bits);
-  if (__any(act && g.periodic && near_face(g, pi, rwrap)))
-    gw_walk<LOOP, T, true>(g, a, ld, L, gid, nU, lpi, act, pi, nl, il, st);
-  else
-    gw_walk<LOOP, T, false>(g, a, ld, L, gid, nU, lpi, act, pi, nl, il, st);
-  // the lpi partial states of an i, combined in lane order through LDS
-  wave_sync();
-  double v[NA];
-  gw_put(st, v);
-#pragma unroll
-  for (int q = 0; q < NA; q++) L.red[q][lane] = v[q];
-  L.j[lane] = st.n;
-  wave_sync();
-  if (act && s == 0) {
-    for (int q = 1; q < lpi; q++) {
-      double w[NA];
-#pragma unroll
-      for (int f = 0; f < NA; f++) w[f] = L.red[f][lane + q];
-      gw_add(st, w);
-      st.n += L.j[lane + q];
-    }
-    st.store(a, i);
-    if (ncount) ncount[i] = st.n;
-  }
-  if (counter) {
-    unsigned long long c = (unsigned long long)((act && s == 0) ? st.n : 0);
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-    if (lane == 0 && c) atomicAdd(counter_stripe(counter), c);
-  }
-}
-
-// Groups whose U did not fit (queued by the build): their 32-bit lists,
-// four lanes per i, one wave per queued group.
-template <int LOOP, typename T>
-__device__ __forceinline__ void gw_overflow_walk(const GridDev& g, SoA& a, const ListDev ld,
-                                                 const int2* __restrict__ groups,
-                                                 int max_active_bin, T a2H,
-                                                 const unsigned int* __restrict__ hmax_bits,
-                                                 unsigned long long* counter,
-                                                 int* __restrict__ ncount) {
-  const int lane = threadIdx.x & 63;
-  const int nq = (int)*ld.govf_n;
-  const double rwrap = (double)__uint_as_float(*ld.rwrap_bits);
-  for (int q = blockIdx.x; q < nq; q += gridDim.x) {
-    const int2 gr = groups[ld.govf[q]];
-    const int il = lane >> 2, s = lane & 3;
-    const int i = il < gr.y ? gr.x + il : -1;
-    bool act = i >= 0 && active_part(a, i, max_active_bin);
-    int nl = 0, lb = 0;
-    double4 pi = make_double4(0., 0., 0., 0.);
-    if (act) {
-      nl = ld.cnt[i];
-      lb = ld.base[i];
-      if (nl > ld.K || lb < 0) act = false;
-    }
-    LoopState<LOOP, T> st;
-    st.n = 0;
-    if (act) {
-      st.load_i(a, i, a2H, hmax_bits);
-      pi = a.pos[i];
-    }
-    if (!act) nl = 0;
-    if (__any(act && g.periodic && near_face(g, pi, rwrap)))
-      walk_entries<4, true, T>(g, a, ld, pi, nl, lb, s, st);
-    else
-      walk_entries<4, false, T>(g, a, ld, pi, nl, lb, s, st);
-    reduce_lanes<4, T>(st);
-    if (act && s == 0) {
-      st.store(a, i);
-      if (ncount) ncount[i] = st.n;
-    }
-    if (counter) {
-      unsigned long long v = (unsigned long long)((act && s == 0) ? st.n : 0);
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-      if (lane == 0 && v) atomicAdd(counter_stripe(counter), v);
-    }
   }
 }
 

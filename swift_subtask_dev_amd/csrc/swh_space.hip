@@ -712,7 +712,7 @@ swh_status swh_space_set_tuning(swh_space* s, const swh_tuning* t) {
   if (!s || !t || t->cell_factor < 1 || t->cell_factor > 4 ||
       (t->loop_variant != 0 && t->loop_variant != 7) ||
       (t->group_size != 0 && t->group_size != 16) || t->cell_scale < 0.f || t->cell_scale > 4.f ||
-      t->diag_mode < 0 || t->diag_mode > 8 || t->diag_mode == 5 ||
+      t->diag_mode < 0 || t->diag_mode > 7 || t->diag_mode == 5 ||
       t->diag_mode == 6 || t->list_capacity < 0 || t->list_capacity > 4096 ||
       (t->list_capacity % 4) != 0 || !(t->list_skin >= 0.f) || t->list_skin > 1.f ||
       t->list_keep < 0 || t->list_keep > 1)

@@ -783,54 +783,3 @@ def test_density_list_reuse(gpu_ctx):
     sp.init_parts(P)
     assert sp.density(P) == no
     sp.close()
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("case", ["sedov", "clustered", "periodic_small", "evolving"])
-def test_group_walks_vs_f64(gpu_ctx, case):
-    """Group walks (diag_mode 8): the density, gradient and force loops read
-    every i's j's from its group's staged candidates in LDS through 16-bit
-    positions (swh_list.h gw_loop). The whole chain (density, ghost reruns,
-    gradient, extra ghost, force) against the fp64 oracle chain: exact
-    counts, h and every chain field at the chain tolerances; then the two
-    timed loops alone on the converged state: density to 2e-6, exact counts."""
-    from swift_subtask_dev_amd import lib
-    from test_gpu_physics import check_chain, evolving_box, oracle_chain
-    P = abi.default_hydro_params()
-    if case == "sedov":
-        parts = ics.sedov_box(16, velocity="divergent", seed=21)
-    elif case == "clustered":
-        parts = ics.clustered_box(16, n_clumps=4, per_clump=1500, seed=23)
-    elif case == "periodic_small":
-        parts = ics.sedov_box(7, velocity="rotating", seed=4)
-    else:
-        parts = evolving_box(n=16, seed=61)
-        P = abi.default_hydro_params(time_base=2e-3, max_active_bin=3)
-    sp = lib.HydroSpace(gpu_ctx)
-    sp.set_tuning(1, 0, 0, diag_mode=8)
-    g = abi.copy_parts(parts)
-    sp.upload(g)
-    sp.rebuild(P)
-    rg = sp.hydro_step(P)
-    sp.download(g, abi.FIELDS_ALL)
-    o, ro = oracle_chain(parts, P)
-    if case == "clustered":  # cancelling div_v: compared as test_clustered_box_chain
-        assert [rg[k] for k in ("density", "gradient", "force")] == \
-            [ro[k] for k in ("density", "gradient", "force")]
-        assert_close(g["h"], o["h"], 1e-6, what="h")
-        assert_close(g["a_hydro"], o["a_hydro"], 1e-4, 1e-3, "a_hydro")
-    else:
-        check_chain(g, rg, o, ro, parts["time_bin"] <= P.max_active_bin)
-    # the timed density loop alone on the converged state
-    sp.upload(g)
-    sp.rebuild(P)
-    sp.init_parts(P)
-    n = sp.density(P)
-    gd = abi.copy_parts(g)
-    sp.download(gd, abi.FIELDS_DENSITY)
-    sp.close()
-    od = abi.copy_parts(g)
-    O.fn("f32", "init_parts")(od.ctypes.data, len(od), C.byref(P))
-    assert n == O.fn("f64", "box_density")(od.ctypes.data, len(od), C.byref(P), None)
-    act = g["time_bin"] <= P.max_active_bin
-    assert_hydro_close(gd[act], od[act], TIGHT, f"group walk {case}")

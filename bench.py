@@ -51,6 +51,7 @@ FLOPS_DENSITY, FLOPS_FORCE = 65, 146   # SURVEY 8d flops per directed interactio
 
 
 RED_DEVICE = "cuda"  # device of the max/sum-over-ranks tensors
+RANKS = {}  # world size, backend and the device of every rank (main)
 
 
 def log(msg):
@@ -846,9 +847,7 @@ def run_cosmo(args, ctx, rank, world, dist, torch):
                                        "owned + halo (rho refreshed between density and force), "
                                        "gravity subtrees owned, gparts replicated"
                                        if world > 1 else "one GPU"),
-                       "world_size": world,
-                       "backend": (dist.get_backend() if dist else None),
-                       "device": torch.cuda.current_device(),
+                       "ranks": RANKS,
                        "cosmology": {"a": P.a, "H": P.H, "Omega_cdm": ics.SCV_OMEGA_CDM,
                                      "Omega_b": ics.SCV_OMEGA_B, "Omega_lambda": ics.SCV_OMEGA_L,
                                      "units": "box (142.248 Mpc), km/s, G = 1"},
@@ -993,6 +992,18 @@ def main():
             dist.init_process_group(backend)
 
     from swift_subtask_dev_amd import abi, decomp, ics, lib
+
+    # which GPU every rank drives (so a multi-GPU line shows its rank layout)
+    global RANKS
+    devs = [device]
+    if dist:
+        t = torch.tensor([device], dtype=torch.int64, device=RED_DEVICE)
+        got = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(got, t)
+        devs = [int(x.item()) for x in got]
+    RANKS = {"world_size": dist.get_world_size() if dist else 1,
+             "backend": dist.get_backend() if dist else None,
+             "device_of_rank": devs, "visible_devices": torch.cuda.device_count()}
 
     if args.workload in ("grav", "cosmo"):
         ctx = lib.Context(device, args.precision)
@@ -1207,12 +1218,14 @@ def main():
                 "force_algorithmic_GBps": b_force / tf / 1e9,
                 "density_fp64_frac": n_density * FLOPS_DENSITY / td / FP64_PEAK,
                 "force_fp64_frac": n_force * FLOPS_FORCE / tf / FP64_PEAK,
-                # tile-loop work counters (variants 4, 5): candidates loaded, staged,
-                # phase-A and phase-B wave steps
+                # the list build's work counters of the counted setup loop
+                # (swh_list.h TileStats): candidates loaded, staged, candidate-test
+                # steps and list-flush steps (force: zeros, it reuses the lists)
                 "density_loop_stats": stats_density,
                 "force_loop_stats": stats_force,
             },
             "cpu_baseline": None,
+            "ranks": RANKS,
         }
         if steady:
             out["steady_state"] = steady

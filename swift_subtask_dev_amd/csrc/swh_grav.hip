@@ -543,6 +543,142 @@ __global__ __launch_bounds__(64) void p2p_small_kernel(
   }
 }
 
+// Small i-leaves with batched sources: one wave per i-leaf, lpi lanes per
+// i-particle as p2p_small_kernel, but the gparts of up to 32 consecutive P-P
+// entries (up to kPPBatch of them) are gathered into the LDS tile at once:
+// the chain of dependent loads (entry -> source leaf -> its gparts) and the
+// two wave barriers are paid once per batch, not once per source leaf. In a
+// cosmological tree (cell_split_size 50, ~16 gparts per leaf, ~300 source
+// leaves per i-leaf under the adaptive MAC) the per-entry chain left the
+// wave waiting on memory for most of its time. Each entry's truncation and
+// M2P acceptance become bits (tmask: truncated entries; mmask, per i: the
+// entries whose multipole this i takes instead, m2p_accept as in
+// mpole_mask); the self term is removed by comparing gpart indices. Sources
+// larger than the tile (no-cache entries against a whole cell) are staged in
+// tile-sized chunks, every LDS index stays below kPPBatch.
+constexpr int kPPBatch = 256;
+
+template <bool MPOLE>
+__global__ __launch_bounds__(64) void p2p_batch_kernel(
+    GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
+    const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
+    double dimz, double r_s_inv, MacParams mac, unsigned long long* counter) {
+  __shared__ double sx[kPPBatch], sy[kPPBatch], sz[kPPBatch], se2[kPPBatch], sh[kPPBatch];
+  __shared__ float sm[kPPBatch];
+  __shared__ int sg[kPPBatch];
+  __shared__ unsigned char sb[kPPBatch];
+  __shared__ int boff[32], bstart[32];
+  const int li = xcd_block_id();
+  const swh_leaf L = leaves[li];
+  const int p0 = pair_off[li], p1 = pair_off[li + 1];
+  if (p0 == p1) return;  // (inner cells overlap their leaves: leave acc alone)
+  const int lane = (int)threadIdx.x;
+  int lpi = 1;  // wave-uniform
+  while (lpi < 8 && L.count * lpi * 2 <= 64) lpi *= 2;
+  const int il = lane / lpi, s = lane % lpi;
+  const int gi = L.start + il;
+  const bool act = il < L.count && g.active[gi];
+  const double4 pi = act ? g.pos[gi] : make_double4(0., 0., 0., 1.);
+  const double hi2 = pi.w * pi.w;
+  const double hv = act ? g.hinv[gi] : 1.;
+  double ax = 0., ay = 0., az = 0., pot = 0.;
+  unsigned long long nint = 0;
+  for (int qb = p0; qb < p1;) {
+    // lane q < 32 reads entry qb + q: its source leaf, flags, the batch prefix
+    int cnt = 0, jst = 0, jl = 0;
+    bool tr = false, am = false;
+    if (lane < 32 && qb + lane < p1) {
+      const swh_leaf_pair pr = pairs[qb + lane];
+      const swh_leaf J = leaves[pr.j];
+      cnt = J.count;
+      jst = J.start;
+      jl = pr.j;
+      tr = pr.truncated != 0;
+      am = pr.allow_mpole && J.count > 1;
+    }
+    const int inc = wave_incl_scan(cnt);
+    // the batch: the entries whose gparts fit the tile (a prefix). A source
+    // larger than the tile (a split cell of a no-cache P-P entry: a
+    // single-gpart cell against a whole cell) is a batch of its own, staged
+    // in tile-sized chunks.
+    const unsigned long long fit = __ballot(cnt > 0 && inc <= kPPBatch);
+    const int B = fit ? __popcll(fit) : 1;
+    const int total = __builtin_amdgcn_readlane(inc, B - 1);
+    const unsigned int tmask = (unsigned int)__ballot(lane < B && tr);
+    unsigned int mmask = 0;  // the entries this i takes through their multipole
+    if (MPOLE) {
+      for (unsigned long long m = __ballot(lane < B && am); m; m &= m - 1) {
+        const int q = __ffsll((long long)m) - 1;
+        const int jq = __builtin_amdgcn_readlane(jl, q);
+        if (act && m2p_accept(mac, mac_source(g.mp[jq]), (float)pi.x, (float)pi.y, (float)pi.z,
+                              (float)pi.w, g.oagn[gi]))
+          mmask |= 1u << q;
+      }
+    }
+    for (int jb = 0; jb < total; jb += kPPBatch) {
+      const int tn = min(kPPBatch, total - jb);
+      wave_sync();  // the previous tile's readers are done
+      if (lane < B) {
+        boff[lane] = inc - cnt;
+        bstart[lane] = jst;
+      }
+      wave_sync();
+      for (int k = lane; k < tn; k += 64) {
+        const int e = jb + k;  // the batch's e-th gpart
+        int b = 0;  // its entry: the largest b with boff[b] <= e
+        for (int st = 16; st > 0; st >>= 1)
+          if (b + st < B && boff[b + st] <= e) b += st;
+        const int gj = bstart[b] + (e - boff[b]);
+        const double4 p = g.pos[gj];
+        sx[k] = p.x;
+        sy[k] = p.y;
+        sz[k] = p.z;
+        se2[k] = p.w * p.w;
+        sh[k] = g.hinv[gj];
+        sm[k] = g.mass[gj];
+        sg[k] = gj;
+        sb[k] = (unsigned char)b;
+      }
+      wave_sync();
+      for (int t = s; t < tn; t += lpi) {
+        const int b = sb[t];
+        const bool use = act && !((mmask >> b) & 1u) && sg[t] != gi;
+        nint += use ? 1ull : 0ull;
+        double dx = sx[t] - pi.x, dy = sy[t] - pi.y, dz = sz[t] - pi.z;
+        if (periodic) {
+          dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
+          dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
+          dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
+        }
+        const double mass = use ? (double)sm[t] : 0.;
+        if ((tmask >> b) & 1u)
+          p2p_pair<true>(dx, dy, dz, hi2, se2[t], hv, sh[t], mass, r_s_inv, ax, ay, az, pot);
+        else
+          p2p_pair<false>(dx, dy, dz, hi2, se2[t], hv, sh[t], mass, r_s_inv, ax, ay, az, pot);
+      }
+    }
+    qb += B;
+  }
+  for (int o = 1; o < lpi; o <<= 1) {  // combine the LPI lanes of each i
+    ax += __shfl_xor(ax, o);
+    ay += __shfl_xor(ay, o);
+    az += __shfl_xor(az, o);
+    pot += __shfl_xor(pot, o);
+  }
+  if (act && s == 0) {
+    double4 a = g.acc[gi];
+    a.x += ax;
+    a.y += ay;
+    a.z += az;
+    a.w += pot;
+    g.acc[gi] = a;
+  }
+  if (counter) {
+    for (int o = 32; o > 0; o >>= 1) nint += __shfl_xor(nint, o);
+    if (lane == 0 && nint) atomicAdd(counter, nint);
+  }
+}
+
 // fp32 mode (SWH_PRECISION_F32): the reference's own float arithmetic,
 // operation by operation (gravity_iact.h), for parity with the float runner.
 __global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
@@ -913,8 +1049,8 @@ swh_status launch_pp(swh_gspace* g, const swh_grav_params* G, const MacParams& m
     // the multipole-free instance keeps the P2P kernel's register budget;
     // small leaves (a deep tree) take one wave per i-leaf
     const bool small = g->max_leaf <= 64;
-    auto k = g->any_mpole ? (small ? p2p_small_kernel<true> : p2p_kernel<true, kGravBlock, kIPer>)
-                          : (small ? p2p_small_kernel<false> : p2p_kernel<false, kGravBlock, kIPer>);
+    auto k = g->any_mpole ? (small ? p2p_batch_kernel<true> : p2p_kernel<true, kGravBlock, kIPer>)
+                          : (small ? p2p_batch_kernel<false> : p2p_kernel<false, kGravBlock, kIPer>);
     hipLaunchKernelGGL(k, dim3(g->nleaves), dim3(small ? 64 : kGravBlock), 0, g->stream,
                        gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
                        g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],

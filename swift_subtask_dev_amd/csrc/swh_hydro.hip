@@ -436,6 +436,8 @@ __device__ __forceinline__ void ghost_part(SoA& a, int i, float* left, float* ri
       right[i] = rgt;
       redo_out = true;
       hf_out = hf;
+      // the rerun walks i's list only while the new H fits its reach
+      stale = list_reach && (double)hf * (double)kGamma > (double)list_reach[i];
       return;
     } else if (hf <= gp.h_min) {
       h_final = (T)gp.h_min;
@@ -499,7 +501,8 @@ template <typename T>
 __global__ __launch_bounds__(1024) void ghost_kernel(
     SoA a, const int* __restrict__ list, int count, int max_active_bin, int* __restrict__ redo,
     int* __restrict__ nredo, float* left, float* right, GhostParams gp, unsigned int* hmax_bits,
-    const float* __restrict__ list_reach, unsigned int* list_stale) {
+    const float* __restrict__ list_reach, unsigned int* list_stale,
+    unsigned int* __restrict__ nstale_redo) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   bool rd = false, stale = false;
   float hf = 0.f;
@@ -517,6 +520,11 @@ __global__ __launch_bounds__(1024) void ghost_kernel(
   // one append per block for the rerun list
   const int slot = block_append(rd, nredo);
   if (rd) redo[slot] = i;
+  // reruns whose new H outgrew their list reach (they would need the
+  // wave-per-particle search): one conditional atomic per wave
+  const unsigned long long ms = __ballot(rd && stale);
+  if ((threadIdx.x & 63) == 0 && ms) atomicAdd(nstale_redo, (unsigned int)__popcll(ms));
+  stale = stale && !rd;  // converged particles: their loops' lists
   // h max and the stale flag: an atomic only when it changes something (all
   // blocks hitting one address serialise at ~10 ns per atomic)
   float m = hf;
@@ -657,6 +665,8 @@ static unsigned int* rwrap_slot(swh_space* s) { return s->counters.as<unsigned i
 // u32[20]: the ghost reruns' search-queue length
 constexpr float kGhostListSkin = 0.01f;
 static unsigned int* search_slot(swh_space* s) { return s->counters.as<unsigned int>() + 20; }
+// u32[22]: the ghost pass's reruns whose new H outgrew their list reach
+static unsigned int* stale_redo_slot(swh_space* s) { return s->counters.as<unsigned int>() + 22; }
 // (u32[19]: the drift's displacement, u32[21]: max |v_full|, swh_space.hip)
 // u32[24]: kept lists found stale by the device check; u32[25]: displacement
 // since the list build (float bits); u32[26]: list builds run on the device;
@@ -933,27 +943,35 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   for (; count > 0 && it < P->max_smoothing_iterations; it++) {
     const float* lreach = (lists && s->list_valid) ? s->nbr_reach.as<const float>() : nullptr;
     SWH_HIP(hipMemsetAsync(cnt + 1, 0, sizeof(int), st));
+    SWH_HIP(hipMemsetAsync(stale_redo_slot(s), 0, sizeof(unsigned int), st));
     const int g = (count + block - 1) / block;
     if (s->ctx->precision == SWH_PRECISION_F64)
       hipLaunchKernelGGL(ghost_kernel<double>, dim3(g), dim3(block), 0, st, soa_of(s), list,
                          count, P->max_active_bin, list2, cnt + 1, s->ghost_left.as<float>(),
-                         s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s));
+                         s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s),
+                         stale_redo_slot(s));
     else
       hipLaunchKernelGGL(ghost_kernel<float>, dim3(g), dim3(block), 0, st, soa_of(s), list,
                          count, P->max_active_bin, list2, cnt + 1, s->ghost_left.as<float>(),
-                         s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s));
+                         s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s),
+                         stale_redo_slot(s));
     SWH_HIP(hipGetLastError());
+    unsigned int nstale = 0;
     SWH_HIP(hipMemcpyAsync(&count, cnt + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+    SWH_HIP(hipMemcpyAsync(&nstale, stale_redo_slot(s), sizeof(nstale), hipMemcpyDeviceToHost, st));
     SWH_HIP(hipStreamSynchronize(st));
     // the new rerun list becomes the input; the old input buffer is reused
     int* done = list ? list : spare;
     list = list2;
     list2 = done;
-    if (count > 0 && lists && (int64_t)count * 8 >= n) {
-      // A large rerun (the first iteration after a drift redoes nearly every
-      // particle): rebuild the lists for the new h, with a 1% skin so the
-      // few later iterations' changes stay within reach and the gradient /
-      // force loops keep them, then walk.
+    const bool many = s->list_valid ? (int64_t)nstale * 8 >= n : (int64_t)count * 8 >= n;
+    if (count > 0 && lists && many) {
+      // Many reruns whose new H outgrew their list reach (the first iteration
+      // after a drift with exact lists: every growing h): rebuild the lists
+      // for the new h, with a 1% skin so the few later iterations' changes
+      // stay within reach and the gradient / force loops keep them, then
+      // walk. Lists built with a skin (swh_tuning.list_skin) usually cover
+      // the reruns: they walk the lists, the few outgrown ones are searched.
       SWH_TRY(build_lists(s, P, false, std::max(s->tuning.list_skin, kGhostListSkin)));
       SWH_HIP(hipMemsetAsync(stale_slot(s), 0, sizeof(unsigned int), st));
     }

@@ -254,71 +254,139 @@ __global__ void gpack_kernel(GLayout L, char* __restrict__ aos, int64_t n, GSoA 
 
 // runner_iact_grav_pp_full / _truncated (gravity_iact.h:47-135) for one
 // pair, fp64: h2 = max(eps_i^2, eps_j^2), h_inv = min(1/eps_i, 1/eps_j).
-template <bool TRUNC>
-__device__ __forceinline__ void p2p_pair(double dx, double dy, double dz, double e2i, double e2j,
-                                         double hvi, double hvj, double mass, double r_s_inv,
-                                         double& ax, double& ay, double& az, double& pot) {
-  // The pair's softening is the larger of the two (h2 = max(eps_i^2, eps_j^2),
-  // h_inv = min(1/eps_i, 1/eps_j)); r2 >= h2 is tested as two compares and
-  // h_inv formed only for softened pairs -- fmax/fmin of doubles canonicalize
-  // both operands (three v_max_f64 each), a quarter of the pair's fp64 work.
-  const double r2 = fma(dx, dx, fma(dy, dy, dz * dz));
-  const double r_inv = rsqrt1_f64(r2 + (double)FLT_MIN);
-  double f_ij, pot_ij;
-  if ((r2 >= e2i) & (r2 >= e2j)) {
-    const double mr = mass * r_inv;
-    f_ij = mr * (r_inv * r_inv);
-    pot_ij = -mr;
-  } else {
-    const double h_inv = hvj < hvi ? hvj : hvi;
-    const double ui = r2 * r_inv * h_inv;
-    const double mh = mass * h_inv;
-    f_ij = mh * (h_inv * h_inv) * grav_force_eval(ui);
-    pot_ij = mh * grav_pot_eval(ui);
-  }
-  if (TRUNC) {
-    const double x = 2. * (r2 * r_inv * r_s_inv);
-    const double exp_x = exp(x);
-    const double alpha = rcp_f64(1. + exp_x);
-    const double corr_pot = 2. * (1. - alpha * exp_x);
-    const double corr_f = 2. * fma(fma(1. - alpha, x, -exp_x), alpha, 1.);
-    f_ij *= corr_f;
-    pot_ij *= corr_pot;
-  }
-  ax = fma(f_ij, dx, ax);
-  ay = fma(f_ij, dy, ay);
-  az = fma(f_ij, dz, az);
-  pot += pot_ij;
+//
+// Split in three so the common case runs branch-free: p2p_newton gives the
+// unsoftened terms of every pair; p2p_soften replaces them for the pairs
+// inside the larger softening (h2 = max(eps_i^2, eps_j^2), h_inv =
+// min(1/eps_i, 1/eps_j)), which the callers reach only when a lane of the
+// wave has r2 below the tile's largest h2 (emax = max(h2_i, max_j h2_j): one
+// compare per pair instead of two, no divergent branch); p2p_trunc applies
+// the long-range truncation. FLT_MIN joins the r2 sum (r2 + FLT_MIN == r2 in
+// fp64 for every r2 above 1e-22, so the softening test is unchanged).
+__device__ __forceinline__ void p2p_newton(double dx, double dy, double dz, double mass,
+                                           double& r2, double& r_inv, double& f_ij,
+                                           double& pot_ij) {
+  r2 = fma(dx, dx, fma(dy, dy, fma(dz, dz, (double)FLT_MIN)));
+  r_inv = rsqrt1_f64(r2);
+  const double mr = mass * r_inv;
+  f_ij = mr * (r_inv * r_inv);
+  pot_ij = -mr;
+}
+__device__ __forceinline__ void p2p_soften(double r2, double r_inv, double e2i, double e2j,
+                                           double hvi, double hvj, double mass, double& f_ij,
+                                           double& pot_ij) {
+  if ((r2 >= e2i) & (r2 >= e2j)) return;
+  const double h_inv = hvj < hvi ? hvj : hvi;
+  const double ui = r2 * r_inv * h_inv;
+  const double mh = mass * h_inv;
+  f_ij = mh * (h_inv * h_inv) * grav_force_eval(ui);
+  pot_ij = mh * grav_pot_eval(ui);
+}
+// exp(-x) for x >= 0 (the truncation's argument, a finite distance ratio):
+// Cody-Waite reduction by ln 2 (fdlibm's split) and a degree-11 Taylor
+// polynomial on |f| <= ln2/2, ~6e-15 relative; no overflow / NaN handling,
+// so it is 16 instructions where the library exp takes ~30.
+// (Horner steps as three-operand v_fma_f64: the compiler otherwise copies
+// each loop-invariant coefficient register before a two-operand v_fmac_f64,
+// a move per term.)
+__device__ __forceinline__ double fma3(double a, double b, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+template <bool FMA3>
+__device__ __forceinline__ double horner_step(double p, double f, double c) {
+  return FMA3 ? fma3(p, f, c) : fma(p, f, c);
+}
+// FMA3: the three-operand form (the batch kernel, whose registers hold the
+// coefficients; the 256-thread tile kernel keeps fma and its register budget)
+template <bool FMA3>
+__device__ __forceinline__ double exp_neg_f64(double x) {
+  const double k = __builtin_rint(x * -1.4426950408889634);  // -x / ln 2
+  const double f = fma(k, -1.90821492927058770002e-10, fma(k, -6.93147180369123816490e-01, -x));
+  double p = horner_step<FMA3>(1. / 39916800., f, 1. / 3628800.);
+  p = horner_step<FMA3>(p, f, 1. / 362880.);
+  p = horner_step<FMA3>(p, f, 1. / 40320.);
+  p = horner_step<FMA3>(p, f, 1. / 5040.);
+  p = horner_step<FMA3>(p, f, 1. / 720.);
+  p = horner_step<FMA3>(p, f, 1. / 120.);
+  p = horner_step<FMA3>(p, f, 1. / 24.);
+  p = horner_step<FMA3>(p, f, 1. / 6.);
+  p = fma(p, f, 0.5);
+  p = fma(p, f, 1.);
+  p = fma(p, f, 1.);
+  return __builtin_ldexp(p, (int)k);
+}
+
+// The long-range truncation of kernel_long_grav_eval (kernel_long_gravity.h:
+// 160-190): with alpha = 1 / (1 + e^x), x = 2 r / r_s, the reference's
+// corr_pot = 2 (1 - alpha e^x) and corr_f = 2 (1 + alpha ((1 - alpha) x -
+// e^x)) are, since alpha e^x = 1 - alpha, 2 alpha and 2 alpha (1 + (1 -
+// alpha) x); alpha = E / (1 + E) from E = e^-x never overflows. tworsi =
+// 2 / r_s.
+template <bool FMA3 = false>
+__device__ __forceinline__ void p2p_trunc(double r2, double r_inv, double tworsi, double& f_ij,
+                                          double& pot_ij) {
+  const double x = r2 * r_inv * tworsi;
+  const double E = exp_neg_f64<FMA3>(x);
+  const double a2 = 2. * E * rcp1_f64(1. + E);  // 2 alpha
+  pot_ij *= a2;
+  f_ij *= a2 * fma(1. - 0.5 * a2, x, 1.);
+}
+
+// Nearest periodic image of a separation (|d| < 1.5 box): d - box rint(d /
+// box), the same image as nearestf's branches (periodic.h:84-90) but three
+// fp64 operations instead of two compares, two adds and four selects.
+__device__ __forceinline__ double nearest_rint(double d, double box, double ibox) {
+  return fma(-box, __builtin_rint(d * ibox), d);
 }
 
 // One LDS tile against this thread's IPER i-particles: every j entry is read
 // once and used IPER times. SELF: the tile may hold an i itself (the
-// i-leaf's own leaf), whose term is removed by a zero mass.
-template <bool TRUNC, bool PERIODIC, bool SELF, int IPER>
+// i-leaf's own leaf), whose term is removed by a zero mass. MASK: the
+// per-source activity act[k] (M2P takers) zeroes masses; without it every
+// lane computes and the caller discards inactive i's. emax[k] = max(h2_i,
+// the tile's largest h2_j): pairs at or beyond it are unsoftened.
+template <bool TRUNC, bool PERIODIC, bool SELF, bool MASK, int IPER>
 __device__ __forceinline__ void p2p_tile(const double* sx, const double* sy, const double* sz,
                                          const double* se2, const double* sh, const float* sm,
                                          int nt, const int* self_local, const double* xi,
                                          const double* yi, const double* zi, const double* hi2,
-                                         const double* hv, const bool* act, double dimx,
-                                         double dimy, double dimz, double r_s_inv, double* ax,
-                                         double* ay, double* az, double* pot) {
+                                         const double* emax, const double* hv, const bool* act,
+                                         double dimx, double dimy, double dimz, double tworsi,
+                                         double* ax, double* ay, double* az, double* pot) {
+  const double idimx = 1. / dimx, idimy = 1. / dimy, idimz = 1. / dimz;
   for (int t = 0; t < nt; t++) {
-    const double xj = sx[t], yj = sy[t], zj = sz[t], e2j = se2[t], hvj = sh[t];
+    const double xj = sx[t], yj = sy[t], zj = sz[t];
     const double mj = (double)sm[t];
 #pragma unroll
     for (int k = 0; k < IPER; k++) {
       double dx = xj - xi[k], dy = yj - yi[k], dz = zj - zi[k];
       if (PERIODIC) {
-        dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
-        dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
-        dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
+        dx = nearest_rint(dx, dimx, idimx);
+        dy = nearest_rint(dy, dimy, idimy);
+        dz = nearest_rint(dz, dimz, idimz);
       }
-      double mass = act[k] ? mj : 0.;
-      if (SELF) mass = t == self_local[k] ? 0. : mass;  // j == i: no term
-      p2p_pair<TRUNC>(dx, dy, dz, hi2[k], e2j, hv[k], hvj, mass, r_s_inv, ax[k],
-                      ay[k], az[k], pot[k]);
+      double ms = mj;
+      if (MASK) ms = act[k] ? ms : 0.;
+      if (SELF) ms = t == self_local[k] ? 0. : ms;  // j == i: no term
+      double r2, ri, f, pt;
+      p2p_newton(dx, dy, dz, ms, r2, ri, f, pt);
+      if (__builtin_expect(__any(r2 < emax[k]), 0))
+        if (r2 < emax[k]) p2p_soften(r2, ri, hi2[k], se2[t], hv[k], sh[t], ms, f, pt);
+      if (TRUNC) p2p_trunc(r2, ri, tworsi, f, pt);
+      ax[k] = fma(f, dx, ax[k]);
+      ay[k] = fma(f, dy, ay[k]);
+      az[k] = fma(f, dz, az[k]);
+      pot[k] += pt;
     }
   }
+}
+
+// Largest value over a wave (lanes without one pass 0).
+__device__ __forceinline__ double wave_max_f64(double v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
 }
 
 // Per pair: which of this thread's i-particles take the source leaf's
@@ -349,13 +417,14 @@ __device__ __forceinline__ void mpole_mask(const GSoA& g, const MacParams& P,
 // the ~400-particle leaves of space_splitsize, 64 x 1 for the small leaves of
 // a deep tree (cell_split_size 50), so the lanes are not left idle.
 template <bool MPOLE, int BLK, int IPER>
-__global__ __launch_bounds__(BLK) void p2p_kernel(
+__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(MPOLE ? 3 : 4))) void p2p_kernel(
     GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
     const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
     double dimz, double r_s_inv, MacParams mac, unsigned long long* counter) {
   __shared__ double sx[BLK], sy[BLK], sz[BLK], se2[BLK],
       sh[BLK];
   __shared__ float sm[BLK];
+  __shared__ double swmax[BLK / 64];  // per wave: the largest staged h2
   const int li = xcd_block_id();
   const swh_leaf L = leaves[li];
   const int p0 = pair_off[li], p1 = pair_off[li + 1];
@@ -392,29 +461,38 @@ __global__ __launch_bounds__(BLK) void p2p_kernel(
       for (int jbase = 0; jbase < J.count; jbase += BLK) {
         const int nt = min(BLK, J.count - jbase);
         __syncthreads();
+        double e2 = 0.;
         if ((int)threadIdx.x < nt) {
           const int gj = J.start + jbase + (int)threadIdx.x;
           const double4 p = g.pos[gj];
           sx[threadIdx.x] = p.x;
           sy[threadIdx.x] = p.y;
           sz[threadIdx.x] = p.z;
-          se2[threadIdx.x] = p.w * p.w;
+          e2 = p.w * p.w;
+          se2[threadIdx.x] = e2;
           sh[threadIdx.x] = g.hinv[gj];
           sm[threadIdx.x] = g.mass[gj];
         }
+        e2 = wave_max_f64(e2);
+        if ((threadIdx.x & 63) == 0) swmax[threadIdx.x / 64] = e2;
         __syncthreads();
+        double tmax = swmax[0];
+#pragma unroll
+        for (int w = 1; w < BLK / 64; w++) tmax = fmax(tmax, swmax[w]);
+        double emax[IPER];
         // the i-leaf's own particles can only sit in a tile of a leaf range
         // overlapping it (block-uniform test)
         const bool self = J.start + jbase < L.start + L.count && L.start < J.start + jbase + nt;
 #pragma unroll
         for (int k = 0; k < IPER; k++) {
+          emax[k] = act[k] ? fmax(hi2[k], tmax) : 0.;  // (inactive lanes: discarded)
           self_local[k] = gi[k] - (J.start + jbase);
           if (actp[k])
             nint += (unsigned long long)(nt - ((self_local[k] >= 0 && self_local[k] < nt) ? 1 : 0));
         }
 #define SWH_P2P_TILE(TR, PE, SE)                                                             \
-  p2p_tile<TR, PE, SE, IPER>(sx, sy, sz, se2, sh, sm, nt, self_local, xi, yi, zi, hi2, hv, actp, dimx, \
-                       dimy, dimz, r_s_inv, ax, ay, az, pot)
+  p2p_tile<TR, PE, SE, MPOLE, IPER>(sx, sy, sz, se2, sh, sm, nt, self_local, xi, yi, zi, hi2, \
+                                    emax, hv, actp, dimx, dimy, dimz, 2. * r_s_inv, ax, ay, az, pot)
         if (self) {
           if (pr.truncated) {
             if (periodic) SWH_P2P_TILE(true, true, true);
@@ -452,110 +530,28 @@ __global__ __launch_bounds__(BLK) void p2p_kernel(
   }
 }
 
-// Small i-leaves (every leaf <= 64 gparts: a deep tree, cell_split_size 50):
-// one wave per i-leaf with LPI = 64 / (count rounded up to a power of two)
-// lanes per i-particle (up to 8), lane s of i taking tile entries s, s + LPI,
-// ..., the LPI partial sums combined by shuffles at the end, so a 12-gpart
-// leaf keeps 48 lanes busy instead of 12. Sources stream through a 64-entry
-// LDS tile per wave; the M2P mask is evaluated per i as in p2p_kernel.
-template <bool MPOLE>
-__global__ __launch_bounds__(64) void p2p_small_kernel(
-    GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
-    const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
-    double dimz, double r_s_inv, MacParams mac, unsigned long long* counter) {
-  __shared__ double sx[64], sy[64], sz[64], se2[64], sh[64];
-  __shared__ float sm[64];
-  const int li = xcd_block_id();
-  const swh_leaf L = leaves[li];
-  const int p0 = pair_off[li], p1 = pair_off[li + 1];
-  if (p0 == p1) return;  // (inner cells overlap their leaves: leave acc alone)
-  const int lane = (int)threadIdx.x;
-  int lpi = 1;  // wave-uniform
-  while (lpi < 8 && L.count * lpi * 2 <= 64) lpi *= 2;
-  const int il = lane / lpi, s = lane % lpi;
-  const int gi = L.start + il;
-  const bool act = il < L.count && g.active[gi];
-  const double4 pi = act ? g.pos[gi] : make_double4(0., 0., 0., 1.);
-  const double hi2 = pi.w * pi.w;
-  const double hv = act ? g.hinv[gi] : 1.;
-  double ax = 0., ay = 0., az = 0., pot = 0.;
-  unsigned long long nint = 0;
-  for (int q = p0; q < p1; q++) {
-    const swh_leaf_pair pr = pairs[q];
-    const swh_leaf J = leaves[pr.j];
-    bool actp = act;
-    if (MPOLE && pr.allow_mpole && J.count > 1 && act)
-      actp = !m2p_accept(mac, mac_source(g.mp[pr.j]), (float)pi.x, (float)pi.y, (float)pi.z,
-                         (float)pi.w, g.oagn[gi]);
-    for (int jbase = 0; jbase < J.count; jbase += 64) {
-      const int nt = min(64, J.count - jbase);
-      wave_sync();
-      if (lane < nt) {
-        const int gj = J.start + jbase + lane;
-        const double4 p = g.pos[gj];
-        sx[lane] = p.x;
-        sy[lane] = p.y;
-        sz[lane] = p.z;
-        se2[lane] = p.w * p.w;
-        sh[lane] = g.hinv[gj];
-        sm[lane] = g.mass[gj];
-      }
-      wave_sync();
-      const int self_local = gi - (J.start + jbase);  // i itself: no term
-      const bool has_self = self_local >= 0 && self_local < nt;
-      if (actp) nint += (unsigned long long)(nt - (has_self ? 1 : 0));
-      if (!__any(actp)) continue;
-      for (int t = s; t < nt; t += lpi) {
-        double dx = sx[t] - pi.x, dy = sy[t] - pi.y, dz = sz[t] - pi.z;
-        if (periodic) {
-          dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
-          dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
-          dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
-        }
-        const double mass = (actp && t != self_local) ? (double)sm[t] : 0.;
-        if (pr.truncated)
-          p2p_pair<true>(dx, dy, dz, hi2, se2[t], hv, sh[t], mass, r_s_inv, ax, ay,
-                         az, pot);
-        else
-          p2p_pair<false>(dx, dy, dz, hi2, se2[t], hv, sh[t], mass, r_s_inv, ax, ay,
-                          az, pot);
-      }
-    }
-  }
-  for (int o = 1; o < lpi; o <<= 1) {  // combine the LPI lanes of each i
-    ax += __shfl_xor(ax, o);
-    ay += __shfl_xor(ay, o);
-    az += __shfl_xor(az, o);
-    pot += __shfl_xor(pot, o);
-  }
-  if (act && s == 0) {
-    double4 a = g.acc[gi];
-    a.x += ax;
-    a.y += ay;
-    a.z += az;
-    a.w += pot;
-    g.acc[gi] = a;
-  }
-  if (counter) {
-    if (s != 0) nint = 0;  // each i's pairs counted once
-    for (int o = 32; o > 0; o >>= 1) nint += __shfl_xor(nint, o);
-    if (lane == 0 && nint) atomicAdd(counter, nint);
-  }
-}
-
-// Small i-leaves with batched sources: one wave per i-leaf, lpi lanes per
-// i-particle as p2p_small_kernel, but the gparts of up to 32 consecutive P-P
-// entries (up to kPPBatch of them) are gathered into the LDS tile at once:
-// the chain of dependent loads (entry -> source leaf -> its gparts) and the
-// two wave barriers are paid once per batch, not once per source leaf. In a
-// cosmological tree (cell_split_size 50, ~16 gparts per leaf, ~300 source
-// leaves per i-leaf under the adaptive MAC) the per-entry chain left the
-// wave waiting on memory for most of its time. Each entry's truncation and
-// M2P acceptance become bits (tmask: truncated entries; mmask, per i: the
-// entries whose multipole this i takes instead, m2p_accept as in
-// mpole_mask); the self term is removed by comparing gpart indices. Sources
-// larger than the tile (no-cache entries against a whole cell) are staged in
-// tile-sized chunks, every LDS index stays below kPPBatch.
+// Small i-leaves (every leaf <= 64 gparts: a deep tree, cell_split_size 50)
+// with batched sources: one wave per i-leaf, LPI = 64 / (count rounded up to
+// a power of two) lanes per i-particle (up to 8), lane s of i taking tile
+// entries s, s + LPI, ... (the LPI partial sums combined by shuffles at the
+// end, so a 12-gpart leaf keeps 48 lanes busy instead of 12). The gparts of
+// up to 32 consecutive P-P entries (up to kPPBatch of them) are gathered into
+// the LDS tile at once: the chain of dependent loads (entry -> source leaf ->
+// its gparts) and the wave barriers are paid once per batch, not once per
+// source leaf (a cosmological tree has ~16 gparts per leaf and ~300 source
+// leaves per i-leaf under the adaptive MAC). Each entry's truncation and M2P
+// acceptance become bits (tmask: truncated entries; mmask, per i: the entries
+// whose multipole this i takes instead, m2p_accept as in mpole_mask); the
+// self term is removed by comparing gpart indices. Sources larger than the
+// tile (no-cache entries against a whole cell) are staged in tile-sized
+// chunks, every LDS index stays below kPPBatch.
+//
+// Periodic boxes: the staging shifts each source gpart to its image nearest
+// the i-leaf's first gpart c. With e the i-leaf's extent around c, a staged
+// source within L/2 - e of c (every dimension) is then the nearest image for
+// every i of the leaf, so the pair loop needs no wrap; a tile holding any
+// source past that bound (a pair separation near L/2: top-level cells of a
+// tiny box) wraps every pair (nearest_rint), as nearestf does.
 constexpr int kPPBatch = 256;
 
 template <bool MPOLE>
@@ -581,8 +577,27 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
   const double4 pi = act ? g.pos[gi] : make_double4(0., 0., 0., 1.);
   const double hi2 = pi.w * pi.w;
   const double hv = act ? g.hinv[gi] : 1.;
+  const double tworsi = 2. * r_s_inv;
+  const double idimx = 1. / dimx, idimy = 1. / dimy, idimz = 1. / dimz;
+  // periodic: the i-leaf's first gpart c and the leaf's extent around it
+  double cx = 0., cy = 0., cz = 0., lim_x = 0., lim_y = 0., lim_z = 0.;
+  if (periodic) {
+    const double4 c = g.pos[L.start];
+    cx = c.x;
+    cy = c.y;
+    cz = c.z;
+    double e = 0.;
+    if (il < L.count) {
+      const double4 q = g.pos[gi];
+      e = fmax(fabs(q.x - cx), fmax(fabs(q.y - cy), fabs(q.z - cz)));
+    }
+    e = wave_max_f64(e);
+    lim_x = 0.5 * dimx * (1. - 1e-12) - e;
+    lim_y = 0.5 * dimy * (1. - 1e-12) - e;
+    lim_z = 0.5 * dimz * (1. - 1e-12) - e;
+  }
   double ax = 0., ay = 0., az = 0., pot = 0.;
-  unsigned long long nint = 0;
+  unsigned int nint = 0;
   for (int qb = p0; qb < p1;) {
     // lane q < 32 reads entry qb + q: its source leaf, flags, the batch prefix
     int cnt = 0, jst = 0, jl = 0;
@@ -615,6 +630,8 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
           mmask |= 1u << q;
       }
     }
+    // per i: the entries it takes by P2P (inactive i: none)
+    const unsigned int pmask = act ? ~mmask : 0u;
     for (int jb = 0; jb < total; jb += kPPBatch) {
       const int tn = min(kPPBatch, total - jb);
       wave_sync();  // the previous tile's readers are done
@@ -623,6 +640,8 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
         bstart[lane] = jst;
       }
       wave_sync();
+      double e2max = 0.;
+      bool far = false;
       for (int k = lane; k < tn; k += 64) {
         const int e = jb + k;  // the batch's e-th gpart
         int b = 0;  // its entry: the largest b with boff[b] <= e
@@ -630,31 +649,48 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
           if (b + st < B && boff[b + st] <= e) b += st;
         const int gj = bstart[b] + (e - boff[b]);
         const double4 p = g.pos[gj];
-        sx[k] = p.x;
-        sy[k] = p.y;
-        sz[k] = p.z;
+        double px = p.x, py = p.y, pz = p.z;
+        if (periodic) {
+          // (no shift: the position itself, bit for bit)
+          px = fma(-dimx, __builtin_rint((px - cx) * idimx), px);
+          py = fma(-dimy, __builtin_rint((py - cy) * idimy), py);
+          pz = fma(-dimz, __builtin_rint((pz - cz) * idimz), pz);
+          far |= (fabs(px - cx) > lim_x) | (fabs(py - cy) > lim_y) | (fabs(pz - cz) > lim_z);
+        }
+        sx[k] = px;
+        sy[k] = py;
+        sz[k] = pz;
         se2[k] = p.w * p.w;
+        e2max = fmax(e2max, p.w * p.w);
         sh[k] = g.hinv[gj];
         sm[k] = g.mass[gj];
         sg[k] = gj;
         sb[k] = (unsigned char)b;
       }
+      const double emax = act ? fmax(hi2, wave_max_f64(e2max)) : 0.;
+      const bool wrap = periodic && __any(far);
       wave_sync();
       for (int t = s; t < tn; t += lpi) {
         const int b = sb[t];
-        const bool use = act && !((mmask >> b) & 1u) && sg[t] != gi;
-        nint += use ? 1ull : 0ull;
+        const bool use = ((pmask >> b) & 1u) & (sg[t] != gi);
+        nint += use;
         double dx = sx[t] - pi.x, dy = sy[t] - pi.y, dz = sz[t] - pi.z;
-        if (periodic) {
-          dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
-          dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
-          dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
+        if (wrap) {
+          dx = nearest_rint(dx, dimx, idimx);
+          dy = nearest_rint(dy, dimy, idimy);
+          dz = nearest_rint(dz, dimz, idimz);
         }
-        const double mass = use ? (double)sm[t] : 0.;
-        if ((tmask >> b) & 1u)
-          p2p_pair<true>(dx, dy, dz, hi2, se2[t], hv, sh[t], mass, r_s_inv, ax, ay, az, pot);
-        else
-          p2p_pair<false>(dx, dy, dz, hi2, se2[t], hv, sh[t], mass, r_s_inv, ax, ay, az, pot);
+        const float mf = sm[t];
+        const double mass = (double)(use ? mf : 0.f);
+        double r2, r_inv, f_ij, pot_ij;
+        p2p_newton(dx, dy, dz, mass, r2, r_inv, f_ij, pot_ij);
+        if (__builtin_expect(__any(r2 < emax), 0))
+          if (r2 < emax) p2p_soften(r2, r_inv, hi2, se2[t], hv, sh[t], mass, f_ij, pot_ij);
+        if ((tmask >> b) & 1u) p2p_trunc<true>(r2, r_inv, tworsi, f_ij, pot_ij);
+        ax = fma(f_ij, dx, ax);
+        ay = fma(f_ij, dy, ay);
+        az = fma(f_ij, dz, az);
+        pot += pot_ij;
       }
     }
     qb += B;
@@ -674,8 +710,9 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
     g.acc[gi] = a;
   }
   if (counter) {
-    for (int o = 32; o > 0; o >>= 1) nint += __shfl_xor(nint, o);
-    if (lane == 0 && nint) atomicAdd(counter, nint);
+    unsigned long long n = nint;
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+    if (lane == 0 && n) atomicAdd(counter, n);
   }
 }
 
@@ -780,7 +817,7 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
 // same stream (both add into acc).
 // SMALL (every leaf <= 64 gparts, one wave per leaf): LPI lanes per i split
 // the leaf's source list (lane s takes entries s, s + LPI, ...) and combine
-// their sums, as p2p_small_kernel does.
+// their sums, as p2p_batch_kernel does.
 template <typename T, bool SMALL>
 __global__ __launch_bounds__(kGravBlock) void m2p_kernel(
     GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,

@@ -10,6 +10,7 @@
 // step's pair lists (swh_list.h); particles the lists do not cover (list
 // overflow, ghost reruns whose h outgrew the list reach) take a
 // wave-per-particle search of the grid cells around them.
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include "swh_gather.h"
@@ -273,12 +274,13 @@ __global__ __launch_bounds__(256) void overflow_kernel(GridDev g, SoA a, ListDev
 // lanes per rerun particle walk its list while its H still fits the list
 // reach; any other one (H grown past its reach, list overflow, no lists) is
 // queued for the wave-per-particle search (overflow_kernel). The subset is the
-// ghost's redo list, in (nearly) sorted order.
+// ghost's redo list (nearly sorted), or its flags in particle order.
 template <typename T>
 __global__ __launch_bounds__(256) void walk_subset_kernel(GridDev g, SoA a, ListDev ld,
                                                           int list_ok,
                                                           const int* __restrict__ subset,
-                                                          int nitems, int max_active_bin,
+                                                          const int8_t* __restrict__ flag,
+                                                          int want, int nitems, int max_active_bin,
                                                           const unsigned int* __restrict__ hmax_bits,
                                                           unsigned long long* counter,
                                                           int* __restrict__ searchq,
@@ -286,7 +288,8 @@ __global__ __launch_bounds__(256) void walk_subset_kernel(GridDev g, SoA a, List
   constexpr int LPI = kWalkLpi;
   const int t = (int)blockIdx.x * (256 / LPI) + (int)threadIdx.x / LPI;
   const int s = (int)threadIdx.x % LPI;
-  const int i = t < nitems ? subset[t] : -1;
+  // the reruns: a compact subset, or (subset null) the particles flagged `want`
+  const int i = t >= nitems ? -1 : subset ? subset[t] : (flag[t] == (int8_t)want ? t : -1);
   bool act = i >= 0 && active_part(a, i, max_active_bin);
   int nl = 0, lb = -1;
   double4 pi = make_double4(0., 0., 0., 0.);
@@ -495,31 +498,49 @@ __device__ __forceinline__ void ghost_part(SoA& a, int i, float* left, float* ri
   a.grad[i] = g;
 }
 
-// One pass of the ghost over `list` (null: the first pass, over every active
-// particle, whose bisection bounds start at [0, h_max]).
+// One pass `it` of the ghost. Its particles: every active one (it = 0, whose
+// bisection bounds start at [0, h_max]), the previous pass's reruns from the
+// compact `list`, or (list null, it > 0) those whose flag holds `it`. The
+// reruns it queues get flag it + 1; pass 0 writes every flag. When `redo` is
+// given they are also appended to it (compaction: one returning atomic per
+// workgroup, which holds the whole workgroup -- used only once the reruns
+// are few); otherwise only counted, and the rerun walks the flags in particle
+// order.
 template <typename T>
 __global__ __launch_bounds__(1024) void ghost_kernel(
-    SoA a, const int* __restrict__ list, int count, int max_active_bin, int* __restrict__ redo,
-    int* __restrict__ nredo, float* left, float* right, GhostParams gp, unsigned int* hmax_bits,
-    const float* __restrict__ list_reach, unsigned int* list_stale,
-    unsigned int* __restrict__ nstale_redo) {
+    SoA a, const int* __restrict__ list, int count, int it, int8_t* __restrict__ flag,
+    int max_active_bin, int* __restrict__ redo, int* __restrict__ nredo, float* left,
+    float* right, GhostParams gp, unsigned int* hmax_bits, const float* __restrict__ list_reach,
+    unsigned int* list_stale, unsigned int* __restrict__ nstale_redo) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   bool rd = false, stale = false;
   float hf = 0.f;
   int i = -1;
   if (t < count) {
-    if (list) {
+    if (it == 0) {
+      if (active_part(a, t, max_active_bin)) {
+        i = t;
+        left[i] = 0.f;
+        right[i] = gp.h_max;
+      }
+    } else if (list) {
       i = list[t];
-    } else if (active_part(a, t, max_active_bin)) {
+    } else if (flag[t] == (int8_t)it) {
       i = t;
-      left[i] = 0.f;
-      right[i] = gp.h_max;
     }
   }
   if (i >= 0) ghost_part<T>(a, i, left, right, gp, list_reach, rd, hf, stale);
-  // one append per block for the rerun list
-  const int slot = block_append(rd, nredo);
-  if (rd) redo[slot] = i;
+  if (it == 0) {
+    if (t < count) flag[t] = rd ? (int8_t)1 : (int8_t)0;
+  } else if (rd) {
+    flag[i] = (int8_t)(it + 1);
+  }
+  if (redo) {
+    const int slot = block_append(rd, nredo);
+    if (rd) redo[slot] = i;
+  } else {
+    block_count(rd, nredo);
+  }
   // reruns whose new H outgrew their list reach (they would need the
   // wave-per-particle search): one conditional atomic per wave
   const unsigned long long ms = __ballot(rd && stale);
@@ -771,8 +792,16 @@ static swh_status check_kept_lists(swh_space* s, const swh_hydro_params* P, bool
   return build_lists(s, P, count, s->tuning.list_skin, keep_stale_slot(s));
 }
 
+// The ghost's reruns (launch_loop's `subset`): a compact list of `nitems`
+// particles, or (list null) the particles among the first `nitems` whose
+// ghost flag is `want`.
+struct Subset {
+  const int* list;
+  int want;
+};
+
 template <int LOOP, typename T>
-static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int nitems,
+static void launch_typed(swh_space* s, const GridDev& gd, const Subset* subset, int nitems,
                          int max_active_bin, T a2H, unsigned long long* ctr, int* ncount) {
   const int block = 256;
   const ListDev ld = list_dev(s);
@@ -780,7 +809,8 @@ static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int
   if (subset) {  // density reruns of the ghost: list walks, then the queued searches
     (void)hipMemsetAsync(search_slot(s), 0, sizeof(unsigned int), s->stream);
     hipLaunchKernelGGL((walk_subset_kernel<T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
-                       s->stream, gd, soa_of(s), ld, s->list_valid ? 1 : 0, subset, nitems,
+                       s->stream, gd, soa_of(s), ld, s->list_valid ? 1 : 0, subset->list,
+                       s->ghost_flag.as<const int8_t>(), subset->want, nitems,
                        max_active_bin, hmax_slot(s), ctr, s->ghost_search.as<int>(),
                        search_slot(s));
     // one wave per queued particle; the queue length is read on the device
@@ -804,7 +834,7 @@ static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int
 }
 
 template <int LOOP>
-static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const int* subset,
+static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const Subset* subset,
                               int nitems, bool count) {
   if (nitems <= 0) return SWH_OK;
   if (!subset && s->ngroups <= 0) return SWH_OK;
@@ -921,10 +951,9 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   SWH_TRY(s->ghost_list.reserve(n * sizeof(int)));
   SWH_TRY(s->ghost_list2.reserve(n * sizeof(int)));
   SWH_TRY(s->ghost_search.reserve(n * sizeof(int)));
+  SWH_TRY(s->ghost_flag.reserve(n * sizeof(int8_t)));
   int* cnt = s->counters.as<int>() + 4;  // slot 5: rerun count
   const int block = 1024;
-  // the first pass runs over every particle (inactive ones return at once)
-  int count = (int)n;
   GhostParams gp;
   gp.h_max = P->h_max;
   gp.h_min = P->h_min;
@@ -934,36 +963,60 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   gp.a2_inv = P->a2_inv;
   gp.H = P->H;
   gp.fac_B = P->a_factor_Balsara_eps;
-  int* list = nullptr;  // first pass: every active particle
-  int* list2 = s->ghost_list.as<int>();
+  // Pass it's particles: every active one (it = 0), then the reruns the pass
+  // before queued -- as flags (ghost_flag == it, the pass and its rerun
+  // running over all n in particle order) while they are many, as a compact
+  // list once the pass's input is at most n/8 (a list pass only appends what
+  // it queues, so its output is small too). The first pass after a drift
+  // queues nearly every particle: compacting 2M reruns through one counter
+  // cost more than walking the flags.
+  int count = (int)n;  // this pass's input size
+  int* list = nullptr;  // this pass's input list (null: flags)
+  int* out = s->ghost_list.as<int>();
   int* spare = s->ghost_list2.as<int>();
   const bool lists = true;
   SWH_HIP(hipMemsetAsync(stale_slot(s), 0, sizeof(unsigned int), st));
+  // profiling only (SWH_GHOST_DEBUG): per iteration the rerun count, the
+  // reruns past their list reach, and the ghost / rebuild / rerun times
+  static const bool dbg = std::getenv("SWH_GHOST_DEBUG") != nullptr;
+  hipEvent_t dev[4] = {nullptr, nullptr, nullptr, nullptr};
+  if (dbg)
+    for (auto& e : dev) SWH_HIP(hipEventCreate(&e));
   int it = 0;
   for (; count > 0 && it < P->max_smoothing_iterations; it++) {
+    if (dbg) SWH_HIP(hipEventRecord(dev[0], st));
     const float* lreach = (lists && s->list_valid) ? s->nbr_reach.as<const float>() : nullptr;
     SWH_HIP(hipMemsetAsync(cnt + 1, 0, sizeof(int), st));
     SWH_HIP(hipMemsetAsync(stale_redo_slot(s), 0, sizeof(unsigned int), st));
+    // output as a list (and always from pass 100 on: the int8 flags stop there)
+    const bool compact = it > 0 && ((int64_t)count * 8 <= n || it >= 100);
+    if (it > 0 && !list) count = (int)n;  // flag input: a pass over every particle
     const int g = (count + block - 1) / block;
+    int* redo = compact ? out : nullptr;
     if (s->ctx->precision == SWH_PRECISION_F64)
       hipLaunchKernelGGL(ghost_kernel<double>, dim3(g), dim3(block), 0, st, soa_of(s), list,
-                         count, P->max_active_bin, list2, cnt + 1, s->ghost_left.as<float>(),
-                         s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s),
-                         stale_redo_slot(s));
+                         count, it, s->ghost_flag.as<int8_t>(), P->max_active_bin, redo,
+                         cnt + 1, s->ghost_left.as<float>(), s->ghost_right.as<float>(), gp,
+                         hmax_slot(s), lreach, stale_slot(s), stale_redo_slot(s));
     else
       hipLaunchKernelGGL(ghost_kernel<float>, dim3(g), dim3(block), 0, st, soa_of(s), list,
-                         count, P->max_active_bin, list2, cnt + 1, s->ghost_left.as<float>(),
-                         s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s),
-                         stale_redo_slot(s));
+                         count, it, s->ghost_flag.as<int8_t>(), P->max_active_bin, redo,
+                         cnt + 1, s->ghost_left.as<float>(), s->ghost_right.as<float>(), gp,
+                         hmax_slot(s), lreach, stale_slot(s), stale_redo_slot(s));
     SWH_HIP(hipGetLastError());
+    if (dbg) SWH_HIP(hipEventRecord(dev[1], st));
+    const int count_in = count;
     unsigned int nstale = 0;
     SWH_HIP(hipMemcpyAsync(&count, cnt + 1, sizeof(int), hipMemcpyDeviceToHost, st));
     SWH_HIP(hipMemcpyAsync(&nstale, stale_redo_slot(s), sizeof(nstale), hipMemcpyDeviceToHost, st));
     SWH_HIP(hipStreamSynchronize(st));
-    // the new rerun list becomes the input; the old input buffer is reused
-    int* done = list ? list : spare;
-    list = list2;
-    list2 = done;
+    if (compact) {  // the new list becomes the input; the old input buffer is reused
+      int* done = list ? list : spare;
+      list = out;
+      out = done;
+    } else {
+      list = nullptr;
+    }
     const bool many = s->list_valid ? (int64_t)nstale * 8 >= n : (int64_t)count * 8 >= n;
     if (count > 0 && lists && many) {
       // Many reruns whose new H outgrew their list reach (the first iteration
@@ -975,8 +1028,25 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
       SWH_TRY(build_lists(s, P, false, std::max(s->tuning.list_skin, kGhostListSkin)));
       SWH_HIP(hipMemsetAsync(stale_slot(s), 0, sizeof(unsigned int), st));
     }
-    if (count > 0) SWH_TRY(launch_loop<LOOP_DENSITY>(s, P, list, count, false));
+    if (dbg) SWH_HIP(hipEventRecord(dev[2], st));
+    if (count > 0) {
+      const Subset sub{list, it + 1};
+      SWH_TRY(launch_loop<LOOP_DENSITY>(s, P, &sub, list ? count : (int)n, false));
+    }
+    if (dbg) {
+      SWH_HIP(hipEventRecord(dev[3], st));
+      SWH_HIP(hipEventSynchronize(dev[3]));
+      float ms[3] = {0.f, 0.f, 0.f};
+      for (int k = 0; k < 3; k++) (void)hipEventElapsedTime(&ms[k], dev[k], dev[k + 1]);
+      std::fprintf(stderr,
+                   "[swh ghost] it %d: in %d, rerun %d (%s), past reach %u, rebuilt %d | ghost "
+                   "%.3f ms, host + rebuild %.3f ms, rerun %.3f ms\n",
+                   it, count_in, count, list ? "list" : "flags", nstale,
+                   (int)(count > 0 && lists && many), ms[0], ms[1], ms[2]);
+    }
   }
+  if (dbg)
+    for (auto& e : dev) (void)hipEventDestroy(e);
   {
     // slots 2 (max h) .. 17 (list-stale flag) in one read
     unsigned int c[18];

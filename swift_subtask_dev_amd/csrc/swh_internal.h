@@ -143,6 +143,9 @@ struct SwhGrid {
   double dx = 0;    // largest displacement since the rebuild (drift): loops widen their reach
 };
 
+// swh_tuning.list_skin of a new space (swifthip.h SWH_DEFAULT_LIST_SKIN)
+constexpr float kDefaultListSkin = SWH_DEFAULT_LIST_SKIN;
+
 // Device-resident particle set, sorted by grid cell in Morton order of the
 // cells (cell_rank maps a linear x-fastest cell index to its Morton rank).
 struct swh_space {
@@ -152,7 +155,7 @@ struct swh_space {
   int64_t n = 0;
   bool built = false;
   SwhGrid grid;
-  swh_tuning tuning{1, 0, 0, 0.f, 0, 0, 0.f, 0};
+  swh_tuning tuning{1, 0, 0, 0.f, 0, 0, kDefaultListSkin, 0};
 
   // AoS image of the caller's records (for write-back of untouched fields)
   swh::DevBuf aos;
@@ -213,6 +216,7 @@ struct swh_space {
   swh::DevBuf ctr_stripes;  // counted launches' per-block counter stripes (swh_hydro.hip)
   swh::DevBuf tmp_soa;     // staging for permutation gathers
   swh::DevBuf ghost_left, ghost_right, ghost_list, ghost_list2, ghost_search;
+  swh::DevBuf ghost_flag;  // per particle: the ghost pass that queued its rerun
   swh::HostBuf hstage;
 };
 

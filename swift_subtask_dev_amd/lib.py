@@ -311,7 +311,7 @@ class HydroSpace:
             pass
 
     def set_tuning(self, cell_factor=1, loop_variant=0, group_size=0, cell_scale=0.0,
-                   diag_mode=0, list_capacity=0, list_skin=0.0, list_keep=0):
+                   diag_mode=0, list_capacity=0, list_skin=abi.DEFAULT_LIST_SKIN, list_keep=0):
         t = abi.Tuning(cell_factor, loop_variant, group_size, cell_scale, diag_mode,
                        list_capacity, list_skin, list_keep)
         _check(self._lib.swh_space_set_tuning(self.handle, C.byref(t)), "set_tuning", self._lib)

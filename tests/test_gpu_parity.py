@@ -344,7 +344,7 @@ def test_box_density_vs_f64(gpu_ctx, cell_factor, variant, group_size, skin):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("variant,group_size,tuning",
-                         [(7, 16, {}), (7, 16, {"list_skin": 0.1}),
+                         [(7, 16, {}), (7, 16, {"list_skin": 0.1}), (7, 16, {"list_skin": 0.0}),
                           (7, 16, {"list_capacity": 24}), (0, 0, {"list_keep": 1})])
 def test_box_chain_vs_f64(gpu_ctx, variant, group_size, tuning):
     """Full SPHENIX chain (density, ghost with h iteration, gradient, extra

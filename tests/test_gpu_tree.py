@@ -148,6 +148,24 @@ def test_tree_zero_opening_angle_is_direct(gpu_ctx):
     compare(gg, gd)
 
 
+def test_tree_periodic_direct_far_pairs(gpu_ctx):
+    """Periodic, untruncated, theta -> 0: every pair is P-P, separations up
+    to half the box, so the batch kernel's staged nearest images (valid
+    within L/2 - the i-leaf extent) fall back to per-pair wrapping in the
+    tiles holding far sources; forces against the oracle's per-pair
+    nearestf."""
+    g, cells, tops = ics.gravity_tree(ics.uniform_gravity_box(10, 1e-3, seed=5), 2, 16)
+    pairs = ics.top_level_pairs(tops)
+    G = params(periodic=True, theta=1e-6, r_cut_max=10.0)
+    gg, go = abi.copy_parts(g), abi.copy_parts(g)
+    st = run_gpu(gpu_ctx, gg, cells, tops, pairs, G)[0]
+    so, _ = run_oracle(go, cells, tops, pairs, G)
+    N = len(g)
+    assert st["n_pp"] == N * (N - 1) and st["n_m2l"] == 0 and st["n_m2p"] == 0
+    assert [st["n_pp"], st["n_m2p"], st["n_m2l"], st["n_pp_tasks"], st["n_skipped"]] == list(so)
+    compare(gg, go)
+
+
 def test_tree_bad_input(gpu_ctx):
     from swift_subtask_dev_amd import lib
     g, cells, tops = ics.gravity_tree(ics.uniform_gravity_box(8, 1e-3, seed=4), 2, 16)

@@ -467,7 +467,7 @@ def step_breakdown(sp, P, stream, torch, local, reps=3):
     return out
 
 
-def steady_state(sp, P, stream, torch, local, n_owned, args, skin=None, steps=None):
+def steady_state(sp, P, stream, torch, local, n_owned, args, skin=None, steps=None, disp=None):
     """K steps of drift + density + force on the device-resident box with the
     pair lists kept while valid (swh_tuning.list_keep). Drift velocities:
     random, |v| ~ 1, dt so that the fastest particle moves `disp` h_min per step
@@ -480,7 +480,7 @@ def steady_state(sp, P, stream, torch, local, n_owned, args, skin=None, steps=No
     from swift_subtask_dev_amd import abi
     skin = args.steady_skin if skin is None else skin
     steps = args.steady_steps if steps is None else steps
-    disp = args.steady_disp
+    disp = args.steady_disp if disp is None else disp
     rng = np.random.Generator(np.random.PCG64(23))
     n = len(local)
     xp = abi.new_xparts(n)
@@ -1133,6 +1133,12 @@ def main():
     if world == 1 and args.diag_mode == 0 and not args.no_steady:
         try:
             steady = steady_state(sp, P, stream, torch, local, n_owned, args)
+            # Where keeping the lists pays: a kept list of skin s stays valid for
+            # ~gamma s / (2 disp) steps while its walks grow as (1 + s)^3, so at
+            # the 0.05 h / step above every skin loses to a rebuild per step; at
+            # 0.01 h / step a 5% skin lasts ~4-5 steps for ~16% more entries.
+            steady["low_velocity"] = steady_state(sp, P, stream, torch, local, n_owned, args,
+                                                  skin=0.05, disp=0.01)
         except Exception as e:  # report, never fake
             log(f"steady state failed: {e}")
         sp.set_tuning(args.cell_factor, args.loop_variant, args.group_size, args.cell_scale,

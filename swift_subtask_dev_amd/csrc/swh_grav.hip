@@ -816,8 +816,8 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
 // the MAC against source leaf j's multipole. Runs after p2p_kernel on the
 // same stream (both add into acc).
 // SMALL (every leaf <= 64 gparts, one wave per leaf): LPI lanes per i split
-// the leaf's source list (lane s takes entries s, s + LPI, ...) and combine
-// their sums, as p2p_batch_kernel does.
+// the leaf's compacted allow_mpole entries and combine their sums, as
+// p2p_batch_kernel does; otherwise a thread per i walks the whole list.
 template <typename T, bool SMALL>
 __global__ __launch_bounds__(kGravBlock) void m2p_kernel(
     GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
@@ -828,21 +828,85 @@ __global__ __launch_bounds__(kGravBlock) void m2p_kernel(
   const int p0 = pair_off[li], p1 = pair_off[li + 1];
   if (p0 == p1) return;  // no sources (a tree's inner cells)
   unsigned long long nm = 0;
-  int lpi = 1, s = 0, stride = (int)blockDim.x, first = (int)threadIdx.x;
-  if (SMALL) {  // wave-uniform
+  if (SMALL) {
+    // One wave per leaf, LPI lanes per i. The P-P entries are read 64 at a
+    // time (one per lane, loads in parallel) and their allow_mpole ones --
+    // ~7% of a cosmological tree's entries -- compacted into LDS; lane s of
+    // each i then takes compacted entries s, s + LPI, ..., so the wave no
+    // longer steps through the other 93% with a dependent pair -> leaf load
+    // chain per step, and every M2P evaluation has its lanes busy.
+    __shared__ int cj[64];
+    __shared__ unsigned char ctr[64];
+    int lpi = 1;  // wave-uniform
     while (lpi < 8 && L.count * lpi * 2 <= 64) lpi *= 2;
-    s = (int)threadIdx.x % lpi;
-    first = (int)threadIdx.x / lpi;
-    stride = 64;  // every lane has its i (or none) in one pass
-  }
-  for (int local = first; SMALL ? local == first : local < L.count; local += stride) {
-    const int i = L.start + local;
-    const bool act = local < L.count && g.active[i];
-    if (!SMALL && !act) continue;
+    const int lane = (int)threadIdx.x;
+    const int s = lane % lpi, il = lane / lpi;
+    const int i = L.start + il;
+    const bool act = il < L.count && g.active[i];
     const double4 p = act ? g.pos[i] : make_double4(0., 0., 0., 1.);
     const float oag = act ? g.oagn[i] : 0.f;
     T F[4] = {(T)0, (T)0, (T)0, (T)0};
-    for (int q = p0 + s; act && q < p1; q += lpi) {
+    for (int qb = p0; qb < p1; qb += 64) {
+      bool am = false;
+      int jl = 0;
+      unsigned char tr = 0;
+      if (qb + lane < p1) {
+        const swh_leaf_pair pr = pairs[qb + lane];
+        am = pr.allow_mpole && leaves[pr.j].count > 1;
+        jl = pr.j;
+        tr = pr.truncated != 0;
+      }
+      const unsigned long long m = __ballot(am);
+      const int nme = __popcll(m);
+      wave_sync();  // the previous chunk's readers are done
+      if (am) {
+        const int r = __popcll(m & ((1ull << lane) - 1ull));
+        cj[r] = jl;
+        ctr[r] = tr;
+      }
+      wave_sync();
+      for (int k = s; act && k < nme; k += lpi) {
+        const swh_multipole& M = g.mp[cj[k]];
+        if (!m2p_accept(mac, mac_source(M), (float)p.x, (float)p.y, (float)p.z, (float)p.w, oag))
+          continue;
+        double dx = M.CoM[0] - p.x, dy = M.CoM[1] - p.y, dz = M.CoM[2] - p.z;
+        if (periodic) {
+          dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
+          dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
+          dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
+        }
+        const T eps = (T)fmaxf((float)p.w, M.max_softening);
+        T f[4];
+        m2p<T>(M.M, (T)dx, (T)dy, (T)dz, eps, ctr[k] != 0, (T)r_s_inv, f);
+        for (int c = 0; c < 4; c++) F[c] += f[c];
+        nm++;
+      }
+    }
+    for (int o = 1; o < lpi; o <<= 1)
+      for (int c = 0; c < 4; c++) F[c] += __shfl_xor(F[c], o);
+    if (act && s == 0 && (F[0] != (T)0 || F[1] != (T)0 || F[2] != (T)0 || F[3] != (T)0)) {
+      double4 a = g.acc[i];
+      a.x += (double)F[1];
+      a.y += (double)F[2];
+      a.z += (double)F[3];
+      a.w += (double)F[0];
+      g.acc[i] = a;
+    }
+    if (counter) {
+      for (int o = 32; o > 0; o >>= 1) nm += __shfl_xor(nm, o);
+      if (lane == 0 && nm) atomicAdd(counter + 1, nm);
+    }
+    return;
+  }
+  // large leaves: a thread per i over the leaf's whole entry list
+  for (int local = (int)threadIdx.x; local < L.count; local += (int)blockDim.x) {
+    const int i = L.start + local;
+    const bool act = g.active[i];
+    if (!act) continue;
+    const double4 p = act ? g.pos[i] : make_double4(0., 0., 0., 1.);
+    const float oag = act ? g.oagn[i] : 0.f;
+    T F[4] = {(T)0, (T)0, (T)0, (T)0};
+    for (int q = p0; q < p1; q++) {
       const swh_leaf_pair pr = pairs[q];
       if (!pr.allow_mpole || leaves[pr.j].count <= 1) continue;
       const swh_multipole& M = g.mp[pr.j];
@@ -860,11 +924,7 @@ __global__ __launch_bounds__(kGravBlock) void m2p_kernel(
       for (int k = 0; k < 4; k++) F[k] += f[k];
       nm++;
     }
-    if (SMALL)
-      for (int o = 1; o < lpi; o <<= 1)
-        for (int k = 0; k < 4; k++) F[k] += __shfl_xor(F[k], o);
-    if (act && s == 0 &&
-        (F[0] != (T)0 || F[1] != (T)0 || F[2] != (T)0 || F[3] != (T)0)) {
+    if (F[0] != (T)0 || F[1] != (T)0 || F[2] != (T)0 || F[3] != (T)0) {
       double4 a = g.acc[i];
       a.x += (double)F[1];
       a.y += (double)F[2];

@@ -274,13 +274,12 @@ __global__ __launch_bounds__(256) void overflow_kernel(GridDev g, SoA a, ListDev
 // lanes per rerun particle walk its list while its H still fits the list
 // reach; any other one (H grown past its reach, list overflow, no lists) is
 // queued for the wave-per-particle search (overflow_kernel). The subset is the
-// ghost's redo list (nearly sorted), or its flags in particle order.
+// ghost's redo list, in (nearly) sorted order.
 template <typename T>
 __global__ __launch_bounds__(256) void walk_subset_kernel(GridDev g, SoA a, ListDev ld,
                                                           int list_ok,
                                                           const int* __restrict__ subset,
-                                                          const int8_t* __restrict__ flag,
-                                                          int want, int nitems, int max_active_bin,
+                                                          int nitems, int max_active_bin,
                                                           const unsigned int* __restrict__ hmax_bits,
                                                           unsigned long long* counter,
                                                           int* __restrict__ searchq,
@@ -288,8 +287,7 @@ __global__ __launch_bounds__(256) void walk_subset_kernel(GridDev g, SoA a, List
   constexpr int LPI = kWalkLpi;
   const int t = (int)blockIdx.x * (256 / LPI) + (int)threadIdx.x / LPI;
   const int s = (int)threadIdx.x % LPI;
-  // the reruns: a compact subset, or (subset null) the particles flagged `want`
-  const int i = t >= nitems ? -1 : subset ? subset[t] : (flag[t] == (int8_t)want ? t : -1);
+  const int i = t < nitems ? subset[t] : -1;
   bool act = i >= 0 && active_part(a, i, max_active_bin);
   int nl = 0, lb = -1;
   double4 pi = make_double4(0., 0., 0., 0.);
@@ -354,7 +352,7 @@ struct GhostParams {
 // converged (final fields written); hf_out = its h, stale = H outgrew its
 // list reach.
 template <typename T>
-__device__ __forceinline__ void ghost_part(SoA& a, int i, float* left, float* right,
+__device__ __forceinline__ void ghost_part(SoA& a, int i, bool first, float* left, float* right,
                                            const GhostParams& gp,
                                            const float* __restrict__ list_reach, bool& redo_out,
                                            float& hf_out, bool& stale) {
@@ -371,7 +369,8 @@ __device__ __forceinline__ void ghost_part(SoA& a, int i, float* left, float* ri
   T h_new;
   bool has_no_neighbours = false;
   bool tidy = false;  // converged-by-clamp branch (runner_ghost.c:1272-1300)
-  float lft = left[i], rgt = right[i];
+  // the bisection bounds: [0, h_max] on the first pass, else the last pass's
+  float lft = first ? 0.f : left[i], rgt = first ? gp.h_max : right[i];
   if (wcount < (T)(1.e-5 * kRoot)) {
     has_no_neighbours = true;
     h_new = (T)2 * h_old;
@@ -432,7 +431,8 @@ __device__ __forceinline__ void ghost_part(SoA& a, int i, float* left, float* ri
       // redo: store h, re-initialise (hydro_init_part), queue for the rerun
       pos.w = (double)hf;
       a.pos[i] = pos;
-      a.th[i].y = 0.f;
+      th.y = 0.f;
+      a.th[i] = th;  // (a whole-record store, not a 4-byte one into it)
       a.dens[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       a.rot[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       left[i] = lft;
@@ -498,63 +498,106 @@ __device__ __forceinline__ void ghost_part(SoA& a, int i, float* left, float* ri
   a.grad[i] = g;
 }
 
-// One pass `it` of the ghost. Its particles: every active one (it = 0, whose
-// bisection bounds start at [0, h_max]), the previous pass's reruns from the
-// compact `list`, or (list null, it > 0) those whose flag holds `it`. The
-// reruns it queues get flag it + 1; pass 0 writes every flag. When `redo` is
-// given they are also appended to it (compaction: one returning atomic per
-// workgroup, which holds the whole workgroup -- used only once the reruns
-// are few); otherwise only counted, and the rerun walks the flags in particle
-// order.
+// One pass `it` of the ghost: over every active particle (it = 0, whose
+// bisection bounds start at [0, h_max]) or the previous pass's `list`; the
+// particles it queues for a rerun are appended to `redo` (one atomic per
+// workgroup).
 template <typename T>
 __global__ __launch_bounds__(1024) void ghost_kernel(
-    SoA a, const int* __restrict__ list, int count, int it, int8_t* __restrict__ flag,
-    int max_active_bin, int* __restrict__ redo, int* __restrict__ nredo, float* left,
-    float* right, GhostParams gp, unsigned int* hmax_bits, const float* __restrict__ list_reach,
-    unsigned int* list_stale, unsigned int* __restrict__ nstale_redo) {
+    SoA a, const int* __restrict__ list, int count, int max_active_bin, int* __restrict__ redo,
+    int* __restrict__ nredo, float* left, float* right, GhostParams gp, unsigned int* hmax_bits,
+    const float* __restrict__ list_reach, unsigned int* ngrown, int* __restrict__ grown_q,
+    unsigned int* __restrict__ nstale_redo) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   bool rd = false, stale = false;
   float hf = 0.f;
   int i = -1;
+  bool first = false;
   if (t < count) {
-    if (it == 0) {
-      if (active_part(a, t, max_active_bin)) {
-        i = t;
-        left[i] = 0.f;
-        right[i] = gp.h_max;
-      }
-    } else if (list) {
+    if (list) {
       i = list[t];
-    } else if (flag[t] == (int8_t)it) {
+    } else if (active_part(a, t, max_active_bin)) {
       i = t;
+      first = true;
     }
   }
-  if (i >= 0) ghost_part<T>(a, i, left, right, gp, list_reach, rd, hf, stale);
-  if (it == 0) {
-    if (t < count) flag[t] = rd ? (int8_t)1 : (int8_t)0;
-  } else if (rd) {
-    flag[i] = (int8_t)(it + 1);
-  }
-  if (redo) {
-    const int slot = block_append(rd, nredo);
-    if (rd) redo[slot] = i;
-  } else {
-    block_count(rd, nredo);
-  }
+  if (i >= 0) ghost_part<T>(a, i, first, left, right, gp, list_reach, rd, hf, stale);
+  const int slot = block_append(rd, nredo);
+  if (rd) redo[slot] = i;
   // reruns whose new H outgrew their list reach (they would need the
   // wave-per-particle search): one conditional atomic per wave
   const unsigned long long ms = __ballot(rd && stale);
   if ((threadIdx.x & 63) == 0 && ms) atomicAdd(nstale_redo, (unsigned int)__popcll(ms));
-  stale = stale && !rd;  // converged particles: their loops' lists
-  // h max and the stale flag: an atomic only when it changes something (all
-  // blocks hitting one address serialise at ~10 ns per atomic)
+  // converged particles whose H outgrew their list reach: queued (few; one
+  // atomic per wave that has any) for the gradient / force loops' searches
+  stale = stale && !rd;
+  const int gs = wave_append(stale, ngrown);
+  if (stale) grown_q[gs] = i;
+  // h max: an atomic only when it changes something (all blocks hitting one
+  // address serialise at ~10 ns per atomic)
   float m = hf;
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  const bool any_stale = __any(stale);
-  if ((threadIdx.x & 63) == 0) {
-    if (m > 0.f) atomic_max_bits_if(hmax_bits, __float_as_uint(m));
-    if (any_stale) atomic_flag_if(list_stale);
+  if ((threadIdx.x & 63) == 0 && m > 0.f) atomic_max_bits_if(hmax_bits, __float_as_uint(m));
+}
+
+// The lists after a ghost that grew some converged H past its list reach R
+// (grown_q): the gradient loop (r < H_i) searches those particles; the force
+// loop (r < max(H_i, H_j)) also every i within H_j of a grown j, whose list may
+// lack j (it holds the j with r < max(R_i, R_j) at the build). One wave per
+// grown particle marks them (mark: u32 per particle, zero between loops) and
+// queues each once; particles already searched as list overflow are left to
+// that search.
+__global__ __launch_bounds__(256) void grown_mark_kernel(GridDev g, SoA a, ListDev ld,
+                                                         const int* __restrict__ grown_q,
+                                                         int ngrown, int force,
+                                                         const int* __restrict__ pcell,
+                                                         unsigned int* __restrict__ cell_R,
+                                                         unsigned int* __restrict__ mark,
+                                                         int* __restrict__ q,
+                                                         unsigned int* __restrict__ qn) {
+  const int lane = (int)threadIdx.x & 63;
+  const int w = (int)blockIdx.x * 4 + (int)threadIdx.x / 64;
+  if (w >= ngrown) return;  // wave-uniform
+  const int j = grown_q[w];
+  auto queue = [&](int i) {
+    if (ld.cnt[i] > ld.K) return;  // list overflow: searched anyway
+    if (atomicExch(&mark[i], 1u) == 0u) q[atomicAdd(qn, 1u)] = i;
+  };
+  if (lane == 0) queue(j);
+  if (!force) return;
+  const double4 pj = a.pos[j];
+  const double Hj = pj.w * (double)kGamma;
+  // the per-cell reach the force searches prune by (adaptive grid) must
+  // cover the grown H too
+  if (cell_R && lane == 0 && pcell[j] >= 0)
+    atomicMax(&cell_R[pcell[j]], __float_as_uint((float)Hj * 1.0000005f));
+  CellRange c;
+  cell_range(g, pj.x, pj.y, pj.z, Hj, c);
+  for (int cz = c.lo[2]; cz <= c.hi[2]; cz++) {
+    double sz;
+    const int wz = wrap_cell(g, c, 2, cz, sz);
+    for (int cy = c.lo[1]; cy <= c.hi[1]; cy++) {
+      double sy;
+      const int wy = wrap_cell(g, c, 1, cy, sy);
+      for (int cx = c.lo[0]; cx <= c.hi[0]; cx++) {
+        double sx;
+        const int wx = wrap_cell(g, c, 0, cx, sx);
+        const int2 r = cell_range_of(g, wx, wy, wz);
+        for (int i = r.x + lane; i < r.y; i += 64) {
+          double dx, dy, dz;
+          const double r2 = separation<double>(g, c, pj, a.pos[i], sx, sy, sz, dx, dy, dz);
+          if (r2 < Hj * Hj * (1. + 1e-6)) queue(i);
+        }
+      }
+    }
   }
+}
+
+__global__ void grown_clear_kernel(const int* __restrict__ q, const unsigned int* __restrict__ qn,
+                                   unsigned int* __restrict__ mark) {
+  const int n = (int)*qn;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x)
+    mark[q[t]] = 0u;
 }
 
 // runner_do_extra_ghost (runner_ghost.c:992-1083): hydro_end_gradient,
@@ -685,6 +728,11 @@ static unsigned int* stale_slot(swh_space* s) { return s->counters.as<unsigned i
 static unsigned int* rwrap_slot(swh_space* s) { return s->counters.as<unsigned int>() + 18; }
 // u32[20]: the ghost reruns' search-queue length
 constexpr float kGhostListSkin = 0.01f;
+// u32[17]: converged particles the ghost grew past their list reach (grown_q);
+// up to n / kGrownSearchMax of them are searched instead of a list rebuild
+constexpr int kGrownSearchMax = 256;
+// u32[28]: the grown particles' search queue (grown_mark_kernel)
+static unsigned int* grown_qn_slot(swh_space* s) { return s->counters.as<unsigned int>() + 28; }
 static unsigned int* search_slot(swh_space* s) { return s->counters.as<unsigned int>() + 20; }
 // u32[22]: the ghost pass's reruns whose new H outgrew their list reach
 static unsigned int* stale_redo_slot(swh_space* s) { return s->counters.as<unsigned int>() + 22; }
@@ -715,6 +763,7 @@ static ListDev list_dev(swh_space* s) {
   d.ovf_n = ovf_slot(s);
   // per-cell reach pruning only pays on an adaptive (clustered) grid
   d.cell_R = s->grid.adaptive ? s->cell_hreach.as<const float>() : nullptr;
+  d.mark = nullptr;
   return d;
 }
 
@@ -770,6 +819,7 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
   s->list_valid = true;
   s->list_check = false;
   s->list_mab = P->max_active_bin;
+  s->grown_n = 0;  // the new lists cover every current H
   return SWH_OK;
 }
 
@@ -792,25 +842,18 @@ static swh_status check_kept_lists(swh_space* s, const swh_hydro_params* P, bool
   return build_lists(s, P, count, s->tuning.list_skin, keep_stale_slot(s));
 }
 
-// The ghost's reruns (launch_loop's `subset`): a compact list of `nitems`
-// particles, or (list null) the particles among the first `nitems` whose
-// ghost flag is `want`.
-struct Subset {
-  const int* list;
-  int want;
-};
-
 template <int LOOP, typename T>
-static void launch_typed(swh_space* s, const GridDev& gd, const Subset* subset, int nitems,
-                         int max_active_bin, T a2H, unsigned long long* ctr, int* ncount) {
+static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int nitems,
+                         int max_active_bin, T a2H, unsigned long long* ctr, int* ncount,
+                         const unsigned int* mark = nullptr) {
   const int block = 256;
-  const ListDev ld = list_dev(s);
+  ListDev ld = list_dev(s);
+  ld.mark = mark;
   constexpr int ppb = block / kWalkLpi;
   if (subset) {  // density reruns of the ghost: list walks, then the queued searches
     (void)hipMemsetAsync(search_slot(s), 0, sizeof(unsigned int), s->stream);
     hipLaunchKernelGGL((walk_subset_kernel<T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
-                       s->stream, gd, soa_of(s), ld, s->list_valid ? 1 : 0, subset->list,
-                       s->ghost_flag.as<const int8_t>(), subset->want, nitems,
+                       s->stream, gd, soa_of(s), ld, s->list_valid ? 1 : 0, subset, nitems,
                        max_active_bin, hmax_slot(s), ctr, s->ghost_search.as<int>(),
                        search_slot(s));
     // one wave per queued particle; the queue length is read on the device
@@ -834,7 +877,7 @@ static void launch_typed(swh_space* s, const GridDev& gd, const Subset* subset, 
 }
 
 template <int LOOP>
-static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const Subset* subset,
+static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const int* subset,
                               int nitems, bool count) {
   if (nitems <= 0) return SWH_OK;
   if (!subset && s->ngroups <= 0) return SWH_OK;
@@ -863,11 +906,45 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const Sub
   unsigned long long* ctr = nullptr;
   if (count) SWH_TRY(stripes_slot(s, &ctr));
   int* ncount = count ? s->ncount.as<int>() : nullptr;
-  if (s->ctx->precision == SWH_PRECISION_F64)
-    launch_typed<LOOP, double>(s, gd, subset, nitems, P->max_active_bin, a2H, ctr, ncount);
+  const bool f64 = s->ctx->precision == SWH_PRECISION_F64;
+  // gradient / force after a ghost that grew a few H past the lists: those
+  // particles (force: and their neighbours within H) are searched
+  const bool grown = !subset && LOOP != LOOP_DENSITY && s->grown_n > 0 && s->list_valid;
+  unsigned int* mark = nullptr;
+  unsigned int* qn = grown_qn_slot(s);
+  if (grown) {
+    if (!s->grown_mark.ptr) {
+      SWH_TRY(s->grown_mark.reserve((size_t)s->n * sizeof(unsigned int)));
+      SWH_HIP(hipMemsetAsync(s->grown_mark.ptr, 0, (size_t)s->n * sizeof(unsigned int),
+                             s->stream));
+    }
+    SWH_TRY(s->grown_search.reserve((size_t)s->n * sizeof(int)));
+    mark = s->grown_mark.as<unsigned int>();
+    SWH_HIP(hipMemsetAsync(qn, 0, sizeof(unsigned int), s->stream));
+    hipLaunchKernelGGL(grown_mark_kernel, dim3((s->grown_n + 3) / 4), dim3(256), 0, s->stream,
+                       gd, soa_of(s), list_dev(s), s->grown_q.as<const int>(), s->grown_n,
+                       LOOP == LOOP_FORCE ? 1 : 0, s->pcell.as<const int>(),
+                       s->grid.adaptive ? s->cell_hreach.as<unsigned int>() : nullptr, mark,
+                       s->grown_search.as<int>(), qn);
+  }
+  if (f64)
+    launch_typed<LOOP, double>(s, gd, subset, nitems, P->max_active_bin, a2H, ctr, ncount, mark);
   else
     launch_typed<LOOP, float>(s, gd, subset, nitems, P->max_active_bin, (float)a2H, ctr,
-                              ncount);
+                              ncount, mark);
+  if (grown) {
+    const ListDev ld = list_dev(s);
+    const int* q = s->grown_search.as<const int>();
+    if (f64)
+      hipLaunchKernelGGL((overflow_kernel<LOOP, double>), dim3(256), dim3(256), 0, s->stream,
+                         gd, soa_of(s), ld, q, qn, P->max_active_bin, a2H, hmax_slot(s), ctr,
+                         ncount);
+    else
+      hipLaunchKernelGGL((overflow_kernel<LOOP, float>), dim3(256), dim3(256), 0, s->stream,
+                         gd, soa_of(s), ld, q, qn, P->max_active_bin, (float)a2H,
+                         hmax_slot(s), ctr, ncount);
+    hipLaunchKernelGGL(grown_clear_kernel, dim3(64), dim3(256), 0, s->stream, q, qn, mark);
+  }
   SWH_HIP(hipGetLastError());
   return SWH_OK;
 }
@@ -951,7 +1028,7 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   SWH_TRY(s->ghost_list.reserve(n * sizeof(int)));
   SWH_TRY(s->ghost_list2.reserve(n * sizeof(int)));
   SWH_TRY(s->ghost_search.reserve(n * sizeof(int)));
-  SWH_TRY(s->ghost_flag.reserve(n * sizeof(int8_t)));
+  SWH_TRY(s->grown_q.reserve(n * sizeof(int)));
   int* cnt = s->counters.as<int>() + 4;  // slot 5: rerun count
   const int block = 1024;
   GhostParams gp;
@@ -963,16 +1040,10 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   gp.a2_inv = P->a2_inv;
   gp.H = P->H;
   gp.fac_B = P->a_factor_Balsara_eps;
-  // Pass it's particles: every active one (it = 0), then the reruns the pass
-  // before queued -- as flags (ghost_flag == it, the pass and its rerun
-  // running over all n in particle order) while they are many, as a compact
-  // list once the pass's input is at most n/8 (a list pass only appends what
-  // it queues, so its output is small too). The first pass after a drift
-  // queues nearly every particle: compacting 2M reruns through one counter
-  // cost more than walking the flags.
-  int count = (int)n;  // this pass's input size
-  int* list = nullptr;  // this pass's input list (null: flags)
-  int* out = s->ghost_list.as<int>();
+  // the first pass runs over every particle (inactive ones return at once)
+  int count = (int)n;
+  int* list = nullptr;  // first pass: every active particle
+  int* list2 = s->ghost_list.as<int>();
   int* spare = s->ghost_list2.as<int>();
   const bool lists = true;
   SWH_HIP(hipMemsetAsync(stale_slot(s), 0, sizeof(unsigned int), st));
@@ -988,21 +1059,17 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
     const float* lreach = (lists && s->list_valid) ? s->nbr_reach.as<const float>() : nullptr;
     SWH_HIP(hipMemsetAsync(cnt + 1, 0, sizeof(int), st));
     SWH_HIP(hipMemsetAsync(stale_redo_slot(s), 0, sizeof(unsigned int), st));
-    // output as a list (and always from pass 100 on: the int8 flags stop there)
-    const bool compact = it > 0 && ((int64_t)count * 8 <= n || it >= 100);
-    if (it > 0 && !list) count = (int)n;  // flag input: a pass over every particle
     const int g = (count + block - 1) / block;
-    int* redo = compact ? out : nullptr;
     if (s->ctx->precision == SWH_PRECISION_F64)
       hipLaunchKernelGGL(ghost_kernel<double>, dim3(g), dim3(block), 0, st, soa_of(s), list,
-                         count, it, s->ghost_flag.as<int8_t>(), P->max_active_bin, redo,
-                         cnt + 1, s->ghost_left.as<float>(), s->ghost_right.as<float>(), gp,
-                         hmax_slot(s), lreach, stale_slot(s), stale_redo_slot(s));
+                         count, P->max_active_bin, list2, cnt + 1, s->ghost_left.as<float>(),
+                         s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s),
+                         s->grown_q.as<int>(), stale_redo_slot(s));
     else
       hipLaunchKernelGGL(ghost_kernel<float>, dim3(g), dim3(block), 0, st, soa_of(s), list,
-                         count, it, s->ghost_flag.as<int8_t>(), P->max_active_bin, redo,
-                         cnt + 1, s->ghost_left.as<float>(), s->ghost_right.as<float>(), gp,
-                         hmax_slot(s), lreach, stale_slot(s), stale_redo_slot(s));
+                         count, P->max_active_bin, list2, cnt + 1, s->ghost_left.as<float>(),
+                         s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s),
+                         s->grown_q.as<int>(), stale_redo_slot(s));
     SWH_HIP(hipGetLastError());
     if (dbg) SWH_HIP(hipEventRecord(dev[1], st));
     const int count_in = count;
@@ -1010,13 +1077,10 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
     SWH_HIP(hipMemcpyAsync(&count, cnt + 1, sizeof(int), hipMemcpyDeviceToHost, st));
     SWH_HIP(hipMemcpyAsync(&nstale, stale_redo_slot(s), sizeof(nstale), hipMemcpyDeviceToHost, st));
     SWH_HIP(hipStreamSynchronize(st));
-    if (compact) {  // the new list becomes the input; the old input buffer is reused
-      int* done = list ? list : spare;
-      list = out;
-      out = done;
-    } else {
-      list = nullptr;
-    }
+    // the new rerun list becomes the input; the old input buffer is reused
+    int* done = list ? list : spare;
+    list = list2;
+    list2 = done;
     const bool many = s->list_valid ? (int64_t)nstale * 8 >= n : (int64_t)count * 8 >= n;
     if (count > 0 && lists && many) {
       // Many reruns whose new H outgrew their list reach (the first iteration
@@ -1029,19 +1093,16 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
       SWH_HIP(hipMemsetAsync(stale_slot(s), 0, sizeof(unsigned int), st));
     }
     if (dbg) SWH_HIP(hipEventRecord(dev[2], st));
-    if (count > 0) {
-      const Subset sub{list, it + 1};
-      SWH_TRY(launch_loop<LOOP_DENSITY>(s, P, &sub, list ? count : (int)n, false));
-    }
+    if (count > 0) SWH_TRY(launch_loop<LOOP_DENSITY>(s, P, list, count, false));
     if (dbg) {
       SWH_HIP(hipEventRecord(dev[3], st));
       SWH_HIP(hipEventSynchronize(dev[3]));
       float ms[3] = {0.f, 0.f, 0.f};
       for (int k = 0; k < 3; k++) (void)hipEventElapsedTime(&ms[k], dev[k], dev[k + 1]);
       std::fprintf(stderr,
-                   "[swh ghost] it %d: in %d, rerun %d (%s), past reach %u, rebuilt %d | ghost "
+                   "[swh ghost] it %d: in %d, rerun %d, past reach %u, rebuilt %d | ghost "
                    "%.3f ms, host + rebuild %.3f ms, rerun %.3f ms\n",
-                   it, count_in, count, list ? "list" : "flags", nstale,
+                   it, count_in, count, nstale,
                    (int)(count > 0 && lists && many), ms[0], ms[1], ms[2]);
     }
   }
@@ -1052,7 +1113,14 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
     unsigned int c[18];
     SWH_HIP(hipMemcpyAsync(c, s->counters.ptr, sizeof(c), hipMemcpyDeviceToHost, st));
     SWH_HIP(hipStreamSynchronize(st));
-    if (lists && s->list_valid && c[17]) s->list_valid = false;  // gradient / force rebuild
+    // converged particles grown past their list reach: a few are searched by
+    // the gradient / force loops (grown_mark_kernel); many -> those loops
+    // rebuild the lists
+    s->grown_n = 0;
+    if (lists && s->list_valid && c[17]) {
+      if ((int64_t)c[17] * kGrownSearchMax > n) s->list_valid = false;
+      else s->grown_n = (int32_t)c[17];
+    }
     float hmax;
     std::memcpy(&hmax, &c[2], sizeof(hmax));
     // a kernel reach of half the periodic box or more would need more than

@@ -207,6 +207,11 @@ struct swh_space {
   swh::DevBuf list_xd0;  // float4: the displacement record (xdiff) at the list build
   bool list_valid = false;
   bool list_check = false;  // kept lists after a drift: the device checks them first
+  // particles the ghost converged with H past their list reach (queue
+  // grown_q, u32[17]): the gradient / force loops search them (and, force,
+  // their neighbours within H) instead of rebuilding every list
+  int32_t grown_n = 0;
+  swh::DevBuf grown_q, grown_mark, grown_search;
   int32_t list_mab = 0, list_K = 0;
   float list_skin_cur = 0.f;  // skin of the lists in use (tuning, or the ghost's rebuild)
   int64_t list_entries = 0;   // last counted build: total entries
@@ -216,7 +221,6 @@ struct swh_space {
   swh::DevBuf ctr_stripes;  // counted launches' per-block counter stripes (swh_hydro.hip)
   swh::DevBuf tmp_soa;     // staging for permutation gathers
   swh::DevBuf ghost_left, ghost_right, ghost_list, ghost_list2, ghost_search;
-  swh::DevBuf ghost_flag;  // per particle: the ghost pass that queued its rerun
   swh::HostBuf hstage;
 };
 

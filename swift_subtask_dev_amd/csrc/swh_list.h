@@ -88,6 +88,7 @@ struct ListDev {
   const float* cell_R;  // per linear grid cell: max R of its particles (cell_reach_kernel);
                         // null on a uniform grid (no per-cell pruning)
   int diag;      // profiling only: 2 = the build writes no entries
+  const unsigned int* mark;  // nullable: particles the walks leave to a search (ghost-grown H)
   const GroupBox* gbox;  // per group (group_box_kernel), read by the build
 };
 
@@ -636,6 +637,7 @@ __device__ __forceinline__ void list_walk(const GridDev& g, SoA& a, const ListDe
     nl = ld.cnt[i];
     lb = ld.base[i];
     if (nl > ld.K || lb < 0) act = false;  // overflow: the search walks it
+    if (ld.mark && ld.mark[i]) act = false;  // grown past the lists: searched
   }
   S st;
   st.n = 0;

@@ -157,23 +157,6 @@ __device__ __forceinline__ int wave_max_i(int v) {
   return v;
 }
 
-// Count the threads with `pred` into *counter: one atomic per workgroup whose
-// result nobody waits for (every thread of the block must call it).
-template <typename C>
-__device__ __forceinline__ void block_count(bool pred, C* counter) {
-  __shared__ int bcnt[16];
-  const int lane = (int)(threadIdx.x & 63), w = (int)(threadIdx.x >> 6);
-  const int nw = (int)((blockDim.x + 63) >> 6);
-  const unsigned long long m = __ballot(pred);
-  if (lane == 0) bcnt[w] = (int)__popcll(m);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int tot = 0;
-    for (int k = 0; k < nw; k++) tot += bcnt[k];
-    if (tot) atomicAdd(counter, (C)tot);
-  }
-}
-
 // Stream compaction with one atomic per workgroup (blockDim.x <= 1024): the
 // threads with `pred` get consecutive slots, in thread order. Every thread of
 // the block must call it (it synchronises the block). Same-address atomics

@@ -783,3 +783,44 @@ def test_density_list_reuse(gpu_ctx):
     sp.init_parts(P)
     assert sp.density(P) == no
     sp.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_chain_few_grown_searched(gpu_ctx, request, adaptive):
+    """Converged smoothing lengths with a few cut by 30%: the ghost grows those
+    back past their list reach (skin 2%), too few to rebuild every list, so
+    the gradient loop searches them and the force loop also their neighbours
+    within the grown H (grown_mark_kernel): one list build in the chain, and
+    the chain still equals the oracle's. The clustered box runs the adaptive
+    grid, whose per-cell reach the grown H must raise."""
+    from swift_subtask_dev_amd import lib
+    P = abi.default_hydro_params()
+    if adaptive:
+        parts, _ = request.getfixturevalue("clustered_state")  # h converged by the GPU
+        parts = abi.copy_parts(parts)
+    else:
+        parts = ics.sedov_box(16, velocity="divergent", pert=0.3, seed=5)
+        conv, _ = box_chain_oracle(parts, P)
+        parts = abi.copy_parts(parts)
+        parts["h"] = conv["h"]
+    cut = np.random.Generator(np.random.PCG64(4)).choice(len(parts), 6, replace=False)
+    parts["h"][cut] *= 0.7
+    g = abi.copy_parts(parts)
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.upload(g)
+    sp.rebuild(P)
+    b0 = sp.info()["list_builds"]
+    rg = sp.hydro_step(P)
+    builds = sp.info()["list_builds"] - b0
+    sp.download(g, abi.FIELDS_ALL)
+    sp.close()
+    o, ro = box_chain_oracle(parts, P)
+    assert builds == 1, builds  # the density loop's; none for the grown few
+    assert rg["gradient"] == ro["gradient"] and rg["force"] == ro["force"]
+    tol_h, tol = (1e-5, 1e-4) if adaptive else (1e-6, 5e-5)
+    assert_close(g["h"], o["h"], tol_h, what="h")
+    assert_close(g["rho"], o["rho"], tol, 1e-4, "rho")
+    assert_close(g["a_hydro"], o["a_hydro"], tol, 1e-3 if adaptive else 1e-4, "a_hydro")
+    assert_close(g["u_dt"], o["u_dt"], tol, 1e-3 if adaptive else 1e-4, "u_dt")
+    assert np.array_equal(g["min_ngb_time_bin"], o["min_ngb_time_bin"])

@@ -554,13 +554,68 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(MPOLE ? 3 :
 // tiny box) wraps every pair (nearest_rint), as nearestf does.
 constexpr int kPPBatch = 256;
 
+// The batch kernel's pair loop over one staged tile: lane s of its i takes
+// entries s, s + lpi, ... MASKED: per pair, the entry's M2P bit (pmask) and
+// the self term (gpart index) zero the mass, and the pairs are counted;
+// otherwise the caller counted them. TR: 0 / 1 = no / every entry truncated,
+// 2 = per entry (tmask).
+struct PairCtx {
+  double4 pi;
+  double hi2, hv, emax, tworsi, dimx, dimy, dimz, idimx, idimy, idimz;
+};
+struct TileLds {
+  const double *sx, *sy, *sz;
+  const float* seps;  // softening: h2 = eps^2 and 1 / eps are exact from the float
+  const float* sm;
+  const int* sg;
+  const unsigned char* sb;
+};
+template <bool MASKED, int TR>
+__device__ __forceinline__ void batch_pairs(const TileLds& tl, const PairCtx& c, int s, int lpi,
+                                            int tn, bool wrap, unsigned int pmask,
+                                            unsigned int tmask, int gi, double& ax, double& ay,
+                                            double& az, double& pot, unsigned int& nint) {
+  for (int t = s; t < tn; t += lpi) {
+    double dx = tl.sx[t] - c.pi.x, dy = tl.sy[t] - c.pi.y, dz = tl.sz[t] - c.pi.z;
+    if (wrap) {
+      dx = nearest_rint(dx, c.dimx, c.idimx);
+      dy = nearest_rint(dy, c.dimy, c.idimy);
+      dz = nearest_rint(dz, c.dimz, c.idimz);
+    }
+    int b = 0;
+    if (MASKED || TR == 2) b = tl.sb[t];
+    double mass;
+    if (MASKED) {
+      const bool use = ((pmask >> b) & 1u) & (tl.sg[t] != gi);
+      nint += use;
+      mass = (double)(use ? tl.sm[t] : 0.f);
+    } else {
+      mass = (double)tl.sm[t];
+    }
+    double r2, r_inv, f_ij, pot_ij;
+    p2p_newton(dx, dy, dz, mass, r2, r_inv, f_ij, pot_ij);
+    if (__builtin_expect(__any(r2 < c.emax), 0))
+      if (r2 < c.emax) {
+        const double ej = (double)tl.seps[t];
+        p2p_soften(r2, r_inv, c.hi2, ej * ej, c.hv, 1. / ej, mass, f_ij, pot_ij);
+      }
+    if (TR == 1 || (TR == 2 && ((tmask >> b) & 1u)))
+      p2p_trunc<true>(r2, r_inv, c.tworsi, f_ij, pot_ij);
+    ax = fma(f_ij, dx, ax);
+    ay = fma(f_ij, dy, ay);
+    az = fma(f_ij, dz, az);
+    pot += pot_ij;
+  }
+}
+
 template <bool MPOLE>
 __global__ __launch_bounds__(64) void p2p_batch_kernel(
     GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
     const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
     double dimz, double r_s_inv, MacParams mac, unsigned long long* counter) {
-  __shared__ double sx[kPPBatch], sy[kPPBatch], sz[kPPBatch], se2[kPPBatch], sh[kPPBatch];
-  __shared__ float sm[kPPBatch];
+  // 37 B per staged gpart (9.5 KB): four waves per SIMD
+  __shared__ double sx[kPPBatch], sy[kPPBatch], sz[kPPBatch];
+  __shared__ float seps[kPPBatch], sm[kPPBatch];
   __shared__ int sg[kPPBatch];
   __shared__ unsigned char sb[kPPBatch];
   __shared__ int boff[32], bstart[32];
@@ -620,6 +675,8 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
     const int B = fit ? __popcll(fit) : 1;
     const int total = __builtin_amdgcn_readlane(inc, B - 1);
     const unsigned int tmask = (unsigned int)__ballot(lane < B && tr);
+    // the i-leaf's own gparts among the batch's sources (self terms to drop)
+    const bool own = __any(lane < B && jst < L.start + L.count && L.start < jst + cnt);
     unsigned int mmask = 0;  // the entries this i takes through their multipole
     if (MPOLE) {
       for (unsigned long long m = __ballot(lane < B && am); m; m &= m - 1) {
@@ -660,9 +717,8 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
         sx[k] = px;
         sy[k] = py;
         sz[k] = pz;
-        se2[k] = p.w * p.w;
+        seps[k] = (float)p.w;  // (the gpart's float epsilon, exactly)
         e2max = fmax(e2max, p.w * p.w);
-        sh[k] = g.hinv[gj];
         sm[k] = g.mass[gj];
         sg[k] = gj;
         sb[k] = (unsigned char)b;
@@ -670,28 +726,26 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
       const double emax = act ? fmax(hi2, wave_max_f64(e2max)) : 0.;
       const bool wrap = periodic && __any(far);
       wave_sync();
-      for (int t = s; t < tn; t += lpi) {
-        const int b = sb[t];
-        const bool use = ((pmask >> b) & 1u) & (sg[t] != gi);
-        nint += use;
-        double dx = sx[t] - pi.x, dy = sy[t] - pi.y, dz = sz[t] - pi.z;
-        if (wrap) {
-          dx = nearest_rint(dx, dimx, idimx);
-          dy = nearest_rint(dy, dimy, idimy);
-          dz = nearest_rint(dz, dimz, idimz);
-        }
-        const float mf = sm[t];
-        const double mass = (double)(use ? mf : 0.f);
-        double r2, r_inv, f_ij, pot_ij;
-        p2p_newton(dx, dy, dz, mass, r2, r_inv, f_ij, pot_ij);
-        if (__builtin_expect(__any(r2 < emax), 0))
-          if (r2 < emax) p2p_soften(r2, r_inv, hi2, se2[t], hv, sh[t], mass, f_ij, pot_ij);
-        if ((tmask >> b) & 1u) p2p_trunc<true>(r2, r_inv, tworsi, f_ij, pot_ij);
-        ax = fma(f_ij, dx, ax);
-        ay = fma(f_ij, dy, ay);
-        az = fma(f_ij, dz, az);
-        pot += pot_ij;
+      // Wave-uniform fast paths: no lane takes a multipole of this batch and
+      // the i-leaf is none of its sources (no self term) -> no per-pair mask,
+      // and the pairs are counted per lane; every or no entry truncated -> no
+      // per-pair truncation bit.
+      const unsigned int bmask = B >= 32 ? 0xffffffffu : (1u << B) - 1u;
+      const bool plain = !__any(act && (mmask & bmask) != 0u) && !own;
+      const int tr = (tmask & bmask) == bmask ? 1 : (tmask & bmask) == 0u ? 0 : 2;
+      const PairCtx pc{pi, hi2, hv, emax, tworsi, dimx, dimy, dimz, idimx, idimy, idimz};
+      const TileLds tl{sx, sy, sz, seps, sm, sg, sb};
+#define SWH_BATCH_PAIRS(M, T)                                                             \
+  batch_pairs<M, T>(tl, pc, s, lpi, tn, wrap, pmask, tmask, gi, ax, ay, az, pot, nint)
+      if (plain) {
+        if (act) nint += (unsigned int)(tn > s ? (tn - s + lpi - 1) / lpi : 0);
+        if (tr == 1) SWH_BATCH_PAIRS(false, 1);
+        else if (tr == 0) SWH_BATCH_PAIRS(false, 0);
+        else SWH_BATCH_PAIRS(false, 2);
+      } else {
+        SWH_BATCH_PAIRS(true, 2);
       }
+#undef SWH_BATCH_PAIRS
     }
     qb += B;
   }

@@ -270,15 +270,41 @@ __global__ __launch_bounds__(256) void overflow_kernel(GridDev g, SoA a, ListDev
   }
 }
 
+// The ghost's rerun lists, compacted into kSegs segments: workgroup b of a
+// ghost pass appends to segment b % kSegs (capacity cap each), so the
+// returning atomics of a pass spread over kSegs counters instead of all
+// ~2,000 workgroups queueing on one (device-scope atomics on one address
+// serialise at ~60 ns: 0.12 ms per pass over 2M particles). Entry t of the
+// list is entry t - (earlier segments' counts) of its segment.
+constexpr int kSegs = 8;
+struct SegList {
+  const int* idx;
+  const unsigned int* cnt;  // kSegs counts
+  int cap;
+};
+__device__ __forceinline__ int seg_at(const SegList& l, int t) {
+#pragma unroll
+  for (int q = 0; q < kSegs; q++) {
+    const int c = (int)l.cnt[q];
+    if (t < c) return l.idx[(size_t)q * l.cap + t];
+    t -= c;
+  }
+  return -1;
+}
+
 // Density on a subset (the ghost's reruns, runner_ghost.c:1503-1546): LPI
 // lanes per rerun particle walk its list while its H still fits the list
 // reach; any other one (H grown past its reach, list overflow, no lists) is
 // queued for the wave-per-particle search (overflow_kernel). The subset is the
 // ghost's redo list, in (nearly) sorted order.
 template <typename T>
-__global__ __launch_bounds__(256) void walk_subset_kernel(GridDev g, SoA a, ListDev ld,
+__global__ __launch_bounds__(256)
+#if SWH_WALK_WPE_DENS > 0
+__attribute__((amdgpu_waves_per_eu(SWH_WALK_WPE_DENS)))
+#endif
+void walk_subset_kernel(GridDev g, SoA a, ListDev ld,
                                                           int list_ok,
-                                                          const int* __restrict__ subset,
+                                                          SegList subset,
                                                           int nitems, int max_active_bin,
                                                           const unsigned int* __restrict__ hmax_bits,
                                                           unsigned long long* counter,
@@ -287,7 +313,7 @@ __global__ __launch_bounds__(256) void walk_subset_kernel(GridDev g, SoA a, List
   constexpr int LPI = kWalkLpi;
   const int t = (int)blockIdx.x * (256 / LPI) + (int)threadIdx.x / LPI;
   const int s = (int)threadIdx.x % LPI;
-  const int i = t < nitems ? subset[t] : -1;
+  const int i = t < nitems ? seg_at(subset, t) : -1;
   bool act = i >= 0 && active_part(a, i, max_active_bin);
   int nl = 0, lb = -1;
   double4 pi = make_double4(0., 0., 0., 0.);
@@ -500,12 +526,13 @@ __device__ __forceinline__ void ghost_part(SoA& a, int i, bool first, float* lef
 
 // One pass `it` of the ghost: over every active particle (it = 0, whose
 // bisection bounds start at [0, h_max]) or the previous pass's `list`; the
-// particles it queues for a rerun are appended to `redo` (one atomic per
-// workgroup).
+// particles it queues for a rerun are appended to segmented `redo` (one
+// atomic per workgroup on its segment's counter).
 template <typename T>
 __global__ __launch_bounds__(1024) void ghost_kernel(
-    SoA a, const int* __restrict__ list, int count, int max_active_bin, int* __restrict__ redo,
-    int* __restrict__ nredo, float* left, float* right, GhostParams gp, unsigned int* hmax_bits,
+    SoA a, SegList list, int count, int max_active_bin, int* __restrict__ redo,
+    unsigned int* __restrict__ nredo, int cap, float* left, float* right, GhostParams gp,
+    unsigned int* hmax_bits,
     const float* __restrict__ list_reach, unsigned int* ngrown, int* __restrict__ grown_q,
     unsigned int* __restrict__ nstale_redo) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -514,16 +541,17 @@ __global__ __launch_bounds__(1024) void ghost_kernel(
   int i = -1;
   bool first = false;
   if (t < count) {
-    if (list) {
-      i = list[t];
+    if (list.idx) {
+      i = seg_at(list, t);
     } else if (active_part(a, t, max_active_bin)) {
       i = t;
       first = true;
     }
   }
   if (i >= 0) ghost_part<T>(a, i, first, left, right, gp, list_reach, rd, hf, stale);
-  const int slot = block_append(rd, nredo);
-  if (rd) redo[slot] = i;
+  const int seg = (int)(blockIdx.x & (kSegs - 1));
+  const int slot = block_append(rd, nredo + seg);
+  if (rd) redo[(size_t)seg * cap + slot] = i;
   // reruns whose new H outgrew their list reach (they would need the
   // wave-per-particle search): one conditional atomic per wave
   const unsigned long long ms = __ballot(rd && stale);
@@ -843,7 +871,7 @@ static swh_status check_kept_lists(swh_space* s, const swh_hydro_params* P, bool
 }
 
 template <int LOOP, typename T>
-static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int nitems,
+static void launch_typed(swh_space* s, const GridDev& gd, const SegList* subset, int nitems,
                          int max_active_bin, T a2H, unsigned long long* ctr, int* ncount,
                          const unsigned int* mark = nullptr) {
   const int block = 256;
@@ -853,7 +881,7 @@ static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int
   if (subset) {  // density reruns of the ghost: list walks, then the queued searches
     (void)hipMemsetAsync(search_slot(s), 0, sizeof(unsigned int), s->stream);
     hipLaunchKernelGGL((walk_subset_kernel<T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
-                       s->stream, gd, soa_of(s), ld, s->list_valid ? 1 : 0, subset, nitems,
+                       s->stream, gd, soa_of(s), ld, s->list_valid ? 1 : 0, *subset, nitems,
                        max_active_bin, hmax_slot(s), ctr, s->ghost_search.as<int>(),
                        search_slot(s));
     // one wave per queued particle; the queue length is read on the device
@@ -877,7 +905,7 @@ static void launch_typed(swh_space* s, const GridDev& gd, const int* subset, int
 }
 
 template <int LOOP>
-static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const int* subset,
+static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const SegList* subset,
                               int nitems, bool count) {
   if (nitems <= 0) return SWH_OK;
   if (!subset && s->ngroups <= 0) return SWH_OK;
@@ -1025,11 +1053,14 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   hipStream_t st = s->stream;
   SWH_TRY(s->ghost_left.reserve(n * sizeof(float)));
   SWH_TRY(s->ghost_right.reserve(n * sizeof(float)));
-  SWH_TRY(s->ghost_list.reserve(n * sizeof(int)));
-  SWH_TRY(s->ghost_list2.reserve(n * sizeof(int)));
+  // segmented rerun lists: segment capacity = the workgroups a pass over n
+  // particles sends to one segment, x 1024
+  const int cap = (int)(((n + 1023) / 1024 + kSegs - 1) / kSegs) * 1024;
+  SWH_TRY(s->ghost_list.reserve((size_t)kSegs * cap * sizeof(int)));
+  SWH_TRY(s->ghost_list2.reserve((size_t)kSegs * cap * sizeof(int)));
   SWH_TRY(s->ghost_search.reserve(n * sizeof(int)));
   SWH_TRY(s->grown_q.reserve(n * sizeof(int)));
-  int* cnt = s->counters.as<int>() + 4;  // slot 5: rerun count
+  SWH_TRY(s->ghost_seg.reserve(2 * kSegs * sizeof(unsigned int)));
   const int block = 1024;
   GhostParams gp;
   gp.h_max = P->h_max;
@@ -1042,8 +1073,9 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   gp.fac_B = P->a_factor_Balsara_eps;
   // the first pass runs over every particle (inactive ones return at once)
   int count = (int)n;
-  int* list = nullptr;  // first pass: every active particle
-  int* list2 = s->ghost_list.as<int>();
+  SegList list{nullptr, s->ghost_seg.as<unsigned int>(), cap};  // first pass: no list
+  int* out = s->ghost_list.as<int>();
+  unsigned int* out_cnt = s->ghost_seg.as<unsigned int>() + kSegs;
   int* spare = s->ghost_list2.as<int>();
   const bool lists = true;
   SWH_HIP(hipMemsetAsync(stale_slot(s), 0, sizeof(unsigned int), st));
@@ -1057,30 +1089,36 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   for (; count > 0 && it < P->max_smoothing_iterations; it++) {
     if (dbg) SWH_HIP(hipEventRecord(dev[0], st));
     const float* lreach = (lists && s->list_valid) ? s->nbr_reach.as<const float>() : nullptr;
-    SWH_HIP(hipMemsetAsync(cnt + 1, 0, sizeof(int), st));
+    SWH_HIP(hipMemsetAsync(out_cnt, 0, kSegs * sizeof(unsigned int), st));
     SWH_HIP(hipMemsetAsync(stale_redo_slot(s), 0, sizeof(unsigned int), st));
     const int g = (count + block - 1) / block;
     if (s->ctx->precision == SWH_PRECISION_F64)
       hipLaunchKernelGGL(ghost_kernel<double>, dim3(g), dim3(block), 0, st, soa_of(s), list,
-                         count, P->max_active_bin, list2, cnt + 1, s->ghost_left.as<float>(),
+                         count, P->max_active_bin, out, out_cnt, cap, s->ghost_left.as<float>(),
                          s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s),
                          s->grown_q.as<int>(), stale_redo_slot(s));
     else
       hipLaunchKernelGGL(ghost_kernel<float>, dim3(g), dim3(block), 0, st, soa_of(s), list,
-                         count, P->max_active_bin, list2, cnt + 1, s->ghost_left.as<float>(),
+                         count, P->max_active_bin, out, out_cnt, cap, s->ghost_left.as<float>(),
                          s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s),
                          s->grown_q.as<int>(), stale_redo_slot(s));
     SWH_HIP(hipGetLastError());
     if (dbg) SWH_HIP(hipEventRecord(dev[1], st));
     const int count_in = count;
-    unsigned int nstale = 0;
-    SWH_HIP(hipMemcpyAsync(&count, cnt + 1, sizeof(int), hipMemcpyDeviceToHost, st));
-    SWH_HIP(hipMemcpyAsync(&nstale, stale_redo_slot(s), sizeof(nstale), hipMemcpyDeviceToHost, st));
+    unsigned int hc[kSegs + 1];  // segment counts, reruns past reach
+    SWH_HIP(hipMemcpyAsync(hc, out_cnt, kSegs * sizeof(unsigned int), hipMemcpyDeviceToHost, st));
+    SWH_HIP(hipMemcpyAsync(&hc[kSegs], stale_redo_slot(s), sizeof(unsigned int),
+                           hipMemcpyDeviceToHost, st));
     SWH_HIP(hipStreamSynchronize(st));
-    // the new rerun list becomes the input; the old input buffer is reused
-    int* done = list ? list : spare;
-    list = list2;
-    list2 = done;
+    count = 0;
+    for (int k = 0; k < kSegs; k++) count += (int)hc[k];
+    const unsigned int nstale = hc[kSegs];
+    // the new rerun list becomes the input; the old input buffers are reused
+    int* done = list.idx ? const_cast<int*>(list.idx) : spare;
+    unsigned int* done_cnt = const_cast<unsigned int*>(list.cnt);
+    list = SegList{out, out_cnt, cap};
+    out = done;
+    out_cnt = done_cnt;
     const bool many = s->list_valid ? (int64_t)nstale * 8 >= n : (int64_t)count * 8 >= n;
     if (count > 0 && lists && many) {
       // Many reruns whose new H outgrew their list reach (the first iteration
@@ -1093,7 +1131,7 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
       SWH_HIP(hipMemsetAsync(stale_slot(s), 0, sizeof(unsigned int), st));
     }
     if (dbg) SWH_HIP(hipEventRecord(dev[2], st));
-    if (count > 0) SWH_TRY(launch_loop<LOOP_DENSITY>(s, P, list, count, false));
+    if (count > 0) SWH_TRY(launch_loop<LOOP_DENSITY>(s, P, &list, count, false));
     if (dbg) {
       SWH_HIP(hipEventRecord(dev[3], st));
       SWH_HIP(hipEventSynchronize(dev[3]));

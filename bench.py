@@ -922,9 +922,9 @@ def main():
                     help="profiling only, results invalid: 1 tile staging only, 2 + candidate tests")
     ap.add_argument("--group-size", type=int, default=int(os.environ.get("SWH_GROUP_SIZE", "0")),
                     help="tile i-group size / row width: 0 (default 16), 16, 32, 64")
-    ap.add_argument("--list-skin", type=float, default=float(os.environ.get("SWH_LIST_SKIN", "0.02")),
+    ap.add_argument("--list-skin", type=float, default=float(os.environ.get("SWH_LIST_SKIN", "0.01")),
                     help="pair-list reach slack over gamma*h (the library default, "
-                         "SWH_DEFAULT_LIST_SKIN = 0.02)")
+                         "SWH_DEFAULT_LIST_SKIN = 0.01)")
     ap.add_argument("--list-capacity", type=int, default=0, help="pair-list entries per particle")
     ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -1160,7 +1160,7 @@ def main():
         b_force = n_owned * (27 * S_IN_FORCE + S_OUT_FORCE)
         achieved = b_dens / td
         # PMC traffic was measured on the default configuration only
-        default_cfg = (args.loop_variant == 0 and args.group_size == 0 and args.list_skin == 0.02
+        default_cfg = (args.loop_variant == 0 and args.group_size == 0 and args.list_skin == 0.01
                        and args.cell_factor == 1 and args.cell_scale == 0 and args.n == 128
                        and world == 1)
         traffic = load_traffic(args.workload) if default_cfg else None

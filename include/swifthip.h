@@ -354,7 +354,7 @@ SWH_API swh_status swh_space_sync(swh_space *s);
 SWH_API swh_status swh_space_query(swh_space *s);
 
 /* Kernel-tuning knobs of the batch loops (bench/diagnostics). */
-#define SWH_DEFAULT_LIST_SKIN 0.02f
+#define SWH_DEFAULT_LIST_SKIN 0.01f
 typedef struct swh_tuning {
   int32_t cell_factor;  /* neighbour-grid cells per H_max (1..4) */
   int32_t loop_variant; /* 0 or 7: pair lists -- the density loop builds the step's lists
@@ -368,10 +368,11 @@ typedef struct swh_tuning {
   int32_t list_capacity; /* list entries per particle (0 = 128); more hits: a wave-per-
                             particle search */
   float list_skin;       /* relative slack of the list reach over gamma h (SWH_DEFAULT_LIST_SKIN
-                            = 0.02 when the space is created: the ghost's h iterations stay
-                            within the lists' reach, so neither the ghost nor the gradient /
-                            force loops rebuild them; 0: exact lists, rebuilt by the ghost
-                            or the next loop whenever an H outgrows its reach) */
+                            = 0.01 when the space is created: nearly all of the ghost's h
+                            iterations stay within the lists' reach, so the ghost does not
+                            rebuild them, and the gradient / force loops search the few
+                            particles that grew past it; 0: exact lists, rebuilt by the
+                            ghost whenever many H outgrow their reach) */
   int32_t list_keep;     /* 1: keep the lists across loops and drifts while they cover every
                             pair, as SWIFT keeps its sorts until dx_max_sort exceeds
                             space_maxreldx (space.h:66): after a drift the device compares

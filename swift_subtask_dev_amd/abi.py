@@ -98,7 +98,7 @@ XPART_DTYPE = np.dtype(
 
 NUM_TIME_BINS = 56  # src/timeline.h:36
 TIME_BIN_INHIBITED = NUM_TIME_BINS + 2
-DEFAULT_LIST_SKIN = 0.02  # swifthip.h SWH_DEFAULT_LIST_SKIN (swh_tuning.list_skin)
+DEFAULT_LIST_SKIN = 0.01  # swifthip.h SWH_DEFAULT_LIST_SKIN (swh_tuning.list_skin)
 
 
 def new_parts(n: int) -> np.ndarray:

@@ -624,8 +624,10 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
   const int p0 = pair_off[li], p1 = pair_off[li + 1];
   if (p0 == p1) return;  // (inner cells overlap their leaves: leave acc alone)
   const int lane = (int)threadIdx.x;
-  int lpi = 1;  // wave-uniform
-  while (lpi < 8 && L.count * lpi * 2 <= 64) lpi *= 2;
+  // lanes per i: as many as fit (not only powers of two: a 20-gpart leaf
+  // keeps 60 lanes busy with 3, not 40 with 2; 91% of the lanes of a
+  // cosmological tree's leaves against 80%)
+  const int lpi = L.count >= 64 ? 1 : min(8, 64 / max(L.count, 1));  // wave-uniform
   const int il = lane / lpi, s = lane % lpi;
   const int gi = L.start + il;
   const bool act = il < L.count && g.active[gi];
@@ -673,10 +675,8 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
     // in tile-sized chunks.
     const unsigned long long fit = __ballot(cnt > 0 && inc <= kPPBatch);
     const int B = fit ? __popcll(fit) : 1;
-    const int total = __builtin_amdgcn_readlane(inc, B - 1);
+    const unsigned int bmask = B >= 32 ? 0xffffffffu : (1u << B) - 1u;
     const unsigned int tmask = (unsigned int)__ballot(lane < B && tr);
-    // the i-leaf's own gparts among the batch's sources (self terms to drop)
-    const bool own = __any(lane < B && jst < L.start + L.count && L.start < jst + cnt);
     unsigned int mmask = 0;  // the entries this i takes through their multipole
     if (MPOLE) {
       for (unsigned long long m = __ballot(lane < B && am); m; m &= m - 1) {
@@ -687,13 +687,27 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
           mmask |= 1u << q;
       }
     }
+    // Entries every active i takes through the multipole are not staged at
+    // all (the M2P acceptance is nearly always uniform over a small leaf);
+    // only the mixed ones need per-pair masks.
+    unsigned int allm = act ? mmask : 0xffffffffu, anym = act ? mmask : 0u;
+    for (int o = 32; o > 0; o >>= 1) {
+      allm &= (unsigned int)__shfl_xor((int)allm, o);
+      anym |= (unsigned int)__shfl_xor((int)anym, o);
+    }
+    const int cnt2 = (lane < B && ((allm >> lane) & 1u)) ? 0 : cnt;
+    const int inc2 = wave_incl_scan(cnt2);
+    const int total2 = __builtin_amdgcn_readlane(inc2, B - 1);
+    // the i-leaf's own gparts among the staged sources (self terms to drop)
+    const bool own = __any(lane < B && cnt2 > 0 && jst < L.start + L.count && L.start < jst + cnt);
+    const bool mixed = (anym & ~allm & bmask) != 0u;
     // per i: the entries it takes by P2P (inactive i: none)
     const unsigned int pmask = act ? ~mmask : 0u;
-    for (int jb = 0; jb < total; jb += kPPBatch) {
-      const int tn = min(kPPBatch, total - jb);
+    for (int jb = 0; jb < total2; jb += kPPBatch) {
+      const int tn = min(kPPBatch, total2 - jb);
       wave_sync();  // the previous tile's readers are done
       if (lane < B) {
-        boff[lane] = inc - cnt;
+        boff[lane] = inc2 - cnt2;  // (an unstaged entry: its successor's offset)
         bstart[lane] = jst;
       }
       wave_sync();
@@ -726,12 +740,11 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
       const double emax = act ? fmax(hi2, wave_max_f64(e2max)) : 0.;
       const bool wrap = periodic && __any(far);
       wave_sync();
-      // Wave-uniform fast paths: no lane takes a multipole of this batch and
-      // the i-leaf is none of its sources (no self term) -> no per-pair mask,
-      // and the pairs are counted per lane; every or no entry truncated -> no
-      // per-pair truncation bit.
-      const unsigned int bmask = B >= 32 ? 0xffffffffu : (1u << B) - 1u;
-      const bool plain = !__any(act && (mmask & bmask) != 0u) && !own;
+      // Wave-uniform fast paths: no staged entry is a multipole for some of
+      // the i's only and the i-leaf is none of the sources (no self term) ->
+      // no per-pair mask, the pairs counted per lane; every or no entry
+      // truncated -> no per-pair truncation bit.
+      const bool plain = !mixed && !own;
       const int tr = (tmask & bmask) == bmask ? 1 : (tmask & bmask) == 0u ? 0 : 2;
       const PairCtx pc{pi, hi2, hv, emax, tworsi, dimx, dimy, dimz, idimx, idimy, idimz};
       const TileLds tl{sx, sy, sz, seps, sm, sg, sb};
@@ -749,11 +762,15 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
     }
     qb += B;
   }
-  for (int o = 1; o < lpi; o <<= 1) {  // combine the LPI lanes of each i
-    ax += __shfl_xor(ax, o);
-    ay += __shfl_xor(ay, o);
-    az += __shfl_xor(az, o);
-    pot += __shfl_xor(pot, o);
+  // combine the LPI lanes of each i into its first (lane il * lpi)
+  {
+    const double bx = ax, by = ay, bz = az, bp = pot;
+    for (int o = 1; o < lpi; o++) {
+      ax += __shfl(bx, lane + o);
+      ay += __shfl(by, lane + o);
+      az += __shfl(bz, lane + o);
+      pot += __shfl(bp, lane + o);
+    }
   }
   if (act && s == 0) {
     double4 a = g.acc[gi];
@@ -891,8 +908,7 @@ __global__ __launch_bounds__(kGravBlock) void m2p_kernel(
     // chain per step, and every M2P evaluation has its lanes busy.
     __shared__ int cj[64];
     __shared__ unsigned char ctr[64];
-    int lpi = 1;  // wave-uniform
-    while (lpi < 8 && L.count * lpi * 2 <= 64) lpi *= 2;
+    const int lpi = L.count >= 64 ? 1 : min(8, 64 / max(L.count, 1));  // wave-uniform
     const int lane = (int)threadIdx.x;
     const int s = lane % lpi, il = lane / lpi;
     const int i = L.start + il;
@@ -936,8 +952,11 @@ __global__ __launch_bounds__(kGravBlock) void m2p_kernel(
         nm++;
       }
     }
-    for (int o = 1; o < lpi; o <<= 1)
-      for (int c = 0; c < 4; c++) F[c] += __shfl_xor(F[c], o);
+    {
+      T B[4] = {F[0], F[1], F[2], F[3]};
+      for (int o = 1; o < lpi; o++)
+        for (int c = 0; c < 4; c++) F[c] += __shfl(B[c], lane + o);
+    }
     if (act && s == 0 && (F[0] != (T)0 || F[1] != (T)0 || F[2] != (T)0 || F[3] != (T)0)) {
       double4 a = g.acc[i];
       a.x += (double)F[1];

@@ -282,6 +282,12 @@ struct SegList {
   const unsigned int* cnt;  // kSegs counts
   int cap;
 };
+__device__ __forceinline__ int seg_total(const SegList& l) {
+  int c = 0;
+#pragma unroll
+  for (int q = 0; q < kSegs; q++) c += (int)l.cnt[q];
+  return c;
+}
 __device__ __forceinline__ int seg_at(const SegList& l, int t) {
 #pragma unroll
   for (int q = 0; q < kSegs; q++) {
@@ -305,12 +311,18 @@ __attribute__((amdgpu_waves_per_eu(SWH_WALK_WPE_DENS)))
 void walk_subset_kernel(GridDev g, SoA a, ListDev ld,
                                                           int list_ok,
                                                           SegList subset,
-                                                          int nitems, int max_active_bin,
+                                                          unsigned int* __restrict__ zero_next,
+                                                          int max_active_bin,
                                                           const unsigned int* __restrict__ hmax_bits,
                                                           unsigned long long* counter,
                                                           int* __restrict__ searchq,
                                                           unsigned int* nsearch) {
   constexpr int LPI = kWalkLpi;
+  // the next ghost pass's output counters (not read by this rerun or the
+  // pass before it): cleared here instead of by a separate launch
+  if (zero_next && blockIdx.x == 0 && threadIdx.x <= kSegs) zero_next[threadIdx.x] = 0u;
+  // the grid may be an upper bound: the count is the device's
+  const int nitems = seg_total(subset);
   const int t = (int)blockIdx.x * (256 / LPI) + (int)threadIdx.x / LPI;
   const int s = (int)threadIdx.x % LPI;
   const int i = t < nitems ? seg_at(subset, t) : -1;
@@ -524,18 +536,23 @@ __device__ __forceinline__ void ghost_part(SoA& a, int i, bool first, float* lef
   a.grad[i] = g;
 }
 
-// One pass `it` of the ghost: over every active particle (it = 0, whose
+// One pass of the ghost: over every active particle (the first, whose
 // bisection bounds start at [0, h_max]) or the previous pass's `list`; the
 // particles it queues for a rerun are appended to segmented `redo` (one
-// atomic per workgroup on its segment's counter).
+// atomic per workgroup on its segment's counter; nredo[kSegs] counts the
+// reruns past their list reach).
 template <typename T>
 __global__ __launch_bounds__(1024) void ghost_kernel(
     SoA a, SegList list, int count, int max_active_bin, int* __restrict__ redo,
-    unsigned int* __restrict__ nredo, int cap, float* left, float* right, GhostParams gp,
-    unsigned int* hmax_bits,
-    const float* __restrict__ list_reach, unsigned int* ngrown, int* __restrict__ grown_q,
-    unsigned int* __restrict__ nstale_redo) {
+    unsigned int* __restrict__ nredo, int cap, unsigned int* __restrict__ nsearch,
+    float* left, float* right, GhostParams gp, unsigned int* hmax_bits,
+    const float* __restrict__ list_reach, unsigned int* ngrown, int* __restrict__ grown_q) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  // the rerun after this pass appends its searches from zero (the previous
+  // rerun's search has run: same stream)
+  if (t == 0) *nsearch = 0u;
+  // a list pass's grid may be an upper bound: its count is the device's
+  if (list.idx) count = seg_total(list);
   bool rd = false, stale = false;
   float hf = 0.f;
   int i = -1;
@@ -555,7 +572,7 @@ __global__ __launch_bounds__(1024) void ghost_kernel(
   // reruns whose new H outgrew their list reach (they would need the
   // wave-per-particle search): one conditional atomic per wave
   const unsigned long long ms = __ballot(rd && stale);
-  if ((threadIdx.x & 63) == 0 && ms) atomicAdd(nstale_redo, (unsigned int)__popcll(ms));
+  if ((threadIdx.x & 63) == 0 && ms) atomicAdd(nredo + kSegs, (unsigned int)__popcll(ms));
   // converged particles whose H outgrew their list reach: queued (few; one
   // atomic per wave that has any) for the gradient / force loops' searches
   stale = stale && !rd;
@@ -762,8 +779,7 @@ constexpr int kGrownSearchMax = 256;
 // u32[28]: the grown particles' search queue (grown_mark_kernel)
 static unsigned int* grown_qn_slot(swh_space* s) { return s->counters.as<unsigned int>() + 28; }
 static unsigned int* search_slot(swh_space* s) { return s->counters.as<unsigned int>() + 20; }
-// u32[22]: the ghost pass's reruns whose new H outgrew their list reach
-static unsigned int* stale_redo_slot(swh_space* s) { return s->counters.as<unsigned int>() + 22; }
+
 // (u32[19]: the drift's displacement, u32[21]: max |v_full|, swh_space.hip)
 // u32[24]: kept lists found stale by the device check; u32[25]: displacement
 // since the list build (float bits); u32[26]: list builds run on the device;
@@ -879,11 +895,12 @@ static void launch_typed(swh_space* s, const GridDev& gd, const SegList* subset,
   ld.mark = mark;
   constexpr int ppb = block / kWalkLpi;
   if (subset) {  // density reruns of the ghost: list walks, then the queued searches
-    (void)hipMemsetAsync(search_slot(s), 0, sizeof(unsigned int), s->stream);
+    // (nitems: an upper bound of the device's count; the ghost pass cleared
+    // the search counter)
     hipLaunchKernelGGL((walk_subset_kernel<T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
-                       s->stream, gd, soa_of(s), ld, s->list_valid ? 1 : 0, *subset, nitems,
-                       max_active_bin, hmax_slot(s), ctr, s->ghost_search.as<int>(),
-                       search_slot(s));
+                       s->stream, gd, soa_of(s), ld, s->list_valid ? 1 : 0, *subset,
+                       s->ghost_zero_next, max_active_bin, hmax_slot(s), ctr,
+                       s->ghost_search.as<int>(), search_slot(s));
     // one wave per queued particle; the queue length is read on the device
     const int sblocks = std::max(1, std::min(2048, (nitems + 3) / 4));
     hipLaunchKernelGGL((overflow_kernel<LOOP_DENSITY, T>), dim3(sblocks), dim3(block), 0,
@@ -1060,7 +1077,9 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   SWH_TRY(s->ghost_list2.reserve((size_t)kSegs * cap * sizeof(int)));
   SWH_TRY(s->ghost_search.reserve(n * sizeof(int)));
   SWH_TRY(s->grown_q.reserve(n * sizeof(int)));
-  SWH_TRY(s->ghost_seg.reserve(2 * kSegs * sizeof(unsigned int)));
+  constexpr int kCnt = kSegs + 1;  // a pass's segment counts + its reruns past reach
+  SWH_TRY(s->ghost_seg.reserve(2 * kCnt * sizeof(unsigned int)));
+  SWH_TRY(s->ghost_host.reserve(64 * kCnt * sizeof(unsigned int)));
   const int block = 1024;
   GhostParams gp;
   gp.h_max = P->h_max;
@@ -1071,78 +1090,123 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
   gp.a2_inv = P->a2_inv;
   gp.H = P->H;
   gp.fac_B = P->a_factor_Balsara_eps;
-  // the first pass runs over every particle (inactive ones return at once)
-  int count = (int)n;
-  SegList list{nullptr, s->ghost_seg.as<unsigned int>(), cap};  // first pass: no list
-  int* out = s->ghost_list.as<int>();
-  unsigned int* out_cnt = s->ghost_seg.as<unsigned int>() + kSegs;
-  int* spare = s->ghost_list2.as<int>();
+  // Pass k writes rerun list L[k % 2] with counts C[k % 2]; its rerun walks
+  // them and clears C[(k + 1) % 2] for pass k + 1. The first pass is
+  // synchronous (its count of reruns past their list reach decides a list
+  // rebuild); later passes are pipelined: pass k, the copy of its counts,
+  // and its rerun (grid sized by pass k - 1's count, the device reading the
+  // real one) are queued before the host waits for pass k's count, so the
+  // GPU runs the rerun while the host reads -- a pass with no reruns costs
+  // an empty rerun launch, not a host round trip per pass.
+  int* L[2] = {s->ghost_list.as<int>(), s->ghost_list2.as<int>()};
+  unsigned int* Cn[2] = {s->ghost_seg.as<unsigned int>(), s->ghost_seg.as<unsigned int>() + kCnt};
+  unsigned int* hc = static_cast<unsigned int*>(s->ghost_host.ptr);
   const bool lists = true;
   SWH_HIP(hipMemsetAsync(stale_slot(s), 0, sizeof(unsigned int), st));
-  // profiling only (SWH_GHOST_DEBUG): per iteration the rerun count, the
-  // reruns past their list reach, and the ghost / rebuild / rerun times
+  SWH_HIP(hipMemsetAsync(Cn[0], 0, 2 * kCnt * sizeof(unsigned int), st));
+  // profiling only (SWH_GHOST_DEBUG): per pass the rerun count, the reruns
+  // past their list reach, and the ghost / host + rebuild / rerun times (the
+  // passes then run synchronously)
   static const bool dbg = std::getenv("SWH_GHOST_DEBUG") != nullptr;
   hipEvent_t dev[4] = {nullptr, nullptr, nullptr, nullptr};
   if (dbg)
     for (auto& e : dev) SWH_HIP(hipEventCreate(&e));
-  int it = 0;
-  for (; count > 0 && it < P->max_smoothing_iterations; it++) {
-    if (dbg) SWH_HIP(hipEventRecord(dev[0], st));
+  // the copies of the passes' counts (the host waits on these, not the stream)
+  struct CountEvents {
+    hipEvent_t e[2] = {nullptr, nullptr};
+    ~CountEvents() {
+      for (auto& x : e)
+        if (x) (void)hipEventDestroy(x);
+    }
+    hipEvent_t& operator[](int k) { return e[k]; }
+  } ev_cnt;
+  for (int k = 0; k < 2; k++) SWH_HIP(hipEventCreateWithFlags(&ev_cnt.e[k], hipEventDisableTiming));
+  auto launch_pass = [&](int k, const SegList& in, int grid_items) -> swh_status {
     const float* lreach = (lists && s->list_valid) ? s->nbr_reach.as<const float>() : nullptr;
-    SWH_HIP(hipMemsetAsync(out_cnt, 0, kSegs * sizeof(unsigned int), st));
-    SWH_HIP(hipMemsetAsync(stale_redo_slot(s), 0, sizeof(unsigned int), st));
-    const int g = (count + block - 1) / block;
+    const int g = (grid_items + block - 1) / block;
     if (s->ctx->precision == SWH_PRECISION_F64)
-      hipLaunchKernelGGL(ghost_kernel<double>, dim3(g), dim3(block), 0, st, soa_of(s), list,
-                         count, P->max_active_bin, out, out_cnt, cap, s->ghost_left.as<float>(),
-                         s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s),
-                         s->grown_q.as<int>(), stale_redo_slot(s));
+      hipLaunchKernelGGL(ghost_kernel<double>, dim3(g), dim3(block), 0, st, soa_of(s), in,
+                         grid_items, P->max_active_bin, L[k & 1], Cn[k & 1], cap,
+                         search_slot(s), s->ghost_left.as<float>(), s->ghost_right.as<float>(),
+                         gp, hmax_slot(s), lreach, stale_slot(s), s->grown_q.as<int>());
     else
-      hipLaunchKernelGGL(ghost_kernel<float>, dim3(g), dim3(block), 0, st, soa_of(s), list,
-                         count, P->max_active_bin, out, out_cnt, cap, s->ghost_left.as<float>(),
-                         s->ghost_right.as<float>(), gp, hmax_slot(s), lreach, stale_slot(s),
-                         s->grown_q.as<int>(), stale_redo_slot(s));
+      hipLaunchKernelGGL(ghost_kernel<float>, dim3(g), dim3(block), 0, st, soa_of(s), in,
+                         grid_items, P->max_active_bin, L[k & 1], Cn[k & 1], cap,
+                         search_slot(s), s->ghost_left.as<float>(), s->ghost_right.as<float>(),
+                         gp, hmax_slot(s), lreach, stale_slot(s), s->grown_q.as<int>());
     SWH_HIP(hipGetLastError());
-    if (dbg) SWH_HIP(hipEventRecord(dev[1], st));
-    const int count_in = count;
-    unsigned int hc[kSegs + 1];  // segment counts, reruns past reach
-    SWH_HIP(hipMemcpyAsync(hc, out_cnt, kSegs * sizeof(unsigned int), hipMemcpyDeviceToHost, st));
-    SWH_HIP(hipMemcpyAsync(&hc[kSegs], stale_redo_slot(s), sizeof(unsigned int),
+    SWH_HIP(hipMemcpyAsync(hc + (k % 64) * kCnt, Cn[k & 1], kCnt * sizeof(unsigned int),
                            hipMemcpyDeviceToHost, st));
+    SWH_HIP(hipEventRecord(ev_cnt[k & 1], st));
+    return SWH_OK;
+  };
+  auto rerun = [&](int k, int grid_items) -> swh_status {
+    const SegList list{L[k & 1], Cn[k & 1], cap};
+    s->ghost_zero_next = Cn[(k + 1) & 1];
+    const swh_status r = launch_loop<LOOP_DENSITY>(s, P, &list, grid_items, false);
+    s->ghost_zero_next = nullptr;
+    return r;
+  };
+  auto total = [&](int k) {
+    int c = 0;
+    for (int q = 0; q < kSegs; q++) c += (int)hc[(k % 64) * kCnt + q];
+    return c;
+  };
+  auto debug_line = [&](int k, int in, int out, bool rebuilt) {
+    if (!dbg) return;
+    (void)hipEventSynchronize(dev[3]);
+    float ms[3] = {0.f, 0.f, 0.f};
+    for (int q = 0; q < 3; q++) (void)hipEventElapsedTime(&ms[q], dev[q], dev[q + 1]);
+    std::fprintf(stderr,
+                 "[swh ghost] it %d: in %d, rerun %d, past reach %u, rebuilt %d | ghost %.3f "
+                 "ms, host + rebuild %.3f ms, rerun %.3f ms\n",
+                 k, in, out, hc[(k % 64) * kCnt + kSegs], (int)rebuilt, ms[0], ms[1], ms[2]);
+  };
+  // pass 0 (synchronous)
+  int it = 0, count = 0;
+  if (P->max_smoothing_iterations > 0) {
+    if (dbg) SWH_HIP(hipEventRecord(dev[0], st));
+    SWH_TRY(launch_pass(0, SegList{nullptr, Cn[1], cap}, (int)n));
+    if (dbg) SWH_HIP(hipEventRecord(dev[1], st));
     SWH_HIP(hipStreamSynchronize(st));
-    count = 0;
-    for (int k = 0; k < kSegs; k++) count += (int)hc[k];
+    count = total(0);
     const unsigned int nstale = hc[kSegs];
-    // the new rerun list becomes the input; the old input buffers are reused
-    int* done = list.idx ? const_cast<int*>(list.idx) : spare;
-    unsigned int* done_cnt = const_cast<unsigned int*>(list.cnt);
-    list = SegList{out, out_cnt, cap};
-    out = done;
-    out_cnt = done_cnt;
+    it = 1;
     const bool many = s->list_valid ? (int64_t)nstale * 8 >= n : (int64_t)count * 8 >= n;
     if (count > 0 && lists && many) {
-      // Many reruns whose new H outgrew their list reach (the first iteration
-      // after a drift with exact lists: every growing h): rebuild the lists
-      // for the new h, with a 1% skin so the few later iterations' changes
-      // stay within reach and the gradient / force loops keep them, then
-      // walk. Lists built with a skin (swh_tuning.list_skin) usually cover
-      // the reruns: they walk the lists, the few outgrown ones are searched.
+      // Many reruns whose new H outgrew their list reach (the first pass after
+      // a drift with exact lists: every growing h): rebuild the lists for the
+      // new h, with a 1% skin so the few later passes' changes stay within
+      // reach and the gradient / force loops keep them, then walk. Lists built
+      // with a skin (swh_tuning.list_skin, 2% by default) cover the reruns:
+      // they walk the lists, the few outgrown ones are searched.
       SWH_TRY(build_lists(s, P, false, std::max(s->tuning.list_skin, kGhostListSkin)));
       SWH_HIP(hipMemsetAsync(stale_slot(s), 0, sizeof(unsigned int), st));
     }
     if (dbg) SWH_HIP(hipEventRecord(dev[2], st));
-    if (count > 0) SWH_TRY(launch_loop<LOOP_DENSITY>(s, P, &list, count, false));
+    if (count > 0) SWH_TRY(rerun(0, count));
+    if (dbg) SWH_HIP(hipEventRecord(dev[3], st));
+    debug_line(0, (int)n, count, count > 0 && lists && many);
+  }
+  // passes 1, 2, ... (pipelined)
+  while (count > 0 && it < P->max_smoothing_iterations) {
+    const int k = it;
+    const SegList in{L[(k - 1) & 1], Cn[(k - 1) & 1], cap};
+    if (dbg) SWH_HIP(hipEventRecord(dev[0], st));
+    SWH_TRY(launch_pass(k, in, count));
     if (dbg) {
-      SWH_HIP(hipEventRecord(dev[3], st));
-      SWH_HIP(hipEventSynchronize(dev[3]));
-      float ms[3] = {0.f, 0.f, 0.f};
-      for (int k = 0; k < 3; k++) (void)hipEventElapsedTime(&ms[k], dev[k], dev[k + 1]);
-      std::fprintf(stderr,
-                   "[swh ghost] it %d: in %d, rerun %d, past reach %u, rebuilt %d | ghost "
-                   "%.3f ms, host + rebuild %.3f ms, rerun %.3f ms\n",
-                   it, count_in, count, nstale,
-                   (int)(count > 0 && lists && many), ms[0], ms[1], ms[2]);
+      SWH_HIP(hipEventRecord(dev[1], st));
+      SWH_HIP(hipEventRecord(dev[2], st));
     }
+    SWH_TRY(rerun(k, count));  // (pass k's reruns are at most its input)
+    if (dbg) SWH_HIP(hipEventRecord(dev[3], st));
+    // the counts of pass k: their copy follows pass k on the stream, ahead
+    // of the rerun just queued, which the GPU runs meanwhile
+    SWH_HIP(hipEventSynchronize(ev_cnt[k & 1]));
+    const int in_count = count;
+    count = total(k);
+    it = k + 1;
+    debug_line(k, in_count, count, false);
   }
   if (dbg)
     for (auto& e : dev) (void)hipEventDestroy(e);
@@ -1159,6 +1223,9 @@ swh_status swh_ghost(swh_space* s, const swh_hydro_params* P, int32_t* iteration
       if ((int64_t)c[17] * kGrownSearchMax > n) s->list_valid = false;
       else s->grown_n = (int32_t)c[17];
     }
+    if (dbg)
+      std::fprintf(stderr, "[swh ghost] converged past their list reach: %u (%s)\n", c[17],
+                   !c[17] ? "-" : s->grown_n ? "searched" : "lists rebuilt");
     float hmax;
     std::memcpy(&hmax, &c[2], sizeof(hmax));
     // a kernel reach of half the periodic box or more would need more than

@@ -221,7 +221,9 @@ struct swh_space {
   swh::DevBuf ctr_stripes;  // counted launches' per-block counter stripes (swh_hydro.hip)
   swh::DevBuf tmp_soa;     // staging for permutation gathers
   swh::DevBuf ghost_left, ghost_right, ghost_list, ghost_list2, ghost_search;
-  swh::DevBuf ghost_seg;  // 2 x kSegs segment counts of the ghost's rerun lists
+  swh::DevBuf ghost_seg;  // 2 x (kSegs + 1) counts of the ghost's rerun lists
+  swh::HostBuf ghost_host;  // pinned: the passes' counts read back
+  unsigned int* ghost_zero_next = nullptr;  // cleared by the rerun launch (swh_ghost)
   swh::HostBuf hstage;
 };
 

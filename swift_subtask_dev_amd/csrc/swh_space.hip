@@ -691,6 +691,7 @@ swh_status swh_space_destroy(swh_space* s) {
                     &s->iperm, &s->vfull_s, &s->agrav_s, &s->hasg_s, &s->list_xd0};
   for (DevBuf* b : bufs) b->release();
   s->hstage.release();
+  s->ghost_host.release();
   if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
   return SWH_OK;

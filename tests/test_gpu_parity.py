@@ -789,7 +789,7 @@ def test_density_list_reuse(gpu_ctx):
 @pytest.mark.parametrize("adaptive", [False, True])
 def test_chain_few_grown_searched(gpu_ctx, request, adaptive):
     """Converged smoothing lengths with a few cut by 30%: the ghost grows those
-    back past their list reach (skin 2%), too few to rebuild every list, so
+    back past their list reach (skin 1%), too few to rebuild every list, so
     the gradient loop searches them and the force loop also their neighbours
     within the grown H (grown_mark_kernel): one list build in the chain, and
     the chain still equals the oracle's. The clustered box runs the adaptive

@@ -13,6 +13,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/${tag}_trace" -o run
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex "$KREGEX" -d "$out/${tag}_pmc_$c" \
     -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 5 --warmup 1 \
+    --no-steady --no-breakdown \
     > "$out/${tag}_pmc_$c.log" 2>&1 || exit $?
 done
 echo "profile $tag done"

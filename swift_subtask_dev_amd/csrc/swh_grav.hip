@@ -886,9 +886,9 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
 // runner_doiact_grav.c:911-1200): every active i of the i-leaf that passes
 // the MAC against source leaf j's multipole. Runs after p2p_kernel on the
 // same stream (both add into acc).
-// SMALL (every leaf <= 64 gparts, one wave per leaf): LPI lanes per i split
-// the leaf's compacted allow_mpole entries and combine their sums, as
-// p2p_batch_kernel does; otherwise a thread per i walks the whole list.
+// SMALL (every leaf <= 64 gparts, one wave per leaf): the accepted (i,
+// entry) pairs are queued and evaluated 64 at a time; otherwise a thread per
+// i walks the whole list.
 template <typename T, bool SMALL>
 __global__ __launch_bounds__(kGravBlock) void m2p_kernel(
     GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
@@ -900,22 +900,30 @@ __global__ __launch_bounds__(kGravBlock) void m2p_kernel(
   if (p0 == p1) return;  // no sources (a tree's inner cells)
   unsigned long long nm = 0;
   if (SMALL) {
-    // One wave per leaf, LPI lanes per i. The P-P entries are read 64 at a
+    // One wave per leaf (<= 64 gparts). The P-P entries are read 64 at a
     // time (one per lane, loads in parallel) and their allow_mpole ones --
-    // ~7% of a cosmological tree's entries -- compacted into LDS; lane s of
-    // each i then takes compacted entries s, s + LPI, ..., so the wave no
-    // longer steps through the other 93% with a dependent pair -> leaf load
-    // chain per step, and every M2P evaluation has its lanes busy.
+    // ~7% of a cosmological tree's entries -- compacted into LDS. Then the
+    // wave tests every (i, entry) pair of the chunk against the MAC, a lane
+    // per entry and i by i, and queues the accepted pairs i-major; the
+    // queue is evaluated 64 pairs at a time with every lane busy (the M2P,
+    // ~500 fp64 instructions, no longer runs with only the lanes whose pair
+    // passed enabled), and each i's terms are summed by a segmented scan
+    // over its contiguous run of the round, then into its LDS accumulator
+    // by the run's last lane: one writer per i per round, in queue order.
+    __shared__ float4 spi[64];  // i: float position and softening (the MAC's inputs)
+    __shared__ float soag[64];  // i: old |a|
     __shared__ int cj[64];
     __shared__ unsigned char ctr[64];
-    const int lpi = L.count >= 64 ? 1 : min(8, 64 / max(L.count, 1));  // wave-uniform
+    __shared__ unsigned short q[64 * 64];  // accepted pairs: i << 8 | entry
+    __shared__ T accs[4][64];
     const int lane = (int)threadIdx.x;
-    const int s = lane % lpi, il = lane / lpi;
-    const int i = L.start + il;
-    const bool act = il < L.count && g.active[i];
-    const double4 p = act ? g.pos[i] : make_double4(0., 0., 0., 1.);
-    const float oag = act ? g.oagn[i] : 0.f;
-    T F[4] = {(T)0, (T)0, (T)0, (T)0};
+    const int gi = L.start + lane;
+    const bool acti = lane < L.count && g.active[gi];
+    const double4 pl = acti ? g.pos[gi] : make_double4(0., 0., 0., 1.);
+    spi[lane] = make_float4((float)pl.x, (float)pl.y, (float)pl.z, (float)pl.w);
+    soag[lane] = acti ? g.oagn[gi] : 0.f;
+    for (int c = 0; c < 4; c++) accs[c][lane] = (T)0;
+    const unsigned long long actm = __ballot(acti);
     for (int qb = p0; qb < p1; qb += 64) {
       bool am = false;
       int jl = 0;
@@ -935,40 +943,65 @@ __global__ __launch_bounds__(kGravBlock) void m2p_kernel(
         ctr[r] = tr;
       }
       wave_sync();
-      for (int k = s; act && k < nme; k += lpi) {
-        const swh_multipole& M = g.mp[cj[k]];
-        if (!m2p_accept(mac, mac_source(M), (float)p.x, (float)p.y, (float)p.z, (float)p.w, oag))
-          continue;
-        double dx = M.CoM[0] - p.x, dy = M.CoM[1] - p.y, dz = M.CoM[2] - p.z;
-        if (periodic) {
-          dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
-          dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
-          dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
+      if (nme == 0) continue;
+      MacSource B{};
+      if (lane < nme) B = mac_source(g.mp[cj[lane]]);
+      int nq = 0;
+      for (unsigned long long am_i = actm; am_i; am_i &= am_i - 1) {
+        const int il = __ffsll((long long)am_i) - 1;
+        const float4 p = spi[il];
+        const bool ok = lane < nme && m2p_accept(mac, B, p.x, p.y, p.z, p.w, soag[il]);
+        const unsigned long long okm = __ballot(ok);
+        if (ok) q[nq + __popcll(okm & ((1ull << lane) - 1ull))] = (unsigned short)(il << 8 | lane);
+        nq += __popcll(okm);
+      }
+      wave_sync();
+      nm += (unsigned long long)nq;
+      for (int r0 = 0; r0 < nq; r0 += 64) {
+        const int it = r0 + lane;
+        const bool valid = it < nq;
+        int il = -1;
+        T f[4] = {(T)0, (T)0, (T)0, (T)0};
+        if (valid) {
+          const unsigned int e = q[it];
+          il = (int)(e >> 8);
+          const int k = (int)(e & 255u);
+          const swh_multipole& M = g.mp[cj[k]];
+          const double4 p = g.pos[L.start + il];
+          double dx = M.CoM[0] - p.x, dy = M.CoM[1] - p.y, dz = M.CoM[2] - p.z;
+          if (periodic) {
+            dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
+            dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
+            dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
+          }
+          const T eps = (T)fmaxf((float)p.w, M.max_softening);
+          m2p<T>(M.M, (T)dx, (T)dy, (T)dz, eps, ctr[k] != 0, (T)r_s_inv, f);
         }
-        const T eps = (T)fmaxf((float)p.w, M.max_softening);
-        T f[4];
-        m2p<T>(M.M, (T)dx, (T)dy, (T)dz, eps, ctr[k] != 0, (T)r_s_inv, f);
-        for (int c = 0; c < 4; c++) F[c] += f[c];
-        nm++;
+        // segmented inclusive scan over the round's runs of equal i
+        for (int o = 1; o < 64; o <<= 1) {
+          const int u = __shfl_up(il, o);
+          T v[4];
+          for (int c = 0; c < 4; c++) v[c] = __shfl_up(f[c], o);
+          if (lane >= o && u == il)
+            for (int c = 0; c < 4; c++) f[c] += v[c];
+        }
+        const int nxt = __shfl_down(il, 1);
+        if (valid && (lane == 63 || it + 1 >= nq || nxt != il))
+          for (int c = 0; c < 4; c++) accs[c][il] += f[c];
+        wave_sync();
       }
     }
-    {
-      T B[4] = {F[0], F[1], F[2], F[3]};
-      for (int o = 1; o < lpi; o++)
-        for (int c = 0; c < 4; c++) F[c] += __shfl(B[c], lane + o);
-    }
-    if (act && s == 0 && (F[0] != (T)0 || F[1] != (T)0 || F[2] != (T)0 || F[3] != (T)0)) {
-      double4 a = g.acc[i];
+    wave_sync();
+    const T F[4] = {accs[0][lane], accs[1][lane], accs[2][lane], accs[3][lane]};
+    if (acti && (F[0] != (T)0 || F[1] != (T)0 || F[2] != (T)0 || F[3] != (T)0)) {
+      double4 a = g.acc[gi];
       a.x += (double)F[1];
       a.y += (double)F[2];
       a.z += (double)F[3];
       a.w += (double)F[0];
-      g.acc[i] = a;
+      g.acc[gi] = a;
     }
-    if (counter) {
-      for (int o = 32; o > 0; o >>= 1) nm += __shfl_xor(nm, o);
-      if (lane == 0 && nm) atomicAdd(counter + 1, nm);
-    }
+    if (counter && lane == 0 && nm) atomicAdd(counter + 1, nm);
     return;
   }
   // large leaves: a thread per i over the leaf's whole entry list

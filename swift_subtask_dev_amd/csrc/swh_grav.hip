@@ -283,9 +283,12 @@ __device__ __forceinline__ void p2p_soften(double r2, double r_inv, double e2i, 
   pot_ij = mh * grav_pot_eval(ui);
 }
 // exp(-x) for x >= 0 (the truncation's argument, a finite distance ratio):
-// Cody-Waite reduction by ln 2 (fdlibm's split) and a degree-11 Taylor
-// polynomial on |f| <= ln2/2, ~6e-15 relative; no overflow / NaN handling,
-// so it is 16 instructions where the library exp takes ~30.
+// Cody-Waite reduction by ln 2 (fdlibm's split), then e^f = 1 + f (1 + f q(f))
+// on |f| <= ln2/2 with q of degree 7 fitted for the least maximum relative
+// error (Lawson-weighted least squares on 2,000 Chebyshev nodes against
+// 40-digit values; max relative error 1.7e-14 checked on 40,001 points):
+// 14 instructions where the library exp takes ~30, no overflow / NaN
+// handling.
 // (Horner steps as three-operand v_fma_f64: the compiler otherwise copies
 // each loop-invariant coefficient register before a two-operand v_fmac_f64,
 // a move per term.)
@@ -304,17 +307,14 @@ template <bool FMA3>
 __device__ __forceinline__ double exp_neg_f64(double x) {
   const double k = __builtin_rint(x * -1.4426950408889634);  // -x / ln 2
   const double f = fma(k, -1.90821492927058770002e-10, fma(k, -6.93147180369123816490e-01, -x));
-  double p = horner_step<FMA3>(1. / 39916800., f, 1. / 3628800.);
-  p = horner_step<FMA3>(p, f, 1. / 362880.);
-  p = horner_step<FMA3>(p, f, 1. / 40320.);
-  p = horner_step<FMA3>(p, f, 1. / 5040.);
-  p = horner_step<FMA3>(p, f, 1. / 720.);
-  p = horner_step<FMA3>(p, f, 1. / 120.);
-  p = horner_step<FMA3>(p, f, 1. / 24.);
-  p = horner_step<FMA3>(p, f, 1. / 6.);
-  p = fma(p, f, 0.5);
-  p = fma(p, f, 1.);
-  p = fma(p, f, 1.);
+  double q = horner_step<FMA3>(2.749299850055968e-06, f, 2.4880793243238282e-05);
+  q = horner_step<FMA3>(q, f, 0.00019841539149942946);
+  q = horner_step<FMA3>(q, f, 0.0013888811176925341);
+  q = horner_step<FMA3>(q, f, 0.008333333095125245);
+  q = horner_step<FMA3>(q, f, 0.04166666696206109);
+  q = horner_step<FMA3>(q, f, 0.16666666667264937);
+  q = horner_step<FMA3>(q, f, 0.49999999999664524);
+  const double p = fma(f, fma(f, q, 1.), 1.);
   return __builtin_ldexp(p, (int)k);
 }
 

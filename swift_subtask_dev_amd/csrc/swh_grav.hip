@@ -448,6 +448,10 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(MPOLE ? 3 :
       hv[k] = act[k] ? g.hinv[gi[k]] : 1.;
       ax[k] = ay[k] = az[k] = pot[k] = 0.;
     }
+    bool anyk = false;  // an i-slot past the first occupied in this wave
+#pragma unroll
+    for (int k = 1; k < IPER; k++) anyk = anyk || act[k];
+    const bool full = __any(anyk);
     for (int q = p0; q < p1; q++) {
       const swh_leaf_pair pr = pairs[q];
       const swh_leaf J = leaves[pr.j];
@@ -490,9 +494,20 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(MPOLE ? 3 :
           if (actp[k])
             nint += (unsigned long long)(nt - ((self_local[k] >= 0 && self_local[k] < nt) ? 1 : 0));
         }
+// (a wave none of whose i-slots past the first is occupied -- the last waves
+// of a ~391-gpart leaf's 512 slots -- runs the one-slot tile: half the pairs;
+// for the plain Newtonian tiles, which keep the kernel within 128 VGPRs)
 #define SWH_P2P_TILE(TR, PE, SE)                                                             \
-  p2p_tile<TR, PE, SE, MPOLE, IPER>(sx, sy, sz, se2, sh, sm, nt, self_local, xi, yi, zi, hi2, \
-                                    emax, hv, actp, dimx, dimy, dimz, 2. * r_s_inv, ax, ay, az, pot)
+  do {                                                                                       \
+    if (SE || TR || PE || full)                                                              \
+      p2p_tile<TR, PE, SE, MPOLE, IPER>(sx, sy, sz, se2, sh, sm, nt, self_local, xi, yi, zi,  \
+                                        hi2, emax, hv, actp, dimx, dimy, dimz, 2. * r_s_inv, \
+                                        ax, ay, az, pot);                                    \
+    else                                                                                     \
+      p2p_tile<TR, PE, SE, MPOLE, 1>(sx, sy, sz, se2, sh, sm, nt, self_local, xi, yi, zi,     \
+                                     hi2, emax, hv, actp, dimx, dimy, dimz, 2. * r_s_inv,    \
+                                     ax, ay, az, pot);                                       \
+  } while (0)
         if (self) {
           if (pr.truncated) {
             if (periodic) SWH_P2P_TILE(true, true, true);
@@ -890,7 +905,7 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
 // entry) pairs are queued and evaluated 64 at a time; otherwise a thread per
 // i walks the whole list.
 template <typename T, bool SMALL>
-__global__ __launch_bounds__(kGravBlock) void m2p_kernel(
+__global__ __launch_bounds__(kGravBlock) __attribute__((amdgpu_waves_per_eu(SMALL ? 3 : 1))) void m2p_kernel(
     GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
     const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
     double dimz, double r_s_inv, MacParams mac, unsigned long long* counter) {

@@ -421,3 +421,39 @@ def test_baseline_chain_from_unconverged_vs_f64(gpu_ctx, which):
     dh = np.abs(o["h"] / parts["h"] - 1.0)
     assert np.median(dh) > 1e-3, np.median(dh)
     check_chain(g, rg, o, ro, np.ones(len(parts), dtype=bool), h_tol=h_tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_iter", [1, 2, 30])
+def test_ghost_iterations_and_unconverged(gpu_ctx, max_iter):
+    """The ghost's pass loop (runner_ghost.c:1085-1596, max_smoothing_iterations):
+    the number of passes and the particles left unconverged after the last
+    allowed pass equal the fp64 oracle's box_ghost on the same unconverged
+    box; too few passes is SWH_ERR_NOT_CONVERGED (SWIFT's "Smoothing length
+    failed to converge"), with the h of the converged particles and the
+    pending reruns as the oracle leaves them."""
+    from swift_subtask_dev_amd import lib
+    parts = ics.sedov_box(16, velocity="divergent", pert=0.3, seed=5)
+    parts["h"] *= np.random.Generator(np.random.PCG64(7)).uniform(0.7, 1.4, len(parts))
+    P = abi.default_hydro_params(max_smoothing_iterations=max_iter)
+    o = abi.copy_parts(parts)
+    N = len(o)
+    O.fn("f32", "init_parts")(o.ctypes.data, N, C.byref(P))
+    O.fn("f64", "box_density")(o.ctypes.data, N, C.byref(P), None)
+    nfail = C.c_longlong(0)
+    it_o = O.fn("f64", "box_ghost")(o.ctypes.data, N, C.byref(P), C.byref(nfail))
+    g = abi.copy_parts(parts)
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.upload(g)
+    sp.rebuild(P)
+    sp.init_parts(P)
+    sp.density(P)
+    it = C.c_int32(0)
+    nu = C.c_int64(0)
+    st = sp._lib.swh_ghost(sp.handle, C.byref(P), C.byref(it), C.byref(nu))
+    sp.download(g, abi.FIELDS_ALL)
+    sp.close()
+    assert it.value == it_o, (it.value, it_o)
+    assert nu.value == nfail.value, (nu.value, nfail.value)
+    assert st == (5 if nfail.value else 0), st  # 5: SWH_ERR_NOT_CONVERGED
+    assert_close(g["h"], o["h"], 1e-6, what="h")

@@ -282,13 +282,15 @@ __device__ __forceinline__ void p2p_soften(double r2, double r_inv, double e2i, 
   f_ij = mh * (h_inv * h_inv) * grav_force_eval(ui);
   pot_ij = mh * grav_pot_eval(ui);
 }
-// exp(-x) for x >= 0 (the truncation's argument, a finite distance ratio):
-// Cody-Waite reduction by ln 2 (fdlibm's split), then e^f = 1 + f (1 + f q(f))
-// on |f| <= ln2/2 with q of degree 7 fitted for the least maximum relative
-// error (Lawson-weighted least squares on 2,000 Chebyshev nodes against
-// 40-digit values; max relative error 1.7e-14 checked on 40,001 points):
-// 14 instructions where the library exp takes ~30, no overflow / NaN
-// handling.
+// 2 exp(-x) for x >= 0 (the truncation's argument, a finite distance ratio):
+// Cody-Waite reduction by ln 2 in one fma (|k| <= x / ln2 keeps k times
+// ln2's rounding error below 1e-15 of f for every x the truncation meets),
+// then e^f = 1 + f (1 + f q(f)) on |f| <= ln2/2 with q of degree 6 fitted for
+// the least maximum relative error (Lawson-weighted least squares on 4,000
+// Chebyshev nodes in extended precision; max relative error 1.3e-12 checked on
+// 200,001 points, four orders below the float a_grav / potential it feeds),
+// every coefficient doubled so the result is 2 e^-x at no cost: 12
+// instructions where the library exp takes ~30, no overflow / NaN handling.
 // (Horner steps as three-operand v_fma_f64: the compiler otherwise copies
 // each loop-invariant coefficient register before a two-operand v_fmac_f64,
 // a move per term.)
@@ -304,17 +306,16 @@ __device__ __forceinline__ double horner_step(double p, double f, double c) {
 // FMA3: the three-operand form (the batch kernel, whose registers hold the
 // coefficients; the 256-thread tile kernel keeps fma and its register budget)
 template <bool FMA3>
-__device__ __forceinline__ double exp_neg_f64(double x) {
+__device__ __forceinline__ double exp_neg_f64_x2(double x) {
   const double k = __builtin_rint(x * -1.4426950408889634);  // -x / ln 2
-  const double f = fma(k, -1.90821492927058770002e-10, fma(k, -6.93147180369123816490e-01, -x));
-  double q = horner_step<FMA3>(2.749299850055968e-06, f, 2.4880793243238282e-05);
-  q = horner_step<FMA3>(q, f, 0.00019841539149942946);
-  q = horner_step<FMA3>(q, f, 0.0013888811176925341);
-  q = horner_step<FMA3>(q, f, 0.008333333095125245);
-  q = horner_step<FMA3>(q, f, 0.04166666696206109);
-  q = horner_step<FMA3>(q, f, 0.16666666667264937);
-  q = horner_step<FMA3>(q, f, 0.49999999999664524);
-  const double p = fma(f, fma(f, q, 1.), 1.);
+  const double f = fma(k, -0.6931471805599453, -x);
+  double q = horner_step<FMA3>(2 * 2.4778829221708597e-05, f, 2 * 0.00019908923481541454);
+  q = horner_step<FMA3>(q, f, 2 * 0.0013889023827227704);
+  q = horner_step<FMA3>(q, f, 2 * 0.008333281839354719);
+  q = horner_step<FMA3>(q, f, 2 * 0.04166666572724781);
+  q = horner_step<FMA3>(q, f, 2 * 0.16666666784287604);
+  q = horner_step<FMA3>(q, f, 2 * 0.500000000012381);
+  const double p = fma(f, fma(f, q, 2.), 2.);
   return __builtin_ldexp(p, (int)k);
 }
 
@@ -322,16 +323,17 @@ __device__ __forceinline__ double exp_neg_f64(double x) {
 // 160-190): with alpha = 1 / (1 + e^x), x = 2 r / r_s, the reference's
 // corr_pot = 2 (1 - alpha e^x) and corr_f = 2 (1 + alpha ((1 - alpha) x -
 // e^x)) are, since alpha e^x = 1 - alpha, 2 alpha and 2 alpha (1 + (1 -
-// alpha) x); alpha = E / (1 + E) from E = e^-x never overflows. tworsi =
-// 2 / r_s.
+// alpha) x); from E = e^-x (never overflows), alpha = E r and 1 - alpha = r
+// with r = 1 / (1 + E). tworsi = 2 / r_s.
 template <bool FMA3 = false>
 __device__ __forceinline__ void p2p_trunc(double r2, double r_inv, double tworsi, double& f_ij,
                                           double& pot_ij) {
   const double x = r2 * r_inv * tworsi;
-  const double E = exp_neg_f64<FMA3>(x);
-  const double a2 = 2. * E * rcp1_f64(1. + E);  // 2 alpha
+  const double E2 = exp_neg_f64_x2<FMA3>(x);      // 2 E
+  const double r = rcp1_f64(fma(E2, 0.5, 1.));     // 1 - alpha
+  const double a2 = E2 * r;                         // 2 alpha
   pot_ij *= a2;
-  f_ij *= a2 * fma(1. - 0.5 * a2, x, 1.);
+  f_ij *= fma(a2 * r, x, a2);
 }
 
 // Nearest periodic image of a separation (|d| < 1.5 box): d - box rint(d /
@@ -917,21 +919,28 @@ __global__ __launch_bounds__(kGravBlock) __attribute__((amdgpu_waves_per_eu(SMAL
   if (SMALL) {
     // One wave per leaf (<= 64 gparts). The P-P entries are read 64 at a
     // time (one per lane, loads in parallel) and their allow_mpole ones --
-    // ~7% of a cosmological tree's entries -- compacted into LDS. Then the
-    // wave tests every (i, entry) pair of the chunk against the MAC, a lane
-    // per entry and i by i, and queues the accepted pairs i-major; the
-    // queue is evaluated 64 pairs at a time with every lane busy (the M2P,
-    // ~500 fp64 instructions, no longer runs with only the lanes whose pair
-    // passed enabled), and each i's terms are summed by a segmented scan
-    // over its contiguous run of the round, then into its LDS accumulator
-    // by the run's last lane: one writer per i per round, in queue order.
+    // ~7% of a cosmological tree's entries -- compacted into LDS until 64
+    // have gathered (or the list ends): one group. The wave then tests every
+    // (entry, active i) pair of the group against the MAC, 64 pairs per
+    // iteration in entry-major order (lane t of an iteration holds pair t0 +
+    // t = entry * nact + i), and appends the accepted ones to a 128-slot LDS
+    // ring; whenever 64 are queued (and once the tests are done) they are
+    // evaluated together with every lane busy (the M2P, ~500 fp64
+    // instructions, no longer runs with only the lanes whose pair passed
+    // enabled). Entry-major keeps a round's multipole reads to a few
+    // multipoles (broadcast from the cache lines) where i-major order read a
+    // different one per lane; each lane adds its terms to its i's LDS
+    // accumulator with ds_add_f64.
     __shared__ float4 spi[64];  // i: float position and softening (the MAC's inputs)
     __shared__ float soag[64];  // i: old |a|
-    __shared__ int cj[64];
-    __shared__ unsigned char ctr[64];
-    __shared__ unsigned short q[64 * 64];  // accepted pairs: i << 8 | entry
+    __shared__ unsigned char actl[64];  // the active i's, compacted
+    __shared__ int cj[128];             // gathered allow_mpole entries: source leaf
+    __shared__ unsigned char ctr[128];  //   and truncation flag
+    __shared__ MacSource sb[64];        // the group's MAC inputs
+    __shared__ unsigned short q[128];   // accepted pairs, a ring: i << 8 | entry
     __shared__ T accs[4][64];
     const int lane = (int)threadIdx.x;
+    const unsigned long long below = (1ull << lane) - 1ull;
     const int gi = L.start + lane;
     const bool acti = lane < L.count && g.active[gi];
     const double4 pl = acti ? g.pos[gi] : make_double4(0., 0., 0., 1.);
@@ -939,49 +948,70 @@ __global__ __launch_bounds__(kGravBlock) __attribute__((amdgpu_waves_per_eu(SMAL
     soag[lane] = acti ? g.oagn[gi] : 0.f;
     for (int c = 0; c < 4; c++) accs[c][lane] = (T)0;
     const unsigned long long actm = __ballot(acti);
-    for (int qb = p0; qb < p1; qb += 64) {
-      bool am = false;
-      int jl = 0;
-      unsigned char tr = 0;
-      if (qb + lane < p1) {
-        const swh_leaf_pair pr = pairs[qb + lane];
-        am = pr.allow_mpole && leaves[pr.j].count > 1;
-        jl = pr.j;
-        tr = pr.truncated != 0;
+    const int nact = __popcll(actm);
+    if (acti) actl[__popcll(actm & below)] = (unsigned char)lane;
+    int nbuf = 0;
+    for (int qb = p0; qb < p1 || nbuf > 0; qb += 64) {
+      if (qb < p1) {
+        bool am = false;
+        int jl = 0;
+        unsigned char tr = 0;
+        if (qb + lane < p1) {
+          const swh_leaf_pair pr = pairs[qb + lane];
+          am = pr.allow_mpole && leaves[pr.j].count > 1;
+          jl = pr.j;
+          tr = pr.truncated != 0;
+        }
+        const unsigned long long m = __ballot(am);
+        wave_sync();  // the previous group's readers are done
+        if (am) {
+          const int r = nbuf + __popcll(m & below);
+          cj[r] = jl;
+          ctr[r] = tr;
+        }
+        nbuf += __popcll(m);
+        wave_sync();
+        if (nbuf < 64 && qb + 64 < p1) continue;  // gather more first
       }
-      const unsigned long long m = __ballot(am);
-      const int nme = __popcll(m);
-      wave_sync();  // the previous chunk's readers are done
-      if (am) {
-        const int r = __popcll(m & ((1ull << lane) - 1ull));
-        cj[r] = jl;
-        ctr[r] = tr;
-      }
+      const int ne = nbuf < 64 ? nbuf : 64;
+      if (ne == 0) continue;
+      if (lane < ne) sb[lane] = mac_source(g.mp[cj[lane]]);
       wave_sync();
-      if (nme == 0) continue;
-      MacSource B{};
-      if (lane < nme) B = mac_source(g.mp[cj[lane]]);
-      int nq = 0;
-      for (unsigned long long am_i = actm; am_i; am_i &= am_i - 1) {
-        const int il = __ffsll((long long)am_i) - 1;
-        const float4 p = spi[il];
-        const bool ok = lane < nme && m2p_accept(mac, B, p.x, p.y, p.z, p.w, soag[il]);
-        const unsigned long long okm = __ballot(ok);
-        if (ok) q[nq + __popcll(okm & ((1ull << lane) - 1ull))] = (unsigned short)(il << 8 | lane);
-        nq += __popcll(okm);
-      }
-      wave_sync();
-      nm += (unsigned long long)nq;
-      for (int r0 = 0; r0 < nq; r0 += 64) {
-        const int it = r0 + lane;
-        const bool valid = it < nq;
+      const int ntest = nact * ne;
+      int k = lane / nact, ii = lane - k * nact;  // this lane's pair: (actl[ii], k)
+      const int dk = 64 / nact, di = 64 - dk * nact;
+      int t0 = 0, qh = 0, qt = 0;  // tests done; ring head and tail
+      while (t0 < ntest || qt > qh) {
+        if (t0 < ntest && qt - qh < 64) {
+          bool ok = false;
+          int il = 0;
+          if (t0 + lane < ntest) {
+            il = actl[ii];
+            const float4 p = spi[il];
+            ok = m2p_accept(mac, sb[k], p.x, p.y, p.z, p.w, soag[il]);
+          }
+          const unsigned long long okm = __ballot(ok);
+          if (ok) q[(qt + __popcll(okm & below)) & 127] = (unsigned short)(il << 8 | k);
+          qt += __popcll(okm);
+          t0 += 64;
+          k += dk;
+          ii += di;
+          if (ii >= nact) {
+            ii -= nact;
+            k++;
+          }
+          wave_sync();
+          continue;
+        }
+        const int nr = qt - qh < 64 ? qt - qh : 64;
+        const bool valid = lane < nr;
         int il = -1;
         T f[4] = {(T)0, (T)0, (T)0, (T)0};
         if (valid) {
-          const unsigned int e = q[it];
+          const unsigned int e = q[(qh + lane) & 127];
           il = (int)(e >> 8);
-          const int k = (int)(e & 255u);
-          const swh_multipole& M = g.mp[cj[k]];
+          const int kk = (int)(e & 255u);
+          const swh_multipole& M = g.mp[cj[kk]];
           const double4 p = g.pos[L.start + il];
           double dx = M.CoM[0] - p.x, dy = M.CoM[1] - p.y, dz = M.CoM[2] - p.z;
           if (periodic) {
@@ -990,21 +1020,29 @@ __global__ __launch_bounds__(kGravBlock) __attribute__((amdgpu_waves_per_eu(SMAL
             dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
           }
           const T eps = (T)fmaxf((float)p.w, M.max_softening);
-          m2p<T>(M.M, (T)dx, (T)dy, (T)dz, eps, ctr[k] != 0, (T)r_s_inv, f);
+          m2p<T>(M.M, (T)dx, (T)dy, (T)dz, eps, ctr[kk] != 0, (T)r_s_inv, f);
         }
-        // segmented inclusive scan over the round's runs of equal i
-        for (int o = 1; o < 64; o <<= 1) {
-          const int u = __shfl_up(il, o);
-          T v[4];
-          for (int c = 0; c < 4; c++) v[c] = __shfl_up(f[c], o);
-          if (lane >= o && u == il)
-            for (int c = 0; c < 4; c++) f[c] += v[c];
-        }
-        const int nxt = __shfl_down(il, 1);
-        if (valid && (lane == 63 || it + 1 >= nq || nxt != il))
-          for (int c = 0; c < 4; c++) accs[c][il] += f[c];
+        if (valid)
+          for (int c = 0; c < 4; c++) atomicAdd(&accs[c][il], f[c]);
+        nm += (unsigned long long)nr;
+        qh += nr;
         wave_sync();
       }
+      // the entries past the group move to the front of the buffer
+      const int rest = nbuf - ne;
+      int jl = 0;
+      unsigned char tr = 0;
+      if (lane < rest) {
+        jl = cj[64 + lane];
+        tr = ctr[64 + lane];
+      }
+      wave_sync();
+      if (lane < rest) {
+        cj[lane] = jl;
+        ctr[lane] = tr;
+      }
+      nbuf = rest;
+      wave_sync();
     }
     wave_sync();
     const T F[4] = {accs[0][lane], accs[1][lane], accs[2][lane], accs[3][lane]};

@@ -68,7 +68,10 @@ def build_variant(kernel: str, force: bool = False, verbose: bool = False,
         "-Wno-unused-function", "-Wno-unused-variable",
         f"-I{INCLUDE}", f"-I{CSRC}", "-fvisibility=hidden",
         "-DSWH_BUILD", *defines,
+        # experiment flags (e.g. -DSWH_M2P_PROF); any set forces a full rebuild
+        *os.environ.get("SWH_EXTRA_FLAGS", "").split(),
     ]
+    force = force or bool(os.environ.get("SWH_EXTRA_FLAGS"))
     objs, cmds = [], []
     for src in HIP_SOURCES:
         s = CSRC / src

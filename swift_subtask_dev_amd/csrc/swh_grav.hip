@@ -282,43 +282,6 @@ __device__ __forceinline__ void p2p_soften(double r2, double r_inv, double e2i, 
   f_ij = mh * (h_inv * h_inv) * grav_force_eval(ui);
   pot_ij = mh * grav_pot_eval(ui);
 }
-// 2 exp(-x) for x >= 0 (the truncation's argument, a finite distance ratio):
-// Cody-Waite reduction by ln 2 in one fma (|k| <= x / ln2 keeps k times
-// ln2's rounding error below 1e-15 of f for every x the truncation meets),
-// then e^f = 1 + f (1 + f q(f)) on |f| <= ln2/2 with q of degree 6 fitted for
-// the least maximum relative error (Lawson-weighted least squares on 4,000
-// Chebyshev nodes in extended precision; max relative error 1.3e-12 checked on
-// 200,001 points, four orders below the float a_grav / potential it feeds),
-// every coefficient doubled so the result is 2 e^-x at no cost: 12
-// instructions where the library exp takes ~30, no overflow / NaN handling.
-// (Horner steps as three-operand v_fma_f64: the compiler otherwise copies
-// each loop-invariant coefficient register before a two-operand v_fmac_f64,
-// a move per term.)
-__device__ __forceinline__ double fma3(double a, double b, double c) {
-  double r;
-  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-template <bool FMA3>
-__device__ __forceinline__ double horner_step(double p, double f, double c) {
-  return FMA3 ? fma3(p, f, c) : fma(p, f, c);
-}
-// FMA3: the three-operand form (the batch kernel, whose registers hold the
-// coefficients; the 256-thread tile kernel keeps fma and its register budget)
-template <bool FMA3>
-__device__ __forceinline__ double exp_neg_f64_x2(double x) {
-  const double k = __builtin_rint(x * -1.4426950408889634);  // -x / ln 2
-  const double f = fma(k, -0.6931471805599453, -x);
-  double q = horner_step<FMA3>(2 * 2.4778829221708597e-05, f, 2 * 0.00019908923481541454);
-  q = horner_step<FMA3>(q, f, 2 * 0.0013889023827227704);
-  q = horner_step<FMA3>(q, f, 2 * 0.008333281839354719);
-  q = horner_step<FMA3>(q, f, 2 * 0.04166666572724781);
-  q = horner_step<FMA3>(q, f, 2 * 0.16666666784287604);
-  q = horner_step<FMA3>(q, f, 2 * 0.500000000012381);
-  const double p = fma(f, fma(f, q, 2.), 2.);
-  return __builtin_ldexp(p, (int)k);
-}
-
 // The long-range truncation of kernel_long_grav_eval (kernel_long_gravity.h:
 // 160-190): with alpha = 1 / (1 + e^x), x = 2 r / r_s, the reference's
 // corr_pot = 2 (1 - alpha e^x) and corr_f = 2 (1 + alpha ((1 - alpha) x -
@@ -625,11 +588,14 @@ __device__ __forceinline__ void batch_pairs(const TileLds& tl, const PairCtx& c,
   }
 }
 
+// MPOLE: mbits[entry] = the lanes whose i takes the entry's multipole (its
+// MAC passed), for m2p_kernel, which then tests nothing itself.
 template <bool MPOLE>
 __global__ __launch_bounds__(64) void p2p_batch_kernel(
     GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
     const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
-    double dimz, double r_s_inv, MacParams mac, unsigned long long* counter) {
+    double dimz, double r_s_inv, MacParams mac, unsigned long long* counter,
+    unsigned long long* __restrict__ mbits) {
   // 37 B per staged gpart (9.5 KB): four waves per SIMD
   __shared__ double sx[kPPBatch], sy[kPPBatch], sz[kPPBatch];
   __shared__ float seps[kPPBatch], sm[kPPBatch];
@@ -696,13 +662,17 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
     const unsigned int tmask = (unsigned int)__ballot(lane < B && tr);
     unsigned int mmask = 0;  // the entries this i takes through their multipole
     if (MPOLE) {
+      unsigned long long mine = 0;  // lane q < B: entry q's accepting lanes
       for (unsigned long long m = __ballot(lane < B && am); m; m &= m - 1) {
         const int q = __ffsll((long long)m) - 1;
         const int jq = __builtin_amdgcn_readlane(jl, q);
-        if (act && m2p_accept(mac, mac_source(g.mp[jq]), (float)pi.x, (float)pi.y, (float)pi.z,
-                              (float)pi.w, g.oagn[gi]))
-          mmask |= 1u << q;
+        const bool ok = act && m2p_accept(mac, mac_source(g.mp[jq]), (float)pi.x, (float)pi.y,
+                                          (float)pi.z, (float)pi.w, g.oagn[gi]);
+        if (ok) mmask |= 1u << q;
+        const unsigned long long okm = __ballot(ok);
+        if (lane == q) mine = okm;
       }
+      if (lane < B) mbits[qb + lane] = mine;
     }
     // Entries every active i takes through the multipole are not staged at
     // all (the M2P acceptance is nearly always uniform over a small leaf);
@@ -906,6 +876,104 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
 // SMALL (every leaf <= 64 gparts, one wave per leaf): the accepted (i,
 // entry) pairs are queued and evaluated 64 at a time; otherwise a thread per
 // i walks the whole list.
+// The pair's M2P terms {potential, a_x, a_y, a_z} for i-leaf gpart gi and
+// the multipole of source leaf j.
+template <typename T>
+__device__ __forceinline__ void m2p_pair(const GSoA& g, int gi, int j, bool truncated,
+                                         int periodic, double dimx, double dimy, double dimz,
+                                         double r_s_inv, T* f) {
+  const swh_multipole& M = g.mp[j];
+  const double4 p = g.pos[gi];
+  double dx = M.CoM[0] - p.x, dy = M.CoM[1] - p.y, dz = M.CoM[2] - p.z;
+  if (periodic) {
+    dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
+    dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
+    dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
+  }
+  const T eps = (T)fmaxf((float)p.w, M.max_softening);
+  m2p<T>(M.M, (T)dx, (T)dy, (T)dz, eps, truncated, (T)r_s_inv, f);
+}
+
+// Small leaves after p2p_batch_kernel<true> (fp64): one wave per leaf, the
+// MAC already decided there (mbits: per entry, the accepting lanes, lpi per
+// i). The entries are read 64 at a time; each lane expands its entry's
+// accepting i's into an LDS queue at its scanned offset (entry-major, so a
+// round's multipole reads are a few multipoles broadcast from their cache
+// lines), and the queue is evaluated 64 pairs per round with every lane busy
+// (the M2P, ~500 fp64 instructions), each lane adding its terms to its i's
+// LDS accumulator with ds_add_f64. The MAC tests were ~55% of the wave time
+// of a kernel that repeated them.
+template <typename T>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void m2p_bits_kernel(
+    GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
+    const swh_leaf_pair* __restrict__ pairs, const unsigned long long* __restrict__ mbits,
+    int periodic, double dimx, double dimy, double dimz, double r_s_inv,
+    unsigned long long* counter) {
+  const int li = xcd_block_id();
+  const swh_leaf L = leaves[li];
+  const int p0 = pair_off[li], p1 = pair_off[li + 1];
+  if (p0 == p1) return;  // no sources (a tree's inner cells)
+  __shared__ int cj[64];
+  __shared__ unsigned char ctr[64];
+  __shared__ unsigned short q[64 * 64];  // i << 8 | entry
+  __shared__ T accs[4][64];
+  const int lane = (int)threadIdx.x;
+  // the P2P kernel's lanes: lpi per i, i = lane / lpi (its lane s = 0 stands for it)
+  const int lpi = L.count >= 64 ? 1 : min(8, 64 / max(L.count, 1));
+  const unsigned long long smask = __ballot(lane % lpi == 0 && lane / lpi < L.count);
+  const unsigned int inv = (65536u + (unsigned)lpi - 1u) / (unsigned)lpi;  // b / lpi, b < 64
+  for (int c = 0; c < 4; c++) accs[c][lane] = (T)0;
+  unsigned long long nm = 0;
+  for (int qb = p0; qb < p1; qb += 64) {
+    unsigned long long m = 0;
+    int jl = 0;
+    unsigned char tr = 0;
+    if (qb + lane < p1) {
+      m = mbits[qb + lane] & smask;
+      if (m) {
+        const swh_leaf_pair pr = pairs[qb + lane];
+        jl = pr.j;
+        tr = pr.truncated != 0;
+      }
+    }
+    const int c = __popcll(m);
+    const int inc = wave_incl_scan(c);
+    const int tot = __builtin_amdgcn_readlane(inc, 63);
+    if (tot == 0) continue;
+    wave_sync();  // the previous chunk's readers are done
+    cj[lane] = jl;
+    ctr[lane] = tr;
+    int at = inc - c;
+    for (unsigned long long mm = m; mm; mm &= mm - 1) {
+      const unsigned int b = (unsigned int)(__ffsll((long long)mm) - 1);
+      q[at++] = (unsigned short)(((b * inv) >> 16) << 8 | (unsigned int)lane);
+    }
+    wave_sync();
+    nm += (unsigned long long)tot;
+    for (int r0 = 0; r0 < tot; r0 += 64) {
+      if (r0 + lane < tot) {
+        const unsigned int e = q[r0 + lane];
+        const int il = (int)(e >> 8), k = (int)(e & 255u);
+        T f[4];
+        m2p_pair<T>(g, L.start + il, cj[k], ctr[k] != 0, periodic, dimx, dimy, dimz, r_s_inv, f);
+        for (int c2 = 0; c2 < 4; c2++) atomicAdd(&accs[c2][il], f[c2]);
+      }
+    }
+  }
+  wave_sync();
+  const T F[4] = {accs[0][lane], accs[1][lane], accs[2][lane], accs[3][lane]};
+  if (lane < L.count && (F[0] != (T)0 || F[1] != (T)0 || F[2] != (T)0 || F[3] != (T)0)) {
+    const int gi = L.start + lane;
+    double4 a = g.acc[gi];
+    a.x += (double)F[1];
+    a.y += (double)F[2];
+    a.z += (double)F[3];
+    a.w += (double)F[0];
+    g.acc[gi] = a;
+  }
+  if (counter && lane == 0 && nm) atomicAdd(counter + 1, nm);
+}
+
 template <typename T, bool SMALL>
 __global__ __launch_bounds__(kGravBlock) __attribute__((amdgpu_waves_per_eu(SMALL ? 3 : 1))) void m2p_kernel(
     GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
@@ -949,6 +1017,7 @@ __global__ __launch_bounds__(kGravBlock) __attribute__((amdgpu_waves_per_eu(SMAL
     for (int c = 0; c < 4; c++) accs[c][lane] = (T)0;
     const unsigned long long actm = __ballot(acti);
     const int nact = __popcll(actm);
+    if (nact == 0) return;  // nothing active in this leaf
     if (acti) actl[__popcll(actm & below)] = (unsigned char)lane;
     int nbuf = 0;
     for (int qb = p0; qb < p1 || nbuf > 0; qb += 64) {
@@ -1011,16 +1080,8 @@ __global__ __launch_bounds__(kGravBlock) __attribute__((amdgpu_waves_per_eu(SMAL
           const unsigned int e = q[(qh + lane) & 127];
           il = (int)(e >> 8);
           const int kk = (int)(e & 255u);
-          const swh_multipole& M = g.mp[cj[kk]];
-          const double4 p = g.pos[L.start + il];
-          double dx = M.CoM[0] - p.x, dy = M.CoM[1] - p.y, dz = M.CoM[2] - p.z;
-          if (periodic) {
-            dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
-            dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
-            dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
-          }
-          const T eps = (T)fmaxf((float)p.w, M.max_softening);
-          m2p<T>(M.M, (T)dx, (T)dy, (T)dz, eps, ctr[kk] != 0, (T)r_s_inv, f);
+          m2p_pair<T>(g, L.start + il, cj[kk], ctr[kk] != 0, periodic, dimx, dimy, dimz,
+                      r_s_inv, f);
         }
         if (valid)
           for (int c = 0; c < 4; c++) atomicAdd(&accs[c][il], f[c]);
@@ -1071,15 +1132,8 @@ __global__ __launch_bounds__(kGravBlock) __attribute__((amdgpu_waves_per_eu(SMAL
       const swh_multipole& M = g.mp[pr.j];
       if (!m2p_accept(mac, mac_source(M), (float)p.x, (float)p.y, (float)p.z, (float)p.w, oag))
         continue;
-      double dx = M.CoM[0] - p.x, dy = M.CoM[1] - p.y, dz = M.CoM[2] - p.z;
-      if (periodic) {
-        dx = dx > 0.5 * dimx ? dx - dimx : (dx < -0.5 * dimx ? dx + dimx : dx);
-        dy = dy > 0.5 * dimy ? dy - dimy : (dy < -0.5 * dimy ? dy + dimy : dy);
-        dz = dz > 0.5 * dimz ? dz - dimz : (dz < -0.5 * dimz ? dz + dimz : dz);
-      }
-      const T eps = (T)fmaxf((float)p.w, M.max_softening);
       T f[4];
-      m2p<T>(M.M, (T)dx, (T)dy, (T)dz, eps, pr.truncated != 0, (T)r_s_inv, f);
+      m2p_pair<T>(g, i, pr.j, pr.truncated != 0, periodic, dimx, dimy, dimz, r_s_inv, f);
       for (int k = 0; k < 4; k++) F[k] += f[k];
       nm++;
     }
@@ -1153,7 +1207,8 @@ swh_status swh_gspace_destroy(swh_gspace* g) {
                     &g->m2l_src,  &g->l2l_list, &g->leaf_ids, &g->leaf_of, &g->m2m_list, &g->tree_d, &g->wf0,
                     &g->wf1,      &g->pp_key,  &g->pp_val,  &g->pp_key2,
                     &g->pp_val2,  &g->mm_key,  &g->mm_val,  &g->mm_key2,
-                    &g->mm_val2,  &g->wsort_tmp, &g->wrec, &g->wcnt, &g->wbase, &g->owned_d};
+                    &g->mm_val2,  &g->wsort_tmp, &g->wrec, &g->wcnt, &g->wbase, &g->owned_d,
+                    &g->m2p_bits};
   for (DevBuf* b : bufs) b->release();
   mesh_release(g);
   (void)hipStreamDestroy(g->stream);
@@ -1305,12 +1360,22 @@ swh_status launch_pp(swh_gspace* g, const swh_grav_params* G, const MacParams& m
     // the multipole-free instance keeps the P2P kernel's register budget;
     // small leaves (a deep tree) take one wave per i-leaf
     const bool small = g->max_leaf <= 64;
-    auto k = g->any_mpole ? (small ? p2p_batch_kernel<true> : p2p_kernel<true, kGravBlock, kIPer>)
-                          : (small ? p2p_batch_kernel<false> : p2p_kernel<false, kGravBlock, kIPer>);
-    hipLaunchKernelGGL(k, dim3(g->nleaves), dim3(small ? 64 : kGravBlock), 0, g->stream,
-                       gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
-                       g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
-                       (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, mac, ctr);
+    if (small) {
+      if (g->any_mpole) SWH_TRY(g->m2p_bits.reserve((size_t)std::max(1, g->npairs) * 8));
+      auto k = g->any_mpole ? p2p_batch_kernel<true> : p2p_batch_kernel<false>;
+      hipLaunchKernelGGL(k, dim3(g->nleaves), dim3(64), 0, g->stream, gsoa_of(g),
+                         g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
+                         g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
+                         (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, mac, ctr,
+                         g->m2p_bits.as<unsigned long long>());
+    } else {
+      auto k = g->any_mpole ? p2p_kernel<true, kGravBlock, kIPer>
+                            : p2p_kernel<false, kGravBlock, kIPer>;
+      hipLaunchKernelGGL(k, dim3(g->nleaves), dim3(kGravBlock), 0, g->stream, gsoa_of(g),
+                         g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
+                         g->pairs.as<const swh_leaf_pair>(), G->periodic, (double)G->dim[0],
+                         (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv, mac, ctr);
+    }
   }
   else
     hipLaunchKernelGGL(p2p_kernel_f32, dim3(g->nleaves), dim3(kGravBlock), 0, g->stream,
@@ -1319,7 +1384,16 @@ swh_status launch_pp(swh_gspace* g, const swh_grav_params* G, const MacParams& m
                        (double)G->dim[1], (double)G->dim[2], (float)G->r_s_inv, mac, ctr);
   SWH_HIP(hipGetLastError());
   if (m2p_start) SWH_HIP(hipEventRecord(m2p_start, g->stream));
-  if (g->any_mpole) {
+  if (g->any_mpole && f64 && g->max_leaf <= 64) {
+    // the batch kernel's MAC results
+    hipLaunchKernelGGL(m2p_bits_kernel<double>, dim3(g->nleaves), dim3(64), 0, g->stream,
+                       gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
+                       g->pairs.as<const swh_leaf_pair>(),
+                       g->m2p_bits.as<const unsigned long long>(), G->periodic,
+                       (double)G->dim[0], (double)G->dim[1], (double)G->dim[2],
+                       (double)G->r_s_inv, ctr);
+    SWH_HIP(hipGetLastError());
+  } else if (g->any_mpole) {
     const bool small = g->max_leaf <= 64;  // one wave per small leaf
     auto k = f64 ? (small ? m2p_kernel<double, true> : m2p_kernel<double, false>)
                  : (small ? m2p_kernel<float, true> : m2p_kernel<float, false>);

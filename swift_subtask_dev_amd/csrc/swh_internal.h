@@ -247,6 +247,7 @@ struct swh_gspace {
   int32_t nleaves = 0, npairs = 0;
   int32_t max_leaf = 0;
   swh::DevBuf counter;
+  swh::DevBuf m2p_bits;  // u64 per pair: the lanes whose i took the entry's multipole (launch_pp)
   // tree gravity (swh_gspace_set_tree / swh_grav_tree)
   std::vector<swh_gcell> tree;   // host copy of the cell table
   swh::DevBuf cell_act;          // int8 per cell: any active gpart

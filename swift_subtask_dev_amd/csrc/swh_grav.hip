@@ -314,7 +314,7 @@ __device__ __forceinline__ double nearest_rint(double d, double box, double ibox
 // the tile's largest h2_j): pairs at or beyond it are unsoftened.
 template <bool TRUNC, bool PERIODIC, bool SELF, bool MASK, int IPER>
 __device__ __forceinline__ void p2p_tile(const double* sx, const double* sy, const double* sz,
-                                         const double* se2, const double* sh, const float* sm,
+                                         const double* se2, const double* sh, const double* sm,
                                          int nt, const int* self_local, const double* xi,
                                          const double* yi, const double* zi, const double* hi2,
                                          const double* emax, const double* hv, const bool* act,
@@ -323,7 +323,7 @@ __device__ __forceinline__ void p2p_tile(const double* sx, const double* sy, con
   const double idimx = 1. / dimx, idimy = 1. / dimy, idimz = 1. / dimz;
   for (int t = 0; t < nt; t++) {
     const double xj = sx[t], yj = sy[t], zj = sz[t];
-    const double mj = (double)sm[t];
+    const double mj = sm[t];
 #pragma unroll
     for (int k = 0; k < IPER; k++) {
       double dx = xj - xi[k], dy = yj - yi[k], dz = zj - zi[k];
@@ -388,7 +388,7 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(MPOLE ? 3 :
     double dimz, double r_s_inv, MacParams mac, unsigned long long* counter) {
   __shared__ double sx[BLK], sy[BLK], sz[BLK], se2[BLK],
       sh[BLK];
-  __shared__ float sm[BLK];
+  __shared__ double sm[BLK];  // (fp64: no conversion per pair)
   __shared__ double swmax[BLK / 64];  // per wave: the largest staged h2
   const int li = xcd_block_id();
   const swh_leaf L = leaves[li];

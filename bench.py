@@ -866,11 +866,12 @@ def run_cosmo(args, ctx, rank, world, dist, torch):
         t_p2p = st["ms"]["p2p"] * 1e-3
         if t_p2p > 0:
             flops = st["n_pp"] * 28.0 / t_p2p
-            out["roofline"] = {"bound": "fp64-vector", "kernel": "p2p_kernel/p2p_small_kernel",
+            out["roofline"] = {"bound": "fp64-vector", "kernel": "p2p_batch_kernel (small leaves; p2p_kernel for leaves > 64)",
                                "achieved": flops / 1e12, "peak": FP64_PEAK / 1e12,
                                "unit": "TFLOP/s", "frac": flops / FP64_PEAK, "traffic": None,
                                "flops_model": "28 flops per directed P2P interaction (the "
-                                              "truncated kernel's erfc/exp terms not counted)"}
+                                              "truncated kernel's e^-x and alpha terms not "
+                                              "counted)"}
             tr = load_traffic("cosmo") if world == 1 else None
             if tr:
                 out["roofline"]["traffic"] = tr.get("bytes_per_launch")

@@ -900,7 +900,8 @@ __device__ __forceinline__ void m2p_pair(const GSoA& g, int gi, int j, bool trun
 // accepting i's into an LDS queue at its scanned offset (entry-major, so a
 // round's multipole reads are a few multipoles broadcast from their cache
 // lines), and the queue is evaluated 64 pairs per round with every lane busy
-// (the M2P, ~500 fp64 instructions), each lane adding its terms to its i's
+// (the M2P, ~500 fp64 instructions; a chunk's last < 64 pairs wait for the
+// next chunk's, so rounds run full), each lane adding its terms to its i's
 // LDS accumulator with ds_add_f64. The MAC tests were ~55% of the wave time
 // of a kernel that repeated them.
 template <typename T>
@@ -913,9 +914,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void m2
   const swh_leaf L = leaves[li];
   const int p0 = pair_off[li], p1 = pair_off[li + 1];
   if (p0 == p1) return;  // no sources (a tree's inner cells)
-  __shared__ int cj[64];
-  __shared__ unsigned char ctr[64];
-  __shared__ unsigned short q[64 * 64];  // i << 8 | entry
+  // the entries of the last two chunks that had any (halves of cj / ctr), and
+  // the queue: pairs left from earlier chunks (< 64) at its front
+  __shared__ int cj[128];
+  __shared__ unsigned char ctr[128];
+  __shared__ unsigned short q[64 * 64 + 64];  // i << 8 | entry slot
   __shared__ T accs[4][64];
   const int lane = (int)threadIdx.x;
   // the P2P kernel's lanes: lpi per i, i = lane / lpi (its lane s = 0 stands for it)
@@ -924,40 +927,64 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void m2
   const unsigned int inv = (65536u + (unsigned)lpi - 1u) / (unsigned)lpi;  // b / lpi, b < 64
   for (int c = 0; c < 4; c++) accs[c][lane] = (T)0;
   unsigned long long nm = 0;
-  for (int qb = p0; qb < p1; qb += 64) {
-    unsigned long long m = 0;
-    int jl = 0;
-    unsigned char tr = 0;
-    if (qb + lane < p1) {
-      m = mbits[qb + lane] & smask;
-      if (m) {
-        const swh_leaf_pair pr = pairs[qb + lane];
-        jl = pr.j;
-        tr = pr.truncated != 0;
+  int nq = 0, half = 0, qb = p0;
+  while (qb < p1 || nq > 0) {
+    int n_eval = nq;  // (the list's end)
+    if (qb < p1) {
+      unsigned long long m = 0;
+      int jl = 0;
+      unsigned char tr = 0;
+      if (qb + lane < p1) {
+        m = mbits[qb + lane] & smask;
+        if (m) {
+          const swh_leaf_pair pr = pairs[qb + lane];
+          jl = pr.j;
+          tr = pr.truncated != 0;
+        }
+      }
+      const int c = __popcll(m);
+      const int inc = wave_incl_scan(c);
+      const int tot = __builtin_amdgcn_readlane(inc, 63);
+      wave_sync();  // the previous round's readers are done
+      // left pairs naming the half this chunk would overwrite (two chunks
+      // back) are evaluated first, and the chunk is read again
+      if (!(tot > 0 && __any(lane < nq && ((q[lane] & 64u) != 0u) == (half != 0)))) {
+        if (tot > 0) {
+          cj[half * 64 + lane] = jl;
+          ctr[half * 64 + lane] = tr;
+          int at = nq + inc - c;
+          for (unsigned long long mm = m; mm; mm &= mm - 1) {
+            const unsigned int b = (unsigned int)(__ffsll((long long)mm) - 1);
+            q[at++] = (unsigned short)(((b * inv) >> 16) << 8 | (unsigned int)(half * 64 + lane));
+          }
+          wave_sync();
+          nm += (unsigned long long)tot;
+          nq += tot;
+          half ^= 1;
+        }
+        qb += 64;
+        // full rounds; the rest (< 64) waits for the next chunk's pairs
+        n_eval = qb < p1 ? (nq & ~63) : nq;
       }
     }
-    const int c = __popcll(m);
-    const int inc = wave_incl_scan(c);
-    const int tot = __builtin_amdgcn_readlane(inc, 63);
-    if (tot == 0) continue;
-    wave_sync();  // the previous chunk's readers are done
-    cj[lane] = jl;
-    ctr[lane] = tr;
-    int at = inc - c;
-    for (unsigned long long mm = m; mm; mm &= mm - 1) {
-      const unsigned int b = (unsigned int)(__ffsll((long long)mm) - 1);
-      q[at++] = (unsigned short)(((b * inv) >> 16) << 8 | (unsigned int)lane);
-    }
-    wave_sync();
-    nm += (unsigned long long)tot;
-    for (int r0 = 0; r0 < tot; r0 += 64) {
-      if (r0 + lane < tot) {
-        const unsigned int e = q[r0 + lane];
-        const int il = (int)(e >> 8), k = (int)(e & 255u);
-        T f[4];
-        m2p_pair<T>(g, L.start + il, cj[k], ctr[k] != 0, periodic, dimx, dimy, dimz, r_s_inv, f);
-        for (int c2 = 0; c2 < 4; c2++) atomicAdd(&accs[c2][il], f[c2]);
+    if (n_eval > 0) {
+      for (int r0 = 0; r0 < n_eval; r0 += 64) {
+        if (r0 + lane < n_eval) {
+          const unsigned int e = q[r0 + lane];
+          const int il = (int)(e >> 8), k = (int)(e & 255u);
+          T f[4];
+          m2p_pair<T>(g, L.start + il, cj[k], ctr[k] != 0, periodic, dimx, dimy, dimz, r_s_inv,
+                      f);
+          for (int c2 = 0; c2 < 4; c2++) atomicAdd(&accs[c2][il], f[c2]);
+        }
       }
+      const int left = nq - n_eval;
+      unsigned short v = 0;
+      if (lane < left) v = q[n_eval + lane];
+      wave_sync();
+      if (lane < left) q[lane] = v;
+      wave_sync();
+      nq = left;
     }
   }
   wave_sync();

@@ -254,6 +254,45 @@ def test_batch_mpole_vs_oracle(gpu_ctx, mac, periodic, truncated):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("periodic,truncated", [(False, 0), (True, 1)])
+def test_batch_mpole_f32_vs_oracle(periodic, truncated):
+    """The fp32 context's small-leaf path (p2p_kernel_f32, then the M2P kernel
+    that applies the MAC itself -- the fp64 path takes the batch P2P kernel's
+    MAC results instead): exact P2P and M2P counts against the fp32 oracle's
+    leaf loop, accelerations and potentials to 1e-5 of the largest component."""
+    from swift_subtask_dev_amd import lib
+    gp = ics.uniform_gravity_box(16, epsilon=0.01, seed=6)
+    gp["old_a_grav_norm"] = np.random.Generator(np.random.PCG64(2)).uniform(20, 200, len(gp))
+    gs, leaves = ics.leaf_cells(gp, 4)  # 64-gpart leaves: the small-leaf kernels
+    offs, pairs = ics.neighbour_pairs(4, periodic=periodic, truncated=truncated)
+    self_pair = pairs["j"] == np.repeat(np.arange(len(leaves)), np.diff(offs))
+    pairs["allow_mpole"] = np.where(self_pair, 0, 1)
+    G = _params(1 if periodic else 0, 1.0 / 0.3 if truncated else 0.0,
+                0.0 if truncated else 1e30, 1.0, **dict(MACS["advanced"], theta=0.9))
+    ctx = lib.Context(0, "f32")
+    g = gs.copy()
+    sp = lib.GravSpace(ctx)
+    sp.upload(g)
+    sp.set_leaves(leaves, offs, pairs)
+    mp = sp.make_multipoles(want=True)
+    n, nm = sp.pp(G, m2p=True)
+    sp.download(g)
+    sp.close()
+    ctx.close()
+    o = gs.copy()
+    nmo = C.c_longlong(0)
+    no = O.fn("f32", "grav_pp_leaves")(o.ctypes.data, leaves.ctypes.data, len(leaves),
+                                       offs.ctypes.data, pairs.ctypes.data, C.byref(G),
+                                       C.cast(mp, C.c_void_p), C.byref(nmo))
+    assert nm == nmo.value and nm > 100, (nm, nmo.value)
+    assert n == no
+    a, b = g["a_grav"].astype(np.float64), o["a_grav"].astype(np.float64)
+    assert np.abs(a - b).max() <= 1e-5 * np.abs(b).max()
+    p, q = g["potential"].astype(np.float64), o["potential"].astype(np.float64)
+    assert np.abs(p - q).max() <= 1e-5 * np.abs(q).max()
+
+
+@pytest.mark.gpu
 def test_batch_mpole_requires_multipoles(gpu_ctx):
     from swift_subtask_dev_amd import lib
     gp = ics.uniform_gravity_box(8, epsilon=0.01, seed=6)

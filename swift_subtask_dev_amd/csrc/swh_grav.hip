@@ -1759,6 +1759,7 @@ struct GWalkOut {
   unsigned long long* mm_key;
   int* mm_val;  // symmetric
   int bits;     // key = cell << bits | other cell
+  int narrow;   // 2 bits <= 32: the keys are stored as 32-bit words (a lighter sort)
 };
 
 // The walk's view of a cell, one 64-byte line (a task reads two of them, not
@@ -1947,12 +1948,16 @@ __global__ __launch_bounds__(256) void gwalk_kernel(
   unsigned int w = wb.mm + (unsigned int)((ex >> 32) & 0xffffull);
   const int bits = o.bits;
   auto pp = [&](int a, int b, int tr, int mpole) {
-    o.pp_key[p] = ((unsigned long long)(unsigned int)a << bits) | (unsigned int)b;
+    const unsigned long long key = ((unsigned long long)(unsigned int)a << bits) | (unsigned int)b;
+    if (o.narrow) reinterpret_cast<unsigned int*>(o.pp_key)[p] = (unsigned int)key;
+    else o.pp_key[p] = key;
     o.pp_val[p] = tr | (mpole << 1);
     p++;
   };
   auto mm = [&](int t, int s, int sym) {
-    o.mm_key[w] = ((unsigned long long)(unsigned int)t << bits) | (unsigned int)s;
+    const unsigned long long key = ((unsigned long long)(unsigned int)t << bits) | (unsigned int)s;
+    if (o.narrow) reinterpret_cast<unsigned int*>(o.mm_key)[w] = (unsigned int)key;
+    else o.mm_key[w] = key;
     o.mm_val[w] = sym;
     w++;
   };
@@ -2003,35 +2008,39 @@ __global__ __launch_bounds__(256) void gwalk_kernel(
 
 // CSR offsets from keys sorted by (cell << bits | other): off[c] = the first
 // entry of cell c (lower bound), c = 0..ncells.
-__global__ void gw_csr_kernel(const unsigned long long* __restrict__ key, int n, int bits,
-                              int ncells, int* __restrict__ off) {
+template <typename K>
+__global__ void gw_csr_kernel(const K* __restrict__ key, int n, int bits, int ncells,
+                              int* __restrict__ off) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c > ncells) return;
+  // (c = ncells: all keys lie below it; 64-bit so that it cannot wrap)
   const unsigned long long v = (unsigned long long)(unsigned int)c << bits;
   int lo = 0, hi = n;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
-    if (key[mid] < v) lo = mid + 1;
+    if ((unsigned long long)key[mid] < v) lo = mid + 1;
     else hi = mid;
   }
   off[c] = lo;
 }
 
-__global__ void gw_unpack_pp(const unsigned long long* __restrict__ key, const int* __restrict__ val,
-                             int n, unsigned long long mask, swh_leaf_pair* __restrict__ out) {
+template <typename K>
+__global__ void gw_unpack_pp(const K* __restrict__ key, const int* __restrict__ val, int n,
+                             unsigned long long mask, swh_leaf_pair* __restrict__ out) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   swh_leaf_pair e;
-  e.j = (int)(key[k] & mask);
+  e.j = (int)((unsigned long long)key[k] & mask);
   e.truncated = val[k] & 1;
   e.allow_mpole = (val[k] >> 1) & 1;
   out[k] = e;
 }
-__global__ void gw_unpack_mm(const unsigned long long* __restrict__ key, const int* __restrict__ val,
-                             int n, unsigned long long mask, int2* __restrict__ out) {
+template <typename K>
+__global__ void gw_unpack_mm(const K* __restrict__ key, const int* __restrict__ val, int n,
+                             unsigned long long mask, int2* __restrict__ out) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
-  out[k] = make_int2((int)(key[k] & mask), val[k]);
+  out[k] = make_int2((int)((unsigned long long)key[k] & mask), val[k]);
 }
 
 // Grow a device buffer keeping its first `used` bytes.
@@ -2055,24 +2064,25 @@ static bool walk_debug() {
 }
 
 // Sort one entry list by key (only the bits keys use) and build its CSR.
+template <typename K>
 static swh_status gw_sort_csr(swh_gspace* g, DevBuf& key, DevBuf& val, DevBuf& key2, DevBuf& val2,
                               int n, int bits, int ncells, DevBuf& off, hipStream_t st) {
   SWH_TRY(off.reserve(((size_t)ncells + 1) * sizeof(int32_t)));
   if (n > 0) {
-    SWH_TRY(key2.reserve((size_t)n * 8));
+    SWH_TRY(key2.reserve((size_t)n * sizeof(K)));
     SWH_TRY(val2.reserve((size_t)n * 4));
     size_t tb = 0;
-    SWH_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.as<unsigned long long>(),
-                                               key2.as<unsigned long long>(), val.as<int>(),
-                                               val2.as<int>(), n, 0, 2 * bits, st));
+    SWH_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, key.as<K>(), key2.as<K>(),
+                                               val.as<int>(), val2.as<int>(), n, 0, 2 * bits,
+                                               st));
     SWH_TRY(g->wsort_tmp.reserve(tb));
     tb = g->wsort_tmp.bytes;
-    SWH_HIP(hipcub::DeviceRadixSort::SortPairs(g->wsort_tmp.ptr, tb, key.as<unsigned long long>(),
-                                               key2.as<unsigned long long>(), val.as<int>(),
-                                               val2.as<int>(), n, 0, 2 * bits, st));
+    SWH_HIP(hipcub::DeviceRadixSort::SortPairs(g->wsort_tmp.ptr, tb, key.as<K>(), key2.as<K>(),
+                                               val.as<int>(), val2.as<int>(), n, 0, 2 * bits,
+                                               st));
   }
-  hipLaunchKernelGGL(gw_csr_kernel, dim3((ncells + 1 + 255) / 256), dim3(256), 0, st,
-                     key2.as<const unsigned long long>(), n, bits, ncells, off.as<int>());
+  hipLaunchKernelGGL(gw_csr_kernel<K>, dim3((ncells + 1 + 255) / 256), dim3(256), 0, st,
+                     key2.as<const K>(), n, bits, ncells, off.as<int>());
   SWH_HIP(hipGetLastError());
   return SWH_OK;
 }
@@ -2089,6 +2099,7 @@ static swh_status device_walk(swh_gspace* g, const swh_grav_params* G, const int
   int bits = 1;
   while ((1ll << bits) < (long long)ncells) bits++;  // <= 31: keys of 2 * bits <= 62 bits
   const unsigned long long mask = (1ull << bits) - 1ull;
+  const bool narrow = 2 * bits <= 32;
   // the tasks that can reach an owned cell (all of them without ownership)
   const bool owns = !g->owned.empty();
   auto own = [&](int c) { return !owns || g->owned[c] != 0; };
@@ -2134,7 +2145,7 @@ static swh_status device_walk(swh_gspace* g, const swh_grav_params* G, const int
     GWCnt* wcnt = g->wcnt.as<GWCnt>();
     GWalkOut o{nxt->as<int4>(), wcnt, g->wbase.as<const GWCnt>(),
                g->pp_key.as<unsigned long long>(), g->pp_val.as<int>(),
-               g->mm_key.as<unsigned long long>(), g->mm_val.as<int>(), bits};
+               g->mm_key.as<unsigned long long>(), g->mm_val.as<int>(), bits, narrow ? 1 : 0};
     const dim3 grid((unsigned)((n_cur + 255) / 256));
     hipLaunchKernelGGL(gwalk_kernel<false>, grid, dim3(256), 0, st, cur->as<const int4>(),
                        (int)n_cur, g->tree_d.as<const swh_gcell>(), g->wrec.as<const GWRec>(), mac,
@@ -2170,22 +2181,34 @@ static swh_status device_walk(swh_gspace* g, const swh_grav_params* G, const int
   *n_pp = npp;
   *n_mm = nmm;
   *n_skip = h.skip;
-  SWH_TRY(gw_sort_csr(g, g->pp_key, g->pp_val, g->pp_key2, g->pp_val2, npp, bits, ncells,
-                      g->pair_off, st));
-  SWH_TRY(gw_sort_csr(g, g->mm_key, g->mm_val, g->mm_key2, g->mm_val2, nmm, bits, ncells,
-                      g->m2l_off, st));
+  // 32-bit keys when they fit: half the radix sort's key traffic
+  auto sort_csr = narrow ? gw_sort_csr<unsigned int> : gw_sort_csr<unsigned long long>;
+  SWH_TRY(sort_csr(g, g->pp_key, g->pp_val, g->pp_key2, g->pp_val2, npp, bits, ncells,
+                   g->pair_off, st));
+  SWH_TRY(sort_csr(g, g->mm_key, g->mm_val, g->mm_key2, g->mm_val2, nmm, bits, ncells,
+                   g->m2l_off, st));
   SWH_TRY(g->pairs.reserve((size_t)std::max(1, npp) * sizeof(swh_leaf_pair)));
   SWH_TRY(g->m2l_src.reserve((size_t)std::max(1, nmm) * sizeof(int2)));
   if (npp > 0) {
-    hipLaunchKernelGGL(gw_unpack_pp, dim3((npp + 255) / 256), dim3(256), 0, st,
-                       g->pp_key2.as<const unsigned long long>(), g->pp_val2.as<const int>(), npp,
-                       mask, g->pairs.as<swh_leaf_pair>());
+    if (narrow)
+      hipLaunchKernelGGL(gw_unpack_pp<unsigned int>, dim3((npp + 255) / 256), dim3(256), 0, st,
+                         g->pp_key2.as<const unsigned int>(), g->pp_val2.as<const int>(), npp,
+                         mask, g->pairs.as<swh_leaf_pair>());
+    else
+      hipLaunchKernelGGL(gw_unpack_pp<unsigned long long>, dim3((npp + 255) / 256), dim3(256),
+                         0, st, g->pp_key2.as<const unsigned long long>(),
+                         g->pp_val2.as<const int>(), npp, mask, g->pairs.as<swh_leaf_pair>());
     SWH_HIP(hipGetLastError());
   }
   if (nmm > 0) {
-    hipLaunchKernelGGL(gw_unpack_mm, dim3((nmm + 255) / 256), dim3(256), 0, st,
-                       g->mm_key2.as<const unsigned long long>(), g->mm_val2.as<const int>(), nmm,
-                       mask, g->m2l_src.as<int2>());
+    if (narrow)
+      hipLaunchKernelGGL(gw_unpack_mm<unsigned int>, dim3((nmm + 255) / 256), dim3(256), 0, st,
+                         g->mm_key2.as<const unsigned int>(), g->mm_val2.as<const int>(), nmm,
+                         mask, g->m2l_src.as<int2>());
+    else
+      hipLaunchKernelGGL(gw_unpack_mm<unsigned long long>, dim3((nmm + 255) / 256), dim3(256),
+                         0, st, g->mm_key2.as<const unsigned long long>(),
+                         g->mm_val2.as<const int>(), nmm, mask, g->m2l_src.as<int2>());
     SWH_HIP(hipGetLastError());
   }
   g->npairs = npp;

@@ -346,16 +346,18 @@ def _grid_parts(O, g, n):
     return abi.copy_parts(np.frombuffer(raw, dtype=np.uint8).view(abi.PART_DTYPE))
 
 
-def parity_vs_cpu(ctx, parts, P, tuning, threads):
+def parity_vs_cpu(ctx, parts, P, tuning, threads, workload="sedov"):
     """Outside the timed region: one density loop (after hydro_init_part) and
     one force loop (after hydro_reset_acceleration) on the bench's own input,
     on the GPU and in the CPU baseline's float port; max relative differences
     per output field, matched by particle id."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib as O
+    import parity_bars as B
     from swift_subtask_dev_amd import abi, lib
 
     n = len(parts)
+    bars = B.BARS["eagle" if workload == "eagle" else "sedov128"]
     eb = abi.EngineBundle(dim=tuple(P.dim), periodic=True, params=P, max_active_bin=P.max_active_bin)
     # GPU
     gd, gf = abi.copy_parts(parts), abi.copy_parts(parts)
@@ -379,7 +381,7 @@ def parity_vs_cpu(ctx, parts, P, tuning, threads):
     cf["u_dt"] = 0
     cf["h_dt"] = 0
     cf["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
-    out = {}
+    out, bar = {}, {}
     for arr, loop, fields in ((cd, 0, ("rho", "wcount", "wcount_dh", "rho_dh", "div_v")),
                               (cf, 2, ("a_hydro", "u_dt", "h_dt"))):
         g = O.fn("f32", "cellgrid_new")(arr.ctypes.data, n, float(P.dim[0]), 20)
@@ -394,17 +396,58 @@ def parity_vs_cpu(ctx, parts, P, tuning, threads):
             b = cpu[f].astype(np.float64).reshape(n, -1)
             floor = (1e-6 if loop == 0 else 1e-4) * max(np.abs(b).max(), 1e-300)
             out[f] = float((np.abs(a - b) / np.maximum(np.abs(b), floor)).max())
+            if f in bars:  # the stated tolerance of tests/parity_bars.py
+                mx, q = B.summary(gpu, cpu, (f,))[f]
+                bar[f] = {"max": mx, "p99.9": q, "bar_max": bars[f][0], "bar_p99.9": bars[f][1],
+                          "ok": bool(mx <= bars[f][0] and q <= bars[f][1])}
         if loop == 2:
             out["min_ngb_time_bin_equal"] = bool(np.array_equal(gpu["min_ngb_time_bin"],
                                                                 cpu["min_ngb_time_bin"]))
     return {"vs": "cpu_baseline float port (same input, one density + one force loop)",
             "max_rel": out,
+            "bars": bar,
+            "bars_source": "tests/parity_bars.py (floor 1e-4 x the column maximum; the same "
+                           "bars test_gpu_physics.py::test_baseline_chain_from_unconverged_vs_f32 "
+                           "asserts on the whole chain)",
             "floor": "1e-6 (density fields) / 1e-4 (force fields) x the column maximum",
             "note": "GPU fp64 against the FLOAT port (the reference's own precision): the "
                     "differences are the port's float rounding (a_hydro ~1e-3 relative where "
                     "pressure-gradient terms cancel); against the f64 oracle the same loops "
                     "hold 2e-6 (density) / 5e-5 (force) with exact counts "
                     "(tests/test_gpu_parity.py, test_gpu_physics.py)"}
+
+
+def chain_vs_f32(raw, gpu, gpu_counts, P, workload):
+    """Outside the timed region: the setup's whole GPU chain (density, ghost,
+    gradient, extra ghost, force, end force from the unconverged input)
+    against the float restatement's chain on the same input, per field under
+    the stated bars of tests/parity_bars.py -- the check
+    test_gpu_physics.py::test_baseline_chain_from_unconverged_vs_f32 asserts."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib as O
+    import parity_bars as B
+    from swift_subtask_dev_amd import abi
+
+    o = abi.copy_parts(raw)
+    n = len(o)
+    O.fn("f32", "init_parts")(o.ctypes.data, n, C.byref(P))
+    counts = {"density": O.fn("f32", "box_density")(o.ctypes.data, n, C.byref(P), None)}
+    nfail = C.c_longlong(0)
+    O.fn("f32", "box_ghost")(o.ctypes.data, n, C.byref(P), C.byref(nfail))
+    counts["gradient"] = O.fn("f32", "box_gradient")(o.ctypes.data, n, C.byref(P), None)
+    O.fn("f32", "box_extra_ghost")(o.ctypes.data, n, C.byref(P))
+    counts["force"] = O.fn("f32", "box_force")(o.ctypes.data, n, C.byref(P), None)
+    O.fn("f32", "box_end_force")(o.ctypes.data, n, C.byref(P))
+    bars = B.BARS["eagle" if workload == "eagle" else "sedov128"]
+    res = {}
+    for f, (mx, q) in B.summary(gpu, o, bars).items():
+        res[f] = {"max": mx, "p99.9": q, "bar_max": bars[f][0], "bar_p99.9": bars[f][1],
+                  "ok": bool(mx <= bars[f][0] and q <= bars[f][1])}
+    cnt = {k: {"gpu": int(gpu_counts[k]), "f32": int(v),
+               "ok": bool(abs(gpu_counts[k] - v) <= B.COUNT_REL * v)} for k, v in counts.items()}
+    return {"vs": "liboracle_f32 whole chain (the reference's float arithmetic) from the same "
+                  "unconverged input", "fields": res, "counts": cnt,
+            "all_ok": all(r["ok"] for r in res.values()) and all(c["ok"] for c in cnt.values())}
 
 
 def step_breakdown(sp, P, stream, torch, local, reps=3):
@@ -1037,11 +1080,14 @@ def main():
     # ---- untimed setup: the full SPHENIX chain on the whole box ----------
     sp = lib.HydroSpace(ctx)
     sp.set_tuning(args.cell_factor, list_capacity=args.list_capacity, list_skin=args.list_skin)
+    # the parity leg's chain check starts from the same unconverged input
+    raw = abi.copy_parts(parts) if (world == 1 and not args.no_cpu_baseline) else None
     sp.upload(parts)
     sp.rebuild(P)
     chain = sp.hydro_step(P)
     sp.download(parts, abi.FIELDS_ALL)
     sp.close()
+    chain_gpu = abi.copy_parts(parts) if raw is not None else None
     if eagle:  # converged h: re-bin on the final smoothing lengths
         log(f"[rank {rank}] eagle stand-in: {len(parts)} parts, h {parts['h'].min():.3g}.."
             f"{parts['h'].max():.3g}, chain ghost iterations {chain['ghost_iterations']}")
@@ -1287,9 +1333,16 @@ def main():
                           0, args.list_capacity, args.list_skin)
                 out["parity"] = parity_vs_cpu(ctx, local, P, tuning,
                                               out["cpu_baseline"]["cores"]
-                                              if out["cpu_baseline"] else 16)
+                                              if out["cpu_baseline"] else 16, args.workload)
+
             except Exception as e:  # report, never fake
                 log(f"parity check failed: {e}")
+        if raw is not None:
+            try:
+                out.setdefault("parity", {})["chain_vs_f32"] = chain_vs_f32(
+                    raw, chain_gpu, chain, P, args.workload)
+            except Exception as e:  # report, never fake
+                log(f"chain parity check failed: {e}")
         print(json.dumps(out), flush=True)
     sp.close()
     ctx.close()

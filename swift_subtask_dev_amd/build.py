@@ -71,7 +71,12 @@ def build_variant(kernel: str, force: bool = False, verbose: bool = False,
         # experiment flags (e.g. -DSWH_M2P_PROF); any set forces a full rebuild
         *os.environ.get("SWH_EXTRA_FLAGS", "").split(),
     ]
-    force = force or bool(os.environ.get("SWH_EXTRA_FLAGS"))
+    # the flags of the objects in objdir: a build with other flags (an
+    # experiment's SWH_EXTRA_FLAGS, or a plain build after one) rebuilds all
+    stamp = objdir / "flags.stamp"
+    flags = " ".join(common)
+    if not stamp.exists() or stamp.read_text() != flags:
+        force = True
     objs, cmds = [], []
     for src in HIP_SOURCES:
         s = CSRC / src
@@ -95,6 +100,7 @@ def build_variant(kernel: str, force: bool = False, verbose: bool = False,
         _run(["gcc", "-O2", "-std=gnu11", "-fPIC", "-shared", "-Wall", f"-I{INCLUDE}", *defines,
               "-o", str(adapter), str(asrc), f"-L{PKG}", f"-l:{lib.name}",
               "-Wl,-rpath,$ORIGIN"])
+    stamp.write_text(flags)
     return lib
 
 

@@ -958,10 +958,12 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const Seg
   unsigned int* mark = nullptr;
   unsigned int* qn = grown_qn_slot(s);
   if (grown) {
-    if (!s->grown_mark.ptr) {
-      SWH_TRY(s->grown_mark.reserve((size_t)s->n * sizeof(unsigned int)));
-      SWH_HIP(hipMemsetAsync(s->grown_mark.ptr, 0, (size_t)s->n * sizeof(unsigned int),
-                             s->stream));
+    // the marks stay zero between uses (grown_clear_kernel); a (re)allocation
+    // -- first use, or an upload that raised n since -- starts them zeroed
+    const size_t mark_bytes = (size_t)s->n * sizeof(unsigned int);
+    if (s->grown_mark.bytes < mark_bytes) {
+      SWH_TRY(s->grown_mark.reserve(mark_bytes));
+      SWH_HIP(hipMemsetAsync(s->grown_mark.ptr, 0, s->grown_mark.bytes, s->stream));
     }
     SWH_TRY(s->grown_search.reserve((size_t)s->n * sizeof(int)));
     mark = s->grown_mark.as<unsigned int>();

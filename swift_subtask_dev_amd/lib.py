@@ -177,6 +177,13 @@ def load(kernel: str = "cubic-spline") -> C.CDLL:
 def load_adapter(kernel: str = "cubic-spline") -> C.CDLL:
     if kernel in _adapters:
         return _adapters[kernel]
+    if "SWH_LIB_PATH" in os.environ and kernel == "cubic-spline":
+        # the adapter links its own $ORIGIN/libswifthip.so: with an override
+        # the process would hold two copies (two contexts, two error states)
+        # and the adapter tests would silently run the in-tree build
+        raise ImportError("SWH_LIB_PATH overrides libswifthip.so, but the SWIFT-signature "
+                          "adapter is linked against the in-tree build: unset SWH_LIB_PATH "
+                          "to load the adapter")
     load(kernel)
     path = ADAPTER_LIBS[kernel]
     if not path.exists():

@@ -1,0 +1,251 @@
+"""BASELINE configs 4 and 5 checked at the sizes bench.py reports.
+
+* Config 4 (GravityTests uniform DM box 256^3, bench.py --workload grav): the
+  bench's own box -- 16,777,216 gparts (seed 256), softening 0.001, a 35^3
+  grid of leaves (42,875, up to ~480 gparts) and every leaf with itself and
+  its 26 neighbours -- run whole on the GPU. A sample of i-leaves (the first
+  1% the CPU baseline times, the largest leaf, 64 random leaves) is compared
+  with the fp64 oracle's runner_doself_grav_pp / runner_dopair_grav_pp
+  restatement (grav_pp_leaves; runner_doiact_grav.c:1788-1871, 1202-1425):
+  a_grav and potential to 1e-6 of the column maximum, the sampled leaves'
+  interaction count exact, and the whole box's count equal to the direct
+  count sum_l n_l (sum over the 27 leaves n_j) - n_l.
+* Config 5 (SmallCosmoVolume stand-in, 64^3 gas + 64^3 DM, bench.py
+  --workload cosmo --gpus 2) sharded as the bench shards it, with the two
+  ranks run in turn on cuda:0: the gas by hydro blocks (decomp.HaloPlan, owned
+  block + read-only halo, swh_space_set_owned) with the halo's rho refreshed
+  point-to-point between the density and force loops (pack_halo /
+  unpack_halo), the gravity by owned subtrees (swh_gspace_set_owned_cells)
+  under the yml's adaptive MAC. The union over ranks equals the oracle's
+  single-domain step: density and force counts add up exactly, the fields at
+  the single-loop tolerances; P2P / M2P / M2L counts add up and the owned
+  gparts' a_grav and potential equal the single-domain GPU step bit for bit
+  and the oracle's to 2e-5.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from test_gpu_parity import TIGHT, _by_id, assert_close, assert_hydro_close
+from swift_subtask_dev_amd import abi, cosmo, decomp, ics
+
+pytestmark = pytest.mark.gpu
+
+KERNEL_GAMMA = 1.825742
+
+
+# ---------------------------------------------------------------------------
+# config 4
+# ---------------------------------------------------------------------------
+def test_grav256_bench_box_sampled_leaves_vs_f64(gpu_ctx):
+    from swift_subtask_dev_amd import lib
+    n = 256
+    gp = ics.uniform_gravity_box(n, epsilon=0.001, seed=256)  # bench.py run_grav's input
+    cdim = int(np.ceil((n ** 3 / 400.0) ** (1.0 / 3.0)))
+    gs, leaves = ics.leaf_cells(gp, cdim)
+    del gp
+    offs, pairs = ics.neighbour_pairs(cdim, periodic=False, truncated=0)
+    nl = len(leaves)
+    assert (cdim, nl) == (35, 42875) and leaves["count"].max() > 450
+    G = abi.GravParams(0, (C.c_float * 3)(1, 1, 1), 0.0, 1e30, abi.NUM_TIME_BINS)
+    # the whole box on the GPU, as the bench times it
+    g = abi.copy_parts(gs)
+    sp = lib.GravSpace(gpu_ctx)
+    sp.upload(g)
+    sp.set_leaves(leaves, offs, pairs)
+    n_all = sp.pp(G)
+    sp.download(g)
+    cnt = leaves["count"].astype(np.int64)
+    nsrc = np.add.reduceat(cnt[pairs["j"]], offs[:-1])  # every leaf has >= 8 sources
+    assert n_all == int((cnt * nsrc).sum() - cnt.sum())
+    # the sampled i-leaves: the CPU baseline's first 1%, the largest, 64 random
+    rng = np.random.Generator(np.random.PCG64(256))
+    sample = np.unique(np.concatenate([np.arange(nl // 100), [int(np.argmax(cnt))],
+                                       rng.choice(nl, 64, replace=False)]))
+    so = np.zeros(nl + 1, dtype=np.int64)
+    so[sample + 1] = np.diff(offs)[sample]
+    so = np.cumsum(so).astype(np.int32)
+    sp_pairs = np.concatenate([pairs[offs[k]:offs[k + 1]] for k in sample])
+    # the sampled lists alone on the GPU: their exact count
+    gsmp = abi.copy_parts(gs)
+    sp.upload(gsmp)
+    sp.set_leaves(leaves, so, sp_pairs)
+    n_smp = sp.pp(G)
+    sp.download(gsmp)
+    sp.close()
+    o = abi.copy_parts(gs)
+    no = O.fn("f64", "grav_pp_leaves")(o.ctypes.data, leaves.ctypes.data, nl, so.ctypes.data,
+                                       sp_pairs.ctypes.data, C.byref(G), None, None)
+    assert n_smp == no
+    idx = np.concatenate([np.arange(leaves["start"][k], leaves["start"][k] + cnt[k])
+                          for k in sample])
+    print(f"\n256^3: {n_all} P2P interactions, sample of {len(sample)} leaves "
+          f"({len(idx)} gparts, {no} interactions), largest leaf {cnt.max()}")
+    for f in ("a_grav", "potential"):
+        # the whole-box run vs the oracle on the sampled leaves' gparts
+        a = g[f][idx].astype(np.float64)
+        b = o[f][idx].astype(np.float64)
+        assert np.abs(a - b).max() <= 1e-6 * np.abs(b).max(), (f, np.abs(a - b).max())
+        # and the sampled run is the whole-box run on those gparts, bit for bit
+        assert np.array_equal(gsmp[f][idx], g[f][idx]), f
+
+
+# ---------------------------------------------------------------------------
+# config 5, sharded over two logical ranks on cuda:0
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def cosmo_volume(gpu_ctx):
+    """The bench's config-5 input after its untimed setup: the gas converged
+    by a whole chain on the GPU, the gravity inputs with old_a_grav_norm from
+    an untimed geometric-MAC step."""
+    from swift_subtask_dev_amd import lib
+    gas, gp = ics.small_cosmo_volume(64)
+    _, P = cosmo.small_cosmo_volume_params()
+    gas["time_bin"] = cosmo.SCV_FIRST_BIN
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.upload(gas)
+    sp.rebuild(P)
+    sp.hydro_step(P)
+    sp.download(gas, abi.FIELDS_ALL)
+    sp.close()
+    return gas, gp, P
+
+
+def _exchange_rho(spaces, plans):
+    """One point-to-point halo refresh of rho between logical ranks sharing a
+    device (what decomp.exchange does across processes)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    recs = {}
+    for r, (sp, plan) in enumerate(zip(spaces, plans)):
+        for q, idx in plan.send.items():
+            ti = torch.from_numpy(idx).to(dev)
+            buf = torch.empty(len(idx) * abi.HALO_RECORD_FLOATS, dtype=torch.float32, device=dev)
+            torch.cuda.synchronize()
+            sp.pack_halo(ti.data_ptr(), len(idx), buf.data_ptr())
+            sp.sync()
+            recs[(r, q)] = buf
+    for q, (sp, plan) in enumerate(zip(spaces, plans)):
+        for r, idx in plan.recv_idx.items():
+            ti = torch.from_numpy(idx).to(dev)
+            buf = recs[(r, q)]
+            assert len(buf) == len(idx) * abi.HALO_RECORD_FLOATS
+            torch.cuda.synchronize()
+            sp.unpack_halo(ti.data_ptr(), len(idx), buf.data_ptr(), abi.HALO_RHO)
+            sp.sync()
+
+
+def test_cosmo_volume_hydro_blocks_two_ranks_vs_f64(gpu_ctx, cosmo_volume):
+    """bench.py --workload cosmo --gpus 2's hydro step on the blocks: density,
+    the rho refresh, force; the union of the owned outputs vs the oracle's
+    single-domain loops on the same converged gas."""
+    from swift_subtask_dev_amd import lib
+    gas, _, P = cosmo_volume
+    world, box = 2, (1.0, 1.0, 1.0)
+    reach = 1.01 * KERNEL_GAMMA * float(gas["h"].max())  # bench.py run_cosmo's halo reach
+    plans = [decomp.HaloPlan(gas["x"], box, world, r, reach) for r in range(world)]
+    locs = [p.local_set(gas) for p in plans]
+    spaces = []
+    nd, nf = [], []
+    for loc, plan in zip(locs, plans):
+        sp = lib.HydroSpace(gpu_ctx)
+        sp.upload(loc)
+        sp.set_owned(plan.n_owned)
+        sp.rebuild(P)
+        sp.init_parts(P)
+        nd.append(sp.density(P))
+        spaces.append(sp)
+    # (struct part's density and force unions share bytes: one download each)
+    dens = [abi.copy_parts(loc) for loc in locs]
+    for sp, d in zip(spaces, dens):
+        sp.download(d, abi.FIELDS_DENSITY)
+    _exchange_rho(spaces, plans)
+    for sp, loc in zip(spaces, locs):
+        sp.reset_acceleration(P)
+        nf.append(sp.force(P))
+        sp.download(loc, abi.FIELDS_FORCE)
+        sp.close()
+    union_d = np.concatenate([d[: p.n_owned] for d, p in zip(dens, plans)])
+    union = np.concatenate([loc[: p.n_owned] for loc, p in zip(locs, plans)])
+    assert len(union) == len(gas) and len(np.unique(union["id"])) == len(gas)
+    # the oracle: one density loop and one force loop on the whole volume
+    od = abi.copy_parts(gas)
+    O.fn("f32", "init_parts")(od.ctypes.data, len(od), C.byref(P))
+    n_od = O.fn("f64", "box_density")(od.ctypes.data, len(od), C.byref(P), None)
+    of = abi.copy_parts(gas)
+    of["rho"] = od["rho"]  # the force loop reads the density loop's rho, as the refresh gives it
+    of["a_hydro"] = 0
+    of["u_dt"] = 0
+    of["h_dt"] = 0
+    of["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
+    n_of = O.fn("f64", "box_force")(of.ctypes.data, len(of), C.byref(P), None)
+    print(f"\ncosmo blocks: density {nd} (oracle {n_od}), force {nf} (oracle {n_of}), "
+          f"owned {[p.n_owned for p in plans]}, halo {[p.n_local - p.n_owned for p in plans]}")
+    assert sum(nd) == n_od and sum(nf) == n_of
+    assert_hydro_close(_by_id(union_d), _by_id(od), TIGHT, "cosmo blocks density")
+    u = _by_id(union)
+    ofi = _by_id(of)
+    for f in ("a_hydro", "u_dt", "h_dt"):
+        assert_close(u[f], ofi[f], 5e-5, 1e-4, f)
+    assert np.array_equal(u["min_ngb_time_bin"], ofi["min_ngb_time_bin"])
+
+
+def test_cosmo_volume_gravity_owned_subtrees_two_ranks_vs_f64(gpu_ctx, cosmo_volume):
+    """The sharded gravity of the same step: the two ranks' owned subtrees
+    (adaptive MAC, r_cut_max 4.5 r_s) on the 64^3 + 64^3 tree, each with the
+    PM mesh of its replicated gparts; the union equals the single-domain
+    step."""
+    from swift_subtask_dev_amd import lib
+    from test_gpu_cosmo_volume import N_MESH, R_S, _oracle_gravity, grav_params
+    _, gp, _ = cosmo_volume
+    world, box = 2, (1.0, 1.0, 1.0)
+    g, cells, tops = ics.gravity_tree(gp, 8, split_size=50)
+    pairs = ics.top_level_pairs(tops)
+    G = grav_params(adaptive=False)
+
+    def run(owned):
+        gs = lib.GravSpace(gpu_ctx)
+        gs.upload(g)
+        gs.set_tree(cells)
+        if owned is not None:
+            gs.set_owned_cells(owned)
+        st = gs.tree(G, tops, pairs)
+        gs.pm_mesh(N_MESH, 1.0, R_S, 1.0)
+        out = abi.copy_parts(g)
+        gs.download(out)
+        gs.close()
+        return out, st
+
+    g0, _ = run(None)  # the untimed geometric step: |a| for the adaptive MAC
+    g["old_a_grav_norm"] = np.linalg.norm(g0["a_grav"].astype(np.float64)
+                                          + g0["a_grav_mesh"].astype(np.float64), axis=1)
+    G = grav_params(adaptive=True)
+    ref, st_ref = run(None)
+    owned = [decomp.gravity_owned_cells(cells, tops, r, world, box) for r in range(world)]
+    assert np.array_equal(owned[0] + owned[1], np.ones(len(cells)))
+    parts, stats = [], []
+    for r in range(world):
+        out, st = run(owned[r])
+        idx = np.concatenate([np.arange(c["start"], c["start"] + c["count"])
+                              for c, o in zip(cells, owned[r]) if o and not c["split"]])
+        parts.append((idx, out))
+        stats.append(st)
+    idx = np.concatenate([p[0] for p in parts])
+    assert len(idx) == len(g) and len(np.unique(idx)) == len(g)
+    for k in ("n_pp", "n_m2p", "n_m2l"):
+        assert sum(s[k] for s in stats) == st_ref[k], (k, [s[k] for s in stats], st_ref[k])
+    for f in ("a_grav", "potential", "a_grav_mesh", "potential_mesh"):
+        for i, out in parts:
+            assert np.array_equal(out[f][i], ref[f][i]), f
+    go, st_o = _oracle_gravity(g, cells, tops, pairs, G)
+    print(f"\ncosmo owned subtrees: {[dict((k, s[k]) for k in ('n_pp', 'n_m2p', 'n_m2l')) for s in stats]}"
+          f" single domain {st_ref} oracle {list(st_o)}")
+    assert [st_ref["n_pp"], st_ref["n_m2p"], st_ref["n_m2l"]] == list(st_o[:3])
+    a_o = go["a_grav"].astype(np.float64)
+    e = np.linalg.norm(ref["a_grav"].astype(np.float64) - a_o, axis=1) / \
+        np.maximum(np.linalg.norm(a_o, axis=1), 1e-30)
+    assert e.max() < 2e-5, e.max()

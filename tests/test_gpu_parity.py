@@ -824,3 +824,41 @@ def test_chain_few_grown_searched(gpu_ctx, request, adaptive):
     assert_close(g["a_hydro"], o["a_hydro"], tol, 1e-3 if adaptive else 1e-4, "a_hydro")
     assert_close(g["u_dt"], o["u_dt"], tol, 1e-3 if adaptive else 1e-4, "u_dt")
     assert np.array_equal(g["min_ngb_time_bin"], o["min_ngb_time_bin"])
+
+
+@pytest.mark.gpu
+def test_grown_after_larger_upload(gpu_ctx):
+    """The grown-particle marks are sized to the space's particle count: a
+    space that took the grown-search path at 16^3 and is then given a larger
+    particle set (20^3) takes it again, with marks for every particle (the
+    buffer is re-reserved and zeroed when n grows), and the chain still equals
+    the oracle's."""
+    from swift_subtask_dev_amd import lib
+    P = abi.default_hydro_params()
+
+    def cut_state(n, seed):
+        parts = ics.sedov_box(n, velocity="divergent", pert=0.3, seed=seed)
+        conv, _ = box_chain_oracle(parts, P)
+        parts = abi.copy_parts(parts)
+        parts["h"] = conv["h"]
+        cut = np.random.Generator(np.random.PCG64(seed)).choice(len(parts), 6, replace=False)
+        parts["h"][cut] *= 0.7
+        return parts
+
+    sp = lib.HydroSpace(gpu_ctx)
+    for n, seed in ((16, 5), (20, 6)):
+        parts = cut_state(n, seed)
+        g = abi.copy_parts(parts)
+        sp.upload(g)
+        sp.rebuild(P)
+        b0 = sp.info()["list_builds"]
+        rg = sp.hydro_step(P)
+        builds = sp.info()["list_builds"] - b0
+        sp.download(g, abi.FIELDS_ALL)
+        o, ro = box_chain_oracle(parts, P)
+        assert builds == 1, (n, builds)  # the grown few searched, not rebuilt
+        assert rg["gradient"] == ro["gradient"] and rg["force"] == ro["force"], n
+        assert_close(g["h"], o["h"], 1e-6, what="h")
+        assert_close(g["a_hydro"], o["a_hydro"], 5e-5, 1e-4, "a_hydro")
+        assert np.array_equal(g["min_ngb_time_bin"], o["min_ngb_time_bin"])
+    sp.close()

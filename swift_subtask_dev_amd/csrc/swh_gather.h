@@ -35,8 +35,14 @@ struct JRec {
   int meta;
 };
 
+// fp64 (the batch path): the sums of iact_nonsym_density_raw, finalized at
+// the store; fp32 (SWH_PRECISION_F32): the reference's own arithmetic.
+#ifndef SWH_DENS_RAW
+#define SWH_DENS_RAW 1
+#endif
 template <typename T>
 struct LoopState<LOOP_DENSITY, T> {
+  static constexpr bool kRaw = SWH_DENS_RAW && sizeof(T) == 8;
   int self, n;
   double reach;
   T hig2, hi_inv, vix, viy, viz;
@@ -53,14 +59,19 @@ struct LoopState<LOOP_DENSITY, T> {
     reach = p.w * (double)kGamma;
     A.zero();
   }
+  __device__ __forceinline__ void iact(T r2, T dx, T dy, T dz, T mj, T vjx, T vjy, T vjz) {
+    if constexpr (kRaw)
+      iact_nonsym_density_raw(r2, dx, dy, dz, hi_inv, vix, viy, viz, mj, vjx, vjy, vjz, A);
+    else
+      iact_nonsym_density<T>(r2, dx, dy, dz, hi_inv, vix, viy, viz, mj, vjx, vjy, vjz, A);
+  }
   __device__ __forceinline__ bool accept(int j, const double4&, T r2) const {
     return (r2 < hig2) & (j != self);
   }
   __device__ __forceinline__ void interact(const SoA& a, int j, const double4&, T dx, T dy,
                                            T dz, T r2) {
     const float4 v = a.vm[j];
-    iact_nonsym_density<T>(r2, dx, dy, dz, hi_inv, vix, viy, viz, (T)v.w, (T)v.x, (T)v.y,
-                           (T)v.z, A);
+    iact(r2, dx, dy, dz, (T)v.w, (T)v.x, (T)v.y, (T)v.z);
     n++;
   }
   static constexpr int kPay = 1;
@@ -72,11 +83,12 @@ struct LoopState<LOOP_DENSITY, T> {
   }
   __device__ __forceinline__ void interact_staged(const float4* p, int, const double4&, T dx,
                                                   T dy, T dz, T r2) {
-    iact_nonsym_density<T>(r2, dx, dy, dz, hi_inv, vix, viy, viz, (T)p[0].w, (T)p[0].x,
-                           (T)p[0].y, (T)p[0].z, A);
+    iact(r2, dx, dy, dz, (T)p[0].w, (T)p[0].x, (T)p[0].y, (T)p[0].z);
     n++;
   }
   __device__ __forceinline__ void store(SoA& a, int i) const {
+    DensityAcc<T> A = this->A;
+    if constexpr (kRaw) A = density_finalize(this->A);
     float4 d = a.dens[i];
     float4 r = a.rot[i];
     a.th[i].y = (float)((T)a.th[i].y + A.rho);

@@ -225,6 +225,65 @@ __device__ __forceinline__ void iact_nonsym_density(T r2, T dx, T dy, T dz, T hi
   A.rot_z += faci * (dvx * dy - dvy * dx);
 }
 
+// The fp64 batch loops' form of runner_iact_nonsym_density: the same sums
+// with the kernel's constant factors taken out of the per-pair work
+// (density_finalize puts them back at the store; fp64 rounding only).
+//   A.rho = sum m_j w        A.wcount = sum w           (w  = W / C_W)
+//   A.rho_dh = sum m_j u dw  A.wcount_dh = sum u dw     (dw = dW/du / C_dW)
+//   A.div_v, A.rot_*: the sums of m_j dw / r (dv . dx), m_j dw / r (dv x dx)
+// with x = u / gamma, w = (1 - x)^3_+ - 4 (1/2 - x)^3_+, dw = 12 (1/2 - x)^2_+
+// - 3 (1 - x)^2_+ for the cubic spline (Wendland C2: w = (1 - x)^4 (1 + 4x),
+// dw = -20 x (1 - x)^3), C_W = kConstant gamma^-3, C_dW = kConstant gamma^-4.
+__device__ __forceinline__ void iact_nonsym_density_raw(double r2, double dx, double dy, double dz,
+                                                        double hi_inv, double vix, double viy,
+                                                        double viz, double mj, double vjx,
+                                                        double vjy, double vjz,
+                                                        DensityAcc<double>& A) {
+  double r, r_inv;
+  r_and_inv(r2, r, r_inv);
+  const double ui = r * hi_inv;
+  const double x = ui * (double)kGammaInv;
+  const double t = fmax(1. - x, 0.);
+#if defined(SWH_KERNEL_WENDLAND_C2)
+  const double t3 = t * t * t;
+  const double w = t3 * t * fma(4., x, 1.);
+  const double dw = -20. * x * t3;
+#else
+  const double q = fmax(0.5 - x, 0.);
+  const double t2 = t * t, q2 = q * q;
+  const double w = fma(-4. * q2, q, t2 * t);
+  const double dw = fma(12., q2, -3. * t2);
+#endif
+  const double udw = ui * dw;
+  A.wcount += w;
+  A.rho = fma(mj, w, A.rho);
+  A.wcount_dh += udw;
+  A.rho_dh = fma(mj, udw, A.rho_dh);
+  const double faci = mj * dw * r_inv;
+  const double dvx = vix - vjx, dvy = viy - vjy, dvz = viz - vjz;
+  const double dvdr = dvx * dx + dvy * dy + dvz * dz;
+  A.div_v -= faci * dvdr;
+  A.rot_x += faci * (dvy * dz - dvz * dy);
+  A.rot_y += faci * (dvz * dx - dvx * dz);
+  A.rot_z += faci * (dvx * dy - dvy * dx);
+}
+
+// The runner_iact_nonsym_density sums from iact_nonsym_density_raw's.
+__device__ __forceinline__ DensityAcc<double> density_finalize(const DensityAcc<double>& R) {
+  constexpr double cw = (double)kConstant * (double)kGammaInvDim;
+  constexpr double cdw = (double)kConstant * (double)kGammaInvDimPlusOne;
+  DensityAcc<double> A;
+  A.rho = cw * R.rho;
+  A.wcount = cw * R.wcount;
+  A.rho_dh = -fma((double)kDim * cw, R.rho, cdw * R.rho_dh);
+  A.wcount_dh = -fma((double)kDim * cw, R.wcount, cdw * R.wcount_dh);
+  A.div_v = cdw * R.div_v;
+  A.rot_x = cdw * R.rot_x;
+  A.rot_y = cdw * R.rot_y;
+  A.rot_z = cdw * R.rot_z;
+  return A;
+}
+
 template <typename T>
 struct GradientAcc {
   T v_sig, laplace_u, alpha_visc_max_ngb;

@@ -958,7 +958,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=128, help="particles per dimension per GPU")
     ap.add_argument("--cell-factor", type=int, default=int(os.environ.get("SWH_CELL_FACTOR", "1")))
-    ap.add_argument("--loop-variant", type=int, default=0, choices=[0, 7, 8],
+    ap.add_argument("--loop-variant", type=int, default=0, choices=[0, 7],
                     help="0 default (7): pair lists")
     ap.add_argument("--cell-scale", type=float, default=float(os.environ.get("SWH_CELL_SCALE", "0")),
                     help="grid cells per H_max as a real number (overrides --cell-factor)")

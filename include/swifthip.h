@@ -359,9 +359,7 @@ typedef struct swh_tuning {
   int32_t cell_factor;  /* neighbour-grid cells per H_max (1..4) */
   int32_t loop_variant; /* 0 or 7: pair lists -- the density loop builds the step's lists
                            (r < max(R_i, R_j), R = gamma h (1 + list_skin)), the density /
-                           gradient / force loops walk them (one wave per i-group builds its
-                           lists); 8: the same lists, on a uniform grid built by one workgroup
-                           per 2x2x2 block of cells from one shared staging (measured slower) */
+                           gradient / force loops walk them */
   int32_t group_size;   /* list-build i-group size: 0 (default) or 16 */
   float cell_scale;     /* if > 0: cells per H_max as a real number (overrides cell_factor) */
   int32_t diag_mode;    /* 0; profiling only (results invalid): 1 = list build stages

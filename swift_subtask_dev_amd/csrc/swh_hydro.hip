@@ -165,20 +165,6 @@ void list_build_kernel(GridDev g, SoA a, ListDev ld,
                                   hmax_bits, counter, diag, lds, tab);
 }
 
-// The block list build (uniform grids, swh_list.h block_build): one
-// 256-thread workgroup per aligned 2x2x2 block of cells.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void list_build_block_kernel(
-    GridDev g, SoA a, ListDev ld, const int2* __restrict__ groups,
-    const int2* __restrict__ blk, int ngroups, int max_active_bin,
-    const unsigned int* __restrict__ hmax_bits, unsigned long long* counter, int diag,
-    const unsigned int* run_if) {
-  __shared__ BlockLds lds;
-  if (skip_build(run_if)) return;
-  const int2 r = blk[xcd_block_id()];
-  block_build<kListLpiBuild>(g, a, ld, groups, r.x, r.x + r.y, ngroups, max_active_bin,
-                             hmax_bits, counter, diag, lds);
-}
-
 #ifndef SWH_WALK_WPE
 #define SWH_WALK_WPE 0
 #endif
@@ -819,7 +805,6 @@ static ListDev list_dev(swh_space* s) {
   d.posf = s->posf.as<const float4>();
   d.diag = s->tuning.diag_mode;
   d.gbox = s->gbox.as<const GroupBox>();
-  d.hbox = s->hbox.as<const GroupBox>();
   d.ovf_n = ovf_slot(s);
   // per-cell reach pruning only pays on an adaptive (clustered) grid
   d.cell_R = s->grid.adaptive ? s->cell_hreach.as<const float>() : nullptr;
@@ -867,23 +852,14 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
                      kGamma * ld.skin1, (float)s->grid.dx, rwrap_slot(s), rwrap_base_slot(s),
                      ovf_slot(s), run_if, nbuild_slot(s));
   SWH_TRY(s->gbox.reserve((size_t)std::max(1, s->ngroups) * sizeof(GroupBox)));
-  const bool block = s->nblk > 0 && !s->grid.adaptive && s->tuning.loop_variant == 8;
-  if (block) SWH_TRY(s->hbox.reserve((size_t)std::max(1, s->ngroups) * 2 * sizeof(GroupBox)));
   ListDev ldb = list_dev(s);
   hipLaunchKernelGGL(group_box_kernel, dim3((s->ngroups + 255) / 256), dim3(256), 0, s->stream,
                      soa_of(s), s->groups.as<const int2>(), s->ngroups, P->max_active_bin,
-                     (double)ld.skin1, s->gbox.as<GroupBox>(),
-                     block ? s->hbox.as<GroupBox>() : nullptr, run_if);
-  if (block)
-    hipLaunchKernelGGL(list_build_block_kernel, dim3(s->nblk), dim3(256), 0, s->stream,
-                       grid_dev(s), soa_of(s), ldb, s->groups.as<const int2>(),
-                       s->blk_groups.as<const int2>(), s->ngroups, P->max_active_bin,
-                       hmax_slot(s), count ? stripes : nullptr, s->tuning.diag_mode, run_if);
-  else
-    hipLaunchKernelGGL(list_build_kernel, dim3(s->ngroups), dim3(64), 0, s->stream,
-                       grid_dev(s), soa_of(s), ldb, s->groups.as<const int2>(), 0, s->ngroups,
-                       P->max_active_bin, hmax_slot(s), count ? stripes : nullptr,
-                       s->tuning.diag_mode, run_if);
+                     (double)ld.skin1, s->gbox.as<GroupBox>(), run_if);
+  hipLaunchKernelGGL(list_build_kernel, dim3(s->ngroups), dim3(64), 0, s->stream, grid_dev(s),
+                     soa_of(s), ldb, s->groups.as<const int2>(), 0, s->ngroups,
+                     P->max_active_bin, hmax_slot(s), count ? stripes : nullptr,
+                     s->tuning.diag_mode, run_if);
   SWH_HIP(hipGetLastError());
   s->list_valid = true;
   s->list_check = false;

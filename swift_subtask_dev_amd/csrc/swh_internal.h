@@ -198,17 +198,12 @@ struct swh_space {
   swh::DevBuf groups;      // int2[ngroups]: i-groups (start, count) of the tile loops
   swh::DevBuf seg_groups, seg_off;
   int32_t ngroups = 0;
-  // the block list build's workgroups (uniform grid): int2 (first i-group,
-  // count) per aligned 2x2x2 block of cells (Morton code >> 3)
-  swh::DevBuf blk_groups, blk_flag;
-  int32_t nblk = 0;
   int64_t loop_stats[4] = {0, 0, 0, 0};  // work counters of the last counted tile loop
   // the step's pair lists (swh_list.h): valid from a density loop until the
   // next upload / rebuild / tuning change, or a ghost that grows an H past its R
   swh::DevBuf nbr, nbr_cnt, nbr_base, nbr_reach, nbr_ovf;
   swh::DevBuf posf;  // float4: position relative to its grid cell's corner, h
   swh::DevBuf gbox;  // GroupBox per i-group: the list build's group boxes
-  swh::DevBuf hbox;  // block build: GroupBox of each group's slots 0-7 and 8-15
   swh::DevBuf list_xd0;  // float4: the displacement record (xdiff) at the list build
   bool list_valid = false;
   bool list_check = false;  // kept lists after a drift: the device checks them first

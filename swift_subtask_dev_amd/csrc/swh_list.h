@@ -90,7 +90,6 @@ struct ListDev {
   int diag;      // profiling only: 2 = the build writes no entries
   const unsigned int* mark;  // nullable: particles the walks leave to a search (ghost-grown H)
   const GroupBox* gbox;  // per group (group_box_kernel), read by the build
-  const GroupBox* hbox;  // block build: per group, the boxes of slots 0-7 and 8-15
 };
 
 __device__ __forceinline__ void box_init(GroupBox& b) {
@@ -109,30 +108,21 @@ __device__ __forceinline__ void box_add(GroupBox& b, const double4& p, double R)
   b.Rg = R > b.Rg ? R : b.Rg;
 }
 
-// halves (nullable, the block build): the boxes of the group's slots 0-7
-// and 8-15 as well.
 __global__ void group_box_kernel(SoA a, const int2* __restrict__ groups, int ngroups,
                                  int max_active_bin, double gs1, GroupBox* __restrict__ out,
-                                 GroupBox* __restrict__ halves, const unsigned int* run_if) {
+                                 const unsigned int* run_if) {
   const int gidx = blockIdx.x * blockDim.x + threadIdx.x;
   if (gidx >= ngroups || (run_if && *run_if == 0u)) return;
   const int2 gr = groups[gidx];
-  GroupBox b, h[2];
+  GroupBox b;
   box_init(b);
-  box_init(h[0]);
-  box_init(h[1]);
   for (int i = gr.x; i < gr.x + gr.y; i++) {
     if (!active_part(a, i, max_active_bin)) continue;
     const double4 p = a.pos[i];
     const double R = p.w * (double)kGamma * gs1;
     box_add(b, p, R);
-    if (halves) box_add(h[i - gr.x >= 8 ? 1 : 0], p, R);
   }
   out[gidx] = b;
-  if (halves) {
-    halves[2 * gidx] = h[0];
-    halves[2 * gidx + 1] = h[1];
-  }
 }
 
 // Per-cell maximum R = gamma h (1 + skin): the list build skips a cell whose
@@ -635,403 +625,6 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
   b.lb = gbase + il;
   b.pi = pi;
   return b;
-}
-
-// ---------------------------------------------------------------------------
-// Block build (uniform grids, loop_variant 8): one 256-thread workgroup per
-// aligned 2x2x2 block of grid cells (Morton code >> 3) builds the lists of
-// the block's i-groups. The workgroup stages ONCE, into LDS, the candidates
-// around the union of its groups' boxes -- the cells the union's reach
-// touches, pruned by list_build's box test against the union box -- so a
-// particle's candidates are loaded ~8 times per build instead of ~32. Each
-// group is then built as two half-groups (its slots 0-7 and 8-15: the first
-// and second eight particles of a cell sorted by sub-cell Morton key, so
-// compact boxes), one wave each with eight lanes per i: the wave copies from
-// the stage the candidates of the cells around its half-box that the box test
-// keeps (rows of cells along x are contiguous in the stage), then tests and
-// flushes them as list_build does. A half-box is ~half a cell, so its pruned
-// region holds ~40% fewer candidates than the whole group's: each i tests
-// fewer. The lists are the same pair sets as list_build's (a superset of
-// every pair the loops accept; the walks' exact fp64 criteria decide), in
-// candidate order.
-//
-// A block whose union spans more than kBlkCells cells, holds more than
-// kBlkCap staged candidates or wraps a whole periodic dimension runs
-// list_build per group instead.
-// ---------------------------------------------------------------------------
-constexpr int kBlkCells = 128;  // cells of a block's union (5 x 5 x 5 fits)
-#ifndef SWH_BLK_CAP
-#define SWH_BLK_CAP 1072
-#endif
-constexpr int kBlkCap = SWH_BLK_CAP;   // staged candidates of a block
-constexpr int kBlkLpi = 8;             // lanes per i of a half-group
-using BlockWaveLds = ListLdsT<kBlkLpi, 128, 128, unsigned char>;
-using FallbackLds = ListLdsT<4, 128, 64, unsigned char>;
-
-struct BlockLds {
-  int pre[kBlkCells + 1];  // the union's cells (x-fastest): prefix of their counts
-                           // (after the staging: of their kept candidates)
-  int kpre[kBlkCells];     // staging: the kept candidates before each cell
-  int j0[kBlkCells];       // first sorted index of each cell minus its prefix
-  float4 off[kBlkCells];   // cell corners relative to the union centre (fp32)
-  double ubox[8];          // union box lo[3], hi[3], largest R of its groups
-  int info[4];             // 0: fallback, 1: candidates of the union's cells
-  int wcnt[4][4];          // staging compaction: kept per (pass slot, wave)
-  int rpre[4][32];         // per wave: prefix of its half-group's row runs
-  int rstart[4][32];       // per wave: first stage slot of each row run minus its prefix
-  union {
-    struct {
-      float4 q[kBlkCap];  // x, y, z relative to the union centre; w = inflated R_j^2
-      int j[kBlkCap];     // sorted index
-    } st;
-    CellTab fb[4];  // fallback: list_build's per-wave cell tables
-  } u;
-  union {
-    BlockWaveLds w[4];
-    FallbackLds fw[4];
-  } v;
-};
-
-// Half h (slots 8h .. 8h + 7) of group gid on one wave, eight lanes per i:
-// list_build's tests and flushes on the stage's candidates that the
-// half-box can reach. cu: the union's cell box, ctr: the union centre,
-// delta: the union's fp32 rounding bound.
-__device__ __forceinline__ void block_half(const SoA& a, const ListDev& ld,
-                                           const int2* __restrict__ groups, int gid, int h,
-                                           int max_active_bin, double Rmax, const GridDev& g,
-                                           const CellRange& cu, const double* ctr, double delta,
-                                           BlockLds& B, unsigned long long* counter, int diag) {
-  constexpr int LPI = kBlkLpi;
-  const int wv = threadIdx.x >> 6;
-  BlockWaveLds& L = B.v.w[wv];
-  int* rpre = B.rpre[wv];
-  int* rstart = B.rstart[wv];
-  const int lane = threadIdx.x & 63;
-  const int il = lane / LPI, s = lane % LPI;
-  const int2 gr = groups[gid];
-  const int slot = 8 * h + il;
-  const int i = slot < gr.y ? gr.x + slot : -1;
-  const bool act = i >= 0 && active_part(a, i, max_active_bin);
-  double4 pi = make_double4(0., 0., 0., 0.);
-  if (act) pi = a.pos[i];
-  const double Ri = act ? pi.w * (double)kGamma * (double)ld.skin1 : 0.;
-  const GroupBox gb = ld.hbox[2 * gid + h];
-  const double Rg = gb.Rg;
-  TileStats ts;
-  const int gbase = gid * kListSlots + 8 * h;  // the half's first list slot
-  int nq = 0, wr = 0;
-  if (Rg > 0.) {
-    const double reach = fmax(Rg, Rmax) + g.dx;
-    const int nx = cu.hi[0] - cu.lo[0] + 1, ny = cu.hi[1] - cu.lo[1] + 1;
-    int lo[3], hi[3];
-    float gc[3], hf[3];
-    for (int k = 0; k < 3; k++) {
-      lo[k] = (int)floor((gb.lo[k] - g.origin[k] - reach) * g.inv_w[k]);
-      hi[k] = (int)floor((gb.hi[k] - g.origin[k] + reach) * g.inv_w[k]);
-      // (non-periodic: the union box is clamped to the grid, so is this)
-      lo[k] = uni_i(max(lo[k], cu.lo[k]) - cu.lo[k]);
-      hi[k] = uni_i(min(hi[k], cu.hi[k]) - cu.lo[k]);
-      gc[k] = uni_f((float)(0.5 * (gb.lo[k] + gb.hi[k]) - ctr[k]));
-      hf[k] = uni_f((float)(0.5 * (gb.hi[k] - gb.lo[k]) + 2. * delta));
-    }
-    // the half's cells: rows along x, each a contiguous run of the stage
-    const int nyr = hi[1] - lo[1] + 1, nrows = nyr * (hi[2] - lo[2] + 1);  // <= 25
-    int rc = 0, rs = 0;
-    if (lane < nrows) {
-      const int iy = lo[1] + lane % nyr, iz = lo[2] + lane / nyr;
-      const int c0 = (iz * ny + iy) * nx;
-      rs = B.pre[c0 + lo[0]];
-      rc = B.pre[c0 + hi[0] + 1] - rs;
-    }
-    const int inc = wave_incl_scan(rc);
-    const int total = __builtin_amdgcn_readlane(inc, 63);
-    wave_sync();
-    if (lane < 32) {
-      rpre[lane] = inc - rc;  // rows past nrows: pre = total (never found)
-      rstart[lane] = rs - (inc - rc);
-    }
-    wave_sync();
-    const float Rg2 = uni_f((float)(Rg + delta) * (float)(Rg + delta) * kThrSlack);
-    const float xi = (float)(pi.x - ctr[0]);
-    const float yi = (float)(pi.y - ctr[1]);
-    const float zi = (float)(pi.z - ctr[2]);
-    const float thr_i = act ? (float)((Ri + delta) * (Ri + delta)) * kThrSlack : -1.f;
-    CellRange cnone = cu;
-    cnone.full[0] = cnone.full[1] = cnone.full[2] = false;
-    int nst = 0;
-    for (int base = 0; base < total; base += 64) {
-      if (nst > BlockWaveLds::kRegion - 64) {  // no room for this pass: consume the region
-        list_pad<LPI>(L, nst);
-        wave_sync();
-        if (diag != 1)
-          list_consume<LPI, false>(g, ld, cnone, xi, yi, zi, thr_i, act, nst, L, nq, wr, il, s,
-                                   gbase, ts);
-        nst = 0;
-        wave_sync();
-      }
-      const int qq = base + lane;
-      int kr = 0;  // its row: the last run starting at or before qq (<= 25 rows)
-#pragma unroll
-      for (int st = 16; st > 0; st >>= 1)
-        if (rpre[kr + st] <= qq) kr += st;
-      const bool val = qq < total;
-      const int k = val ? rstart[kr] + qq : 0;
-      const float4 q = B.u.st.q[k];
-      bool keep = false;
-      if (val) {
-        const float ex = fmaxf(fabsf(q.x - gc[0]) - hf[0], 0.f);
-        const float ey = fmaxf(fabsf(q.y - gc[1]) - hf[1], 0.f);
-        const float ez = fmaxf(fabsf(q.z - gc[2]) - hf[2], 0.f);
-        keep = ex * ex + ey * ey + ez * ez <= fmaxf(Rg2, q.w);
-      }
-      const unsigned long long m = __ballot(keep);
-      if (keep) {
-        const int d = nst + __popcll(m & ((1ull << lane) - 1ull));
-        L.cx[d] = q.x;
-        L.cy[d] = q.y;
-        L.cz[d] = q.z;
-        L.cw[d] = q.w;
-        L.candj[d] = B.u.st.j[k];
-      }
-      nst += __popcll(m);
-      ts.loaded += val ? 1u : 0u;
-      ts.staged += keep ? 1u : 0u;
-    }
-    list_pad<LPI>(L, nst);
-    wave_sync();
-    if (diag != 1 && nst > 0)
-      list_consume<LPI, false>(g, ld, cnone, xi, yi, zi, thr_i, act, nst, L, nq, wr, il, s,
-                               gbase, ts);
-  }
-  list_finish(ld, i, act, Ri, wr, gbase + il, s, counter, ts);
-}
-
-// The lists of the i-groups [gs, ge) of one block (a 256-thread workgroup).
-template <int LPI>
-__device__ __forceinline__ void block_build(const GridDev& g, const SoA& a, const ListDev& ld,
-                                            const int2* __restrict__ groups, int gs, int ge,
-                                            int ngroups, int max_active_bin,
-                                            const unsigned int* __restrict__ hmax_bits,
-                                            unsigned long long* counter, int diag, BlockLds& B) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const double skin1 = (double)ld.skin1;
-  const double Rmax = (double)__uint_as_float(*hmax_bits) * (double)kGamma * skin1;
-  // 1. the union box of the block's groups (those with an active particle)
-  if (wv == 0) {
-    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300}, Rg = 0.;
-    for (int k = gs + lane; k < ge; k += 64) {
-      const GroupBox b = ld.gbox[k];
-      if (b.Rg > 0.) {
-        for (int d = 0; d < 3; d++) {
-          lo[d] = fmin(lo[d], b.lo[d]);
-          hi[d] = fmax(hi[d], b.hi[d]);
-        }
-        Rg = fmax(Rg, b.Rg);
-      }
-    }
-    for (int d = 0; d < 3; d++) {
-      lo[d] = wave_min_d(lo[d]);
-      hi[d] = wave_max_d(hi[d]);
-    }
-    Rg = wave_max_d(Rg);
-    if (lane == 0) {
-      for (int d = 0; d < 3; d++) {
-        B.ubox[d] = lo[d];
-        B.ubox[3 + d] = hi[d];
-      }
-      B.ubox[6] = Rg;
-    }
-  }
-  __syncthreads();
-  const double Rgu = B.ubox[6];
-  CellRange cu;
-  double ctr[3] = {0., 0., 0.}, half[3] = {0., 0., 0.}, D2 = 0.;
-  bool fallback = false;
-  int ncells = 0;
-  double delta = 0.;
-  if (Rgu > 0.) {
-    const double reach = fmax(Rgu, Rmax) + g.dx;
-    for (int k = 0; k < 3; k++) {
-      const double lo = B.ubox[k], hi = B.ubox[3 + k];
-      cu.lo[k] = (int)floor((lo - g.origin[k] - reach) * g.inv_w[k]);
-      cu.hi[k] = (int)floor((hi - g.origin[k] + reach) * g.inv_w[k]);
-      cu.full[k] = false;
-      if (g.periodic) {
-        if (cu.hi[k] - cu.lo[k] + 1 >= g.cdim[k]) fallback = true;  // wraps a whole dimension
-      } else {
-        cu.lo[k] = max(cu.lo[k], 0);
-        cu.hi[k] = min(cu.hi[k], g.cdim[k] - 1);
-      }
-      if (cu.hi[k] - cu.lo[k] + 1 > 5) fallback = true;  // (a half-group's rows: <= 25)
-      ctr[k] = 0.5 * (lo + hi);
-      half[k] = 0.5 * (hi - lo);
-      const double ext = half[k] + reach;
-      D2 += ext * ext;
-    }
-    ncells = (cu.hi[0] - cu.lo[0] + 1) * (cu.hi[1] - cu.lo[1] + 1) * (cu.hi[2] - cu.lo[2] + 1);
-    if (ncells > kBlkCells) fallback = true;
-    // list_build's rounding bound with the union's extent
-    const double wmax = fmax(g.w[0], fmax(g.w[1], g.w[2]));
-    delta = 16. * kUnitRound * (sqrt(D2) + wmax);
-  }
-  // 2. the union's cell table (wave 0; cells x-fastest from cu.lo)
-  if (Rgu > 0. && !fallback && wv == 0) {
-    const int nx = cu.hi[0] - cu.lo[0] + 1, nxy = nx * (cu.hi[1] - cu.lo[1] + 1);
-    int run = 0;
-    for (int cb = 0; cb < kBlkCells; cb += 64) {
-      const int cl = cb + lane;
-      int cnt = 0, j0 = 0;
-      float4 off = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (cl < ncells) {
-        const int iz = cl / nxy, rxy = cl - iz * nxy, iy = rxy / nx, ix = rxy - iy * nx;
-        double sx, sy, sz;
-        const int wx = wrap_cell(g, cu, 0, cu.lo[0] + ix, sx);
-        const int wy = wrap_cell(g, cu, 1, cu.lo[1] + iy, sy);
-        const int wz = wrap_cell(g, cu, 2, cu.lo[2] + iz, sz);
-        const int2 sp = cell_range_of(g, wx, wy, wz);
-        j0 = sp.x;
-        cnt = sp.y - sp.x;
-        off = make_float4((float)(g.origin[0] + wx * g.w[0] + sx - ctr[0]),
-                          (float)(g.origin[1] + wy * g.w[1] + sy - ctr[1]),
-                          (float)(g.origin[2] + wz * g.w[2] + sz - ctr[2]), 0.f);
-      }
-      const int inc = wave_incl_scan(cnt);
-      B.pre[cl] = run + inc - cnt;  // cells past ncells: pre = total (never found)
-      B.j0[cl] = j0 - (run + inc - cnt);
-      B.off[cl] = off;
-      run += __builtin_amdgcn_readlane(inc, 63);
-    }
-    if (lane == 0) {
-      B.pre[kBlkCells] = run;
-      B.info[1] = run;
-    }
-  }
-  if (tid == 0) {
-    B.info[0] = (Rgu > 0. && fallback) ? 1 : 0;
-    if (Rgu <= 0. || fallback) B.info[1] = 0;
-  }
-  __syncthreads();
-  fallback = B.info[0] != 0;
-  const int total = B.info[1];
-  // 3. stage the union's candidates the union box can reach (list_build's box
-  // test against the union box), in candidate order (cells x-fastest): four
-  // per thread in flight, compacted across the workgroup, the stage's cell
-  // prefix rewritten to the kept candidates
-  if (!fallback && total > 0) {
-    const float gs1 = (float)((double)kGamma * skin1);
-    const float deltaf = (float)delta;
-    const float hx = (float)(half[0] + delta), hy = (float)(half[1] + delta),
-                hz = (float)(half[2] + delta);
-    const float Rgu2 = (float)(Rgu + delta) * (float)(Rgu + delta) * kThrSlack;
-    int nst = 0;  // staged so far (block-uniform)
-    for (int base = 0; base < total; base += 256 * 4) {
-      int kc[4], jj[4];
-      float4 q[4], off[4];
-      bool val[4], keep[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++) kc[u] = 0;
-#pragma unroll
-      for (int st = 64; st > 0; st >>= 1) {
-        int pv[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) pv[u] = B.pre[kc[u] + st];
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-          if (pv[u] <= base + 256 * u + tid) kc[u] += st;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const int k = base + 256 * u + tid;
-        val[u] = k < total;
-        jj[u] = val[u] ? B.j0[kc[u]] + k : 0;
-        off[u] = B.off[kc[u]];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; u++) q[u] = val[u] ? ld.posf[jj[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
-      unsigned long long m[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        q[u].x += off[u].x;  // relative to the union centre
-        q[u].y += off[u].y;
-        q[u].z += off[u].z;
-        const float Rj = q[u].w * gs1 + deltaf;
-        q[u].w = Rj * Rj * kThrSlack;
-        const float ex = fmaxf(fabsf(q[u].x) - hx, 0.f);
-        const float ey = fmaxf(fabsf(q[u].y) - hy, 0.f);
-        const float ez = fmaxf(fabsf(q[u].z) - hz, 0.f);
-        keep[u] = val[u] && ex * ex + ey * ey + ez * ez <= fmaxf(Rgu2, q[u].w);
-        m[u] = __ballot(keep[u]);
-      }
-      if (lane == 0) {
-#pragma unroll
-        for (int u = 0; u < 4; u++) B.wcnt[u][wv] = (int)__popcll(m[u]);
-      }
-      __syncthreads();
-      int o = nst;
-      int kept_before[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        int before = 0, all = 0;
-        for (int w = 0; w < 4; w++) {
-          const int c = B.wcnt[u][w];
-          before += w < wv ? c : 0;
-          all += c;
-        }
-        // kept candidates before this one (in candidate order)
-        kept_before[u] = o + before + __popcll(m[u] & ((1ull << lane) - 1ull));
-        if (keep[u] && kept_before[u] < kBlkCap) {
-          B.u.st.q[kept_before[u]] = q[u];
-          B.u.st.j[kept_before[u]] = jj[u];
-        }
-        o += all;
-      }
-      __syncthreads();  // (wcnt is rewritten by the next pass)
-      // the cell prefix over the kept candidates: a cell's first candidate
-      // position k = pre[c] maps to the kept count before it
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const int k = base + 256 * u + tid;
-        // (empty cells share their successor's prefix: every cell whose pre
-        // equals k takes the same kept count)
-        if (val[u] && B.pre[kc[u]] == k) {
-          for (int c = kc[u]; c >= 0 && B.pre[c] == k; c--) B.kpre[c] = kept_before[u];
-        }
-      }
-      nst = o;
-    }
-    // cells whose first position is past every candidate: the total kept
-    for (int c = tid; c < kBlkCells; c += 256)
-      if (B.pre[c] >= total) B.kpre[c] = nst;
-    __syncthreads();
-    for (int c = tid; c < kBlkCells; c += 256) B.pre[c] = B.kpre[c];
-    if (tid == 0) B.pre[kBlkCells] = nst;
-    __syncthreads();
-    if (nst > kBlkCap) fallback = true;  // (block-uniform)
-    if (!fallback) {
-      // 4. the half-groups, one wave each: (group, half) items wv, wv + 4, ...
-      const int nitems = 2 * (ge - gs);
-      for (int t = wv; t < nitems; t += 4) {
-        const int gid = gs + (t >> 1), h = t & 1;
-        block_half(a, ld, groups, gid, h, max_active_bin, Rmax, g, cu, ctr, delta, B, counter,
-                   diag);
-      }
-      return;
-    }
-    __syncthreads();  // the stage is about to become the fallback's cell tables
-  }
-  if (fallback) {
-    for (int gid = gs + wv; gid < ge; gid += 4)
-      (void)list_build<4>(g, a, ld, groups, gid, ngroups, max_active_bin, hmax_bits, counter,
-                          diag, B.v.fw[wv], B.u.fb[wv]);
-  } else {  // no active particle in the block: the groups' i-slots are unlisted
-    for (int gid = gs + wv; gid < ge; gid += 4) {
-      const int2 gr = groups[gid];
-      const int il = lane / 4, s = lane % 4;
-      TileStats ts;
-      list_finish(ld, il < gr.y ? gr.x + il : -1, false, 0., 0, gid * kListSlots + il, s, counter,
-                  ts);
-    }
-  }
 }
 
 // Does particle x need the nearest-image wrap (within R of a periodic face)?

@@ -273,27 +273,6 @@ __device__ __forceinline__ BlockSpan block_span(const uint32_t* __restrict__ cod
   return b;
 }
 
-// Block heads of the Morton-ranked cells: rank r starts a new aligned 2x2x2
-// block (code >> 3) of the block list build (swh_list.h block_build).
-__global__ void blk_head_kernel(const uint32_t* __restrict__ code, int ncell,
-                                int* __restrict__ flag) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < ncell) flag[r] = (r == 0 || (code[r] >> 3) != (code[r - 1] >> 3)) ? 1 : 0;
-}
-// idx = inclusive scan of the heads: block b = idx[r] - 1 starts at group
-// seg_off[r]; then the counts from the next block's first group.
-__global__ void blk_first_kernel(const uint32_t* __restrict__ code, const int* __restrict__ idx,
-                                 const int* __restrict__ seg_off, int ncell,
-                                 int2* __restrict__ blk) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < ncell && (r == 0 || (code[r] >> 3) != (code[r - 1] >> 3)))
-    blk[idx[r] - 1] = make_int2(seg_off[r], 0);
-}
-__global__ void blk_count_kernel(int2* __restrict__ blk, int nblk, int ngroups) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < nblk) blk[b].y = (b + 1 < nblk ? blk[b + 1].x : ngroups) - blk[b].x;
-}
-
 template <bool WRITE>
 __global__ void group_kernel(const uint32_t* __restrict__ code, const int* __restrict__ cs,
                              int ncell, int kGroupMax, int* __restrict__ ngroup,
@@ -703,13 +682,12 @@ swh_status swh_space_destroy(swh_space* s) {
   DevBuf* bufs[] = {&s->aos, &s->pos, &s->vm, &s->th, &s->fc, &s->tb, &s->dens, &s->rot,
                     &s->grad, &s->acc, &s->hdt, &s->mintb, &s->perm, &s->ncount,
                     &s->cell_start, &s->cell_rank, &s->cell_code, &s->cell_span, &s->cell_hreach,
-                    &s->blk_groups, &s->blk_flag,
                     &s->vfull_c, &s->agrav_c, &s->hasg_c, &s->xdiff, &s->pcell, &s->cell_lin, &s->groups, &s->seg_groups,
                     &s->seg_off, &s->keys, &s->keys2, &s->idx, &s->idx2, &s->sort_tmp,
                     &s->scan_tmp, &s->counters, &s->tmp_soa, &s->ghost_left,
                     &s->ghost_right, &s->ghost_list, &s->ghost_list2, &s->ghost_search, &s->ghost_seg, &s->grown_q,
                     &s->grown_mark, &s->grown_search,
-                    &s->nbr, &s->nbr_cnt, &s->nbr_base, &s->nbr_reach, &s->nbr_ovf, &s->posf, &s->gbox, &s->hbox, &s->ctr_stripes,
+                    &s->nbr, &s->nbr_cnt, &s->nbr_base, &s->nbr_reach, &s->nbr_ovf, &s->posf, &s->gbox, &s->ctr_stripes,
                     &s->iperm, &s->vfull_s, &s->agrav_s, &s->hasg_s, &s->list_xd0};
   for (DevBuf* b : bufs) b->release();
   s->hstage.release();
@@ -734,7 +712,7 @@ swh_status swh_space_set_stream(swh_space* s, void* stream) {
 
 swh_status swh_space_set_tuning(swh_space* s, const swh_tuning* t) {
   if (!s || !t || t->cell_factor < 1 || t->cell_factor > 4 ||
-      (t->loop_variant != 0 && t->loop_variant != 7 && t->loop_variant != 8) ||
+      (t->loop_variant != 0 && t->loop_variant != 7) ||
       (t->group_size != 0 && t->group_size != 16) || t->cell_scale < 0.f || t->cell_scale > 4.f ||
       t->diag_mode < 0 || t->diag_mode > 7 || t->diag_mode == 5 ||
       t->diag_mode == 6 || t->list_capacity < 0 || t->list_capacity > 4096 ||
@@ -1174,32 +1152,6 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
                      s->cell_code.as<const uint32_t>(), s->cell_start.as<const int>(), nc,
                      gmax, nullptr, s->seg_off.as<const int>(), s->groups.as<int2>());
   SWH_HIP(hipGetLastError());
-  // 6. the block list build's workgroups: the i-groups of each aligned
-  // 2x2x2 block of cells (groups are emitted in Morton rank order)
-  s->nblk = 0;
-  if (!g.adaptive) {
-    SWH_TRY(s->blk_flag.reserve(((size_t)nc + 1) * 2 * sizeof(int)));
-    int* flag = s->blk_flag.as<int>();
-    int* idx = flag + nc + 1;
-    hipLaunchKernelGGL(blk_head_kernel, dim3(cgrid), dim3(block), 0, st,
-                       s->cell_code.as<const uint32_t>(), nc, flag);
-    size_t bb = 0;
-    SWH_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, bb, flag, idx, nc, st));
-    SWH_TRY(s->scan_tmp.reserve(bb));
-    bb = s->scan_tmp.bytes;
-    SWH_HIP(hipcub::DeviceScan::InclusiveSum(s->scan_tmp.ptr, bb, flag, idx, nc, st));
-    int nblk = 0;
-    SWH_HIP(hipMemcpyAsync(&nblk, idx + nc - 1, sizeof(int), hipMemcpyDeviceToHost, st));
-    SWH_HIP(hipStreamSynchronize(st));
-    SWH_TRY(s->blk_groups.reserve((size_t)std::max(1, nblk) * sizeof(int2)));
-    hipLaunchKernelGGL(blk_first_kernel, dim3(cgrid), dim3(block), 0, st,
-                       s->cell_code.as<const uint32_t>(), idx, s->seg_off.as<const int>(), nc,
-                       s->blk_groups.as<int2>());
-    hipLaunchKernelGGL(blk_count_kernel, dim3((nblk + block - 1) / block), dim3(block), 0, st,
-                       s->blk_groups.as<int2>(), nblk, ng);
-    SWH_HIP(hipGetLastError());
-    s->nblk = nblk;
-  }
   SWH_TRY(space_hmax_to_device(s));
   s->built = true;
   return SWH_OK;

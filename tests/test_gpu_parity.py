@@ -862,51 +862,3 @@ def test_grown_after_larger_upload(gpu_ctx):
         assert_close(g["a_hydro"], o["a_hydro"], 5e-5, 1e-4, "a_hydro")
         assert np.array_equal(g["min_ngb_time_bin"], o["min_ngb_time_bin"])
     sp.close()
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("case", ["sedov24", "periodic_small", "open_box", "headline128"])
-def test_block_build_equals_group_build(gpu_ctx, case):
-    """The block list build (loop_variant 8: one workgroup per 2x2x2 block of
-    cells staging its union once) and the per-group build (the default) give
-    the same step: identical density / gradient / force
-    interaction counts and ghost passes, and the same chain outputs up to the
-    fp64 summation order of marginal list entries (1e-12 relative; h, whose
-    ghost decisions could in principle flip on such a difference, equal)."""
-    from swift_subtask_dev_amd import lib
-    if case == "headline128":
-        parts = ics.sedov_slabs(128, 1)
-        P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
-        P.max_active_bin = 1
-    elif case == "periodic_small":  # 4^3 cells: unions wrap whole dimensions (per-group fallback)
-        parts = ics.sedov_box(8, velocity="divergent", pert=0.2, seed=3)
-        P = abi.default_hydro_params()
-    elif case == "open_box":
-        parts = ics.sedov_box(20, velocity="divergent", pert=0.2, seed=4)
-        P = abi.default_hydro_params(periodic=False)
-    else:
-        parts = ics.sedov_box(24, velocity="divergent", pert=0.3, seed=2)
-        P = abi.default_hydro_params()
-    out = {}
-    for name, variant in (("block", 8), ("group", 0)):
-        g = abi.copy_parts(parts)
-        sp = lib.HydroSpace(gpu_ctx)
-        sp.set_tuning(1, variant)
-        sp.upload(g)
-        sp.rebuild(P)
-        sp.init_parts(P)
-        nd = sp.density(P)
-        stats = sp.info()["loop_stats"]
-        sp.upload(g)
-        sp.rebuild(P)
-        res = sp.hydro_step(P)
-        sp.download(g, abi.FIELDS_ALL)
-        sp.close()
-        out[name] = (nd, res, g, stats)
-    (nd0, r0, g0, st0), (nd8, r8, g8, st8) = out["block"], out["group"]
-    print(f"\n{case}: block build stats {st0}, group build stats {st8}; {r0}")
-    assert nd0 == nd8 and r0 == r8, (nd0, nd8, r0, r8)
-    assert np.array_equal(g0["h"], g8["h"])
-    for f in ("rho", "pressure", "v_sig", "a_hydro", "u_dt", "h_dt", "div_v"):
-        assert_close(g0[f], g8[f], 1e-12, 1e-9, f)
-    assert np.array_equal(g0["min_ngb_time_bin"], g8["min_ngb_time_bin"])

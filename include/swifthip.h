@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SWH_ABI_VERSION 9
+#define SWH_ABI_VERSION 10
 
 #if defined(__GNUC__)
 #define SWH_API __attribute__((visibility("default")))
@@ -475,6 +475,8 @@ typedef struct swh_grav_tree_stats {
    * stream): multipoles (P2M + M2M), walk, P2P, M2P, M2L + L2L + L2P */
   float ms_multipoles, ms_walk, ms_p2p, ms_m2p, ms_down;
   int32_t reserved;
+  int64_t n_pp_truncated; /* of n_pp: pairs of truncated entries (periodic, beyond r_cut_min:
+                             runner_dopair/doself_grav_pp_truncated) -- ABI v10 */
 } swh_grav_tree_stats;
 SWH_API swh_status swh_gspace_set_tree(swh_gspace *g, const swh_gcell *cells, int32_t ncells);
 /* Ownership for a step sharded over ranks (i-cells owned per GPU,

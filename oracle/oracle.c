@@ -2982,6 +2982,10 @@ API long long PFX(grav_pp_leaves)(struct gpart *g, const int *leaves, int nleave
   const real dim[3] = {(real)G->dim[0], (real)G->dim[1], (real)G->dim[2]};
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : total, total_m2p)
   for (int l = 0; l < nleaves; l++) {
+    /* a "leaf" without entries is left alone: in a tree's cell list the
+     * split cells overlap their progeny's ranges, and another thread's
+     * update of those gparts must not be overwritten by a += 0 */
+    if (off[l] == off[l + 1]) continue;
     const int s = leaves[2 * l], c = leaves[2 * l + 1];
     for (int pid = s; pid < s + c; pid++) {
       struct gpart *gp = &g[pid];
@@ -3340,6 +3344,7 @@ API void PFX(grav_tree_owned)(struct gpart *g, int n, const struct oracle_gcell 
       if (d > maxdep) maxdep = d;
     }
     for (int d = maxdep; d >= 0; d--)
+#pragma omp parallel for schedule(dynamic, 64)
       for (int c = 0; c < ncells; c++) {
         if (dep[c] != d) continue;
         if (!cells[c].split) {
@@ -3361,8 +3366,50 @@ API void PFX(grav_tree_owned)(struct gpart *g, int n, const struct oracle_gcell 
   w.act = act;
   w.own = owned;
   w.G = G;
-  for (int k = 0; k < nself; k++) otw_self(&w, self_cells[k]);
-  for (int k = 0; k < npair; k++) otw_pair(&w, pair_cells[2 * k], pair_cells[2 * k + 1]);
+  /* the recursive tasks (independent, as SWIFT's runners execute them,
+   * runner_main.c:207-208, 257-258) over the threads in chunks of 64
+   * consecutive tasks; the chunks' entries are joined in task order, so the
+   * lists equal a serial walk's */
+  {
+    const long long ntask = (long long)nself + npair, kChunk = 64;
+    const long long nchunk = (ntask + kChunk - 1) / kChunk;
+    struct otree_walk *part =
+        (struct otree_walk *)calloc((size_t)(nchunk > 0 ? nchunk : 1), sizeof(struct otree_walk));
+#pragma omp parallel for schedule(dynamic, 1)
+    for (long long ch = 0; ch < nchunk; ch++) {
+      struct otree_walk *pw = &part[ch];
+      *pw = w;
+      pw->pp = NULL;
+      pw->mm = NULL;
+      pw->npp = pw->cap_pp = pw->nmm = pw->cap_mm = pw->skipped = 0;
+      const long long t1 = (ch + 1) * kChunk < ntask ? (ch + 1) * kChunk : ntask;
+      for (long long t = ch * kChunk; t < t1; t++) {
+        if (t < nself) otw_self(pw, self_cells[t]);
+        else otw_pair(pw, pair_cells[2 * (t - nself)], pair_cells[2 * (t - nself) + 1]);
+      }
+    }
+    long long npp = 0, nmm = 0;
+    for (long long ch = 0; ch < nchunk; ch++) {
+      npp += part[ch].npp;
+      nmm += part[ch].nmm;
+      w.skipped += part[ch].skipped;
+    }
+    w.pp = (int *)malloc(sizeof(int) * 4 * (size_t)(npp > 0 ? npp : 1));
+    w.mm = (int *)malloc(sizeof(int) * 3 * (size_t)(nmm > 0 ? nmm : 1));
+    for (long long ch = 0; ch < nchunk; ch++) {
+      if (part[ch].npp)
+        memcpy(w.pp + 4 * w.npp, part[ch].pp, sizeof(int) * 4 * (size_t)part[ch].npp);
+      if (part[ch].nmm)
+        memcpy(w.mm + 3 * w.nmm, part[ch].mm, sizeof(int) * 3 * (size_t)part[ch].nmm);
+      w.npp += part[ch].npp;
+      w.nmm += part[ch].nmm;
+      free(part[ch].pp);
+      free(part[ch].mm);
+    }
+    w.cap_pp = w.npp;
+    w.cap_mm = w.nmm;
+    free(part);
+  }
   /* P-P: CSR over i-cells in walk order per cell */
   int *leaves = (int *)malloc(sizeof(int) * 2 * (size_t)ncells);
   int *off = (int *)calloc((size_t)ncells + 1, sizeof(int));
@@ -3438,6 +3485,8 @@ API void PFX(grav_tree_owned)(struct gpart *g, int n, const struct oracle_gcell 
     if (dd > maxd) maxd = dd;
   }
   for (int dd = 1; dd <= maxd; dd++) {
+    /* the cells of one depth are independent (each reads only its parent) */
+#pragma omp parallel for schedule(dynamic, 64)
     for (int c = 0; c < ncells; c++) {
       if (depth[c] != dd) continue;
       const int p = parent[c];
@@ -3456,6 +3505,7 @@ API void PFX(grav_tree_owned)(struct gpart *g, int n, const struct oracle_gcell 
         }
     }
   }
+#pragma omp parallel for schedule(dynamic, 64)
   for (int c = 0; c < ncells; c++) {
     if (cells[c].split) continue;
     const real *Fc = F + 35 * (size_t)c;

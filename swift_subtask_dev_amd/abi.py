@@ -223,7 +223,8 @@ class GravTreeStats(C.Structure):
     _fields_ = [("n_pp", C.c_int64), ("n_m2p", C.c_int64), ("n_m2l", C.c_int64),
                 ("n_pp_tasks", C.c_int64), ("n_skipped", C.c_int64),
                 ("ms_multipoles", C.c_float), ("ms_walk", C.c_float), ("ms_p2p", C.c_float),
-                ("ms_m2p", C.c_float), ("ms_down", C.c_float), ("reserved", C.c_int32)]
+                ("ms_m2p", C.c_float), ("ms_down", C.c_float), ("reserved", C.c_int32),
+                ("n_pp_truncated", C.c_int64)]
 
 
 MPOLE_TERMS = 35

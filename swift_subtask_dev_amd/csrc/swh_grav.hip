@@ -869,6 +869,48 @@ __global__ __launch_bounds__(kGravBlock) void p2p_kernel_f32(
   }
 }
 
+// Stats only (swh_grav_tree with stats, after the step): the P2P pairs of
+// truncated entries, SURVEY 8d's 43-flop pairs. One wave per i-leaf, a lane
+// per active i (64 at a time); an i that took an allow_mpole entry through
+// its multipole (the batch kernel's MAC bits when it ran, m2p_accept as in
+// mpole_mask otherwise) has no pairs with it; the self pair is not one.
+__global__ __launch_bounds__(64) void pp_trunc_count_kernel(
+    GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
+    const swh_leaf_pair* __restrict__ pairs, MacParams mac, int any_mpole,
+    const unsigned long long* __restrict__ mbits, unsigned long long* counter) {
+  const int li = blockIdx.x;
+  const swh_leaf L = leaves[li];
+  const int p0 = pair_off[li], p1 = pair_off[li + 1];
+  if (p0 == p1) return;
+  const int lane = (int)threadIdx.x;
+  // the batch kernel's lanes per i (its MAC bits are per lane)
+  const int lpi = L.count >= 64 ? 1 : min(8, 64 / max(L.count, 1));
+  unsigned long long n = 0;
+  for (int ib = 0; ib < L.count; ib += 64) {
+    const int il = ib + lane;
+    const int gi = L.start + il;
+    const bool act = il < L.count && g.active[gi];
+    const double4 pi = act ? g.pos[gi] : make_double4(0., 0., 0., 1.);
+    for (int q = p0; q < p1; q++) {
+      const swh_leaf_pair pr = pairs[q];
+      if (!pr.truncated) continue;
+      const swh_leaf J = leaves[pr.j];
+      bool m2p = false;
+      if (any_mpole && pr.allow_mpole && J.count > 1 && act) {
+        if (mbits)
+          m2p = (mbits[q] >> (il * lpi)) & 1ull;
+        else
+          m2p = m2p_accept(mac, mac_source(g.mp[pr.j]), (float)pi.x, (float)pi.y, (float)pi.z,
+                           (float)pi.w, g.oagn[gi]);
+      }
+      if (act && !m2p)
+        n += (unsigned long long)(J.count - ((gi >= J.start && gi < J.start + J.count) ? 1 : 0));
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+  if (lane == 0 && n) atomicAdd(counter, n);
+}
+
 // M2P of the allow_mpole pairs (runner_dopair_grav_pm_full / _truncated,
 // runner_doiact_grav.c:911-1200): every active i of the i-leaf that passes
 // the MAC against source leaf j's multipole. Runs after p2p_kernel on the
@@ -2575,9 +2617,9 @@ swh_status swh_grav_tree_tasks(swh_gspace* g, const swh_grav_params* G,
   g->mpoles_valid = true;  // the same cell table: the multipoles stay
   if (stats) SWH_HIP(hipEventRecord(ev[2], g->stream));
   // P2P + M2P
-  SWH_TRY(g->counter.reserve(2 * sizeof(unsigned long long)));
+  SWH_TRY(g->counter.reserve(3 * sizeof(unsigned long long)));
   unsigned long long* ctr = g->counter.as<unsigned long long>();
-  SWH_HIP(hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned long long), g->stream));
+  SWH_HIP(hipMemsetAsync(ctr, 0, 3 * sizeof(unsigned long long), g->stream));
   if (npp > 0) SWH_TRY(launch_pp(g, G, mac_params(G), ctr, stats ? ev[3] : nullptr));
   if (stats) SWH_HIP(hipEventRecord(ev[4], g->stream));
   // M2L
@@ -2604,12 +2646,25 @@ swh_status swh_grav_tree_tasks(swh_gspace* g, const swh_grav_params* G,
     if (!(flags & SWH_TREE_NO_DOWN)) SWH_TRY(tree_down(g));
   }
   if (stats) SWH_HIP(hipEventRecord(ev[5], g->stream));
-  unsigned long long h[2] = {0, 0};
+  // stats: the P2P pairs of truncated entries (a counting pass after the
+  // step, outside its timed phases)
+  if (stats && npp > 0) {
+    SWH_HIP(hipMemsetAsync(ctr + 2, 0, sizeof(unsigned long long), g->stream));
+    const bool small = f64 && g->max_leaf <= 64;  // (the batch kernel's mbits are valid)
+    hipLaunchKernelGGL(pp_trunc_count_kernel, dim3(g->nleaves), dim3(64), 0, g->stream,
+                       gsoa_of(g), g->leaves.as<const swh_leaf>(), g->pair_off.as<const int>(),
+                       g->pairs.as<const swh_leaf_pair>(), mac_params(G), g->any_mpole ? 1 : 0,
+                       small && g->any_mpole ? g->m2p_bits.as<const unsigned long long>() : nullptr,
+                       ctr + 2);
+    SWH_HIP(hipGetLastError());
+  }
+  unsigned long long h[3] = {0, 0, 0};
   SWH_HIP(hipMemcpyAsync(h, ctr, sizeof(h), hipMemcpyDeviceToHost, g->stream));
   SWH_HIP(hipStreamSynchronize(g->stream));
   if (stats) {
     stats->n_pp = (int64_t)h[0];
     stats->n_m2p = (int64_t)h[1];
+    stats->n_pp_truncated = (int64_t)h[2];
     stats->n_m2l = nmm;
     stats->n_pp_tasks = npp;
     stats->n_skipped = skipped;

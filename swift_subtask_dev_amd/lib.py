@@ -503,16 +503,21 @@ class GravSpace:
             self.handle, owned.ctypes.data_as(C.POINTER(C.c_uint8)), len(owned)),
             "set_owned_cells", self._lib)
 
-    def tree(self, G: abi.GravParams, self_cells, pair_cells) -> dict:
+    def tree(self, G: abi.GravParams, self_cells, pair_cells, stats: bool = True) -> dict:
         """runner_doself_recursive_grav on self_cells, runner_dopair_recursive_grav
-        on pair_cells (n x 2), then the down pass."""
+        on pair_cells (n x 2), then the down pass. stats=False: no phase
+        events and no counting pass (returns None)."""
         sc = np.ascontiguousarray(self_cells, dtype=np.int32)
         pc = np.ascontiguousarray(pair_cells, dtype=np.int32).reshape(-1)
         st = abi.GravTreeStats()
         _check(self._lib.swh_grav_tree(self.handle, C.byref(G), _ptr(sc), len(sc), _ptr(pc),
-                                       len(pc) // 2, C.byref(st)), "grav_tree", self._lib)
+                                       len(pc) // 2, C.byref(st) if stats else None),
+               "grav_tree", self._lib)
+        if not stats:
+            return None
         return {"n_pp": st.n_pp, "n_m2p": st.n_m2p, "n_m2l": st.n_m2l,
                 "n_pp_tasks": st.n_pp_tasks, "n_skipped": st.n_skipped,
+                "n_pp_truncated": st.n_pp_truncated,
                 "ms": {"multipoles": st.ms_multipoles, "walk": st.ms_walk, "p2p": st.ms_p2p,
                        "m2p": st.ms_m2p, "down": st.ms_down}}
 

@@ -100,7 +100,8 @@ def test_params_struct_size():
     # swh_gcell: start, count, split, progeny[8]; swh_grav_tree_stats: 5 int64
     assert C.sizeof(abi.GCell) == 96 == abi.GCELL_DTYPE.itemsize
     assert abi.GCell.loc.offset == 48 and abi.GCell.width.offset == 72
-    assert C.sizeof(abi.GravTreeStats) == 64
+    assert C.sizeof(abi.GravTreeStats) == 72  # ABI v10: + int64 n_pp_truncated at 64
+    assert abi.GravTreeStats.n_pp_truncated.offset == 64
     # swh_multipole: CoM, r_max, 35 terms, 5 powers, 2 floats
     assert C.sizeof(abi.Multipole) == 4 * 8 + 35 * 4 + 5 * 4 + 2 * 4
 

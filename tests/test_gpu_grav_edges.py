@@ -43,7 +43,11 @@ def _grav_params(periodic=False, theta=0.5, r_cut_max=0.0, r_s_inv=0.0, r_cut_mi
 
 def _close(g, o, rel=1e-6):
     a, b = g["a_grav"].astype(np.float64), o["a_grav"].astype(np.float64)
-    assert np.abs(a - b).max() <= rel * np.abs(b).max(), np.abs(a - b).max() / np.abs(b).max()
+    e = np.abs(a - b).max(axis=1)
+    if e.max() > rel * np.abs(b).max():
+        for k in np.argsort(-e)[:6]:
+            print(f"gpart {k}: x {g['x'][k]} gpu {a[k]} oracle {b[k]}")
+    assert e.max() <= rel * np.abs(b).max(), e.max() / np.abs(b).max()
     p, q = g["potential"].astype(np.float64), o["potential"].astype(np.float64)
     assert np.abs(p - q).max() <= rel * np.abs(q).max()
 

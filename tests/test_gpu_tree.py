@@ -196,3 +196,35 @@ def test_device_walk_equals_host_walk(gpu_ctx, monkeypatch):
     sd.pop("ms"), sh.pop("ms")  # phase timings
     assert sd == sh and sd["n_m2l"] > 0 and sd["n_skipped"] > 0
     compare(gd, gh, rel=1e-9)
+
+
+def test_tree_truncated_pair_count(gpu_ctx):
+    """n_pp_truncated (the P2P pairs of truncated entries, which SURVEY 8d
+    prices at 43 flops against 28 for Newtonian pairs): every pair when the
+    box is periodic and r_cut_min is 0 (runner_dopair/doself_grav_pp take the
+    truncated kernels for any cell pair farther than r_cut_min), none when
+    the box is not periodic; with r_cut_min beyond every separation only the
+    no-cache entries (runner_dopair_grav_pp_no_cache, always truncated in a
+    periodic box) keep them, fewer than with r_cut_min = 0.08, fewer than
+    all. The P2P counts themselves equal the oracle's."""
+    g, cells, tops = ics.gravity_tree(clumpy_box(12, seed=11), 2, split_size=24)
+    pairs = ics.top_level_pairs(tops)
+    r_s = 1.25 / 16
+    cases = {"all": params(periodic=True, theta=0.5, r_s_inv=1 / r_s, r_cut_min=0.0,
+                           r_cut_max=10.0),
+             "open": params(periodic=False, theta=0.5),
+             "none": params(periodic=True, theta=0.5, r_s_inv=1 / r_s, r_cut_min=1e3,
+                            r_cut_max=1e4),
+             "some": params(periodic=True, theta=0.5, r_s_inv=1 / r_s, r_cut_min=0.08,
+                            r_cut_max=10.0)}
+    got = {}
+    for k, G in cases.items():
+        gg, go = abi.copy_parts(g), abi.copy_parts(g)
+        st = run_gpu(gpu_ctx, gg, cells, tops, pairs, G)[0]
+        so, _ = run_oracle(go, cells, tops, pairs, G)
+        assert st["n_pp"] == so[0] and st["n_pp"] > 0, (k, st["n_pp"], so[0])
+        got[k] = (st["n_pp_truncated"], st["n_pp"])
+    print(f"\n{got}")
+    assert got["all"][0] == got["all"][1]
+    assert got["open"][0] == 0
+    assert 0 < got["none"][0] < got["some"][0] < got["some"][1]

@@ -533,6 +533,9 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(MPOLE ? 3 :
 // source past that bound (a pair separation near L/2: top-level cells of a
 // tiny box) wraps every pair (nearest_rint), as nearestf does.
 constexpr int kPPBatch = 256;
+#ifndef SWH_P2P_EXP
+#define SWH_P2P_EXP 0
+#endif
 
 // The batch kernel's pair loop over one staged tile: lane s of its i takes
 // entries s, s + lpi, ... MASKED: per pair, the entry's M2P bit (pmask) and
@@ -591,7 +594,7 @@ __device__ __forceinline__ void batch_pairs(const TileLds& tl, const PairCtx& c,
 // MPOLE: mbits[entry] = the lanes whose i takes the entry's multipole (its
 // MAC passed), for m2p_kernel, which then tests nothing itself.
 template <bool MPOLE>
-__global__ __launch_bounds__(64) void p2p_batch_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2p_batch_kernel(
     GSoA g, const swh_leaf* __restrict__ leaves, const int* __restrict__ pair_off,
     const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
     double dimz, double r_s_inv, MacParams mac, unsigned long long* counter,
@@ -602,6 +605,14 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
   __shared__ int sg[kPPBatch];
   __shared__ unsigned char sb[kPPBatch];
   __shared__ int boff[32], bstart[32];
+  // the MAC tests' scratch (1.5 KB) over sx: used between tiles only
+  static_assert(32 * sizeof(MacSource) + 64 * 4 + 32 * 8 + 32 * 4 <= sizeof(double) * kPPBatch,
+                "MAC scratch fits sx");
+  MacSource* const mac_ms = reinterpret_cast<MacSource*>(sx);
+  unsigned long long* const mac_qmask =
+      reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(sx) + 32 * sizeof(MacSource));
+  unsigned int* const mac_imask = reinterpret_cast<unsigned int*>(mac_qmask + 32);
+  int* const mac_q = reinterpret_cast<int*>(mac_imask + 64);
   const int li = xcd_block_id();
   const swh_leaf L = leaves[li];
   const int p0 = pair_off[li], p1 = pair_off[li + 1];
@@ -619,6 +630,24 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
   const double hv = act ? g.hinv[gi] : 1.;
   const double tworsi = 2. * r_s_inv;
   const double idimx = 1. / dimx, idimy = 1. / dimy, idimz = 1. / dimz;
+  // the MAC's float view of i (gravity_cache_populate)
+  const float4 pf = make_float4((float)pi.x, (float)pi.y, (float)pi.z, (float)pi.w);
+  const float oag = MPOLE && act ? g.oagn[gi] : 0.f;
+  // the MAC's test lanes: lane = kk * count + ii tests i-slot ii (its data
+  // from lane ii * lpi), epr entries per round; ibits = the lanes of ii
+  const int nI = max(L.count, 1), epr = max(1, 64 / nI);
+  const int kk = lane / nI, ii = lane - kk * nI;
+  const int tsrc = ii * lpi;  // < 64: count * lpi <= 64
+  float4 t_pf = make_float4(0.f, 0.f, 0.f, 0.f);
+  float t_oag = 0.f;
+  bool t_act = false;
+  if (MPOLE) {
+    t_pf = make_float4(__shfl(pf.x, tsrc), __shfl(pf.y, tsrc), __shfl(pf.z, tsrc),
+                       __shfl(pf.w, tsrc));
+    t_oag = __shfl(oag, tsrc);
+    t_act = __shfl((int)act, tsrc) != 0 && kk < epr && ii < L.count;
+  }
+  const unsigned long long ibits = ((1ull << lpi) - 1ull) << tsrc;
   // periodic: the i-leaf's first gpart c and the leaf's extent around it
   double cx = 0., cy = 0., cz = 0., lim_x = 0., lim_y = 0., lim_z = 0.;
   if (periodic) {
@@ -651,6 +680,10 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
       tr = pr.truncated != 0;
       am = pr.allow_mpole && J.count > 1;
     }
+    // every lane loads its own entry's multipole fields at once (a chain of
+    // one load per tested entry otherwise: the kernel's largest stall)
+    MacSource msrc{};
+    if (MPOLE && am) msrc = mac_source(g.mp[jl]);
     const int inc = wave_incl_scan(cnt);
     // the batch: the entries whose gparts fit the tile (a prefix). A source
     // larger than the tile (a split cell of a no-cache P-P entry: a
@@ -662,15 +695,34 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
     const unsigned int tmask = (unsigned int)__ballot(lane < B && tr);
     unsigned int mmask = 0;  // the entries this i takes through their multipole
     if (MPOLE) {
+      // The MAC tests of the batch, one (i, entry) test per lane: the entries
+      // with allow_mpole are listed in LDS (scratch over the tile, whose last
+      // readers are done) and lane (kk, ii) tests i-slot ii against entries
+      // kk, kk + EPR, ...; the results gather by LDS OR into per-i entry masks
+      // (mmask) and per-entry lane masks (mbits).
+      const unsigned long long amb = __ballot(lane < B && am);
       unsigned long long mine = 0;  // lane q < B: entry q's accepting lanes
-      for (unsigned long long m = __ballot(lane < B && am); m; m &= m - 1) {
-        const int q = __ffsll((long long)m) - 1;
-        const int jq = __builtin_amdgcn_readlane(jl, q);
-        const bool ok = act && m2p_accept(mac, mac_source(g.mp[jq]), (float)pi.x, (float)pi.y,
-                                          (float)pi.z, (float)pi.w, g.oagn[gi]);
-        if (ok) mmask |= 1u << q;
-        const unsigned long long okm = __ballot(ok);
-        if (lane == q) mine = okm;
+      if (amb) {
+        const int nq = __popcll(amb);
+        wave_sync();
+        if (lane < B && am) {
+          const int r = __popcll(amb & ((1ull << lane) - 1ull));
+          mac_ms[r] = msrc;
+          mac_q[r] = lane;
+        }
+        mac_imask[lane] = 0u;
+        if (lane < 32) mac_qmask[lane] = 0ull;
+        wave_sync();
+        if (t_act)
+          for (int k = kk; k < nq; k += epr)
+            if (m2p_accept(mac, mac_ms[k], t_pf.x, t_pf.y, t_pf.z, t_pf.w, t_oag)) {
+              const int q = mac_q[k];
+              atomicOr(&mac_imask[ii], 1u << q);
+              atomicOr(&mac_qmask[q], ibits);
+            }
+        wave_sync();
+        if (act) mmask = mac_imask[il];
+        if (lane < B) mine = mac_qmask[lane];
       }
       if (lane < B) mbits[qb + lane] = mine;
     }
@@ -684,7 +736,7 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
     }
     const int cnt2 = (lane < B && ((allm >> lane) & 1u)) ? 0 : cnt;
     const int inc2 = wave_incl_scan(cnt2);
-    const int total2 = __builtin_amdgcn_readlane(inc2, B - 1);
+    const int total2 = SWH_P2P_EXP == 2 ? 0 : __builtin_amdgcn_readlane(inc2, B - 1);
     // the i-leaf's own gparts among the staged sources (self terms to drop)
     const bool own = __any(lane < B && cnt2 > 0 && jst < L.start + L.count && L.start < jst + cnt);
     const bool mixed = (anym & ~allm & bmask) != 0u;
@@ -735,8 +787,13 @@ __global__ __launch_bounds__(64) void p2p_batch_kernel(
       const int tr = (tmask & bmask) == bmask ? 1 : (tmask & bmask) == 0u ? 0 : 2;
       const PairCtx pc{pi, hi2, hv, emax, tworsi, dimx, dimy, dimz, idimx, idimy, idimz};
       const TileLds tl{sx, sy, sz, seps, sm, sg, sb};
+#if SWH_P2P_EXP == 1 || SWH_P2P_EXP == 3  // experiments (wrong results): 1 staging + MAC
+// only, 2 entries + MAC only, 3 staging only
+#define SWH_BATCH_PAIRS(M, T) (void)0
+#else
 #define SWH_BATCH_PAIRS(M, T)                                                             \
   batch_pairs<M, T>(tl, pc, s, lpi, tn, wrap, pmask, tmask, gi, ax, ay, az, pot, nint)
+#endif
       if (plain) {
         if (act) nint += (unsigned int)(tn > s ? (tn - s + lpi - 1) / lpi : 0);
         if (tr == 1) SWH_BATCH_PAIRS(false, 1);

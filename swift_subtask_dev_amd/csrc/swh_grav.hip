@@ -554,11 +554,11 @@ struct TileLds {
   const unsigned char* sb;
 };
 template <bool MASKED, int TR>
-__device__ __forceinline__ void batch_pairs(const TileLds& tl, const PairCtx& c, int s, int lpi,
+__device__ __forceinline__ void batch_pairs(const TileLds& tl, const PairCtx& c, int t0, int lpi,
                                             int tn, bool wrap, unsigned int pmask,
                                             unsigned int tmask, int gi, double& ax, double& ay,
                                             double& az, double& pot, unsigned int& nint) {
-  for (int t = s; t < tn; t += lpi) {
+  for (int t = t0; t < tn; t += lpi) {
     double dx = tl.sx[t] - c.pi.x, dy = tl.sy[t] - c.pi.y, dz = tl.sz[t] - c.pi.z;
     if (wrap) {
       dx = nearest_rint(dx, c.dimx, c.idimx);
@@ -604,7 +604,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2
   __shared__ float seps[kPPBatch], sm[kPPBatch];
   __shared__ int sg[kPPBatch];
   __shared__ unsigned char sb[kPPBatch];
-  __shared__ int boff[32], bstart[32];
+  __shared__ int boff[32], bstart[32], bent[32];  // per slot: position, gpart, entry
   // the MAC tests' scratch (1.5 KB) over sx: used between tiles only
   static_assert(32 * sizeof(MacSource) + 64 * 4 + 32 * 8 + 32 * 4 <= sizeof(double) * kPPBatch,
                 "MAC scratch fits sx");
@@ -691,7 +691,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2
     // in tile-sized chunks.
     const unsigned long long fit = __ballot(cnt > 0 && inc <= kPPBatch);
     const int B = fit ? __popcll(fit) : 1;
-    const unsigned int bmask = B >= 32 ? 0xffffffffu : (1u << B) - 1u;
     const unsigned int tmask = (unsigned int)__ballot(lane < B && tr);
     unsigned int mmask = 0;  // the entries this i takes through their multipole
     if (MPOLE) {
@@ -734,27 +733,42 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2
       allm &= (unsigned int)__shfl_xor((int)allm, o);
       anym |= (unsigned int)__shfl_xor((int)anym, o);
     }
-    const int cnt2 = (lane < B && ((allm >> lane) & 1u)) ? 0 : cnt;
-    const int inc2 = wave_incl_scan(cnt2);
-    const int total2 = SWH_P2P_EXP == 2 ? 0 : __builtin_amdgcn_readlane(inc2, B - 1);
-    // the i-leaf's own gparts among the staged sources (self terms to drop)
-    const bool own = __any(lane < B && cnt2 > 0 && jst < L.start + L.count && L.start < jst + cnt);
-    const bool mixed = (anym & ~allm & bmask) != 0u;
+    const bool inb = lane < B;
+    const int cnt2 = (inb && ((allm >> lane) & 1u)) ? 0 : (inb ? cnt : 0);
+    // Staging order: first the entries every i takes alike (plain), then the
+    // ones that need per-pair masks -- a multipole for some of the i's only
+    // (mixed), or the i-leaf's own gparts (self terms to drop) -- so only the
+    // tile's tail runs the masked pair loop. slot = an entry's place in that
+    // order, pos = its first staged position.
+    const bool ownq = cnt2 > 0 && jst < L.start + L.count && L.start < jst + cnt;
+    const bool maskq = inb && (ownq || (((anym & ~allm) >> lane) & 1u));
+    const int cA = maskq ? 0 : cnt2, cM = maskq ? cnt2 : 0;
+    const int incA = wave_incl_scan(cA), incM = wave_incl_scan(cM);
+    const int totalA = __builtin_amdgcn_readlane(incA, 63);
+    const int total2 = SWH_P2P_EXP == 2 ? 0 : totalA + __builtin_amdgcn_readlane(incM, 63);
+    const unsigned long long ballA = __ballot(inb && !maskq), ballM = __ballot(maskq);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const int slot = maskq ? __popcll(ballA) + __popcll(ballM & below) : __popcll(ballA & below);
+    const int posq = maskq ? totalA + incM - cM : incA - cA;
+    // plain entries all / none / some truncated
+    const unsigned int bA = (unsigned int)ballA;
+    const int trA = (tmask & bA) == bA ? 1 : (tmask & bA) == 0u ? 0 : 2;
     // per i: the entries it takes by P2P (inactive i: none)
     const unsigned int pmask = act ? ~mmask : 0u;
     for (int jb = 0; jb < total2; jb += kPPBatch) {
       const int tn = min(kPPBatch, total2 - jb);
       wave_sync();  // the previous tile's readers are done
-      if (lane < B) {
-        boff[lane] = inc2 - cnt2;  // (an unstaged entry: its successor's offset)
-        bstart[lane] = jst;
+      if (inb) {
+        boff[slot] = posq;  // (an unstaged entry: its successor's offset)
+        bstart[slot] = jst;
+        bent[slot] = lane;
       }
       wave_sync();
       double e2max = 0.;
       bool far = false;
       for (int k = lane; k < tn; k += 64) {
         const int e = jb + k;  // the batch's e-th gpart
-        int b = 0;  // its entry: the largest b with boff[b] <= e
+        int b = 0;  // its entry's slot: the largest b with boff[b] <= e
         for (int st = 16; st > 0; st >>= 1)
           if (b + st < B && boff[b + st] <= e) b += st;
         const int gj = bstart[b] + (e - boff[b]);
@@ -774,34 +788,31 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2
         e2max = fmax(e2max, p.w * p.w);
         sm[k] = g.mass[gj];
         sg[k] = gj;
-        sb[k] = (unsigned char)b;
+        sb[k] = (unsigned char)bent[b];
       }
       const double emax = act ? fmax(hi2, wave_max_f64(e2max)) : 0.;
       const bool wrap = periodic && __any(far);
       wave_sync();
-      // Wave-uniform fast paths: no staged entry is a multipole for some of
-      // the i's only and the i-leaf is none of the sources (no self term) ->
-      // no per-pair mask, the pairs counted per lane; every or no entry
-      // truncated -> no per-pair truncation bit.
-      const bool plain = !mixed && !own;
-      const int tr = (tmask & bmask) == bmask ? 1 : (tmask & bmask) == 0u ? 0 : 2;
+      // The plain part [0, tA): no per-pair mask, the pairs counted per lane;
+      // every or no entry truncated -> no per-pair truncation bit. The
+      // masked part [tA, tn) tests each pair's entry bit and self index.
+      const int tA = SWH_P2P_EXP == 4 ? tn : min(tn, max(0, totalA - jb));
       const PairCtx pc{pi, hi2, hv, emax, tworsi, dimx, dimy, dimz, idimx, idimy, idimz};
       const TileLds tl{sx, sy, sz, seps, sm, sg, sb};
 #if SWH_P2P_EXP == 1 || SWH_P2P_EXP == 3  // experiments (wrong results): 1 staging + MAC
 // only, 2 entries + MAC only, 3 staging only
-#define SWH_BATCH_PAIRS(M, T) (void)0
+#define SWH_BATCH_PAIRS(M, T, T0, T1) (void)0
 #else
-#define SWH_BATCH_PAIRS(M, T)                                                             \
-  batch_pairs<M, T>(tl, pc, s, lpi, tn, wrap, pmask, tmask, gi, ax, ay, az, pot, nint)
+#define SWH_BATCH_PAIRS(M, T, T0, T1)                                                          \
+  batch_pairs<M, T>(tl, pc, (T0) + s, lpi, T1, wrap, pmask, tmask, gi, ax, ay, az, pot, nint)
 #endif
-      if (plain) {
-        if (act) nint += (unsigned int)(tn > s ? (tn - s + lpi - 1) / lpi : 0);
-        if (tr == 1) SWH_BATCH_PAIRS(false, 1);
-        else if (tr == 0) SWH_BATCH_PAIRS(false, 0);
-        else SWH_BATCH_PAIRS(false, 2);
-      } else {
-        SWH_BATCH_PAIRS(true, 2);
+      if (tA > 0) {
+        if (act) nint += (unsigned int)(tA > s ? (tA - s + lpi - 1) / lpi : 0);
+        if (trA == 1) SWH_BATCH_PAIRS(false, 1, 0, tA);
+        else if (trA == 0) SWH_BATCH_PAIRS(false, 0, 0, tA);
+        else SWH_BATCH_PAIRS(false, 2, 0, tA);
       }
+      if (tA < tn) SWH_BATCH_PAIRS(true, 2, tA, tn);
 #undef SWH_BATCH_PAIRS
     }
     qb += B;

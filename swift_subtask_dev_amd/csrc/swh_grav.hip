@@ -547,39 +547,40 @@ struct PairCtx {
   double hi2, hv, emax, tworsi, dimx, dimy, dimz, idimx, idimy, idimz;
 };
 struct TileLds {
-  const double *sx, *sy, *sz;
+  const double *sx, *sy, *sz, *sm;  // one array, kPPBatch apart: one address per pair
   const float* seps;  // softening: h2 = eps^2 and 1 / eps are exact from the float
-  const float* sm;
-  const int* sg;
   const unsigned char* sb;
 };
 template <bool MASKED, int TR>
 __device__ __forceinline__ void batch_pairs(const TileLds& tl, const PairCtx& c, int t0, int lpi,
                                             int tn, bool wrap, unsigned int pmask,
-                                            unsigned int tmask, int gi, double& ax, double& ay,
+                                            unsigned int tmask, int self_t, double& ax, double& ay,
                                             double& az, double& pot, unsigned int& nint) {
-  for (int t = t0; t < tn; t += lpi) {
-    double dx = tl.sx[t] - c.pi.x, dy = tl.sy[t] - c.pi.y, dz = tl.sz[t] - c.pi.z;
+  // one address per pair: the loop runs over x's slot, y, z and the mass sit
+  // kPPBatch slots on; the slot index is derived only where it is needed
+  const double* const end = tl.sx + tn;
+  for (const double* px = tl.sx + t0; px < end; px += lpi) {
+    double dx = px[0] - c.pi.x, dy = px[kPPBatch] - c.pi.y, dz = px[2 * kPPBatch] - c.pi.z;
     if (wrap) {
       dx = nearest_rint(dx, c.dimx, c.idimx);
       dy = nearest_rint(dy, c.dimy, c.idimy);
       dz = nearest_rint(dz, c.dimz, c.idimz);
     }
     int b = 0;
-    if (MASKED || TR == 2) b = tl.sb[t];
+    if (MASKED || TR == 2) b = tl.sb[px - tl.sx];
     double mass;
     if (MASKED) {
-      const bool use = ((pmask >> b) & 1u) & (tl.sg[t] != gi);
+      const bool use = ((pmask >> b) & 1u) & ((int)(px - tl.sx) != self_t);
       nint += use;
-      mass = (double)(use ? tl.sm[t] : 0.f);
+      mass = use ? px[3 * kPPBatch] : 0.;
     } else {
-      mass = (double)tl.sm[t];
+      mass = px[3 * kPPBatch];
     }
     double r2, r_inv, f_ij, pot_ij;
     p2p_newton(dx, dy, dz, mass, r2, r_inv, f_ij, pot_ij);
     if (__builtin_expect(__any(r2 < c.emax), 0))
       if (r2 < c.emax) {
-        const double ej = (double)tl.seps[t];
+        const double ej = (double)tl.seps[px - tl.sx];
         p2p_soften(r2, r_inv, c.hi2, ej * ej, c.hv, 1. / ej, mass, f_ij, pot_ij);
       }
     if (TR == 1 || (TR == 2 && ((tmask >> b) & 1u)))
@@ -599,10 +600,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2
     const swh_leaf_pair* __restrict__ pairs, int periodic, double dimx, double dimy,
     double dimz, double r_s_inv, MacParams mac, unsigned long long* counter,
     unsigned long long* __restrict__ mbits) {
-  // 37 B per staged gpart (9.5 KB): four waves per SIMD
-  __shared__ double sx[kPPBatch], sy[kPPBatch], sz[kPPBatch];
-  __shared__ float seps[kPPBatch], sm[kPPBatch];
-  __shared__ int sg[kPPBatch];
+  // 37 B per staged gpart (9.6 KB): four waves per SIMD
+  __shared__ double stile[4 * kPPBatch];  // x, y, z, mass
+  double* const sx = stile;
+  double* const sy = stile + kPPBatch;
+  double* const sz = stile + 2 * kPPBatch;
+  double* const sm = stile + 3 * kPPBatch;
+  __shared__ float seps[kPPBatch];
   __shared__ unsigned char sb[kPPBatch];
   __shared__ int boff[32], bstart[32], bent[32];  // per slot: position, gpart, entry
   // the MAC tests' scratch (1.5 KB) over sx: used between tiles only
@@ -786,8 +790,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2
         sz[k] = pz;
         seps[k] = (float)p.w;  // (the gpart's float epsilon, exactly)
         e2max = fmax(e2max, p.w * p.w);
-        sm[k] = g.mass[gj];
-        sg[k] = gj;
+        sm[k] = (double)g.mass[gj];
         sb[k] = (unsigned char)bent[b];
       }
       const double emax = act ? fmax(hi2, wave_max_f64(e2max)) : 0.;
@@ -798,13 +801,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2
       // masked part [tA, tn) tests each pair's entry bit and self index.
       const int tA = SWH_P2P_EXP == 4 ? tn : min(tn, max(0, totalA - jb));
       const PairCtx pc{pi, hi2, hv, emax, tworsi, dimx, dimy, dimz, idimx, idimy, idimz};
-      const TileLds tl{sx, sy, sz, seps, sm, sg, sb};
+      const TileLds tl{sx, sy, sz, sm, seps, sb};
+      // this i's own tile position (its self term), or -1
+      int self_t = -1;
+      for (unsigned long long m = __ballot(inb && ownq); m; m &= m - 1) {
+        const int q = __ffsll((long long)m) - 1;
+        const int js = __builtin_amdgcn_readlane(jst, q), jc = __builtin_amdgcn_readlane(cnt, q);
+        const int t = __builtin_amdgcn_readlane(posq, q) + (gi - js) - jb;
+        if (gi >= js && gi < js + jc && t >= 0 && t < tn) self_t = t;
+      }
 #if SWH_P2P_EXP == 1 || SWH_P2P_EXP == 3  // experiments (wrong results): 1 staging + MAC
 // only, 2 entries + MAC only, 3 staging only
 #define SWH_BATCH_PAIRS(M, T, T0, T1) (void)0
 #else
 #define SWH_BATCH_PAIRS(M, T, T0, T1)                                                          \
-  batch_pairs<M, T>(tl, pc, (T0) + s, lpi, T1, wrap, pmask, tmask, gi, ax, ay, az, pot, nint)
+  batch_pairs<M, T>(tl, pc, (T0) + s, lpi, T1, wrap, pmask, tmask, self_t, ax, ay, az, pot, nint)
 #endif
       if (tA > 0) {
         if (act) nint += (unsigned int)(tA > s ? (tA - s + lpi - 1) / lpi : 0);

@@ -524,6 +524,18 @@ def steady_state(sp, P, stream, torch, local, n_owned, args, skin=None, steps=No
     skin = args.steady_skin if skin is None else skin
     steps = args.steady_steps if steps is None else steps
     disp = args.steady_disp if disp is None else disp
+    # Skin policy from the displacement per step: a list of skin s stays valid
+    # while every particle's H + 2 dx_max <= its build reach H (1 + s), i.e.
+    # ~kernel_gamma s / (2 disp) steps, and its walks grow as (1 + s)^3. A
+    # list that cannot outlive two steps costs more than it saves: then every
+    # density loop rebuilds with the headline's skin (no keep check).
+    life = KERNEL_GAMMA * skin / (2.0 * disp)
+    keep = 1
+    policy = f"kept lists, skin {skin} (~{life:.2f} steps per build)"
+    if life < 2.0:
+        policy = (f"rebuild per step, skin {args.list_skin}: a skin-{skin} list would last "
+                  f"{life:.2f} steps")
+        skin, keep = args.list_skin, 0
     rng = np.random.Generator(np.random.PCG64(23))
     n = len(local)
     xp = abi.new_xparts(n)
@@ -533,7 +545,7 @@ def steady_state(sp, P, stream, torch, local, n_owned, args, skin=None, steps=No
     dt = disp * h / vmax
     D = abi.DriftParams(dt, 0.0, 0.0, 0.0, 0.0)
     sp.set_tuning(args.cell_factor, args.loop_variant, args.group_size, args.cell_scale, 0,
-                  args.list_capacity, skin, 1)
+                  args.list_capacity, skin, keep)
 
     def reset():
         sp.upload(local)
@@ -584,7 +596,8 @@ def steady_state(sp, P, stream, torch, local, n_owned, args, skin=None, steps=No
     return {"note": "untimed by the headline: drift + density + force per step with the pair "
                     "lists kept across drifts while valid (device check, rebuilt on the device "
                     "when a particle's H + 2 D exceeds its build reach)",
-            "steps": steps, "list_skin": skin, "displacement_per_step_over_h": disp,
+            "steps": steps, "list_skin": skin, "skin_policy": policy,
+            "displacement_per_step_over_h": disp,
             "rebin_every": rebin, "list_builds": int(builds),
             "steps_per_list_build": steps / max(1, builds),
             "interactions": nd + nf, "ms_per_step": el / steps * 1e3,
@@ -1186,8 +1199,9 @@ def main():
             steady = steady_state(sp, P, stream, torch, local, n_owned, args)
             # Where keeping the lists pays: a kept list of skin s stays valid for
             # ~gamma s / (2 disp) steps while its walks grow as (1 + s)^3, so at
-            # the 0.05 h / step above every skin loses to a rebuild per step; at
-            # 0.01 h / step a 5% skin lasts ~4-5 steps for ~16% more entries.
+            # the 0.05 h / step above every skin loses to a rebuild per step (the
+            # policy in steady_state then rebuilds); at 0.01 h / step a 5% skin
+            # lasts ~4-5 steps for ~16% more entries.
             steady["low_velocity"] = steady_state(sp, P, stream, torch, local, n_owned, args,
                                                   skin=0.05, disp=0.01)
         except Exception as e:  # report, never fake

@@ -152,7 +152,10 @@ __device__ __forceinline__ double horner_step(double p, double f, double c) {
 // coefficients; the 256-thread tile kernel keeps fma and its register budget)
 template <bool FMA3>
 __device__ __forceinline__ double exp_neg_f64_x2(double x) {
-  const double k = __builtin_rint(x * -1.4426950408889634);  // -x / ln 2
+  // k = rint(-x / ln 2) by the 1.5 * 2^52 shifter: one fma rounds to an
+  // integer held in the low word (no conversion for the ldexp)
+  const double kd = fma(x, -1.4426950408889634, 6755399441055744.0);
+  const double k = kd - 6755399441055744.0;
   const double f = fma(k, -0.6931471805599453, -x);
   double q = horner_step<FMA3>(2 * 2.4778829221708597e-05, f, 2 * 0.00019908923481541454);
   q = horner_step<FMA3>(q, f, 2 * 0.0013889023827227704);
@@ -161,7 +164,7 @@ __device__ __forceinline__ double exp_neg_f64_x2(double x) {
   q = horner_step<FMA3>(q, f, 2 * 0.16666666784287604);
   q = horner_step<FMA3>(q, f, 2 * 0.500000000012381);
   const double p = fma(f, fma(f, q, 2.), 2.);
-  return __builtin_ldexp(p, (int)k);
+  return __builtin_ldexp(p, __double2loint(kd));
 }
 
 // D_soft_k(u) of the Wendland-C2 softening (kernel_gravity.h:169-275).

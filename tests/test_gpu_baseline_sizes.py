@@ -238,9 +238,17 @@ def test_cosmo_volume_gravity_owned_subtrees_two_ranks_vs_f64(gpu_ctx, cosmo_vol
     assert len(idx) == len(g) and len(np.unique(idx)) == len(g)
     for k in ("n_pp", "n_m2p", "n_m2l"):
         assert sum(s[k] for s in stats) == st_ref[k], (k, [s[k] for s in stats], st_ref[k])
-    for f in ("a_grav", "potential", "a_grav_mesh", "potential_mesh"):
+    for f in ("a_grav", "potential"):
         for i, out in parts:
             assert np.array_equal(out[f][i], ref[f][i]), f
+    # the PM mesh is every rank's own (replicated gparts); its CIC assignment
+    # adds with fp64 atomics, whose order varies run to run: the float fields
+    # may differ in the last bit
+    for f in ("a_grav_mesh", "potential_mesh"):
+        scale = np.abs(ref[f].astype(np.float64)).max()
+        for i, out in parts:
+            d = np.abs(out[f][i].astype(np.float64) - ref[f][i].astype(np.float64)).max()
+            assert d <= 1e-6 * scale, (f, d / scale)
     go, st_o = _oracle_gravity(g, cells, tops, pairs, G)
     print(f"\ncosmo owned subtrees: {[dict((k, s[k]) for k in ('n_pp', 'n_m2p', 'n_m2l')) for s in stats]}"
           f" single domain {st_ref} oracle {list(st_o)}")

@@ -555,7 +555,7 @@ def steady_state(sp, P, stream, torch, local, n_owned, args, skin=None, steps=No
 
     reset()
     w = min(sp.info()["cell_width"])
-    rebin = max(1, int(0.5 * w / (vmax * dt)))
+    rebin = max(1, int(args.steady_rebin * w / (vmax * dt)))
 
     def run(count, ev=None):
         nd = nf = 0
@@ -993,6 +993,8 @@ def main():
     ap.add_argument("--no-steady", action="store_true", help="skip the untimed steady-state run")
     ap.add_argument("--steady-skin", type=float, default=0.1)
     ap.add_argument("--steady-steps", type=int, default=24)
+    ap.add_argument("--steady-rebin", type=float, default=0.25,
+                    help="re-bin the space once the fastest particle can have moved this many cell widths")
     ap.add_argument("--steady-disp", type=float, default=0.05,
                     help="steady state: displacement of the fastest particle per step / h")
     ap.add_argument("--no-breakdown", action="store_true",

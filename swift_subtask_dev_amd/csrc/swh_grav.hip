@@ -716,7 +716,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2
         mac_imask[lane] = 0u;
         if (lane < 32) mac_qmask[lane] = 0ull;
         wave_sync();
-        if (t_act)
+        if (t_act && SWH_P2P_EXP != 3)
           for (int k = kk; k < nq; k += epr)
             if (m2p_accept(mac, mac_ms[k], t_pf.x, t_pf.y, t_pf.z, t_pf.w, t_oag)) {
               const int q = mac_q[k];

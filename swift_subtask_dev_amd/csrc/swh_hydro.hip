@@ -57,29 +57,49 @@ __device__ __forceinline__ unsigned int rwrap_of(float base, float dx) {
   return __float_as_uint(base + dx * (1.f + 1e-4f));
 }
 
-__global__ void list_prep_kernel(const unsigned int* hmax_bits, float gs1, float dx,
-                                 unsigned int* rwrap, unsigned int* rwrap_base,
-                                 unsigned int* ovf_n, const unsigned int* run_if,
-                                 unsigned int* nbuilds) {
-  if (threadIdx.x == 0 && !skip_build(run_if)) {
-    const float base = __uint_as_float(*hmax_bits) * gs1 * (1.f + 1e-4f) + 1e-30f;
+// The list build's preparation in one pass over the i-groups (16 lanes per
+// group, four groups per wave; the groups partition every particle in a
+// cell): each particle's cell-local fp32 position for the staging (posf) and
+// the displacement record at build time (xd0 = xdiff: a kept list measures
+// drifts from here), and each group's box over its active particles
+// (GroupBox), reduced across the group's 16 lanes -- the build's waves read
+// it with scalar loads. Thread 0 resets the build's device counters.
+__global__ __launch_bounds__(256) void group_prep_kernel(
+    GridDev g, SoA a, const int* __restrict__ pcell, const float4* __restrict__ xdiff,
+    const int2* __restrict__ groups, int ngroups, int max_active_bin, double gs1,
+    float4* __restrict__ posf, float4* __restrict__ xd0, GroupBox* __restrict__ gbox,
+    const unsigned int* hmax_bits, float rgs1, float dx, unsigned int* rwrap,
+    unsigned int* rwrap_base, unsigned int* ovf_n, unsigned int* nbuilds,
+    const unsigned int* run_if) {
+  if (skip_build(run_if)) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const float base = __uint_as_float(*hmax_bits) * rgs1 * (1.f + 1e-4f) + 1e-30f;
     *rwrap_base = __float_as_uint(base);
     *rwrap = rwrap_of(base, dx);
     *ovf_n = 0u;
     *nbuilds += 1u;
   }
-}
-
-// Cell-local fp32 positions for the build's staging, and the displacement
-// record at build time (xd0 = xdiff: a kept list measures drifts from here).
-__global__ void posf_kernel(GridDev g, const double4* __restrict__ pos,
-                            const int* __restrict__ pcell, const float4* __restrict__ xdiff,
-                            int64_t n, float4* __restrict__ posf, float4* __restrict__ xd0,
-                            const unsigned int* run_if) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || skip_build(run_if)) return;
-  posf[i] = pcell[i] >= 0 ? cell_local(g, pos[i], pcell[i]) : make_float4(0.f, 0.f, 0.f, 0.f);
-  xd0[i] = xdiff[i];
+  const int gidx = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4);
+  const int r = (int)(threadIdx.x & 15);
+  const int2 gr = gidx < ngroups ? groups[gidx] : make_int2(0, 0);
+  GroupBox b;
+  box_init(b);
+  for (int k = r; k < gr.y; k += 16) {
+    const int i = gr.x + k;
+    const double4 p = a.pos[i];
+    const int pc = pcell[i];
+    posf[i] = pc >= 0 ? cell_local(g, p, pc) : make_float4(0.f, 0.f, 0.f, 0.f);
+    xd0[i] = xdiff[i];
+    if (active_part(a, i, max_active_bin)) box_add(b, p, p.w * (double)kGamma * gs1);
+  }
+  for (int o = 8; o > 0; o >>= 1) {
+    for (int d = 0; d < 3; d++) {
+      b.lo[d] = fmin(b.lo[d], __shfl_xor(b.lo[d], o, 16));
+      b.hi[d] = fmax(b.hi[d], __shfl_xor(b.hi[d], o, 16));
+    }
+    b.Rg = fmax(b.Rg, __shfl_xor(b.Rg, o, 16));
+  }
+  if (gidx < ngroups && r == 0) gbox[gidx] = b;
 }
 
 __global__ void zero_u32_kernel(unsigned int* __restrict__ p, int64_t n,
@@ -844,18 +864,15 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
                        s->stream, s->pos.as<const double4>(), s->pcell.as<const int>(), s->n,
                        (float)(kGamma * ld.skin1), s->cell_hreach.as<unsigned int>(), run_if);
   }
-  hipLaunchKernelGGL(posf_kernel, dim3((int)((s->n + 255) / 256)), dim3(256), 0, s->stream,
-                     grid_dev(s), s->pos.as<const double4>(), s->pcell.as<const int>(),
-                     s->xdiff.as<const float4>(), s->n, s->posf.as<float4>(),
-                     s->list_xd0.as<float4>(), run_if);
-  hipLaunchKernelGGL(list_prep_kernel, dim3(1), dim3(64), 0, s->stream, hmax_slot(s),
-                     kGamma * ld.skin1, (float)s->grid.dx, rwrap_slot(s), rwrap_base_slot(s),
-                     ovf_slot(s), run_if, nbuild_slot(s));
   SWH_TRY(s->gbox.reserve((size_t)std::max(1, s->ngroups) * sizeof(GroupBox)));
   ListDev ldb = list_dev(s);
-  hipLaunchKernelGGL(group_box_kernel, dim3((s->ngroups + 255) / 256), dim3(256), 0, s->stream,
-                     soa_of(s), s->groups.as<const int2>(), s->ngroups, P->max_active_bin,
-                     (double)ld.skin1, s->gbox.as<GroupBox>(), run_if);
+  hipLaunchKernelGGL(group_prep_kernel, dim3(std::max(1, (s->ngroups + 15) / 16)), dim3(256), 0,
+                     s->stream, grid_dev(s), soa_of(s), s->pcell.as<const int>(),
+                     s->xdiff.as<const float4>(), s->groups.as<const int2>(), s->ngroups,
+                     P->max_active_bin, (double)ld.skin1, s->posf.as<float4>(),
+                     s->list_xd0.as<float4>(), s->gbox.as<GroupBox>(), hmax_slot(s),
+                     (float)(kGamma * ld.skin1), (float)s->grid.dx, rwrap_slot(s),
+                     rwrap_base_slot(s), ovf_slot(s), nbuild_slot(s), run_if);
   hipLaunchKernelGGL(list_build_kernel, dim3(s->ngroups), dim3(64), 0, s->stream, grid_dev(s),
                      soa_of(s), ldb, s->groups.as<const int2>(), 0, s->ngroups,
                      P->max_active_bin, hmax_slot(s), count ? stripes : nullptr,

@@ -64,9 +64,9 @@ __device__ __forceinline__ size_t list_at(int base, int KS, int k) {
   return list_lane(base, KS) + list_off4(k & 3, k >> 2);
 }
 
-// Per i-group box of the list build (group_box_kernel): the active
+// Per i-group box of the list build (group_prep_kernel): the active
 // particles' bounding box and the largest R = gamma h (1 + skin); Rg = 0: no
-// active particle. One thread per group computes it, so the build's waves
+// active particle. The group's 16 lanes reduce it once, so the build's waves
 // read it with scalar loads instead of reducing across lanes.
 struct GroupBox {
   double lo[3], hi[3], Rg, pad;
@@ -89,7 +89,7 @@ struct ListDev {
                         // null on a uniform grid (no per-cell pruning)
   int diag;      // profiling only: 2 = the build writes no entries
   const unsigned int* mark;  // nullable: particles the walks leave to a search (ghost-grown H)
-  const GroupBox* gbox;  // per group (group_box_kernel), read by the build
+  const GroupBox* gbox;  // per group (group_prep_kernel), read by the build
 };
 
 __device__ __forceinline__ void box_init(GroupBox& b) {
@@ -106,23 +106,6 @@ __device__ __forceinline__ void box_add(GroupBox& b, const double4& p, double R)
   b.hi[1] = p.y > b.hi[1] ? p.y : b.hi[1];
   b.hi[2] = p.z > b.hi[2] ? p.z : b.hi[2];
   b.Rg = R > b.Rg ? R : b.Rg;
-}
-
-__global__ void group_box_kernel(SoA a, const int2* __restrict__ groups, int ngroups,
-                                 int max_active_bin, double gs1, GroupBox* __restrict__ out,
-                                 const unsigned int* run_if) {
-  const int gidx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gidx >= ngroups || (run_if && *run_if == 0u)) return;
-  const int2 gr = groups[gidx];
-  GroupBox b;
-  box_init(b);
-  for (int i = gr.x; i < gr.x + gr.y; i++) {
-    if (!active_part(a, i, max_active_bin)) continue;
-    const double4 p = a.pos[i];
-    const double R = p.w * (double)kGamma * gs1;
-    box_add(b, p, R);
-  }
-  out[gidx] = b;
 }
 
 // Per-cell maximum R = gamma h (1 + skin): the list build skips a cell whose

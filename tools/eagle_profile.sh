@@ -7,7 +7,7 @@ tag="$1"
 set -o pipefail
 export TMPDIR=/tmp
 out=gpurun_out
-K="list_build|walk_kernel|overflow_kernel|posf_kernel|group_box|init_kernel|reset_acc"
+K="list_build|walk_kernel|overflow_kernel|posf_kernel|group_box|group_prep|init_kernel|reset_acc"
 for w in eagle sedov; do
   timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline --no-steady --no-breakdown \
     > "$out/${tag}_${w}_bench.log" 2>&1 || exit $?

@@ -46,7 +46,7 @@ out = {"source": f"profiles/{tag} PMC passes (rocprofv3 --pmc FETCH_SIZE | WRITE
        "kernels": traffic}
 # one density loop of the list path = the kernels it launches: positions
 # staging, list prep + build, the walk and the overflow search
-DENSITY_LIST = ("posf_kernel", "list_prep_kernel", "cell_reach_kernel", "list_build_kernel",
+DENSITY_LIST = ("group_prep_kernel", "cell_reach_kernel", "list_build_kernel",
                 "walk_kernel<0, double>", "density_walk_kernel<double>",
                 "overflow_kernel<0, double>")
 parts = {k: v for k, v in traffic.items() if any(k.endswith(d) or d in k for d in DENSITY_LIST)}

@@ -4,7 +4,7 @@
 # PMC (FETCH_SIZE and WRITE_SIZE in separate passes, kernel-trace only).
 # usage: tools/profile_round.sh <tag>     -> gpurun_out/<tag>_*
 tag="$1"
-KREGEX="${KREGEX:-list_build|walk_kernel|overflow_kernel|posf_kernel|list_prep|cell_reach|init_kernel|reset_kernel}"
+KREGEX="${KREGEX:-list_build|walk_kernel|overflow_kernel|group_prep|cell_reach|init_kernel|reset_kernel}"
 set -o pipefail
 out=gpurun_out
 timeout -k 10 300 python bench.py > "$out/${tag}_bench.log" 2>&1 || exit $?

@@ -16,7 +16,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-DENSITY = ["swh::posf_kernel", "swh::group_box_kernel", "swh::list_build_kernel",
+DENSITY = ["swh::posf_kernel", "swh::group_box_kernel", "swh::group_prep_kernel", "swh::list_build_kernel",
            "void swh::density_walk_kernel<double>", "void swh::overflow_kernel<0, double>"]
 MAIN_OVF_GRID = 64 * 256
 

@@ -852,11 +852,15 @@ def run_cosmo(args, ctx, rank, world, dist, torch):
             hydro()
             th.join()
         else:
-            # one host thread: the hydro loops are queued on their stream (no host
-            # wait), then the gravity step runs its chain on the high-priority
-            # gravity stream; the hydro kernels fill the CUs the chain leaves idle
+            # one host thread: the gravity chain (the step's critical path) is
+            # queued first on its high-priority stream -- the tree walk's levels
+            # return to the host, then the P2P and M2P are queued -- and the
+            # hydro loops are queued on their own stream behind it (no host
+            # wait), filling the CUs the chain leaves idle
+            gs.tree(G, tops, pairs, stats=False)
             hydro_async()
-            gravity()
+            gs.pm_mesh(N_mesh, 1.0, r_s, 1.0)
+            gs.sync()
             hs.sync()
 
     def timed(fn):

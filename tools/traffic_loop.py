@@ -7,7 +7,8 @@ taken at the main loops' grid (64 workgroups) only: the ghost's rerun
 searches launch the same kernel on larger grids.
 usage: python tools/traffic_loop.py <pmc tag> <workload>
   reads gpurun_out/<tag>_pmc_{FETCH_SIZE,WRITE_SIZE}/run_counter_collection.csv,
-  writes profiles/traffic_<workload>.json (bench.py load_traffic)."""
+  writes profiles/traffic_<workload>.json (traffic_density.json for sedov; bench.py
+  load_traffic)."""
 import collections
 import csv
 import json
@@ -46,6 +47,8 @@ out = {"source": f"profiles/{tag} PMC passes (rocprofv3 --pmc FETCH_SIZE | WRITE
                  "overflow kernels at the main loops' grid)",
        "kernels": kern, "density_kernels": dens,
        "bytes_per_launch": sum(kern[k]["bytes_per_launch"] for k in dens)}
-(ROOT / "profiles" / f"traffic_{workload}.json").write_text(json.dumps(out, indent=1) + "\n")
+# bench.py load_traffic: the Sedov headline reads traffic_density.json
+name = "traffic_density.json" if workload == "sedov" else f"traffic_{workload}.json"
+(ROOT / "profiles" / name).write_text(json.dumps(out, indent=1) + "\n")
 print(json.dumps({k: round(v["bytes_per_launch"] / 1e6, 1) for k, v in kern.items()}),
       "density loop MB:", round(out["bytes_per_launch"] / 1e6, 1))

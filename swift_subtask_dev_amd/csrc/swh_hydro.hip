@@ -246,17 +246,22 @@ __global__ __launch_bounds__(256) void overflow_kernel(GridDev g, SoA a, ListDev
     const double Hi = pi.w * (double)kGamma;
     CellRange c;
     cell_range(g, pi.x, pi.y, pi.z, st.reach, c);
-    for (int cz = c.lo[2]; cz <= c.hi[2]; cz++) {
-      double sz;
-      const int wz = wrap_cell(g, c, 2, cz, sz);
-      for (int cy = c.lo[1]; cy <= c.hi[1]; cy++) {
-        double sy;
-        const int wy = wrap_cell(g, c, 1, cy, sy);
-        for (int cx = c.lo[0]; cx <= c.hi[0]; cx++) {
-          double sx;
-          const int wx = wrap_cell(g, c, 0, cx, sx);
-          const int2 r = cell_range_of(g, wx, wy, wz);
-          if (r.y <= r.x) continue;
+    // The cells of the range are tested 64 at a time, one per lane (a large
+    // reach spans many cells, most of them pruned), then the accepted ones
+    // are walked by all lanes in the range's order (z, y, x).
+    const int nx = c.hi[0] - c.lo[0] + 1, ny = c.hi[1] - c.lo[1] + 1;
+    const int ncr = nx * ny * (c.hi[2] - c.lo[2] + 1);
+    for (int base = 0; base < ncr; base += 64) {
+      const int q = base + lane;
+      bool ok = false;
+      int2 r = make_int2(0, 0);
+      double sx = 0., sy = 0., sz = 0.;
+      if (q < ncr) {
+        const int wx = wrap_cell(g, c, 0, c.lo[0] + q % nx, sx);
+        const int wy = wrap_cell(g, c, 1, c.lo[1] + (q / nx) % ny, sy);
+        const int wz = wrap_cell(g, c, 2, c.lo[2] + q / (nx * ny), sz);
+        r = cell_range_of(g, wx, wy, wz);
+        if (r.y > r.x) {
           // box gap between i and this image of the cell (its particles may
           // stand g.dx outside it after a drift)
           const double cl[3] = {g.origin[0] + wx * g.w[0] + sx, g.origin[1] + wy * g.w[1] + sy,
@@ -272,13 +277,18 @@ __global__ __launch_bounds__(256) void overflow_kernel(GridDev g, SoA a, ListDev
           const double Rc = LOOP != LOOP_FORCE ? Hi
                             : ld.cell_R           ? fmax(Hi, (double)ld.cell_R[lin])
                                                   : st.reach;
-          if (gap2 > Rc * Rc * (1. + 1e-6) + 1e-300) continue;
-          for (int j = r.x + lane; j < r.y; j += 64) {
-            const double4 pj = a.pos[j];
-            T dx, dy, dz;
-            const T r2 = separation<T>(g, c, pi, pj, sx, sy, sz, dx, dy, dz);
-            if (st.accept(j, pj, r2)) st.interact(a, j, pj, dx, dy, dz, r2);
-          }
+          ok = gap2 <= Rc * Rc * (1. + 1e-6) + 1e-300;
+        }
+      }
+      for (unsigned long long m = __ballot(ok); m; m &= m - 1) {
+        const int b = __ffsll((long long)m) - 1;
+        const int j0 = __shfl(r.x, b), j1 = __shfl(r.y, b);
+        const double bx = __shfl(sx, b), by = __shfl(sy, b), bz = __shfl(sz, b);
+        for (int j = j0 + lane; j < j1; j += 64) {
+          const double4 pj = a.pos[j];
+          T dx, dy, dz;
+          const T r2 = separation<T>(g, c, pi, pj, bx, by, bz, dx, dy, dz);
+          if (st.accept(j, pj, r2)) st.interact(a, j, pj, dx, dy, dz, r2);
         }
       }
     }

@@ -755,8 +755,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2
     const int slot = maskq ? __popcll(ballA) + __popcll(ballM & below) : __popcll(ballA & below);
     const int posq = maskq ? totalA + incM - cM : incA - cA;
     // plain entries all / none / some truncated
-    const unsigned int bA = (unsigned int)ballA;
+    const unsigned int bA = (unsigned int)ballA, bM = (unsigned int)ballM;
     const int trA = (tmask & bA) == bA ? 1 : (tmask & bA) == 0u ? 0 : 2;
+    const bool trM = (tmask & bM) == bM;  // every masked entry truncated
     // per i: the entries it takes by P2P (inactive i: none)
     const unsigned int pmask = act ? ~mmask : 0u;
     for (int jb = 0; jb < total2; jb += kPPBatch) {
@@ -823,7 +824,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2
         else if (trA == 0) SWH_BATCH_PAIRS(false, 0, 0, tA);
         else SWH_BATCH_PAIRS(false, 2, 0, tA);
       }
-      if (tA < tn) SWH_BATCH_PAIRS(true, 2, tA, tn);
+      if (tA < tn) {
+        if (trM) SWH_BATCH_PAIRS(true, 1, tA, tn);
+        else SWH_BATCH_PAIRS(true, 2, tA, tn);
+      }
 #undef SWH_BATCH_PAIRS
     }
     qb += B;

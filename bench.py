@@ -557,11 +557,19 @@ def steady_state(sp, P, stream, torch, local, n_owned, args, skin=None, steps=No
     w = min(sp.info()["cell_width"])
     rebin = max(1, int(args.steady_rebin * w / (vmax * dt)))
 
+    per_step = []
+
     def run(count, ev=None):
         nd = nf = 0
         for k in range(steps):
             if k > 0 and k % rebin == 0:
                 sp.rebuild(P)
+            # hydro_reset_acceleration first: the drift's hydro_predict_extra
+            # then sees h_dt = 0 and keeps h (this loop has no ghost, so the
+            # force loop's h_dt comes from un-finalised densities and would
+            # blow h up on a clustered box); the force loop still starts
+            # from zeroed accumulators
+            sp.reset_acceleration(P)
             sp.drift(D, P)
             sp.init_parts(P)
             if ev:
@@ -569,8 +577,6 @@ def steady_state(sp, P, stream, torch, local, n_owned, args, skin=None, steps=No
             r = sp.density(P, count=count)
             if ev:
                 ev[k][1].record(stream)
-            sp.reset_acceleration(P)
-            if ev:
                 ev[k][2].record(stream)
             q = sp.force(P, count=count)
             if ev:
@@ -578,6 +584,7 @@ def steady_state(sp, P, stream, torch, local, n_owned, args, skin=None, steps=No
             if count:
                 nd += r
                 nf += q
+                per_step.append((int(r), int(q)))
         return nd, nf
 
     b0 = sp.info()["list_builds"]
@@ -601,6 +608,7 @@ def steady_state(sp, P, stream, torch, local, n_owned, args, skin=None, steps=No
             "rebin_every": rebin, "list_builds": int(builds),
             "steps_per_list_build": steps / max(1, builds),
             "interactions": nd + nf, "ms_per_step": el / steps * 1e3,
+            "interactions_first_last_step": [per_step[0], per_step[-1]] if per_step else None,
             "interactions_per_s": (nd + nf) / el,
             "density_ms": td, "force_ms": tf,
             "density_roofline_frac": b_d / (td * 1e-3) / HBM_PEAK}

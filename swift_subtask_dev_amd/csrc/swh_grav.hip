@@ -511,20 +511,23 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(MPOLE ? 3 :
 }
 
 // Small i-leaves (every leaf <= 64 gparts: a deep tree, cell_split_size 50)
-// with batched sources: one wave per i-leaf, LPI = 64 / (count rounded up to
-// a power of two) lanes per i-particle (up to 8), lane s of i taking tile
-// entries s, s + LPI, ... (the LPI partial sums combined by shuffles at the
-// end, so a 12-gpart leaf keeps 48 lanes busy instead of 12). The gparts of
+// with batched sources: one wave per i-leaf, LPI = floor(64 / count) lanes
+// per i-particle (up to 8), lane s of i taking tile entries s, s + LPI, ...
+// (the LPI partial sums combined by shuffles at the end, so a 12-gpart leaf
+// keeps 60 lanes busy instead of 12). The gparts of
 // up to 32 consecutive P-P entries (up to kPPBatch of them) are gathered into
 // the LDS tile at once: the chain of dependent loads (entry -> source leaf ->
 // its gparts) and the wave barriers are paid once per batch, not once per
 // source leaf (a cosmological tree has ~16 gparts per leaf and ~300 source
 // leaves per i-leaf under the adaptive MAC). Each entry's truncation and M2P
 // acceptance become bits (tmask: truncated entries; mmask, per i: the entries
-// whose multipole this i takes instead, m2p_accept as in mpole_mask); the
-// self term is removed by comparing gpart indices. Sources larger than the
-// tile (no-cache entries against a whole cell) are staged in tile-sized
-// chunks, every LDS index stays below kPPBatch.
+// whose multipole this i takes instead, m2p_accept as in mpole_mask, tested
+// one (i, entry) pair per lane); entries every active i takes through the
+// multipole are not staged, and the entries that need per-pair masks (a
+// mixed M2P decision, the i-leaf's own gparts: the self term, by tile
+// position) are staged at the tile's tail, so only the tail runs the masked
+// loop. Sources larger than the tile (no-cache entries against a whole cell)
+// are staged in tile-sized chunks, every LDS index stays below kPPBatch.
 //
 // Periodic boxes: the staging shifts each source gpart to its image nearest
 // the i-leaf's first gpart c. With e the i-leaf's extent around c, a staged

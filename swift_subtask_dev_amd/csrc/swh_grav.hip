@@ -640,6 +640,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2
   // the MAC's float view of i (gravity_cache_populate)
   const float4 pf = make_float4((float)pi.x, (float)pi.y, (float)pi.z, (float)pi.w);
   const float oag = MPOLE && act ? g.oagn[gi] : 0.f;
+  const unsigned long long actmask = __ballot(act);  // the lanes of active i's
   // the MAC's test lanes: lane = kk * count + ii tests i-slot ii (its data
   // from lane ii * lpi), epr entries per round; ibits = the lanes of ii
   const int nI = max(L.count, 1), epr = max(1, 64 / nI);
@@ -700,6 +701,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2
     const int B = fit ? __popcll(fit) : 1;
     const unsigned int tmask = (unsigned int)__ballot(lane < B && tr);
     unsigned int mmask = 0;  // the entries this i takes through their multipole
+    unsigned long long mine = 0;  // lane q < B: entry q's accepting lanes
     if (MPOLE) {
       // The MAC tests of the batch, one (i, entry) test per lane: the entries
       // with allow_mpole are listed in LDS (scratch over the tile, whose last
@@ -707,7 +709,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2
       // kk, kk + EPR, ...; the results gather by LDS OR into per-i entry masks
       // (mmask) and per-entry lane masks (mbits).
       const unsigned long long amb = __ballot(lane < B && am);
-      unsigned long long mine = 0;  // lane q < B: entry q's accepting lanes
       if (amb) {
         const int nq = __popcll(amb);
         wave_sync();
@@ -735,11 +736,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2
     // Entries every active i takes through the multipole are not staged at
     // all (the M2P acceptance is nearly always uniform over a small leaf);
     // only the mixed ones need per-pair masks.
-    unsigned int allm = act ? mmask : 0xffffffffu, anym = act ? mmask : 0u;
-    for (int o = 32; o > 0; o >>= 1) {
-      allm &= (unsigned int)__shfl_xor((int)allm, o);
-      anym |= (unsigned int)__shfl_xor((int)anym, o);
-    }
+    // (allm bit q: every active lane takes entry q's multipole; anym: some)
+    const unsigned long long mact = mine & actmask;
+    const unsigned int allm = (unsigned int)__ballot(mact == actmask);
+    const unsigned int anym = (unsigned int)__ballot(mact != 0ull);
     const bool inb = lane < B;
     const int cnt2 = (inb && ((allm >> lane) & 1u)) ? 0 : (inb ? cnt : 0);
     // Staging order: first the entries every i takes alike (plain), then the
@@ -750,10 +750,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void p2
     const bool ownq = cnt2 > 0 && jst < L.start + L.count && L.start < jst + cnt;
     const bool maskq = inb && (ownq || (((anym & ~allm) >> lane) & 1u));
     const int cA = maskq ? 0 : cnt2, cM = maskq ? cnt2 : 0;
-    const int incA = wave_incl_scan(cA), incM = wave_incl_scan(cM);
+    const unsigned long long ballA = __ballot(inb && !maskq), ballM = __ballot(maskq);
+    const int incA = wave_incl_scan(cA), incM = ballM ? wave_incl_scan(cM) : 0;
     const int totalA = __builtin_amdgcn_readlane(incA, 63);
     const int total2 = SWH_P2P_EXP == 2 ? 0 : totalA + __builtin_amdgcn_readlane(incM, 63);
-    const unsigned long long ballA = __ballot(inb && !maskq), ballM = __ballot(maskq);
     const unsigned long long below = (1ull << lane) - 1ull;
     const int slot = maskq ? __popcll(ballA) + __popcll(ballM & below) : __popcll(ballA & below);
     const int posq = maskq ? totalA + incM - cM : incA - cA;

@@ -26,6 +26,14 @@ def oracle64():
 
 @pytest.fixture(scope="session")
 def gpu_ctx():
+    # torch's HIP runtime first, as bench.py does: a test that shares device
+    # buffers through torch then finds the device whatever ran before it
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
     from swift_subtask_dev_amd import lib
     ctx = lib.Context(0, "f64")
     yield ctx

@@ -491,6 +491,46 @@ def test_clustered_adaptive_grid_loops_vs_f64(gpu_ctx, clustered_state, capacity
     assert info["cdim"][0] > 1.0 / (float(parts["h"].max()) * 1.825742) * 1.3
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("bins", ["mixed", "one_low"])
+def test_force_min_ngb_time_bin(gpu_ctx, clustered_state, bins):
+    """The time-bin limiter of the force loop (runner_iact_nonsym_timebin):
+    mixed bins 3/4/6 with random initial minima (some under every bin
+    present), and one particle alone in bin 2 among bin-5 particles:
+    min_ngb_time_bin equal to the f64 oracle's, exact counts."""
+    from swift_subtask_dev_amd import lib
+    parts, _ = clustered_state
+    P = abi.default_hydro_params(max_active_bin=abi.NUM_TIME_BINS)
+    rng = np.random.Generator(np.random.PCG64(2024 + len(bins)))
+    n = len(parts)
+    base = abi.copy_parts(parts)
+    base["time_bin"] = rng.choice([3, 4, 6], n) if bins == "mixed" else 5
+    if bins == "one_low":
+        base["time_bin"][n // 2] = 2
+    base["time_bin"][rng.choice(n, 30, replace=False)] = abi.TIME_BIN_INHIBITED
+    # the initial minima stay (no reset_acceleration: the force adds into
+    # the zeroed accumulators of the upload)
+    base["min_ngb_time_bin"] = rng.choice([2, 3, 5, abi.NUM_TIME_BINS + 1], n)
+    base["a_hydro"] = 0
+    base["u_dt"] = 0
+    base["h_dt"] = 0
+    gf = abi.copy_parts(base)
+    sp = lib.HydroSpace(gpu_ctx)
+    sp.upload(gf)
+    sp.rebuild(P)
+    nf = sp.force(P)
+    sp.download(gf, abi.FIELDS_FORCE)
+    sp.close()
+    of = abi.copy_parts(base)
+    assert nf == O.fn("f64", "box_force")(of.ctypes.data, len(of), C.byref(P), None)
+    a, b = _by_id(gf), _by_id(of)
+    live = a["time_bin"] != abi.TIME_BIN_INHIBITED
+    assert np.array_equal(a["min_ngb_time_bin"][live], b["min_ngb_time_bin"][live])
+    assert_close(a["a_hydro"][live], b["a_hydro"][live], 5e-5, 1e-4, "a_hydro")
+    if bins == "one_low":  # the bin-2 particle's neighbours took its bin
+        assert (b["min_ngb_time_bin"][live] == 2).sum() > 10
+
+
 # ---------------------------------------------------------------------------
 # Per-task force / gradient through the adapter on prepared inputs
 # ---------------------------------------------------------------------------

@@ -126,8 +126,12 @@ __global__ void cell_reach_kernel(const double4* __restrict__ pos, const int* __
   atomicMax(&cell_R[lin], __float_as_uint((float)(pos[j].w * (double)gs1) * 1.0000005f));
 }
 
+// Candidates per lane per staging pass. Two: a 256-slot region then takes
+// two passes before its consume (four filled it in one pass, so every pass
+// consumed a part-full region); EAGLE's density loop 1.65 -> 1.60 ms, Sedov
+// unchanged (profiles/r05y_stage_units_ab.txt).
 #ifndef SWH_STAGE_U
-#define SWH_STAGE_U 4
+#define SWH_STAGE_U 2
 #endif
 
 // A build wave's LDS: its staged candidate region and its i's pending hits.

@@ -991,13 +991,15 @@ swh_status swh_space_rebuild(swh_space* s, const swh_hydro_params* P, double min
   // (clustered boxes) cells sized by H_max would hold whole clumps: size them
   // by the typical H instead (the geometric mean, at least H_max / 6: on the
   // EAGLE stand-in 0.75 x and H_max / 8 enumerated more cells per group and
-  // took 1.72 against 1.66 ms per density loop);
+  // took 1.72 against 1.66 ms per density loop), divided by 1.1 since the
+  // build stages two candidates per lane per pass (EAGLE stand-in: cdim 86 ->
+  // 94, density loop 1.59 -> 1.45 ms; profiles/r05z5_eagle_cell_sweep.txt);
   // the large-h particles then reach over more cells, and the list build
   // prunes cells by their own maximum H (SWIFT's per-cell h_max in DOPAIR2,
   // runner_doiact_functions_hydro.h:1424-1530).
   const double h_geo = std::exp(bb[7] / (double)n) * (double)kGamma;
   g.adaptive = g.hmax > 1.5 * h_geo;
-  const double h_cell = g.adaptive ? std::max(h_geo, g.hmax / 6.) : g.hmax;
+  const double h_cell = g.adaptive ? std::max(h_geo, g.hmax / 6.) / 1.1 : g.hmax;
   double width = min_cell_width > 0 ? min_cell_width : h_cell / cells_per_h;
   if (!(width > 0)) width = 1.0;
   int64_t total = 1;

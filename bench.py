@@ -188,7 +188,7 @@ def cpu_worker_main(kind, path, meta):
         G = abi.GravParams.from_buffer_copy(z["G"].tobytes())
         g = z["gparts"].view(abi.GPART_DTYPE).reshape(-1).copy()
         cells, tops, pc = z["cells"].view(abi.GCELL_DTYPE), z["tops"], z["pairs"]
-        stats = (C.c_longlong * 5)()
+        stats = (C.c_longlong * 6)()
         t0 = time.perf_counter()
         O.fn("f32", "grav_tree")(g.ctypes.data, len(g), cells.ctypes.data, len(cells),
                                  tops.ctypes.data, len(tops), pc.ctypes.data, len(pc) // 2,
@@ -704,6 +704,7 @@ def run_grav(args, ctx, rank, world, dist, torch):
         if tr:
             out["roofline"]["traffic"] = tr.get("bytes_per_launch")
             out["roofline"]["traffic_source"] = tr.get("source")
+            out["roofline"]["traffic_commit"] = tr.get("commit")
         if world == 1 and not args.no_cpu_baseline:
             try:
                 # bounded sample: the first 1% of the i-leaves with their full
@@ -946,6 +947,7 @@ def run_cosmo(args, ctx, rank, world, dist, torch):
             if tr:
                 out["roofline"]["traffic"] = tr.get("bytes_per_launch")
                 out["roofline"]["traffic_source"] = tr.get("source")
+                out["roofline"]["traffic_commit"] = tr.get("commit")
         if world == 1 and not args.no_cpu_baseline:
             try:
                 threads = cpu_share_threads()
@@ -980,6 +982,44 @@ def run_cosmo(args, ctx, rank, world, dist, torch):
     gs.close()
 
 
+# BASELINE.json configs 3-5, run after the headline by the default 1-GPU
+# bench (bench.py --workload ...): each child prints one JSON line with its
+# own value, ms_per_step, roofline (the PMC traffic named by commit) and
+# cpu_baseline
+OTHER_CONFIGS = {
+    "config3_eagle": ["--workload", "eagle"],
+    "config4_grav256": ["--workload", "grav", "--n", "256"],
+    "config5_cosmo": ["--workload", "cosmo"],
+}
+
+
+def other_configs(args):
+    import subprocess
+
+    res = {}
+    for name, extra in OTHER_CONFIGS.items():
+        cmd = [sys.executable, str(Path(__file__).resolve()), *extra, "--steps", str(args.steps),
+               "--warmup", str(args.warmup), "--no-configs"]
+        if args.no_cpu_baseline:
+            cmd.append("--no-cpu-baseline")
+        t0 = time.perf_counter()
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=400)
+            sys.stderr.write(r.stderr[-4000:])
+            lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            if r.returncode != 0 or not lines:
+                res[name] = {"error": f"exit {r.returncode}", "stderr_tail": r.stderr[-800:]}
+            else:
+                res[name] = json.loads(lines[-1])
+        except Exception as e:  # report, never fake
+            res[name] = {"error": str(e)[-300:]}
+        res[name]["command"] = " ".join(["python", "bench.py", *cmd[2:]])
+        res[name]["wall_s"] = time.perf_counter() - t0
+        log(f"{name}: {res[name].get('value')} {res[name].get('unit', '')} "
+            f"({res[name]['wall_s']:.0f} s)")
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1011,6 +1051,9 @@ def main():
                     help="steady state: displacement of the fastest particle per step / h")
     ap.add_argument("--no-breakdown", action="store_true",
                     help="skip the untimed full-step breakdown (drift, rebuild, chain)")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the BASELINE configs 3-5 lines the default 1-GPU run appends "
+                         "(each a child bench.py run, untimed by the headline)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong: the 128^3 box split over the GPUs (the metric); "
                          "weak: one 128^3 box per GPU")
@@ -1295,6 +1338,7 @@ def main():
                 # committed profile named here (not re-measured by this run)
                 "traffic_source": (traffic.get("source", "profiles/traffic_density.json")
                                    if traffic else None),
+                "traffic_commit": traffic.get("commit") if traffic else None,
                 "bytes_model": f"N*(27*{S_IN_DENSITY}+{S_OUT_DENSITY}) = {b_dens} B per launch",
                 "launch_ms": td * 1e3,
             },
@@ -1375,9 +1419,15 @@ def main():
                     raw, chain_gpu, chain, P, args.workload)
             except Exception as e:  # report, never fake
                 log(f"chain parity check failed: {e}")
-        print(json.dumps(out), flush=True)
     sp.close()
     ctx.close()
+    if rank == 0:
+        if (world == 1 and not eagle and strong and not args.no_configs and args.n == 128
+                and args.diag_mode == 0):
+            # the other BASELINE configs, each its own bench.py run after this
+            # process has released its GPU memory (untimed by the headline)
+            out["configs"] = other_configs(args)
+        print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
 

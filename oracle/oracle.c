@@ -2974,13 +2974,14 @@ static long long grav_pp(struct gpart *gi, int ni, const struct gpart *gj, int n
  * `real` and is written back once (the per-task float write-back of
  * gravity_cache_write_back would add float rounding of every partial sum).
  * Positions: direct differences, nearest image when periodic. */
-API long long PFX(grav_pp_leaves)(struct gpart *g, const int *leaves, int nleaves,
-                                  const int *off, const int *pairs,
-                                  const struct oracle_grav_params *G,
-                                  const struct oracle_multipole *mp, long long *n_m2p) {
-  long long total = 0, total_m2p = 0;
+static long long PFX(grav_pp_leaves_impl)(struct gpart *g, const int *leaves, int nleaves,
+                                          const int *off, const int *pairs,
+                                          const struct oracle_grav_params *G,
+                                          const struct oracle_multipole *mp, long long *n_m2p,
+                                          long long *n_trunc) {
+  long long total = 0, total_m2p = 0, total_trunc = 0;
   const real dim[3] = {(real)G->dim[0], (real)G->dim[1], (real)G->dim[2]};
-#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total, total_m2p)
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total, total_m2p, total_trunc)
   for (int l = 0; l < nleaves; l++) {
     /* a "leaf" without entries is left alone: in a tree's cell list the
      * split cells overlap their progeny's ranges, and another thread's
@@ -3044,6 +3045,7 @@ API long long PFX(grav_pp_leaves)(struct gpart *g, const int *leaves, int nleave
           a_z += f_ij * dz;
           pot += pot_ij;
           total++;
+          total_trunc += trunc ? 1 : 0;
         }
       }
       gp->a_grav[0] += (float)a_x;
@@ -3053,7 +3055,15 @@ API long long PFX(grav_pp_leaves)(struct gpart *g, const int *leaves, int nleave
     }
   }
   if (n_m2p) *n_m2p = total_m2p;
+  if (n_trunc) *n_trunc = total_trunc;
   return total;
+}
+
+API long long PFX(grav_pp_leaves)(struct gpart *g, const int *leaves, int nleaves,
+                                  const int *off, const int *pairs,
+                                  const struct oracle_grav_params *G,
+                                  const struct oracle_multipole *mp, long long *n_m2p) {
+  return PFX(grav_pp_leaves_impl)(g, leaves, nleaves, off, pairs, G, mp, n_m2p, NULL);
 }
 
 /* runner_doself_grav_pp (runner_doiact_grav.c:1788-1871): cache frame =
@@ -3429,8 +3439,9 @@ API void PFX(grav_tree_owned)(struct gpart *g, int n, const struct oracle_gcell 
     e[1] = w.pp[4 * q + 2];
     e[2] = w.pp[4 * q + 3];
   }
-  long long n_m2p = 0;
-  const long long n_pp = PFX(grav_pp_leaves)(g, leaves, ncells, off, pairs, G, mp, &n_m2p);
+  long long n_m2p = 0, n_trunc = 0;
+  const long long n_pp =
+      PFX(grav_pp_leaves_impl)(g, leaves, ncells, off, pairs, G, mp, &n_m2p, &n_trunc);
   /* M2L (field tensor at the target's CoM) */
   real *F = (real *)calloc((size_t)ncells * 35, sizeof(real));
   /* by target (a stable counting sort: each target sums its sources in walk
@@ -3541,6 +3552,7 @@ API void PFX(grav_tree_owned)(struct gpart *g, int n, const struct oracle_gcell 
     stats[2] = w.nmm;
     stats[3] = w.npp;
     stats[4] = w.skipped;
+    stats[5] = n_trunc; /* P2P pairs of truncated entries (swh_grav_tree_stats.n_pp_truncated) */
   }
   free(F); free(moff); free(mord); free(depth); free(fill); free(pairs); free(off); free(leaves);
   free(w.pp); free(w.mm); free(parent); free(act); free(mp);

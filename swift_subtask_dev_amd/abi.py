@@ -96,6 +96,9 @@ XPART_DTYPE = np.dtype(
     }
 )
 
+# include/swifthip.h SWH_ABI_VERSION: the ctypes layouts below are written for it
+ABI_VERSION = 10
+
 NUM_TIME_BINS = 56  # src/timeline.h:36
 TIME_BIN_INHIBITED = NUM_TIME_BINS + 2
 DEFAULT_LIST_SKIN = 0.01  # swifthip.h SWH_DEFAULT_LIST_SKIN (swh_tuning.list_skin)

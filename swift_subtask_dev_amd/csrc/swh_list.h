@@ -391,6 +391,8 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
                                            unsigned long long* counter, int diag, LDS& L,
                                            CellTab& T) {
   constexpr int kStageU = LDS::kStageU;
+  // one int8 start mark per candidate of a staging pass
+  static_assert(64 * kStageU <= (int)sizeof(CellTab::mark), "a pass's marks must fit CellTab::mark");
   const int lane = threadIdx.x & 63;
   const int il = lane / LPI, s = lane % LPI;
   const int2 gr = gid < ngroups ? groups[gid] : make_int2(0, 0);
@@ -507,7 +509,7 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
       int cur = -1;  // the cell of the last candidate of the previous pass
       for (int base = 0; base < total; base += 64 * kStageU) {
         if (nst > LDS::kRegion - 64 * kStageU) {  // no room for this pass: consume the region
-          list_pad(L, nst);
+          list_pad<LPI>(L, nst);
           wave_sync();
           if (diag != 1) {
             if (wrap)
@@ -593,7 +595,7 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
       }
       wave_sync();  // the next batch rewrites the cell table
     }
-    list_pad(L, nst);
+    list_pad<LPI>(L, nst);
     wave_sync();
     if (diag != 1 && nst > 0) {
       if (wrap)

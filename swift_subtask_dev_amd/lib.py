@@ -167,6 +167,12 @@ def load(kernel: str = "cubic-spline") -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    ver = lib.swh_abi_version()
+    if ver != abi.ABI_VERSION:
+        # a struct such as swh_grav_tree_stats grew between versions: a mismatched
+        # library would write past (or leave unset) the ctypes layouts' fields
+        raise ImportError(f"{path} has C ABI v{ver}; these bindings are written for "
+                          f"v{abi.ABI_VERSION} (rebuild it)")
     got = lib.swh_kernel_name().decode()
     if got != kernel:
         raise ImportError(f"{path} was built for the {got} kernel, not {kernel}")

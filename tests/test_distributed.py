@@ -226,8 +226,10 @@ def _compare_step(out, ref, rtol):
         assert err <= rtol, f"{k}: max err {err:.3e} (scale {scale:.3e})"
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_block_decomposition_full_step_matches_single_domain(world):
+    """world 8 is the 2x2x2 split of the metric's 8-GPU line: every rank has
+    7 peers, the corner and edge halos included."""
     from swift_subtask_dev_amd import abi, ics
 
     n = 16

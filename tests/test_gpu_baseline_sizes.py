@@ -115,9 +115,10 @@ def cosmo_volume(gpu_ctx):
     return gas, gp, P
 
 
-def _exchange_rho(spaces, plans):
-    """One point-to-point halo refresh of rho between logical ranks sharing a
-    device (what decomp.exchange does across processes)."""
+def _exchange_rho(spaces, plans, fields=abi.HALO_RHO):
+    """One point-to-point halo refresh (rho by default) between logical ranks
+    sharing a device (what decomp.exchange does across processes). Returns
+    the records moved per rank (sent, received)."""
     import torch
     dev = torch.device("cuda", 0)
     recs = {}
@@ -135,17 +136,22 @@ def _exchange_rho(spaces, plans):
             buf = recs[(r, q)]
             assert len(buf) == len(idx) * abi.HALO_RECORD_FLOATS
             torch.cuda.synchronize()
-            sp.unpack_halo(ti.data_ptr(), len(idx), buf.data_ptr(), abi.HALO_RHO)
+            sp.unpack_halo(ti.data_ptr(), len(idx), buf.data_ptr(), fields)
             sp.sync()
+    return [(sum(len(v) for v in p.send.values()), sum(len(v) for v in p.recv_idx.values()))
+            for p in plans]
 
 
-def test_cosmo_volume_hydro_blocks_two_ranks_vs_f64(gpu_ctx, cosmo_volume):
-    """bench.py --workload cosmo --gpus 2's hydro step on the blocks: density,
+@pytest.mark.parametrize("world", [2, 8])
+def test_cosmo_volume_hydro_blocks_ranks_vs_f64(gpu_ctx, cosmo_volume, world):
+    """bench.py --workload cosmo --gpus N's hydro step on the blocks: density,
     the rho refresh, force; the union of the owned outputs vs the oracle's
-    single-domain loops on the same converged gas."""
+    single-domain loops on the same converged gas. world 8 is the 2x2x2 grid
+    of the metric's 8-GPU line: every rank receives its corner and edge halos
+    from 7 peers."""
     from swift_subtask_dev_amd import lib
     gas, _, P = cosmo_volume
-    world, box = 2, (1.0, 1.0, 1.0)
+    box = (1.0, 1.0, 1.0)
     reach = 1.01 * KERNEL_GAMMA * float(gas["h"].max())  # bench.py run_cosmo's halo reach
     plans = [decomp.HaloPlan(gas["x"], box, world, r, reach) for r in range(world)]
     locs = [p.local_set(gas) for p in plans]
@@ -163,7 +169,9 @@ def test_cosmo_volume_hydro_blocks_two_ranks_vs_f64(gpu_ctx, cosmo_volume):
     dens = [abi.copy_parts(loc) for loc in locs]
     for sp, d in zip(spaces, dens):
         sp.download(d, abi.FIELDS_DENSITY)
-    _exchange_rho(spaces, plans)
+    moved = _exchange_rho(spaces, plans)
+    if world == 8:
+        assert all(len(p.peers()) == 7 for p in plans)
     for sp, loc in zip(spaces, locs):
         sp.reset_acceleration(P)
         nf.append(sp.force(P))
@@ -184,7 +192,9 @@ def test_cosmo_volume_hydro_blocks_two_ranks_vs_f64(gpu_ctx, cosmo_volume):
     of["min_ngb_time_bin"] = abi.NUM_TIME_BINS + 1
     n_of = O.fn("f64", "box_force")(of.ctypes.data, len(of), C.byref(P), None)
     print(f"\ncosmo blocks: density {nd} (oracle {n_od}), force {nf} (oracle {n_of}), "
-          f"owned {[p.n_owned for p in plans]}, halo {[p.n_local - p.n_owned for p in plans]}")
+          f"owned {[p.n_owned for p in plans]}, halo {[p.n_local - p.n_owned for p in plans]}, "
+          f"records sent/received per rank {moved} "
+          f"({abi.HALO_RECORD_FLOATS * 4} B each)")
     assert sum(nd) == n_od and sum(nf) == n_of
     assert_hydro_close(_by_id(union_d), _by_id(od), TIGHT, "cosmo blocks density")
     u = _by_id(union)
@@ -194,15 +204,16 @@ def test_cosmo_volume_hydro_blocks_two_ranks_vs_f64(gpu_ctx, cosmo_volume):
     assert np.array_equal(u["min_ngb_time_bin"], ofi["min_ngb_time_bin"])
 
 
-def test_cosmo_volume_gravity_owned_subtrees_two_ranks_vs_f64(gpu_ctx, cosmo_volume):
-    """The sharded gravity of the same step: the two ranks' owned subtrees
+@pytest.mark.parametrize("world", [2, 8])
+def test_cosmo_volume_gravity_owned_subtrees_ranks_vs_f64(gpu_ctx, cosmo_volume, world):
+    """The sharded gravity of the same step: the ranks' owned subtrees
     (adaptive MAC, r_cut_max 4.5 r_s) on the 64^3 + 64^3 tree, each with the
     PM mesh of its replicated gparts; the union equals the single-domain
-    step."""
+    step (world 8: eight owned subtree sets of the 2x2x2 block grid)."""
     from swift_subtask_dev_amd import lib
     from test_gpu_cosmo_volume import N_MESH, R_S, _oracle_gravity, grav_params
     _, gp, _ = cosmo_volume
-    world, box = 2, (1.0, 1.0, 1.0)
+    box = (1.0, 1.0, 1.0)
     g, cells, tops = ics.gravity_tree(gp, 8, split_size=50)
     pairs = ics.top_level_pairs(tops)
     G = grav_params(adaptive=False)
@@ -226,7 +237,8 @@ def test_cosmo_volume_gravity_owned_subtrees_two_ranks_vs_f64(gpu_ctx, cosmo_vol
     G = grav_params(adaptive=True)
     ref, st_ref = run(None)
     owned = [decomp.gravity_owned_cells(cells, tops, r, world, box) for r in range(world)]
-    assert np.array_equal(owned[0] + owned[1], np.ones(len(cells)))
+    assert np.array_equal(np.sum(owned, axis=0), np.ones(len(cells)))
+    assert all(o.any() for o in owned)
     parts, stats = [], []
     for r in range(world):
         out, st = run(owned[r])

@@ -77,7 +77,7 @@ def _gpu_gravity(ctx, g, cells, tops, pairs, G):
 
 def _oracle_gravity(g, cells, tops, pairs, G):
     o = abi.copy_parts(g)
-    st = np.zeros(5, dtype=np.int64)
+    st = np.zeros(6, dtype=np.int64)
     O.fn("f64", "grav_tree")(o.ctypes.data, len(o), cells.ctypes.data, len(cells),
                              tops.ctypes.data, len(tops), pairs.ctypes.data, len(pairs),
                              C.byref(G), st.ctypes.data, None)
@@ -88,7 +88,7 @@ def _oracle_gravity(g, cells, tops, pairs, G):
 
 def _compare_gravity(gg, go, st_g, st_o):
     assert [st_g["n_pp"], st_g["n_m2p"], st_g["n_m2l"], st_g["n_pp_tasks"],
-            st_g["n_skipped"]] == list(st_o), (st_g, st_o)
+            st_g["n_skipped"], st_g["n_pp_truncated"]] == list(st_o), (st_g, st_o)
     a_o = go["a_grav"].astype(np.float64)
     scale = np.linalg.norm(a_o, axis=1)
     e = np.linalg.norm(gg["a_grav"].astype(np.float64) - a_o, axis=1) / np.maximum(scale, 1e-30)

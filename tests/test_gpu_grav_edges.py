@@ -93,12 +93,13 @@ def test_tree_no_cache_source_larger_than_tile(gpu_ctx, theta, periodic):
     st = gs.tree(G, tops, pairs)
     gs.download(gg)
     gs.close()
-    so = np.zeros(5, dtype=np.int64)
+    so = np.zeros(6, dtype=np.int64)
     ft = np.zeros((len(cells), 35), dtype=np.float32)
     O.fn("f64", "grav_tree")(go.ctypes.data, len(go), cells.ctypes.data, len(cells),
                              tops.ctypes.data, len(tops), pairs.ctypes.data, len(pairs),
                              C.byref(G), so.ctypes.data, ft.ctypes.data)
-    assert [st["n_pp"], st["n_m2p"], st["n_m2l"], st["n_pp_tasks"], st["n_skipped"]] == list(so)
+    assert [st["n_pp"], st["n_m2p"], st["n_m2l"], st["n_pp_tasks"], st["n_skipped"],
+            st["n_pp_truncated"]] == list(so)
     # the lonely gpart's no-cache entry took every gpart of the clump's cell
     lonely = int(np.argmin(np.abs(g["x"][:, 0] - 0.75) + np.abs(g["x"][:, 1] - 0.25)
                            + np.abs(g["x"][:, 2] - 0.25)))

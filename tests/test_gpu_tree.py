@@ -38,7 +38,7 @@ def clumpy_box(n=16, seed=3):
 
 
 def run_oracle(g, cells, tops, pairs, G):
-    st = np.zeros(5, dtype=np.int64)
+    st = np.zeros(6, dtype=np.int64)
     ft = np.zeros((len(cells), 35), dtype=np.float32)
     O.fn("f64", "grav_tree")(g.ctypes.data, len(g), cells.ctypes.data, len(cells),
                              tops.ctypes.data, len(tops), pairs.ctypes.data, len(pairs),
@@ -223,6 +223,9 @@ def test_tree_truncated_pair_count(gpu_ctx):
         st = run_gpu(gpu_ctx, gg, cells, tops, pairs, G)[0]
         so, _ = run_oracle(go, cells, tops, pairs, G)
         assert st["n_pp"] == so[0] and st["n_pp"] > 0, (k, st["n_pp"], so[0])
+        # the exact count of truncated pairs (the cosmo line prices them at 43
+        # flops): the oracle counts the pairs of its truncated entries
+        assert st["n_pp_truncated"] == so[5], (k, st["n_pp_truncated"], so[5])
         got[k] = (st["n_pp_truncated"], st["n_pp"])
     print(f"\n{got}")
     assert got["all"][0] == got["all"][1]

@@ -46,7 +46,7 @@ def _owned_gparts(cells, owned):
 
 
 def _oracle(g, cells, tops, pairs, G, owned=None):
-    st = np.zeros(5, dtype=np.int64)
+    st = np.zeros(6, dtype=np.int64)
     own = owned.ctypes.data if owned is not None else None
     O.fn("f64", "grav_tree_owned")(g.ctypes.data, len(g), cells.ctypes.data, len(cells),
                                    np.ascontiguousarray(tops, dtype=np.int32).ctypes.data,
@@ -81,9 +81,10 @@ def _check_union(out, ref, ref_stats, ncells, n):
         assert sum(r["stats"][k] for r in out) == ref_stats[k], k
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_tree_gravity_matches_single_domain(world):
-    """gloo world 2 / 4 on the CPU, the oracle standing in for the device."""
+    """gloo world 2 / 4 / 8 on the CPU, the oracle standing in for the device
+    (8: the 2x2x2 block grid of config 5 on 8 GPUs)."""
     g, cells, tops, pairs, G = _case()
     st = _oracle(g, cells, tops, pairs, G)
     assert st[2] > 0 and st[1] > 0  # M2L and M2P both in play
@@ -125,7 +126,7 @@ def _gpu_owned(ctx, g, cells, tops, pairs, G, owned):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_gpu_sharded_tree_gravity_matches_single_domain(gpu_ctx, world, monkeypatch):
     """Each rank's ownership run in turn on cuda:0: the union equals the
     library's single-domain step bit for bit (the device and host walks),

@@ -636,7 +636,7 @@ def _tree_params(periodic=False, theta=0.5, r_cut_max=0.0, r_s_inv=0.0, r_cut_mi
 
 def oracle_tree(g, cells, tops, G, pairs=None):
     pairs = ics.top_level_pairs(tops) if pairs is None else pairs
-    stats = np.zeros(5, dtype=np.int64)
+    stats = np.zeros(6, dtype=np.int64)
     ft = np.zeros((len(cells), 35), dtype=np.float32)
     O.fn("f64", "grav_tree")(g.ctypes.data, len(g), cells.ctypes.data, len(cells),
                              tops.ctypes.data, len(tops), pairs.ctypes.data, len(pairs),

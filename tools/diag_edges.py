@@ -28,7 +28,7 @@ for rep in range(3):
     gs.close()
     res.append((gg, st))
 go = abi.copy_parts(g)
-so = np.zeros(5, dtype=np.int64)
+so = np.zeros(6, dtype=np.int64)
 O.fn("f64", "grav_tree")(go.ctypes.data, len(go), cells.ctypes.data, len(cells), tops.ctypes.data,
                          len(tops), pairs.ctypes.data, len(pairs), C.byref(G), so.ctypes.data, None)
 print("oracle stats", list(so))

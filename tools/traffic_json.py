@@ -12,6 +12,21 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
+
+
+def measured_commit():
+    """The commit whose kernels the PMC passes ran (the tree gpurun shipped
+    is HEAD when this runs right after the call; '+dirty' if csrc/ differs)."""
+    import subprocess
+    try:
+        c = subprocess.run(["git", "-C", str(ROOT), "rev-parse", "--short", "HEAD"],
+                           capture_output=True, text=True).stdout.strip()
+        d = subprocess.run(["git", "-C", str(ROOT), "status", "--porcelain", "--",
+                            "swift_subtask_dev_amd/csrc"], capture_output=True, text=True).stdout
+        return c + ("+dirty" if d.strip() else "")
+    except OSError:
+        return None
+
 tag, workload, sub = sys.argv[1:4]
 vals = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -22,7 +37,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
     vals[c] = statistics.median(v)
 rd = 2.0 * vals["FETCH_SIZE"] * 1024
 wr = vals["WRITE_SIZE"] * 1024
-out = {"source": f"profiles/{tag} PMC passes (rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE, "
+out = {"commit": measured_commit(), "source": f"profiles/{tag} PMC passes (rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE, "
                  "kernel-trace only; FETCH_SIZE x2 gfx950 correction; median over dispatches)",
        "kernel": sub, "read_bytes": rd, "write_bytes": wr, "bytes_per_launch": rd + wr}
 (ROOT / "profiles" / f"traffic_{workload}.json").write_text(json.dumps(out, indent=1) + "\n")

@@ -17,6 +17,21 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
+
+
+def measured_commit():
+    """The commit whose kernels the PMC passes ran (the tree gpurun shipped
+    is HEAD when this runs right after the call; '+dirty' if csrc/ differs)."""
+    import subprocess
+    try:
+        c = subprocess.run(["git", "-C", str(ROOT), "rev-parse", "--short", "HEAD"],
+                           capture_output=True, text=True).stdout.strip()
+        d = subprocess.run(["git", "-C", str(ROOT), "status", "--porcelain", "--",
+                            "swift_subtask_dev_amd/csrc"], capture_output=True, text=True).stdout
+        return c + ("+dirty" if d.strip() else "")
+    except OSError:
+        return None
+
 DENSITY = ["swh::posf_kernel", "swh::group_box_kernel", "swh::group_prep_kernel", "swh::list_build_kernel",
            "void swh::density_walk_kernel<double>", "void swh::overflow_kernel<0, double>"]
 MAIN_OVF_GRID = 64 * 256
@@ -42,7 +57,7 @@ for k, m in sorted(med.items()):
     wr = m.get("WRITE_SIZE", 0.0) * 1024
     kern[k] = {"read_bytes": rd, "write_bytes": wr, "bytes_per_launch": rd + wr}
 dens = [k for k in DENSITY if k in kern]
-out = {"source": f"profiles/{tag} PMC passes (rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE, "
+out = {"commit": measured_commit(), "source": f"profiles/{tag} PMC passes (rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE, "
                  "kernel-trace only; FETCH_SIZE x2 gfx950 correction; median over dispatches; "
                  "overflow kernels at the main loops' grid)",
        "kernels": kern, "density_kernels": dens,

@@ -157,9 +157,14 @@ struct hydro_props {
   struct diffusion_global_data diffusion;
 };
 
+struct cell;
 struct space {
   int periodic;
   double dim[3];
+  /* the top-level grid (src/space.h): runner_do_grav_long_range's loop */
+  struct cell *cells_top;
+  int *cells_with_particles_top;
+  int nr_cells_with_particles;
 };
 
 struct pm_mesh {
@@ -264,6 +269,7 @@ struct cell {
     struct gravity_tensors *multipole;
     integertime_t ti_end_min;
     integertime_t ti_old_part;
+    integertime_t ti_old_multipole;
   } grav;
 };
 

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define SWH_ABI_VERSION 10
+#define SWH_ABI_VERSION 11
 
 #if defined(__GNUC__)
 #define SWH_API __attribute__((visibility("default")))
@@ -520,6 +520,25 @@ SWH_API swh_status swh_gspace_set_multipoles(swh_gspace *g, const swh_multipole 
  * potentials, swh_gspace_field_tensors returns the pushed-down tensors. */
 SWH_API swh_status swh_gspace_grav_down(swh_gspace *g, const swh_grav_params *G,
                                         const float *fields);
+/* M-M interactions of explicit pairs of the caller's multipoles (ABI v11):
+ * SWIFT's M-M tasks outside the recursive walk -- runner_dopair_grav_mm_progenies
+ * (src/runner_doiact_grav.c:2067-2093) and runner_do_grav_long_range
+ * (2441-2530). pairs[3k], pairs[3k+1], pairs[3k+2] = target, source,
+ * symmetric: the target's field tensor (at its CoM) receives the source's
+ * M2L, with gravity_M2L_symmetric's softening (the larger max_softening of
+ * the two) when symmetric != 0, else gravity_M2L_nonsym's (the source's);
+ * a symmetric M-M pair is given as two entries. fields: nmp x 35 floats
+ * (struct grav_tensor's F order), overwritten: each target's sums, zero for
+ * the multipoles that receive nothing. Thread-safe like the per-task calls. */
+SWH_API swh_status swh_grav_m2l_pairs(swh_context *ctx, const swh_grav_params *G,
+                                      const swh_multipole *mp, int32_t nmp,
+                                      const int32_t *pairs, int32_t npairs, float *fields);
+/* gravity_M2L_accept_symmetric (src/multipole_accept.h:78-205) of A and B at
+ * squared CoM distance r2, in the reference's float arithmetic -- the MAC the
+ * tree walk uses. For cell_can_use_pair_mm's rebuild-time decision
+ * (src/cell.c:1420-1460) pass CoM_rebuild / r_max_rebuild. Returns 1 / 0. */
+SWH_API int swh_grav_m2l_accept(const swh_grav_params *G, const swh_multipole *A,
+                                const swh_multipole *B, double r2);
 SWH_API swh_status swh_gspace_sync(swh_gspace *g);
 /* Without waiting: SWH_OK when the gspace's stream is idle, SWH_BUSY otherwise. */
 SWH_API swh_status swh_gspace_query(swh_gspace *g);

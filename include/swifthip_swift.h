@@ -19,6 +19,8 @@
  *   runner_doself_recursive_grav,       src/runner_doiact_grav.h:33-37  (runner_doiact_grav.c:2386,
  *   runner_dopair_recursive_grav,                                        2208, 65)
  *   runner_do_grav_down                 src/runner_doiact_grav.h:28
+ *   runner_dopair_grav_mm_progenies     src/runner_doiact_grav.h:39-41  (runner_doiact_grav.c:2067)
+ *   runner_do_grav_long_range           src/runner_doiact_grav.h:43     (runner_doiact_grav.c:2441)
  *
  * Inside a SWIFT build these are compiled against SWIFT's headers and linked
  * instead of the CPU template instances; in this repo they are
@@ -97,6 +99,17 @@ SWHS_API void runner_dopair_recursive_grav(struct runner *r, struct cell *ci, st
 SWHS_API void runner_do_grav_down(struct runner *r, struct cell *c, int timer);
 SWHS_API void runner_dopair_grav_pp(struct runner *r, struct cell *ci, struct cell *cj,
                                     const int symmetric, const int allow_mpole);
+/* The M-M tasks outside the recursive walk (src/runner_doiact_grav.h:39-43):
+ * the progeny pairs flagged well separated at the last rebuild (task flags,
+ * bit 8 i + j), and one cell against every far top-level cell
+ * (cell_can_use_pair_mm on the rebuild data, r_cut_max skip). The M2L sums
+ * are added into c->grav.multipole->pot (interacted = 1) on the GPU's
+ * results; a multipole older than e->ti_current is drifted with SWIFT's
+ * cell_drift_multipole when the adapter is linked into SWIFT, else refused
+ * ("Undrifted multipole"). */
+SWHS_API void runner_dopair_grav_mm_progenies(struct runner *r, const long long flags,
+                                              struct cell *ci, struct cell *cj);
+SWHS_API void runner_do_grav_long_range(struct runner *r, struct cell *ci, int timer);
 
 #ifdef __cplusplus
 }

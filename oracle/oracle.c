@@ -3321,6 +3321,59 @@ static double xpow_o(const double dx[3], int t) {
 /* Field tensors of the whole walk: F (35 per cell, real) after the down
  * pass; stats = {n_pp, n_m2p, n_m2l, n_pp_tasks, n_skipped}. The gparts'
  * a_grav / potential receive P2P + M2P (grav_pp_leaves) and L2P. */
+/* gravity_M2L_nonsym / gravity_M2L_symmetric + gravity_M2L_apply
+ * (multipole.h:1600-2095): source A's field tensor at target B's CoM added
+ * into Ft; sym: softening max(eps_A, eps_B), else eps_A. */
+static void m2l_add(const struct oracle_grav_params *G, const struct oracle_multipole *Bm,
+                    const struct oracle_multipole *Am, int sym, real *Ft) {
+  real dx[3];
+  for (int k = 0; k < 3; k++) {
+    dx[k] = (real)(Bm->CoM[k] - Am->CoM[k]);
+    if (G->periodic) dx[k] = nearest_r(dx[k], (real)G->dim[k]);
+  }
+  const real r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+  const real r_inv = (real)(1. / SQRT(r2));
+  const float eps_f = sym ? (Am->max_softening > Bm->max_softening ? Am->max_softening
+                                                                   : Bm->max_softening)
+                          : Am->max_softening;
+  struct m2p_derivs d;
+  m2p_radial(dx[0], dx[1], dx[2], r2, r_inv, (real)eps_f, G->periodic, (real)G->r_s_inv, &d);
+  for (int kk = 0; kk < 35; kk++) {
+    const int ok = mp_a[kk] + mp_b[kk] + mp_c[kk];
+    for (int nn = 0; nn < 35; nn++) {
+      if (nn >= 1 && nn <= 3) continue; /* dipole about the CoM */
+      const int on = mp_a[nn] + mp_b[nn] + mp_c[nn];
+      if (ok + on > 4) continue;
+      Ft[kk] += (real)Am->M[nn] *
+                m2p_D(&d, mp_a[kk] + mp_a[nn], mp_b[kk] + mp_b[nn], mp_c[kk] + mp_c[nn]);
+    }
+  }
+}
+
+/* M-M pairs {target, source, symmetric} of explicit multipoles (the
+ * reference's runner_dopair_grav_mm_progenies / runner_do_grav_long_range
+ * M-M calls, runner_doiact_grav.c:1881-2095, 2441-2530): F[35 t ..] = the
+ * sums in pair order (zeroed first). */
+API void PFX(grav_m2l_pairs)(const struct oracle_grav_params *G,
+                             const struct oracle_multipole *mp, int nmp, const int *pairs,
+                             int npairs, double *F) {
+  memset(F, 0, sizeof(double) * 35 * (size_t)nmp);
+  real Ft[35];
+  for (int q = 0; q < npairs; q++) {
+    const int t = pairs[3 * q], so = pairs[3 * q + 1], sym = pairs[3 * q + 2];
+    for (int k = 0; k < 35; k++) Ft[k] = (real)F[35 * (size_t)t + k];
+    m2l_add(G, &mp[t], &mp[so], sym, Ft);
+    for (int k = 0; k < 35; k++) F[35 * (size_t)t + k] = (double)Ft[k];
+  }
+}
+
+/* gravity_M2L_accept_symmetric (multipole_accept.h:190-205) */
+API int PFX(grav_m2l_accept_symmetric)(const struct oracle_grav_params *G,
+                                       const struct oracle_multipole *A,
+                                       const struct oracle_multipole *B, double r2) {
+  return m2l_accept_o(G, A, B, (float)r2) && m2l_accept_o(G, B, A, (float)r2);
+}
+
 /* owned (NULL: every cell): the decomposition stand-in of
  * swh_gspace_set_owned_cells -- entries only for owned targets */
 API void PFX(grav_tree_owned)(struct gpart *g, int n, const struct oracle_gcell *cells,
@@ -3461,30 +3514,7 @@ API void PFX(grav_tree_owned)(struct gpart *g, int n, const struct oracle_gcell 
   for (long long qq = moff[tc]; qq < moff[tc + 1]; qq++) {
     const long long q = mord[qq];
     const int t = w.mm[3 * q], s = w.mm[3 * q + 1], sym = w.mm[3 * q + 2];
-    const struct oracle_multipole *Bm = &mp[t], *Am = &mp[s];
-    real dx[3];
-    for (int k = 0; k < 3; k++) {
-      dx[k] = (real)(Bm->CoM[k] - Am->CoM[k]);
-      if (G->periodic) dx[k] = nearest_r(dx[k], (real)G->dim[k]);
-    }
-    const real r2 = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
-    const real r_inv = (real)(1. / SQRT(r2));
-    const float eps_f = sym ? (Am->max_softening > Bm->max_softening ? Am->max_softening
-                                                                     : Bm->max_softening)
-                            : Am->max_softening;
-    struct m2p_derivs d;
-    m2p_radial(dx[0], dx[1], dx[2], r2, r_inv, (real)eps_f, G->periodic, (real)G->r_s_inv, &d);
-    real *Ft = F + 35 * (size_t)t;
-    for (int kk = 0; kk < 35; kk++) {
-      const int ok = mp_a[kk] + mp_b[kk] + mp_c[kk];
-      for (int nn = 0; nn < 35; nn++) {
-        if (nn >= 1 && nn <= 3) continue; /* dipole about the CoM */
-        const int on = mp_a[nn] + mp_b[nn] + mp_c[nn];
-        if (ok + on > 4) continue;
-        Ft[kk] += (real)Am->M[nn] *
-                  m2p_D(&d, mp_a[kk] + mp_a[nn], mp_b[kk] + mp_b[nn], mp_c[kk] + mp_c[nn]);
-      }
-    }
+    m2l_add(G, &mp[t], &mp[s], sym, F + 35 * (size_t)t);
   }
   /* down pass: parents before children (depth order), then L2P */
   int *depth = (int *)malloc(sizeof(int) * (size_t)ncells);

@@ -97,7 +97,7 @@ XPART_DTYPE = np.dtype(
 )
 
 # include/swifthip.h SWH_ABI_VERSION: the ctypes layouts below are written for it
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 NUM_TIME_BINS = 56  # src/timeline.h:36
 TIME_BIN_INHIBITED = NUM_TIME_BINS + 2
@@ -344,7 +344,9 @@ class HydroProps(C.Structure):
 
 
 class Space(C.Structure):
-    _fields_ = [("periodic", C.c_int), ("dim", C.c_double * 3)]
+    _fields_ = [("periodic", C.c_int), ("dim", C.c_double * 3),
+                ("cells_top", C.c_void_p), ("cells_with_particles_top", C.POINTER(C.c_int)),
+                ("nr_cells_with_particles", C.c_int)]
 
 
 class PmMesh(C.Structure):
@@ -425,7 +427,7 @@ class CellHydro(C.Structure):
 class CellGrav(C.Structure):
     _fields_ = [("parts", C.c_void_p), ("count", C.c_int),
                 ("multipole", C.POINTER(GravityTensors)), ("ti_end_min", C.c_longlong),
-                ("ti_old_part", C.c_longlong)]
+                ("ti_old_part", C.c_longlong), ("ti_old_multipole", C.c_longlong)]
 
 
 class Cell(C.Structure):

@@ -2823,6 +2823,97 @@ swh_status swh_gspace_grav_down(swh_gspace* g, const swh_grav_params* G, const f
   return SWH_OK;
 }
 
+// M-M interactions of explicit (target <- source) pairs of the caller's
+// multipoles: SWIFT's M-M tasks outside the recursive walk,
+// runner_dopair_grav_mm_progenies (runner_doiact_grav.c:2067-2093, the
+// well-separated progeny pairs flagged at the rebuild) and
+// runner_do_grav_long_range (2441-2530, a cell against every far top-level
+// cell). pairs[3k..3k+2] = {target, source, symmetric}: symmetric selects
+// gravity_M2L_symmetric's softening (the larger of the two), else
+// gravity_M2L_nonsym's (the source's); a symmetric M-M pair is two entries.
+// The tree's m2l_kernel over a CSR by target (targets sum their sources in
+// the given order); fields[35 t ..] = target t's sums, zero for the others.
+swh_status swh_grav_m2l_pairs(swh_context* ctx, const swh_grav_params* G, const swh_multipole* mp,
+                              int32_t nmp, const int32_t* pairs, int32_t npairs, float* fields) {
+  if (!ctx || !G || (nmp > 0 && (!mp || !fields)) || (npairs > 0 && !pairs) || nmp < 0 ||
+      npairs < 0)
+    return SWH_ERR_ARG;
+  if (nmp == 0) return SWH_OK;
+  std::vector<int> off((size_t)nmp + 1, 0);
+  for (int32_t k = 0; k < npairs; k++) {
+    const int t = pairs[3 * k], so = pairs[3 * k + 1];
+    if (t < 0 || t >= nmp || so < 0 || so >= nmp || t == so) {
+      set_error("swh_grav_m2l_pairs: pair %d = (%d, %d) out of range or self", (int)k, t, so);
+      return SWH_ERR_ARG;
+    }
+    off[(size_t)t + 1]++;
+  }
+  for (int32_t c = 0; c < nmp; c++) off[(size_t)c + 1] += off[(size_t)c];
+  std::vector<int2> src((size_t)std::max(1, npairs));
+  {
+    std::vector<int> fill(off.begin(), off.end() - 1);
+    for (int32_t k = 0; k < npairs; k++)
+      src[(size_t)fill[(size_t)pairs[3 * k]]++] =
+          make_int2(pairs[3 * k + 1], pairs[3 * k + 2] ? 1 : 0);
+  }
+  TaskWorker* w = ctx->lease();
+  if (!w) return SWH_ERR_HIP;
+  struct Unlease {
+    swh_context* c;
+    TaskWorker* w;
+    ~Unlease() { c->unlease(w); }
+  } unl{ctx, w};
+  SWH_HIP(hipSetDevice(ctx->device));
+  const size_t bm = (size_t)nmp * sizeof(swh_multipole);
+  const size_t bo = off.size() * sizeof(int), bs = src.size() * sizeof(int2);
+  const size_t bf = (size_t)nmp * SWH_MPOLE_TERMS * sizeof(double);
+  SWH_TRY(w->dparts.reserve(bm));
+  SWH_TRY(w->dind.reserve(bo));
+  SWH_TRY(w->dself.reserve(bs));
+  SWH_TRY(w->dparts2.reserve(bf));
+  SWH_TRY(w->hstage.reserve(bf));
+  SWH_HIP(hipMemcpyAsync(w->dparts.ptr, mp, bm, hipMemcpyHostToDevice, w->stream));
+  SWH_HIP(hipMemcpyAsync(w->dind.ptr, off.data(), bo, hipMemcpyHostToDevice, w->stream));
+  SWH_HIP(hipMemcpyAsync(w->dself.ptr, src.data(), bs, hipMemcpyHostToDevice, w->stream));
+  SWH_HIP(hipMemsetAsync(w->dparts2.ptr, 0, bf, w->stream));
+  if (npairs > 0) {
+    const dim3 mg((unsigned)(((int64_t)nmp * kM2LLanes + 255) / 256));
+    if (ctx->precision == SWH_PRECISION_F64)
+      hipLaunchKernelGGL((m2l_kernel<double>), mg, dim3(256), 0, w->stream,
+                         w->dparts.as<const swh_multipole>(), (int)nmp, w->dind.as<const int>(),
+                         w->dself.as<const int2>(), G->periodic, (double)G->dim[0],
+                         (double)G->dim[1], (double)G->dim[2], (double)G->r_s_inv,
+                         w->dparts2.as<double>());
+    else
+      hipLaunchKernelGGL((m2l_kernel<float>), mg, dim3(256), 0, w->stream,
+                         w->dparts.as<const swh_multipole>(), (int)nmp, w->dind.as<const int>(),
+                         w->dself.as<const int2>(), G->periodic, (double)G->dim[0],
+                         (double)G->dim[1], (double)G->dim[2], (float)G->r_s_inv,
+                         w->dparts2.as<double>());
+    SWH_HIP(hipGetLastError());
+  }
+  SWH_HIP(hipMemcpyAsync(w->hstage.ptr, w->dparts2.ptr, bf, hipMemcpyDeviceToHost, w->stream));
+  SWH_HIP(hipStreamSynchronize(w->stream));
+  const double* h = static_cast<const double*>(w->hstage.ptr);
+  for (size_t k = 0; k < (size_t)nmp * SWH_MPOLE_TERMS; k++) fields[k] = (float)h[k];
+  return SWH_OK;
+}
+
+// gravity_M2L_accept_symmetric (multipole_accept.h:78-176, 190-205) on the
+// caller's multipoles at squared CoM distance r2: the tree walk's own MAC
+// (m2l_accept, in the reference's float arithmetic). For the rebuild-time
+// decisions of cell_can_use_pair_mm (cell.c:1420-1460, use_rebuild_data)
+// the caller passes CoM_rebuild / r_max_rebuild.
+int swh_grav_m2l_accept(const swh_grav_params* G, const swh_multipole* A, const swh_multipole* B,
+                        double r2) {
+  if (!G || !A || !B) return 0;
+  const MacParams mac = mac_params(G);
+  return (m2l_accept(mac, m2l_side(*A), m2l_side(*B), (float)r2) &&
+          m2l_accept(mac, m2l_side(*B), m2l_side(*A), (float)r2))
+             ? 1
+             : 0;
+}
+
 swh_status swh_gspace_field_tensors(swh_gspace* g, float* out) {
   if (!g || !out) return SWH_ERR_ARG;
   const size_t n = g->tree.size() * SWH_MPOLE_TERMS;

@@ -867,3 +867,216 @@ void runner_do_grav_down(struct runner *r, struct cell *c, int timer) {
   swhs_tree_free(&t);
   report(s);
 }
+
+/* ------------------------------------------------------------------------ */
+/* The M-M tasks outside the recursive walk: runner_dopair_grav_mm_progenies */
+/* (runner_doiact_grav.c:2067-2093) and runner_do_grav_long_range            */
+/* (2441-2530). Each task's M-M pairs go to the GPU as one batch             */
+/* (swh_grav_m2l_pairs: the tree's M2L kernel on SWIFT's own multipoles); the */
+/* sums are added into c->grav.multipole->pot as gravity_M2L_apply does.     */
+/* ------------------------------------------------------------------------ */
+
+/* SWIFT's cell_drift_multipole (src/cell_drift.c:1178) when the adapter is
+ * linked into SWIFT; absent here (the tests hand in drifted multipoles). */
+extern void cell_drift_multipole(struct cell *c, const struct engine *e) __attribute__((weak));
+
+static int cell_is_active_gravity_mm(const struct cell *c, const struct engine *e) {
+  return c->grav.ti_end_min == e->ti_current; /* src/active.h:258-262 */
+}
+
+static int swhs_drift_multipole(struct cell *c, const struct engine *e) {
+  if (c->grav.ti_old_multipole >= e->ti_current) return 1;
+  if (!cell_drift_multipole) {
+    SWH_ADAPTER_ERROR("Undrifted multipole (cell_drift_multipole is SWIFT's)");
+    return 0;
+  }
+  cell_drift_multipole(c, e);
+  return 1;
+}
+
+struct swhs_mm {
+  struct cell **cells; /* distinct cells, index = multipole slot */
+  int32_t *pairs;      /* {target, source, symmetric} */
+  int ncells, npairs, cap_c, cap_p;
+};
+
+static int swhs_mm_slot(struct swhs_mm *b, struct cell *c) {
+  for (int k = 0; k < b->ncells; k++)
+    if (b->cells[k] == c) return k;
+  if (b->ncells == b->cap_c) {
+    b->cap_c = b->cap_c ? 2 * b->cap_c : 16;
+    b->cells = (struct cell **)realloc(b->cells, (size_t)b->cap_c * sizeof(struct cell *));
+  }
+  b->cells[b->ncells] = c;
+  return b->ncells++;
+}
+
+static void swhs_mm_add(struct swhs_mm *b, struct cell *t, struct cell *s, int sym) {
+  if (b->npairs == b->cap_p) {
+    b->cap_p = b->cap_p ? 2 * b->cap_p : 64;
+    b->pairs = (int32_t *)realloc(b->pairs, (size_t)b->cap_p * 3 * sizeof(int32_t));
+  }
+  int32_t *q = b->pairs + 3 * (size_t)b->npairs++;
+  q[0] = swhs_mm_slot(b, t);
+  q[1] = swhs_mm_slot(b, s);
+  q[2] = sym;
+}
+
+/* runner_dopair_grav_mm (runner_doiact_grav.c:2032-2064): symmetric when both
+ * cells are active and local, else the active local one receives. */
+static int swhs_mm_pair(struct swhs_mm *b, const struct engine *e, struct cell *ci,
+                        struct cell *cj) {
+  const int do_i = cell_is_active_gravity_mm(ci, e) && (ci->nodeID == e->nodeID);
+  const int do_j = cell_is_active_gravity_mm(cj, e) && (cj->nodeID == e->nodeID);
+  if (!ci->grav.multipole || !cj->grav.multipole) {
+    SWH_ADAPTER_ERROR("M-M interaction without cell multipoles");
+    return 0;
+  }
+  if (!swhs_drift_multipole(ci, e) || !swhs_drift_multipole(cj, e)) return 0;
+  if (do_i && do_j) {
+    swhs_mm_add(b, ci, cj, 1);
+    swhs_mm_add(b, cj, ci, 1);
+  } else if (do_i) {
+    swhs_mm_add(b, ci, cj, 0);
+  } else if (do_j) {
+    swhs_mm_add(b, cj, ci, 0);
+  }
+  return 1;
+}
+
+/* The batch on the GPU; each target's sums added into its field tensor. */
+static void swhs_mm_run(struct swhs_mm *b, const struct engine *e) {
+  if (b->npairs > 0) {
+    swh_grav_params G;
+    grav_params_of(e, &G);
+    swh_multipole *mp = (swh_multipole *)calloc((size_t)b->ncells, sizeof(swh_multipole));
+    float *f = (float *)malloc((size_t)b->ncells * SWH_MPOLE_TERMS * sizeof(float));
+    for (int k = 0; k < b->ncells; k++) multipole_of(b->cells[k]->grav.multipole, &mp[k]);
+    const swh_status s = swh_grav_m2l_pairs(swhs_ctx, &G, mp, b->ncells, b->pairs, b->npairs, f);
+    if (s == SWH_OK) {
+      char *target = (char *)calloc((size_t)b->ncells, 1);
+      for (int q = 0; q < b->npairs; q++) target[b->pairs[3 * q]] = 1;
+      for (int k = 0; k < b->ncells; k++) {
+        if (!target[k]) continue;
+        struct grav_tensor *pot = &b->cells[k]->grav.multipole->pot;
+        tensor_from(pot, f + (size_t)k * SWH_MPOLE_TERMS, 1);
+        pot->interacted = 1;
+      }
+      free(target);
+    }
+    free(f);
+    free(mp);
+    report(s);
+  }
+  free(b->cells);
+  free(b->pairs);
+}
+
+/* runner_dopair_grav_mm_progenies (runner_doiact_grav.c:2067-2093) */
+void runner_dopair_grav_mm_progenies(struct runner *r, const long long flags, struct cell *ci,
+                                     struct cell *cj) {
+  const struct engine *e = r->e;
+  if (!swhs_ctx) SWH_ADAPTER_ERROR("swifthip_swift_init() was not called");
+  /* (runner_clear_grav_flags: the cells' unskip flags are the scheduler's,
+   * which this drop-in does not hold) */
+  struct swhs_mm b = {0};
+  int ok = 1;
+  for (int i = 0; ok && i < 8; i++) {
+    if (ci->progeny[i] == NULL) continue;
+    for (int j = 0; ok && j < 8; j++) {
+      if (cj->progeny[j] == NULL) continue;
+      /* did the last rebuild flag this progeny pair well separated? */
+      if (flags & (1ULL << (i * 8 + j))) ok = swhs_mm_pair(&b, e, ci->progeny[i], cj->progeny[j]);
+    }
+  }
+  if (!ok) b.npairs = 0;
+  swhs_mm_run(&b, e);
+}
+
+/* cell_min_dist2_same_size (src/cell.h:696-750) */
+static double swhs_nearest(double d, double L) {
+  return d > 0.5 * L ? d - L : (d < -0.5 * L ? d + L : d);
+}
+static double swhs_min4(double a, double b, double c, double d) {
+  const double x = a < b ? a : b, y = c < d ? c : d;
+  return x < y ? x : y;
+}
+static double cell_min_dist2_same_size(const struct cell *ci, const struct cell *cj, int periodic,
+                                       const double dim[3]) {
+  double d2 = 0.;
+  for (int k = 0; k < 3; k++) {
+    const double imin = ci->loc[k], imax = ci->loc[k] + ci->width[k];
+    const double jmin = cj->loc[k], jmax = cj->loc[k] + cj->width[k];
+    double dk;
+    if (periodic)
+      dk = swhs_min4(fabs(swhs_nearest(imin - jmin, dim[k])), fabs(swhs_nearest(imin - jmax, dim[k])),
+                     fabs(swhs_nearest(imax - jmin, dim[k])), fabs(swhs_nearest(imax - jmax, dim[k])));
+    else
+      dk = swhs_min4(fabs(imin - jmin), fabs(imin - jmax), fabs(imax - jmin), fabs(imax - jmax));
+    d2 += dk * dk;
+  }
+  return d2;
+}
+
+/* cell_can_use_pair_mm (src/cell.c:1420-1460) with use_rebuild_data = 1,
+ * is_tree_walk = 0: the MAC of the rebuild-time CoMs and sizes */
+static int cell_can_use_pair_mm_rebuild(const struct cell *ci, const struct cell *cj,
+                                        const struct engine *e, const swh_grav_params *G) {
+  const struct gravity_tensors *A = ci->grav.multipole, *B = cj->grav.multipole;
+  double r2 = 0.;
+  for (int k = 0; k < 3; k++) {
+    double d = A->CoM_rebuild[k] - B->CoM_rebuild[k];
+    if (e->s->periodic) d = swhs_nearest(d, e->s->dim[k]);
+    r2 += d * d;
+  }
+  swh_multipole ma, mb;
+  multipole_of(A, &ma);
+  multipole_of(B, &mb);
+  ma.r_max = A->r_max_rebuild;
+  mb.r_max = B->r_max_rebuild;
+  return swh_grav_m2l_accept(G, &ma, &mb, r2);
+}
+
+/* runner_do_grav_long_range (runner_doiact_grav.c:2441-2530) */
+void runner_do_grav_long_range(struct runner *r, struct cell *ci, int timer) {
+  (void)timer;
+  const struct engine *e = r->e;
+  if (!swhs_ctx) SWH_ADAPTER_ERROR("swifthip_swift_init() was not called");
+  const struct space *s = e->s;
+  const int periodic = e->mesh->periodic;
+  const double dim[3] = {e->mesh->dim[0], e->mesh->dim[1], e->mesh->dim[2]};
+  const double max_distance2 = e->mesh->r_cut_max * e->mesh->r_cut_max;
+  if (!cell_is_active_gravity(ci, e)) return;
+  if (ci->nodeID != e->nodeID) {
+    SWH_ADAPTER_ERROR("Non-local cell in long-range gravity task!");
+    return;
+  }
+  if (!ci->grav.multipole) {
+    SWH_ADAPTER_ERROR("long-range gravity without cell multipoles");
+    return;
+  }
+  if (!swhs_drift_multipole(ci, e)) return;
+  struct gravity_tensors *const multi_i = ci->grav.multipole;
+  struct cell *top = ci;
+  while (top->parent != NULL) top = top->parent;
+  swh_grav_params G;
+  grav_params_of(e, &G);
+  struct swhs_mm b = {0};
+  for (int n = 0; n < s->nr_cells_with_particles; ++n) {
+    struct cell *cj = &s->cells_top[s->cells_with_particles_top[n]];
+    const struct gravity_tensors *multi_j = cj->grav.multipole;
+    if (top == cj) continue;                /* no self contribution */
+    if (multi_j->m_pole.M_000 == 0.f) continue;  /* empty */
+    if (periodic && cell_min_dist2_same_size(top, cj, periodic, dim) > max_distance2) {
+      multi_i->pot.interacted = 1; /* beyond the truncated forces: the mesh's */
+      continue;
+    }
+    if (cell_can_use_pair_mm_rebuild(top, cj, e, &G)) {
+      /* runner_dopair_grav_mm_nonsym(r, ci, cj): the active local ci receives */
+      if (cell_is_active_gravity_mm(ci, e) && ci->nodeID == e->nodeID)
+        swhs_mm_add(&b, ci, cj, 0);
+      multi_i->pot.interacted = 1;
+    }
+  }
+  swhs_mm_run(&b, e);
+}

@@ -50,6 +50,7 @@ HIP_SYMBOLS = [
     "swh_grav_tree_tasks", "swh_gspace_field_tensors", "swh_gspace_multipoles",
     "swh_gspace_set_multipoles", "swh_gspace_grav_down",
     "swh_gspace_download", "swh_gspace_sync", "swh_gspace_query", "swh_gspace_pm_mesh",
+    "swh_grav_m2l_pairs", "swh_grav_m2l_accept",
 ]
 ADAPTER_SYMBOLS = [
     "swifthip_swift_init", "swifthip_swift_finalize", "swifthip_swift_last_error",
@@ -63,7 +64,7 @@ ADAPTER_SYMBOLS = [
     "runner_dosub_self1_density", "runner_dosub_pair1_density", "runner_dosub_self1_gradient",
     "runner_dosub_pair1_gradient", "runner_dosub_self2_force", "runner_dosub_pair2_force",
     "runner_dosub_subset_density", "swifthip_swift_part_layout", "swifthip_swift_gpart_layout",
-    "swifthip_swift_split_pairs",
+    "swifthip_swift_split_pairs", "runner_dopair_grav_mm_progenies", "runner_do_grav_long_range",
 ]
 
 
@@ -162,6 +163,9 @@ def load(kernel: str = "cubic-spline") -> C.CDLL:
         "swh_gspace_sync": (C.c_int, [vp]),
         "swh_gspace_query": (C.c_int, [vp]),
         "swh_gspace_pm_mesh": (C.c_int, [vp, P(abi.PMParams), vp]),
+        "swh_grav_m2l_pairs": (C.c_int, [vp, P(abi.GravParams), vp, i32, vp, i32, vp]),
+        "swh_grav_m2l_accept": (C.c_int, [P(abi.GravParams), P(abi.Multipole),
+                                          P(abi.Multipole), dp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)

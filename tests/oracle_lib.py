@@ -86,6 +86,9 @@ def load(prec: str = "f32", kernel: str = "cubic-spline") -> C.CDLL:
                             P(abi.GravParams), vp, vp])
     sig("grav_tree_owned", None, [vp, C.c_int, vp, C.c_int, vp, C.c_int, vp, C.c_int,
                                   P(abi.GravParams), vp, vp, vp])
+    sig("grav_m2l_pairs", None, [P(abi.GravParams), vp, C.c_int, vp, C.c_int, vp])
+    sig("grav_m2l_accept_symmetric", C.c_int, [P(abi.GravParams), P(abi.Multipole),
+                                               P(abi.Multipole), C.c_double])
     sig("pm_mesh", None, [vp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_float, vp])
     if prec == "f32":
         for n in ("iact_density", "iact_force", "iact_gradient"):

@@ -226,6 +226,10 @@ def load_adapter(kernel: str = "cubic-spline") -> C.CDLL:
         getattr(ad, n).restype = None
     ad.runner_dopair_recursive_grav.argtypes = [vp, vp, vp, C.c_int]
     ad.runner_dopair_recursive_grav.restype = None
+    ad.runner_dopair_grav_mm_progenies.argtypes = [vp, C.c_longlong, vp, vp]
+    ad.runner_dopair_grav_mm_progenies.restype = None
+    ad.runner_do_grav_long_range.argtypes = [vp, vp, C.c_int]
+    ad.runner_do_grav_long_range.restype = None
     _adapters[kernel] = ad
     return ad
 

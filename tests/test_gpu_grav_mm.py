@@ -140,9 +140,11 @@ def test_mm_progenies_vs_oracle(gpu_ctx, adapter, inactive):
 @pytest.mark.parametrize("periodic", [False, True])
 def test_long_range_vs_oracle(gpu_ctx, adapter, periodic):
     g, cells, tops, mp, cs, tens = _tree(gpu_ctx, 4, seed=17, periodic=periodic)
-    r_s = 1.25 / 64  # r_cut_max 0.088: top cells one cell apart (0.25) are skipped
+    # 4^3 top cells of width 0.25: gaps 0.25 (one cell between along an axis)
+    # stay within r_cut_max = 0.3, diagonal gaps (0.35, 0.43) are skipped
+    r_s = 0.3 / 4.5
     r_cut_max = 4.5 * r_s if periodic else 0.0
-    theta = 0.6
+    theta = 0.95
     tops_i = np.asarray(tops, dtype=np.int32)
     with_parts = np.ascontiguousarray(tops_i[cells["count"][tops_i] > 0])
     mesh = abi.PmMesh(1 if periodic else 0, (C.c_double * 3)(1, 1, 1),

@@ -14,7 +14,7 @@ for r in $(seq 1 "$reps"); do
     args=$A; envs=$SWH_AB_ENV_A
     if [ $v = B ]; then args=$B; envs=$SWH_AB_ENV_B; fi
     log="$out/${tag}_${v}${r}.log"
-    env $envs timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-steady --no-breakdown \
+    env $envs timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-steady --no-breakdown --no-configs \
       $args > "$log" 2>&1 || exit $?
     tail -1 "$log" | python -c "
 import json, sys

@@ -14,7 +14,7 @@ C="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_I
 D="TA_BUSY_avr TA_BUSY_max GRBM_GUI_ACTIVE"
 for p in A B C D; do
   timeout -s KILL 120 rocprofv3 --pmc ${!p} --kernel-include-regex "$regex" -d gpurun_out/${tag}_$p \
-    -o run --output-format csv -- python bench.py --no-cpu-baseline "$@" \
+    -o run --output-format csv -- python bench.py --no-configs --no-cpu-baseline "$@" \
     > gpurun_out/${tag}_$p.log 2>&1 || exit $?
 done
 python tools/sq_json.py gpurun_out/${tag} > gpurun_out/${tag}_sq.json

@@ -76,7 +76,8 @@ def test_tree_vs_oracle_newtonian(gpu_ctx, theta):
     gg, go = abi.copy_parts(g), abi.copy_parts(g)
     st = run_gpu(gpu_ctx, gg, cells, tops, pairs, G)[0]
     so, fo = run_oracle(go, cells, tops, pairs, G)
-    assert [st["n_pp"], st["n_m2p"], st["n_m2l"], st["n_pp_tasks"], st["n_skipped"]] == list(so)
+    assert [st["n_pp"], st["n_m2p"], st["n_m2l"], st["n_pp_tasks"], st["n_skipped"],
+            st["n_pp_truncated"]] == list(so)
     assert st["n_m2l"] > 0 and st["n_m2p"] > 0
     compare(gg, go)
 
@@ -105,7 +106,8 @@ def test_tree_periodic_truncated(gpu_ctx):
     gg, go = abi.copy_parts(g), abi.copy_parts(g)
     st = run_gpu(gpu_ctx, gg, cells, tops, pairs, G)[0]
     so, _ = run_oracle(go, cells, tops, pairs, G)
-    assert [st["n_pp"], st["n_m2p"], st["n_m2l"], st["n_pp_tasks"], st["n_skipped"]] == list(so)
+    assert [st["n_pp"], st["n_m2p"], st["n_m2l"], st["n_pp_tasks"], st["n_skipped"],
+            st["n_pp_truncated"]] == list(so)
     assert st["n_skipped"] > 0
     compare(gg, go)
 
@@ -123,7 +125,8 @@ def test_tree_activity_and_adaptive_mac(gpu_ctx):
     gg, go = abi.copy_parts(g), abi.copy_parts(g)
     st = run_gpu(gpu_ctx, gg, cells, tops, pairs, G)[0]
     so, _ = run_oracle(go, cells, tops, pairs, G)
-    assert [st["n_pp"], st["n_m2p"], st["n_m2l"], st["n_pp_tasks"], st["n_skipped"]] == list(so)
+    assert [st["n_pp"], st["n_m2p"], st["n_m2l"], st["n_pp_tasks"], st["n_skipped"],
+            st["n_pp_truncated"]] == list(so)
     inactive = g["time_bin"] != 1
     assert np.all(gg["a_grav"][inactive] == 0)
     compare(gg[~inactive], go[~inactive])
@@ -162,7 +165,8 @@ def test_tree_periodic_direct_far_pairs(gpu_ctx):
     so, _ = run_oracle(go, cells, tops, pairs, G)
     N = len(g)
     assert st["n_pp"] == N * (N - 1) and st["n_m2l"] == 0 and st["n_m2p"] == 0
-    assert [st["n_pp"], st["n_m2p"], st["n_m2l"], st["n_pp_tasks"], st["n_skipped"]] == list(so)
+    assert [st["n_pp"], st["n_m2p"], st["n_m2l"], st["n_pp_tasks"], st["n_skipped"],
+            st["n_pp_truncated"]] == list(so)
     compare(gg, go)
 
 

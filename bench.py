@@ -605,6 +605,9 @@ def steady_state(sp, P, stream, torch, local, n_owned, args, skin=None, steps=No
                     "when a particle's H + 2 D exceeds its build reach)",
             "steps": steps, "list_skin": skin, "skin_policy": policy,
             "displacement_per_step_over_h": disp,
+            "h_during_drift": "frozen: each step resets the accelerations (h_dt = 0) before its "
+                              "drift, so hydro_predict_extra keeps h and only positions move "
+                              "(this loop has no ghost to finalise h_dt)",
             "rebin_every": rebin, "list_builds": int(builds),
             "steps_per_list_build": steps / max(1, builds),
             "interactions": nd + nf, "ms_per_step": el / steps * 1e3,

@@ -185,57 +185,6 @@ void list_build_kernel(GridDev g, SoA a, ListDev ld,
                                   hmax_bits, counter, diag, lds, tab);
 }
 
-// A density loop's list build with the density walk of the group's
-// particles in the same wave, right after its lists are written (the build
-// wave's 16 i-slots x 4 lanes are the walk's layout): the entries come back
-// from L2 instead of HBM, and on a CU the waves still building (VALU, LDS)
-// overlap those walking (gathers, fp64). The walk is list_walk's per-lane
-// work on the same entries in the same order, so the sums are those of
-// density_walk_kernel bit for bit; particles past the list capacity are left
-// to overflow_kernel.
-#ifndef SWH_BUILD_DENS_WPE
-#define SWH_BUILD_DENS_WPE 4
-#endif
-template <typename T>
-__global__ __launch_bounds__(64)
-#if SWH_BUILD_DENS_WPE > 0
-__attribute__((amdgpu_waves_per_eu(SWH_BUILD_DENS_WPE)))
-#endif
-void list_build_density_kernel(
-    GridDev g, SoA a, ListDev ld, const int2* __restrict__ groups, int g0, int ngroups,
-    int max_active_bin, const unsigned int* __restrict__ hmax_bits, unsigned long long* counter,
-    int* __restrict__ ncount) {
-  __shared__ ListLds<kListLpiBuild> lds;
-  __shared__ CellTab tab;
-  const BuildSlot b = list_build<kListLpiBuild>(g, a, ld, groups, g0 + xcd_block_id(), ngroups,
-                                                max_active_bin, hmax_bits, counter, 0, lds, tab);
-  // the lists this wave's lanes just wrote, visible to all its lanes
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  using S = LoopState<LOOP_DENSITY, T>;
-  const int s = (int)(threadIdx.x % kListLpiBuild);
-  const bool act = b.act && b.nl <= ld.K;
-  S st;
-  st.n = 0;
-  if (act) st.load_i(a, b.i, (T)0, hmax_bits);
-  const int nl = act ? b.nl : 0;
-  const double rwrap = (double)__uint_as_float(*ld.rwrap_bits);
-  if (__any(act && g.periodic && near_face(g, b.pi, rwrap)))
-    walk_entries<kListLpiBuild, true, T>(g, a, ld, b.pi, nl, b.lb, s, st);
-  else
-    walk_entries<kListLpiBuild, false, T>(g, a, ld, b.pi, nl, b.lb, s, st);
-  reduce_lanes<kListLpiBuild, T>(st);
-  if (act && s == 0) {
-    st.store(a, b.i);
-    if (ncount) ncount[b.i] = st.n;
-  }
-  if (counter) {
-    unsigned long long v = (unsigned long long)((act && s == 0) ? st.n : 0);
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(counter_stripe(counter), v);
-  }
-}
-
 #ifndef SWH_WALK_WPE
 #define SWH_WALK_WPE 0
 #endif
@@ -897,8 +846,7 @@ static ListDev list_dev(swh_space* s) {
 // a device flag; the build kernels do nothing unless it is set (kept lists
 // that the device check found stale).
 static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool count,
-                              float skin, const unsigned int* run_if = nullptr,
-                              bool fuse_density = false) {
+                              float skin, const unsigned int* run_if = nullptr) {
   const int K = s->tuning.list_capacity > 0 ? s->tuning.list_capacity : 128;
   unsigned long long* stripes = nullptr;
   if (count) SWH_TRY(stripes_slot(s, &stripes));
@@ -935,16 +883,10 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
                      s->list_xd0.as<float4>(), s->gbox.as<GroupBox>(), hmax_slot(s),
                      (float)(kGamma * ld.skin1), (float)s->grid.dx, rwrap_slot(s),
                      rwrap_base_slot(s), ovf_slot(s), nbuild_slot(s), run_if);
-  if (fuse_density)  // the density walk of the built lists in the same waves (fp64)
-    hipLaunchKernelGGL((list_build_density_kernel<double>), dim3(s->ngroups), dim3(64), 0,
-                       s->stream, grid_dev(s), soa_of(s), ldb, s->groups.as<const int2>(), 0,
-                       s->ngroups, P->max_active_bin, hmax_slot(s), count ? stripes : nullptr,
-                       count ? s->ncount.as<int>() : nullptr);
-  else
-    hipLaunchKernelGGL(list_build_kernel, dim3(s->ngroups), dim3(64), 0, s->stream, grid_dev(s),
-                       soa_of(s), ldb, s->groups.as<const int2>(), 0, s->ngroups,
-                       P->max_active_bin, hmax_slot(s), count ? stripes : nullptr,
-                       s->tuning.diag_mode, run_if);
+  hipLaunchKernelGGL(list_build_kernel, dim3(s->ngroups), dim3(64), 0, s->stream, grid_dev(s),
+                     soa_of(s), ldb, s->groups.as<const int2>(), 0, s->ngroups,
+                     P->max_active_bin, hmax_slot(s), count ? stripes : nullptr,
+                     s->tuning.diag_mode, run_if);
   SWH_HIP(hipGetLastError());
   s->list_valid = true;
   s->list_check = false;
@@ -975,7 +917,7 @@ static swh_status check_kept_lists(swh_space* s, const swh_hydro_params* P, bool
 template <int LOOP, typename T>
 static void launch_typed(swh_space* s, const GridDev& gd, const SegList* subset, int nitems,
                          int max_active_bin, T a2H, unsigned long long* ctr, int* ncount,
-                         const unsigned int* mark = nullptr, bool walked = false) {
+                         const unsigned int* mark = nullptr) {
   const int block = 256;
   ListDev ld = list_dev(s);
   ld.mark = mark;
@@ -994,9 +936,7 @@ static void launch_typed(swh_space* s, const GridDev& gd, const SegList* subset,
                        search_slot(s), max_active_bin, a2H, hmax_slot(s), ctr, ncount);
     return;
   }
-  if (walked) {
-    // the list build walked the listed particles (list_build_density_kernel)
-  } else if (LOOP == LOOP_DENSITY && sizeof(T) == 8)  // (the fp32 walk would spill)
+  if (LOOP == LOOP_DENSITY && sizeof(T) == 8)  // (the fp32 walk would spill)
     hipLaunchKernelGGL((density_walk_kernel<T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
                        s->stream, gd, soa_of(s), ld, 0, nitems, max_active_bin, a2H,
                        hmax_slot(s), ctr, ncount);
@@ -1009,23 +949,11 @@ static void launch_typed(swh_space* s, const GridDev& gd, const SegList* subset,
                      ncount);
 }
 
-// The density walk fused into the list build (list_build_density_kernel);
-// SWH_FUSE_DENSITY=0: the separate density_walk_kernel after the build.
-static bool fuse_density_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("SWH_FUSE_DENSITY");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 template <int LOOP>
 static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const SegList* subset,
                               int nitems, bool count) {
   if (nitems <= 0) return SWH_OK;
   if (!subset && s->ngroups <= 0) return SWH_OK;
-  const bool f64 = s->ctx->precision == SWH_PRECISION_F64;
-  bool walked = false;  // the build ran the density walk too
   if (!subset) {
     // The density loop builds the step's lists; gradient and force reuse them
     // while no particle's H has outgrown its list reach (ghost: stale flag).
@@ -1038,8 +966,7 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const Seg
     if (keep && fresh && s->list_check) {
       SWH_TRY(check_kept_lists(s, P, count));
     } else if ((LOOP == LOOP_DENSITY && !(keep && fresh)) || !fresh) {
-      walked = LOOP == LOOP_DENSITY && f64 && s->tuning.diag_mode == 0 && fuse_density_enabled();
-      SWH_TRY(build_lists(s, P, count, s->tuning.list_skin, nullptr, walked));
+      SWH_TRY(build_lists(s, P, count, s->tuning.list_skin));
     } else if (s->list_check) {  // gradient / force right after a drift
       SWH_TRY(check_kept_lists(s, P, count));
     }
@@ -1052,6 +979,7 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const Seg
   unsigned long long* ctr = nullptr;
   if (count) SWH_TRY(stripes_slot(s, &ctr));
   int* ncount = count ? s->ncount.as<int>() : nullptr;
+  const bool f64 = s->ctx->precision == SWH_PRECISION_F64;
   // gradient / force after a ghost that grew a few H past the lists: those
   // particles (force: and their neighbours within H) are searched
   const bool grown = !subset && LOOP != LOOP_DENSITY && s->grown_n > 0 && s->list_valid;
@@ -1075,8 +1003,7 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const Seg
                        s->grown_search.as<int>(), qn);
   }
   if (f64)
-    launch_typed<LOOP, double>(s, gd, subset, nitems, P->max_active_bin, a2H, ctr, ncount, mark,
-                               walked);
+    launch_typed<LOOP, double>(s, gd, subset, nitems, P->max_active_bin, a2H, ctr, ncount, mark);
   else
     launch_typed<LOOP, float>(s, gd, subset, nitems, P->max_active_bin, (float)a2H, ctr,
                               ncount, mark);

@@ -219,24 +219,6 @@ void density_walk_kernel(GridDev g, SoA a, ListDev ld, int i0, int n, int max_ac
                                        ncount);
 }
 
-// The density walk over the particles of i-groups [g0, g1) (one chunk of
-// the density loop's build / walk pipeline, launch_loop): the range is read
-// from the groups on the device; the grid covers 16 particles per group and
-// the blocks past the range's end exit.
-template <typename T>
-__global__ __launch_bounds__(256)
-#if SWH_WALK_WPE_DENS > 0
-__attribute__((amdgpu_waves_per_eu(SWH_WALK_WPE_DENS)))
-#endif
-void density_walk_groups_kernel(GridDev g, SoA a, ListDev ld, const int2* __restrict__ groups,
-                                int g0, int g1, int max_active_bin, T a2H,
-                                const unsigned int* __restrict__ hmax_bits,
-                                unsigned long long* counter, int* __restrict__ ncount) {
-  const int2 first = groups[g0], last = groups[g1 - 1];
-  list_walk<LOOP_DENSITY, T, kWalkLpi>(g, a, ld, first.x, last.x + last.y, max_active_bin, a2H,
-                                       hmax_bits, counter, ncount);
-}
-
 // The list's overflow particles (more than K hits: a large H in a dense
 // region): one wave per particle searches the cells around it, the 64 lanes
 // striding over each cell's particles, cells farther than max(H_i, the
@@ -863,29 +845,8 @@ static ListDev list_dev(swh_space* s) {
 // Build the step's pair lists for the active particles. run_if (nullable):
 // a device flag; the build kernels do nothing unless it is set (kept lists
 // that the device check found stale).
-// Chunks of the density loop's build / walk pipeline: the build of i-group
-// chunk c + 1 (VALU- and latency-bound) runs beside the walk of chunk c
-// (gather-bound) on a second stream. SWH_DENS_PIPE = chunks (1: no pipeline).
-static int dens_pipe_chunks() {
-  static const int c = [] {
-    const char* e = std::getenv("SWH_DENS_PIPE");
-    const int v = e ? std::atoi(e) : 1;
-    return v < 1 ? 1 : (v > 16 ? 16 : v);
-  }();
-  return c;
-}
-
-static swh_status pipe_init(swh_space* s) {
-  if (!s->aux) SWH_HIP(hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking));
-  for (hipEvent_t& e : s->pipe_ev)
-    if (!e) SWH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  if (!s->aux_done) SWH_HIP(hipEventCreateWithFlags(&s->aux_done, hipEventDisableTiming));
-  return SWH_OK;
-}
-
 static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool count,
-                              float skin, const unsigned int* run_if = nullptr,
-                              int chunks = 1) {
+                              float skin, const unsigned int* run_if = nullptr) {
   const int K = s->tuning.list_capacity > 0 ? s->tuning.list_capacity : 128;
   unsigned long long* stripes = nullptr;
   if (count) SWH_TRY(stripes_slot(s, &stripes));
@@ -922,16 +883,10 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
                      s->list_xd0.as<float4>(), s->gbox.as<GroupBox>(), hmax_slot(s),
                      (float)(kGamma * ld.skin1), (float)s->grid.dx, rwrap_slot(s),
                      rwrap_base_slot(s), ovf_slot(s), nbuild_slot(s), run_if);
-  for (int c = 0; c < chunks; c++) {
-    // chunk c: groups [g0, g1); an event after each for the pipelined walk
-    const int g0 = (int)((int64_t)s->ngroups * c / chunks);
-    const int g1 = (int)((int64_t)s->ngroups * (c + 1) / chunks);
-    hipLaunchKernelGGL(list_build_kernel, dim3(std::max(1, g1 - g0)), dim3(64), 0, s->stream,
-                       grid_dev(s), soa_of(s), ldb, s->groups.as<const int2>(), g0, g1,
-                       P->max_active_bin, hmax_slot(s), count ? stripes : nullptr,
-                       s->tuning.diag_mode, run_if);
-    if (chunks > 1) SWH_HIP(hipEventRecord(s->pipe_ev[c], s->stream));
-  }
+  hipLaunchKernelGGL(list_build_kernel, dim3(s->ngroups), dim3(64), 0, s->stream, grid_dev(s),
+                     soa_of(s), ldb, s->groups.as<const int2>(), 0, s->ngroups,
+                     P->max_active_bin, hmax_slot(s), count ? stripes : nullptr,
+                     s->tuning.diag_mode, run_if);
   SWH_HIP(hipGetLastError());
   s->list_valid = true;
   s->list_check = false;
@@ -962,7 +917,7 @@ static swh_status check_kept_lists(swh_space* s, const swh_hydro_params* P, bool
 template <int LOOP, typename T>
 static void launch_typed(swh_space* s, const GridDev& gd, const SegList* subset, int nitems,
                          int max_active_bin, T a2H, unsigned long long* ctr, int* ncount,
-                         const unsigned int* mark = nullptr, int chunks = 1) {
+                         const unsigned int* mark = nullptr) {
   const int block = 256;
   ListDev ld = list_dev(s);
   ld.mark = mark;
@@ -981,22 +936,7 @@ static void launch_typed(swh_space* s, const GridDev& gd, const SegList* subset,
                        search_slot(s), max_active_bin, a2H, hmax_slot(s), ctr, ncount);
     return;
   }
-  if (LOOP == LOOP_DENSITY && sizeof(T) == 8 && chunks > 1) {
-    // the pipelined walk: chunk c on the aux stream once its lists are built,
-    // then the space's stream waits for the last one
-    for (int c = 0; c < chunks; c++) {
-      const int g0 = (int)((int64_t)s->ngroups * c / chunks);
-      const int g1 = (int)((int64_t)s->ngroups * (c + 1) / chunks);
-      if (g1 <= g0) continue;
-      (void)hipStreamWaitEvent(s->aux, s->pipe_ev[c], 0);
-      const int np = kListSlots * (g1 - g0);
-      hipLaunchKernelGGL((density_walk_groups_kernel<T>), dim3((np + ppb - 1) / ppb), dim3(block),
-                         0, s->aux, gd, soa_of(s), ld, s->groups.as<const int2>(), g0, g1,
-                         max_active_bin, a2H, hmax_slot(s), ctr, ncount);
-    }
-    (void)hipEventRecord(s->aux_done, s->aux);
-    (void)hipStreamWaitEvent(s->stream, s->aux_done, 0);
-  } else if (LOOP == LOOP_DENSITY && sizeof(T) == 8)  // (the fp32 walk would spill)
+  if (LOOP == LOOP_DENSITY && sizeof(T) == 8)  // (the fp32 walk would spill)
     hipLaunchKernelGGL((density_walk_kernel<T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
                        s->stream, gd, soa_of(s), ld, 0, nitems, max_active_bin, a2H,
                        hmax_slot(s), ctr, ncount);
@@ -1014,8 +954,6 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const Seg
                               int nitems, bool count) {
   if (nitems <= 0) return SWH_OK;
   if (!subset && s->ngroups <= 0) return SWH_OK;
-  const bool f64 = s->ctx->precision == SWH_PRECISION_F64;
-  int chunks = 1;  // > 1: the density loop's build / walk pipeline
   if (!subset) {
     // The density loop builds the step's lists; gradient and force reuse them
     // while no particle's H has outgrown its list reach (ghost: stale flag).
@@ -1028,12 +966,7 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const Seg
     if (keep && fresh && s->list_check) {
       SWH_TRY(check_kept_lists(s, P, count));
     } else if ((LOOP == LOOP_DENSITY && !(keep && fresh)) || !fresh) {
-      if (LOOP == LOOP_DENSITY && f64 && s->tuning.diag_mode == 0 && dens_pipe_chunks() > 1 &&
-          s->ngroups >= 64 * dens_pipe_chunks()) {
-        SWH_TRY(pipe_init(s));
-        chunks = dens_pipe_chunks();
-      }
-      SWH_TRY(build_lists(s, P, count, s->tuning.list_skin, nullptr, chunks));
+      SWH_TRY(build_lists(s, P, count, s->tuning.list_skin));
     } else if (s->list_check) {  // gradient / force right after a drift
       SWH_TRY(check_kept_lists(s, P, count));
     }
@@ -1046,6 +979,7 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const Seg
   unsigned long long* ctr = nullptr;
   if (count) SWH_TRY(stripes_slot(s, &ctr));
   int* ncount = count ? s->ncount.as<int>() : nullptr;
+  const bool f64 = s->ctx->precision == SWH_PRECISION_F64;
   // gradient / force after a ghost that grew a few H past the lists: those
   // particles (force: and their neighbours within H) are searched
   const bool grown = !subset && LOOP != LOOP_DENSITY && s->grown_n > 0 && s->list_valid;
@@ -1069,8 +1003,7 @@ static swh_status launch_loop(swh_space* s, const swh_hydro_params* P, const Seg
                        s->grown_search.as<int>(), qn);
   }
   if (f64)
-    launch_typed<LOOP, double>(s, gd, subset, nitems, P->max_active_bin, a2H, ctr, ncount, mark,
-                               chunks);
+    launch_typed<LOOP, double>(s, gd, subset, nitems, P->max_active_bin, a2H, ctr, ncount, mark);
   else
     launch_typed<LOOP, float>(s, gd, subset, nitems, P->max_active_bin, (float)a2H, ctr,
                               ncount, mark);

@@ -225,11 +225,6 @@ struct swh_space {
   swh::HostBuf ghost_host;  // pinned: the passes' counts read back
   unsigned int* ghost_zero_next = nullptr;  // cleared by the rerun launch (swh_ghost)
   swh::HostBuf hstage;
-  // the density loop's build / walk pipeline (swh_hydro.hip): the walk of
-  // group chunk c runs on `aux` while chunk c + 1 builds on `stream`
-  hipStream_t aux = nullptr;
-  hipEvent_t pipe_ev[17] = {};
-  hipEvent_t aux_done = nullptr;
 };
 
 struct swh_gspace {

@@ -692,13 +692,6 @@ swh_status swh_space_destroy(swh_space* s) {
   for (DevBuf* b : bufs) b->release();
   s->hstage.release();
   s->ghost_host.release();
-  if (s->aux) {
-    (void)hipStreamSynchronize(s->aux);
-    (void)hipStreamDestroy(s->aux);
-  }
-  for (hipEvent_t& e : s->pipe_ev)
-    if (e) (void)hipEventDestroy(e);
-  if (s->aux_done) (void)hipEventDestroy(s->aux_done);
   if (s->own_stream && s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
   return SWH_OK;

@@ -1214,6 +1214,8 @@ def main():
             ev[1].record(stream)
         if exchanger:  # the force loop reads the neighbours' new rho
             exchanger.refresh(abi.HALO_RHO)
+        if ev:
+            ev[4].record(stream)
         sp.reset_acceleration(P)
         if ev:
             ev[2].record(stream)
@@ -1227,7 +1229,7 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(events[k])
@@ -1238,6 +1240,18 @@ def main():
     elapsed = time.perf_counter() - t0
     t_dens = [e[0].elapsed_time(e[1]) * 1e-3 for e in events]
     t_force = [e[2].elapsed_time(e[3]) * 1e-3 for e in events]
+    # the halo refresh of rho (pack, point-to-point swap, unpack) per rank
+    halo = None
+    if plan is not None and world > 1:
+        rec_b = abi.HALO_RECORD_FLOATS * 4
+        mine = {"rank": rank, "owned": int(n_owned), "halo": int(len(local) - n_owned),
+                "peers": len(plan.peers()),
+                "records_sent": int(sum(len(v) for v in plan.send.values())),
+                "records_received": int(sum(c for _, c in plan.recv.values())),
+                "record_bytes": rec_b,
+                "exchange_ms": statistics.mean(e[1].elapsed_time(e[4]) for e in events)}
+        halo = [None] * world
+        dist.all_gather_object(halo, mine)
 
     tot = torch.tensor([float(n_density + n_force) * args.steps, float(n_owned)],
                        dtype=torch.float64, device=RED_DEVICE)
@@ -1360,6 +1374,12 @@ def main():
             "cpu_baseline": None,
             "ranks": RANKS,
         }
+        if halo:
+            out["halo_exchange"] = {
+                "per_rank": halo,
+                "note": "one rho refresh per step between the density and force loops "
+                        "(decomp.DeviceHalo: pack, batch_isend_irecv, unpack on the space's "
+                        "stream); exchange_ms = HIP events around it, mean over the timed steps"}
         if steady:
             out["steady_state"] = steady
         if breakdown:

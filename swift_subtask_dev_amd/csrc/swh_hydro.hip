@@ -62,13 +62,15 @@ __device__ __forceinline__ unsigned int rwrap_of(float base, float dx) {
 // cell): each particle's cell-local fp32 position for the staging (posf) and
 // the displacement record at build time (xd0 = xdiff: a kept list measures
 // drifts from here), and each group's box over its active particles
-// (GroupBox), reduced across the group's 16 lanes -- the build's waves read
-// it with scalar loads. Thread 0 resets the build's device counters.
+// (GroupBox), reduced across the group's 16 lanes, turned into the group's
+// BuildPlan (cell range, centre, rounding bound) that the build's waves read
+// with scalar loads. Thread 0 resets the build's device counters.
 __global__ __launch_bounds__(256) void group_prep_kernel(
     GridDev g, SoA a, const int* __restrict__ pcell, const float4* __restrict__ xdiff,
     const int2* __restrict__ groups, int ngroups, int max_active_bin, double gs1,
-    float4* __restrict__ posf, float4* __restrict__ xd0, GroupBox* __restrict__ gbox,
-    const unsigned int* hmax_bits, float rgs1, float dx, unsigned int* rwrap,
+    float4* __restrict__ posf, float4* __restrict__ xd0, BuildPlan* __restrict__ plan,
+    const unsigned int* hmax_bits, float rgs1, float dx,
+    unsigned int* rwrap,
     unsigned int* rwrap_base, unsigned int* ovf_n, unsigned int* nbuilds,
     const unsigned int* run_if) {
   if (skip_build(run_if)) return;
@@ -99,7 +101,11 @@ __global__ __launch_bounds__(256) void group_prep_kernel(
     }
     b.Rg = fmax(b.Rg, __shfl_xor(b.Rg, o, 16));
   }
-  if (gidx < ngroups && r == 0) gbox[gidx] = b;
+  if (gidx < ngroups && r == 0) {
+    BuildPlan p;
+    build_plan(g, b, (double)__uint_as_float(*hmax_bits) * (double)kGamma * gs1, p);
+    plan[gidx] = p;
+  }
 }
 
 __global__ void zero_u32_kernel(unsigned int* __restrict__ p, int64_t n,
@@ -834,7 +840,7 @@ static ListDev list_dev(swh_space* s) {
   d.ovf = s->nbr_ovf.as<int>();
   d.posf = s->posf.as<const float4>();
   d.diag = s->tuning.diag_mode;
-  d.gbox = s->gbox.as<const GroupBox>();
+  d.plan = s->gplan.as<const BuildPlan>();
   d.ovf_n = ovf_slot(s);
   // per-cell reach pruning only pays on an adaptive (clustered) grid
   d.cell_R = s->grid.adaptive ? s->cell_hreach.as<const float>() : nullptr;
@@ -874,13 +880,13 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
                        s->stream, s->pos.as<const double4>(), s->pcell.as<const int>(), s->n,
                        (float)(kGamma * ld.skin1), s->cell_hreach.as<unsigned int>(), run_if);
   }
-  SWH_TRY(s->gbox.reserve((size_t)std::max(1, s->ngroups) * sizeof(GroupBox)));
+  SWH_TRY(s->gplan.reserve((size_t)std::max(1, s->ngroups) * sizeof(BuildPlan)));
   ListDev ldb = list_dev(s);
   hipLaunchKernelGGL(group_prep_kernel, dim3(std::max(1, (s->ngroups + 15) / 16)), dim3(256), 0,
                      s->stream, grid_dev(s), soa_of(s), s->pcell.as<const int>(),
                      s->xdiff.as<const float4>(), s->groups.as<const int2>(), s->ngroups,
                      P->max_active_bin, (double)ld.skin1, s->posf.as<float4>(),
-                     s->list_xd0.as<float4>(), s->gbox.as<GroupBox>(), hmax_slot(s),
+                     s->list_xd0.as<float4>(), s->gplan.as<BuildPlan>(), hmax_slot(s),
                      (float)(kGamma * ld.skin1), (float)s->grid.dx, rwrap_slot(s),
                      rwrap_base_slot(s), ovf_slot(s), nbuild_slot(s), run_if);
   hipLaunchKernelGGL(list_build_kernel, dim3(s->ngroups), dim3(64), 0, s->stream, grid_dev(s),

@@ -203,7 +203,7 @@ struct swh_space {
   // next upload / rebuild / tuning change, or a ghost that grows an H past its R
   swh::DevBuf nbr, nbr_cnt, nbr_base, nbr_reach, nbr_ovf;
   swh::DevBuf posf;  // float4: position relative to its grid cell's corner, h
-  swh::DevBuf gbox;  // GroupBox per i-group: the list build's group boxes
+  swh::DevBuf gplan;  // BuildPlan per i-group: the list build's wave-uniform setup
   swh::DevBuf list_xd0;  // float4: the displacement record (xdiff) at the list build
   bool list_valid = false;
   bool list_check = false;  // kept lists after a drift: the device checks them first

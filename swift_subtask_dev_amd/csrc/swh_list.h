@@ -72,6 +72,22 @@ struct GroupBox {
   double lo[3], hi[3], Rg, pad;
 };
 
+// The wave-uniform part of a group's list build, computed once per group by
+// group_prep_kernel from its box (so the build wave starts from scalar loads
+// instead of ~170 VALU instructions of fp64 setup): the cell range around the
+// box out to reach = max(R_group, R_max) + dx, the box centre and half
+// extent, and the rounding bound delta of the fp32 relative coordinates.
+struct BuildPlan {
+  double ctr[3], half[3];
+  double Rg, Rmax, delta;
+  int lo[3], hi[3];
+  int full;  // bit k: the range spans the periodic box along k
+  int nx, nxy, ncells;
+  float hf[3], Rgf, deltaf, inv_nx, inv_nxy;
+  int pad[1];
+};
+static_assert(sizeof(BuildPlan) % 16 == 0, "plans are read as 16-byte words");
+
 struct ListDev {
   int* nbr;      // entries: sorted j indices
   int* cnt;      // per particle: entries found (> K: overflow, searched instead)
@@ -89,7 +105,7 @@ struct ListDev {
                         // null on a uniform grid (no per-cell pruning)
   int diag;      // profiling only: 2 = the build writes no entries
   const unsigned int* mark;  // nullable: particles the walks leave to a search (ghost-grown H)
-  const GroupBox* gbox;  // per group (group_prep_kernel), read by the build
+  const BuildPlan* plan;  // per group (group_prep_kernel), read by the build
 };
 
 __device__ __forceinline__ void box_init(GroupBox& b) {
@@ -106,6 +122,52 @@ __device__ __forceinline__ void box_add(GroupBox& b, const double4& p, double R)
   b.hi[1] = p.y > b.hi[1] ? p.y : b.hi[1];
   b.hi[2] = p.z > b.hi[2] ? p.z : b.hi[2];
   b.Rg = R > b.Rg ? R : b.Rg;
+}
+
+
+__device__ __forceinline__ void build_plan(const GridDev& g, const GroupBox& b, double Rmax,
+                                           BuildPlan& p) {
+  p.Rg = b.Rg;
+  p.Rmax = Rmax;
+  // r < max(R_i, R_j); cells are enumerated out to reach + dx (drift)
+  const double reach = fmax(b.Rg, Rmax) + g.dx;
+  double D2 = 0.;
+  p.full = 0;
+  for (int k = 0; k < 3; k++) {
+    int lo = (int)floor((b.lo[k] - g.origin[k] - reach) * g.inv_w[k]);
+    int hi = (int)floor((b.hi[k] - g.origin[k] + reach) * g.inv_w[k]);
+    bool full = false;
+    if (g.periodic) {
+      full = (hi - lo + 1 >= g.cdim[k]);
+      if (full) {
+        lo = 0;
+        hi = g.cdim[k] - 1;
+      }
+    } else {
+      lo = max(lo, 0);
+      hi = min(hi, g.cdim[k] - 1);
+    }
+    p.lo[k] = lo;
+    p.hi[k] = hi;
+    p.full |= full ? 1 << k : 0;
+    p.ctr[k] = 0.5 * (b.lo[k] + b.hi[k]);
+    p.half[k] = 0.5 * (b.hi[k] - b.lo[k]);
+    const double ext = full ? g.dim[k] : p.half[k] + reach;
+    D2 += ext * ext;
+  }
+  p.nx = p.hi[0] - p.lo[0] + 1;
+  p.nxy = p.nx * (p.hi[1] - p.lo[1] + 1);
+  p.ncells = p.nxy * (p.hi[2] - p.lo[2] + 1);
+  // Rounding bound of the fp32 relative coordinates: a candidate is staged
+  // as fl(local) + fl(cell offset) with |local| <= w, |offset| <= D + w and
+  // |sum| <= D (kThrSlack's argument, swh_wave.h, with 2(D + w) in place of D).
+  const double wmax = fmax(g.w[0], fmax(g.w[1], g.w[2]));
+  p.delta = 16. * kUnitRound * (sqrt(D2) + wmax);
+  p.deltaf = (float)p.delta;
+  for (int k = 0; k < 3; k++) p.hf[k] = (float)(p.half[k] + p.delta);
+  p.Rgf = (float)(b.Rg + p.delta);
+  p.inv_nx = 1.f / (float)p.nx;
+  p.inv_nxy = 1.f / (float)p.nxy;
 }
 
 // Per-cell maximum R = gamma h (1 + skin): the list build skips a cell whose
@@ -402,61 +464,38 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
   double4 pi = make_double4(0., 0., 0., 0.);
   if (act) pi = a.pos[i];
   const double Ri = act ? pi.w * (double)kGamma * skin1 : 0.;
-  // group box and reach (wave-uniform)
-  const GroupBox gb = ld.gbox[gid < ngroups ? gid : 0];
-  const double Rg = gid < ngroups ? gb.Rg : 0.;
-  const double lo[3] = {gb.lo[0], gb.lo[1], gb.lo[2]};
-  const double hi[3] = {gb.hi[0], gb.hi[1], gb.hi[2]};
+  // the group's build plan (wave-uniform: scalar loads)
+  const BuildPlan& P = ld.plan[gid < ngroups ? gid : 0];
+  const double Rg = gid < ngroups ? P.Rg : 0.;
   TileStats ts;
   const int gbase = gid * kListSlots;
   int nq = 0, wr = 0;
   if (Rg > 0.) {
-    const double Rmax = (double)__uint_as_float(*hmax_bits) * (double)kGamma * skin1;
-    // r < max(R_i, R_j); cells are enumerated out to reach + dx (drift)
-    const double reach = fmax(Rg, Rmax) + g.dx;
+    const double Rmax = P.Rmax;
     CellRange c;
     double ctr[3], half[3];
-    double D2 = 0.;
     for (int k = 0; k < 3; k++) {
-      c.lo[k] = uni_i((int)floor((lo[k] - g.origin[k] - reach) * g.inv_w[k]));
-      c.hi[k] = uni_i((int)floor((hi[k] - g.origin[k] + reach) * g.inv_w[k]));
-      c.full[k] = false;
-      if (g.periodic) {
-        c.full[k] = (c.hi[k] - c.lo[k] + 1 >= g.cdim[k]);
-        if (c.full[k]) {
-          c.lo[k] = 0;
-          c.hi[k] = g.cdim[k] - 1;
-        }
-      } else {
-        c.lo[k] = max(c.lo[k], 0);
-        c.hi[k] = min(c.hi[k], g.cdim[k] - 1);
-      }
-      ctr[k] = uni_d(0.5 * (lo[k] + hi[k]));
-      half[k] = 0.5 * (hi[k] - lo[k]);
-      const double ext = c.full[k] ? g.dim[k] : half[k] + reach;
-      D2 += ext * ext;
+      c.lo[k] = P.lo[k];
+      c.hi[k] = P.hi[k];
+      c.full[k] = (P.full >> k) & 1;
+      ctr[k] = P.ctr[k];
+      half[k] = P.half[k];
     }
-    const int nx = c.hi[0] - c.lo[0] + 1;
-    const int ny = c.hi[1] - c.lo[1] + 1;
-    const int nxy = nx * ny;
-    const int ncells = nxy * (c.hi[2] - c.lo[2] + 1);
-    // Rounding bound of the fp32 relative coordinates: a candidate is staged
-    // as fl(local) + fl(cell offset) with |local| <= w, |offset| <= D + w and
-    // |sum| <= D (kThrSlack's argument, swh_wave.h, with 2(D + w) in place of D).
-    const double wmax = fmax(g.w[0], fmax(g.w[1], g.w[2]));
-    const double delta = 16. * kUnitRound * (sqrt(D2) + wmax);
-    const float deltaf = uni_f((float)delta);
+    const int nx = P.nx;
+    const int nxy = P.nxy;
+    const int ncells = P.ncells;
+    const double delta = P.delta;
+    const float deltaf = P.deltaf;
     const float xi = (float)(pi.x - ctr[0]);
     const float yi = (float)(pi.y - ctr[1]);
     const float zi = (float)(pi.z - ctr[2]);
     const float thr_i = act ? (float)((Ri + delta) * (Ri + delta)) * kThrSlack : -1.f;
-    const float hxf = uni_f((float)(half[0] + delta)), hyf = uni_f((float)(half[1] + delta)),
-                hzf = uni_f((float)(half[2] + delta));
-    const float Rgf = uni_f((float)(Rg + delta));
+    const float hxf = P.hf[0], hyf = P.hf[1], hzf = P.hf[2];
+    const float Rgf = P.Rgf;
     const float gs1 = (float)((double)kGamma * skin1);
-    const bool wrap = c.full[0] || c.full[1] || c.full[2];
+    const bool wrap = P.full != 0;
     const float bx = (float)g.dim[0], by = (float)g.dim[1], bz = (float)g.dim[2];
-    const float inv_nx = 1.f / (float)nx, inv_nxy = 1.f / (float)nxy;
+    const float inv_nx = P.inv_nx, inv_nxy = P.inv_nxy;
     // Staging, in batches of up to 64 cells (one lane per cell: its sorted
     // range and the offset of its lower corner from the group centre go to
     // LDS with a prefix sum of the counts). Candidates are then streamed

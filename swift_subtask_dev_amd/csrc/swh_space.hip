@@ -687,7 +687,7 @@ swh_status swh_space_destroy(swh_space* s) {
                     &s->scan_tmp, &s->counters, &s->tmp_soa, &s->ghost_left,
                     &s->ghost_right, &s->ghost_list, &s->ghost_list2, &s->ghost_search, &s->ghost_seg, &s->grown_q,
                     &s->grown_mark, &s->grown_search,
-                    &s->nbr, &s->nbr_cnt, &s->nbr_base, &s->nbr_reach, &s->nbr_ovf, &s->posf, &s->gbox, &s->ctr_stripes,
+                    &s->nbr, &s->nbr_cnt, &s->nbr_base, &s->nbr_reach, &s->nbr_ovf, &s->posf, &s->gplan, &s->ctr_stripes,
                     &s->iperm, &s->vfull_s, &s->agrav_s, &s->hasg_s, &s->list_xd0};
   for (DevBuf* b : bufs) b->release();
   s->hstage.release();

@@ -276,9 +276,18 @@ __device__ __forceinline__ void list_flush(const ListDev& ld, LDS& L, int& nq, i
       for (int q = 0; q < 4; q++) sl[q] = t + q * LPI < nk ? list[t + q * LPI] : 0;
 #pragma unroll
       for (int q = 0; q < 4; q++) jv[q] = L.candj[sl[q]];
+      if (LPI == 4 && (wr & 15) == 0 && t + 3 * LPI < nk) {
+        // an i's first flush (wr = 0, the usual case) puts a lane's four
+        // entries wr + t + 4q in one 16-byte word of the walk layout
+        // (list_off4: entry k -> column k % 4, row k / 4, rows 4w..4w+3 of
+        // window w together): one store
+        *reinterpret_cast<int4*>(&ld.nbr[list_at(gbase + il, ld.KS, wr + t)]) =
+            make_int4(jv[0], jv[1], jv[2], jv[3]);
+      } else {
 #pragma unroll
-      for (int q = 0; q < 4; q++)
-        if (t + q * LPI < nk) ld.nbr[list_at(gbase + il, ld.KS, wr + t + q * LPI)] = jv[q];
+        for (int q = 0; q < 4; q++)
+          if (t + q * LPI < nk) ld.nbr[list_at(gbase + il, ld.KS, wr + t + q * LPI)] = jv[q];
+      }
     }
   }
   wr += nq;

@@ -41,10 +41,10 @@ namespace swh {
 constexpr int kListSlots = 16;   // list columns per i-group (max group size)
 constexpr int kListLpiBuild = 4;  // lanes per i in the list build
 #ifndef SWH_LIST_REGION
-#define SWH_LIST_REGION 256
+#define SWH_LIST_REGION 192
 #endif
 #ifndef SWH_LIST_ICAP
-#define SWH_LIST_ICAP 96
+#define SWH_LIST_ICAP 64
 #endif
 constexpr int kListRegion = SWH_LIST_REGION;  // staged candidates per region of the build
 constexpr int kListBlk = 8;  // candidates per lane per test block of the build

@@ -844,8 +844,6 @@ static ListDev list_dev(swh_space* s) {
   d.ovf_n = ovf_slot(s);
   // per-cell reach pruning only pays on an adaptive (clustered) grid
   d.cell_R = s->grid.adaptive ? s->cell_hreach.as<const float>() : nullptr;
-  // per-cell displacement bounds once particles have drifted (build_lists)
-  d.cell_dx = s->grid.dx > 0. ? s->cell_dx.as<const float>() : nullptr;
   d.mark = nullptr;
   return d;
 }
@@ -872,7 +870,6 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
   SWH_TRY(s->posf.reserve((size_t)s->n * sizeof(float4)));
   SWH_TRY(s->list_xd0.reserve((size_t)s->n * sizeof(float4)));
   SWH_TRY(s->cell_hreach.reserve((size_t)std::max(1, s->grid.ncell) * sizeof(float)));
-  SWH_TRY(s->cell_dx.reserve((size_t)std::max(1, s->grid.ncell) * sizeof(float)));
   s->list_K = K;
   const ListDev ld = list_dev(s);
   if (ld.cell_R) {
@@ -884,13 +881,6 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
                        (float)(kGamma * ld.skin1), s->cell_hreach.as<unsigned int>(), run_if);
   }
   SWH_TRY(s->gplan.reserve((size_t)std::max(1, s->ngroups) * sizeof(BuildPlan)));
-  if (s->grid.dx > 0.) {  // drifted since the rebuild: the cells' displacement bounds
-    hipLaunchKernelGGL(zero_u32_kernel, dim3((s->grid.ncell + 255) / 256), dim3(256), 0,
-                       s->stream, s->cell_dx.as<unsigned int>(), (int64_t)s->grid.ncell, run_if);
-    hipLaunchKernelGGL(cell_disp_kernel, dim3((int)((s->n + 255) / 256)), dim3(256), 0, s->stream,
-                       s->xdiff.as<const float4>(), s->pcell.as<const int>(), s->n,
-                       s->cell_dx.as<unsigned int>(), run_if);
-  }
   ListDev ldb = list_dev(s);
   hipLaunchKernelGGL(group_prep_kernel, dim3(std::max(1, (s->ngroups + 15) / 16)), dim3(256), 0,
                      s->stream, grid_dev(s), soa_of(s), s->pcell.as<const int>(),

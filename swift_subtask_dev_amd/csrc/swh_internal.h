@@ -194,7 +194,6 @@ struct swh_space {
   swh::DevBuf cell_code;   // uint32[ncell]: Morton code of each rank (ascending)
   swh::DevBuf cell_span;   // int2[ncell]: linear cell -> sorted range
   swh::DevBuf cell_hreach; // float[ncell]: max R = gamma h (1 + skin) of the cell (list build)
-  swh::DevBuf cell_dx;     // float[ncell]: max displacement of the cell's particles since the rebuild
   int rank_cdim[3] = {0, 0, 0};  // grid the rank table was built for
   swh::DevBuf groups;      // int2[ngroups]: i-groups (start, count) of the tile loops
   swh::DevBuf seg_groups, seg_off;

@@ -103,8 +103,6 @@ struct ListDev {
   unsigned int* ovf_n;
   const float* cell_R;  // per linear grid cell: max R of its particles (cell_reach_kernel);
                         // null on a uniform grid (no per-cell pruning)
-  const float* cell_dx;  // per linear grid cell: max displacement of its particles since
-                         // the rebuild (cell_disp_kernel; null before any drift)
   int diag;      // profiling only: 2 = the build writes no entries
   const unsigned int* mark;  // nullable: particles the walks leave to a search (ghost-grown H)
   const BuildPlan* plan;  // per group (group_prep_kernel), read by the build
@@ -179,21 +177,6 @@ __device__ __forceinline__ void build_plan(const GridDev& g, const GroupBox& b, 
 // rebuild): after a drift it may stand outside that cell's box, and the build
 // stages it from there (the box gaps allow for g.dx); inhibited particles
 // (pcell < 0) are in no cell.
-// Per-cell displacement bound since the rebuild (after a drift): the largest
-// |xdiff| of the particles the cell's sorted range holds, float bits, rounded
-// up (the list build's per-cell pruning, SWIFT's cell dx_max_part).
-__global__ void cell_disp_kernel(const float4* __restrict__ xdiff, const int* __restrict__ pcell,
-                                 int64_t n, unsigned int* __restrict__ cell_dx,
-                                 const unsigned int* run_if) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n || (run_if && *run_if == 0u)) return;
-  const int lin = pcell[j];
-  if (lin < 0) return;
-  const float4 d = xdiff[j];
-  const float r = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z) * (1.f + 1e-5f) + 1e-30f;
-  atomicMax(&cell_dx[lin], __float_as_uint(r));
-}
-
 __global__ void cell_reach_kernel(const double4* __restrict__ pos, const int* __restrict__ pcell,
                                   int64_t n, float gs1, unsigned int* __restrict__ cell_R,
                                   const unsigned int* run_if) {
@@ -553,19 +536,15 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
         ox = (float)dox;
         oy = (float)doy;
         oz = (float)doz;
-        if (cnt > 0 && ((ld.cell_R && Rmax > Rg) || ld.cell_dx)) {
+        if (cnt > 0 && ld.cell_R && Rmax > Rg) {
           // prune by the cell's own reach: box gap group <-> cell (an axis
-          // spanning the whole periodic box has no gap). After a drift the
-          // cell's particles stand up to its own displacement bound outside
-          // its box (SWIFT's per-cell dx_max_part): the range was widened by
-          // the largest one, and the cells of that ring whose particles
-          // moved less are dropped here
-          const int lin = (wz * g.cdim[1] + wy) * g.cdim[0] + wx;
-          const double cdx = ld.cell_dx ? (double)ld.cell_dx[lin] : g.dx;
-          const double gx = c.full[0] ? 0. : fmax(fmax(dox - half[0], -half[0] - dox - g.w[0]) - cdx, 0.);
-          const double gy = c.full[1] ? 0. : fmax(fmax(doy - half[1], -half[1] - doy - g.w[1]) - cdx, 0.);
-          const double gz = c.full[2] ? 0. : fmax(fmax(doz - half[2], -half[2] - doz - g.w[2]) - cdx, 0.);
-          const double Rc = fmax(Rg, ld.cell_R ? (double)ld.cell_R[lin] : Rmax) + delta;
+          // spanning the whole periodic box has no gap)
+          // (the cell's particles may stand g.dx outside its box after a drift)
+          const double gx = c.full[0] ? 0. : fmax(fmax(dox - half[0], -half[0] - dox - g.w[0]) - g.dx, 0.);
+          const double gy = c.full[1] ? 0. : fmax(fmax(doy - half[1], -half[1] - doy - g.w[1]) - g.dx, 0.);
+          const double gz = c.full[2] ? 0. : fmax(fmax(doz - half[2], -half[2] - doz - g.w[2]) - g.dx, 0.);
+          const double Rc = fmax(Rg, (double)ld.cell_R[(wz * g.cdim[1] + wy) * g.cdim[0] + wx]) +
+                            delta;
           if (gx * gx + gy * gy + gz * gz > Rc * Rc * (1. + 1e-6)) cnt = 0;
         }
       }

@@ -681,7 +681,7 @@ swh_status swh_space_destroy(swh_space* s) {
   (void)hipStreamSynchronize(s->stream);
   DevBuf* bufs[] = {&s->aos, &s->pos, &s->vm, &s->th, &s->fc, &s->tb, &s->dens, &s->rot,
                     &s->grad, &s->acc, &s->hdt, &s->mintb, &s->perm, &s->ncount,
-                    &s->cell_start, &s->cell_rank, &s->cell_code, &s->cell_span, &s->cell_hreach, &s->cell_dx,
+                    &s->cell_start, &s->cell_rank, &s->cell_code, &s->cell_span, &s->cell_hreach,
                     &s->vfull_c, &s->agrav_c, &s->hasg_c, &s->xdiff, &s->pcell, &s->cell_lin, &s->groups, &s->seg_groups,
                     &s->seg_off, &s->keys, &s->keys2, &s->idx, &s->idx2, &s->sort_tmp,
                     &s->scan_tmp, &s->counters, &s->tmp_soa, &s->ghost_left,

@@ -450,6 +450,61 @@ def chain_vs_f32(raw, gpu, gpu_counts, P, workload):
             "all_ok": all(r["ok"] for r in res.values()) and all(c["ok"] for c in cnt.values())}
 
 
+def flow_vs_f32(ctx, n=64):
+    """Outside the timed region: the terms the Sedov input (v = 0) leaves at
+    zero -- the artificial viscosity of approaching pairs, the diffusion, the
+    switch evolution -- on ics.flow_box(n) (converging, shearing flow, lumpy
+    u): the GPU's whole chain against the float restatement's and the f64
+    oracle's chains, under tests/parity_bars.py's flow64 bars (the check
+    test_gpu_physics.py::test_flow_chain_vs_f32_and_f64 asserts)."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib as O
+    import parity_bars as B
+    from swift_subtask_dev_amd import abi, ics, lib
+
+    parts = ics.flow_box(n)
+    P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
+    P.max_active_bin = 1
+    g = abi.copy_parts(parts)
+    sp = lib.HydroSpace(ctx)
+    sp.upload(g)
+    sp.rebuild(P)
+    res = sp.hydro_step(P)
+    sp.download(g, abi.FIELDS_ALL)
+    sp.close()
+    chains = {}
+    for prec in ("f32", "f64"):
+        o = abi.copy_parts(parts)
+        N = len(o)
+        O.fn("f32", "init_parts")(o.ctypes.data, N, C.byref(P))
+        cnt = {"density": O.fn(prec, "box_density")(o.ctypes.data, N, C.byref(P), None)}
+        nfail = C.c_longlong(0)
+        O.fn(prec, "box_ghost")(o.ctypes.data, N, C.byref(P), C.byref(nfail))
+        cnt["gradient"] = O.fn(prec, "box_gradient")(o.ctypes.data, N, C.byref(P), None)
+        O.fn(prec, "box_extra_ghost")(o.ctypes.data, N, C.byref(P))
+        cnt["force"] = O.fn(prec, "box_force")(o.ctypes.data, N, C.byref(P), None)
+        O.fn(prec, "box_end_force")(o.ctypes.data, N, C.byref(P))
+        chains[prec] = (o[np.argsort(o["id"], kind="stable")], cnt)
+    g = g[np.argsort(g["id"], kind="stable")]
+    (o32, c32), (o64, c64) = chains["f32"], chains["f64"]
+    bars = B.BARS["flow64"]
+    sg, so = B.summary(g, o32, bars), B.summary(o64, o32, bars)
+    fields = {f: {"max": sg[f][0], "p99.9": sg[f][1], "bar_max": bars[f][0],
+                  "bar_p99.9": bars[f][1], "f64_oracle_max": so[f][0], "f64_oracle_p99.9": so[f][1],
+                  "ok": bool(sg[f][0] <= bars[f][0] and sg[f][1] <= bars[f][1]
+                             and sg[f][0] <= 1.1 * so[f][0] + 1e-6
+                             and sg[f][1] <= 1.1 * so[f][1] + 1e-6)} for f in bars}
+    counts = {k: {"gpu": int(res[k]), "f32": int(c32[k]), "f64": int(c64[k]),
+                  "ok": bool(abs(res[k] - c32[k]) <= B.COUNT_REL * c32[k] and res[k] == c64[k])}
+              for k in ("density", "gradient", "force")}
+    return {"vs": f"ics.flow_box({n}) (converging shearing flow: mu_ij < 0 viscosity, diffusion "
+                  "and switches live): the GPU chain against liboracle_f32's chain (bars) and "
+                  "liboracle_f64's (counts exact)",
+            "viscous_heating_frac": float((o64["u_dt"] > 0).mean()),
+            "fields": fields, "counts": counts,
+            "all_ok": all(v["ok"] for v in fields.values()) and all(v["ok"] for v in counts.values())}
+
+
 def step_breakdown(sp, P, stream, torch, local, reps=3):
     """Per-phase times of a whole SWIFT hydro step on the device-resident box,
     measured AFTER the timed region (not part of `value`): drift (drift_part +
@@ -1442,6 +1497,11 @@ def main():
                     raw, chain_gpu, chain, P, args.workload)
             except Exception as e:  # report, never fake
                 log(f"chain parity check failed: {e}")
+            if not eagle:
+                try:
+                    out.setdefault("parity", {})["flow_vs_f32"] = flow_vs_f32(ctx)
+                except Exception as e:  # report, never fake
+                    log(f"flow parity check failed: {e}")
     sp.close()
     ctx.close()
     if rank == 0:

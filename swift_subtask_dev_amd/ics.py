@@ -96,6 +96,29 @@ def sedov_box(n: int, eta: float = 1.2348, pert: float = 0.1, seed: int = 0x5EED
     return p
 
 
+def flow_box(n: int, seed: int = 64) -> np.ndarray:
+    """A periodic n^3 box in a converging, shearing flow with a lumpy internal
+    energy, smoothing lengths off target (the ghost iterates) and switch
+    state as an earlier step leaves it (div_v_previous_step, alphas): every
+    term of the SPHENIX chain is live -- the artificial viscosity of
+    approaching pairs (mu_ij < 0), the diffusion, the viscosity switch
+    (hydro_iact.h:130-609, hydro.h:714-934). All particles active."""
+    rng = _rng(seed)
+    p = sedov_box(n, pert=0.3, seed=seed)
+    N = len(p)
+    x = p["x"]
+    v = -2.0 * (x - 0.5) + rng.normal(0.0, 0.3, (N, 3))
+    v[:, 0] += 0.8 * np.sin(2 * np.pi * x[:, 1])  # shear: rot_v != 0
+    p["v"] = v.astype(np.float32)
+    p["u"] = (1.0 + 0.5 * np.sin(2 * np.pi * x[:, 0]) * np.cos(2 * np.pi * x[:, 2])
+              + 0.2 * rng.uniform(size=N)).astype(np.float32)
+    p["h"] *= rng.uniform(0.85, 1.2, N)
+    p["div_v_previous_step"] = rng.uniform(-4.0, 4.0, N)
+    p["visc_alpha"] = rng.uniform(0.0, 1.5, N)
+    p["diff_alpha"] = rng.uniform(0.0, 0.8, N)
+    return p
+
+
 def clustered_box(n_bg: int, n_clumps: int = 8, per_clump: int = 4096, seed: int = 6,
                   eta: float = 1.2348) -> np.ndarray:
     """EAGLE_6-like stand-in: a uniform background lattice plus

@@ -444,6 +444,38 @@ def test_baseline_chain_from_unconverged_vs_f32(gpu_ctx, which):
         assert gm <= 1.1 * om + 1e-6 and gq <= 1.1 * oq + 1e-6, (f, sg[f], so[f])
 
 
+def test_flow_chain_vs_f32_and_f64(gpu_ctx):
+    """The terms the Sedov headline leaves at zero against the reference's
+    own float precision: ics.flow_box(64) (converging, shearing flow, lumpy
+    u, h off target, earlier switch state) through the whole GPU chain vs
+    the f32 oracle chain under tests/parity_bars.py's flow64 bars and the
+    "no farther than the f64 oracle" rule, and vs the f64 oracle chain at
+    check_chain's tolerances. bench.py's parity block reports the same
+    comparison (parity.flow_vs_f32)."""
+    import parity_bars as B
+    parts = ics.flow_box(64)
+    P = abi.default_hydro_params((1.0, 1.0, 1.0), True)
+    P.max_active_bin = 1
+    g, rg = gpu_chain(gpu_ctx, parts, P)
+    o, ro = oracle_chain(parts, P)
+    o32, ro32 = oracle_chain(parts, P, precision="f32")
+    check_chain(g, rg, o, ro, np.ones(len(parts), dtype=bool))
+    bars = B.BARS["flow64"]
+    for k in ("density", "gradient", "force"):
+        assert abs(rg[k] - ro32[k]) <= B.COUNT_REL * ro32[k], (k, rg[k], ro32[k])
+        assert abs(rg[k] - ro32[k]) <= abs(ro[k] - ro32[k]), (k, rg[k], ro[k], ro32[k])
+    g, o, o32 = _by_id(g), _by_id(o), _by_id(o32)
+    # the viscosity of approaching pairs is live: viscous heating du/dt > 0
+    # across the converging box
+    assert (o["u_dt"] > 0).mean() > 0.5
+    sg, so = B.summary(g, o32, bars), B.summary(o, o32, bars)
+    print(f"\nflow64 vs the f32 chain (max, p99.9): gpu {sg}\n  f64 oracle {so}")
+    for f, (tmax, tq) in bars.items():
+        (gm, gq), (om, oq) = sg[f], so[f]
+        assert gm <= tmax and gq <= tq, (f, sg[f], bars[f])
+        assert gm <= 1.1 * om + 1e-6 and gq <= 1.1 * oq + 1e-6, (f, sg[f], so[f])
+
+
 @pytest.mark.parametrize("which", ["sedov128", "eagle"])
 def test_baseline_chain_from_unconverged_vs_f64(gpu_ctx, which):
     """h at the BASELINE sizes: the GPU's whole chain (density, ghost

@@ -243,8 +243,13 @@ __global__ void rank_scatter_kernel(const int* __restrict__ sorted_lin, int ncel
 // fit. A block at level L = the aligned 2^L-cube of cells sharing code >> 3L;
 // its cells are one contiguous rank range (ranks sorted by code). One thread
 // per cell; the first cell of a leaf block emits its group. Cells holding more
-// than kGroupMax particles are split into chunks of kGroupMax.
+// than kGroupMax particles are split into full chunks of kGroupMax; the
+// remainder joins the sibling run that follows it (round 6: at the 128^3
+// lattice's 18-particle cells it no longer takes a build wave of its own).
 constexpr int kMaxLevel = 10;  // 30-bit codes
+#ifndef SWH_GROUP_TAIL_MERGE
+#define SWH_GROUP_TAIL_MERGE 1
+#endif
 
 __device__ __forceinline__ int lower_bound_u32(const uint32_t* __restrict__ a, int n,
                                                uint32_t v) {
@@ -286,51 +291,66 @@ __global__ void group_kernel(const uint32_t* __restrict__ code, const int* __res
     if (WRITE) out[off[r] + ng] = make_int2(start, count);
     ng++;
   };
-  if (n0 > kGroupMax) {  // oversized cell: chunks
-    for (int s = 0; s < n0; s += kGroupMax) emit(cs[r] + s, min(kGroupMax, n0 - s));
-  } else {
-    int L = 0;  // largest level whose block holds <= kGroupMax particles
-    BlockSpan leaf;
-    leaf.r0 = r;
-    leaf.r1 = r + 1;
-    leaf.count = n0;
+  // the level of the largest block around this cell that holds <= kGroupMax
+  // particles (an oversized cell: level 0, the cell itself, split into chunks)
+  int L = 0;
+  BlockSpan leaf;
+  leaf.r0 = r;
+  leaf.r1 = r + 1;
+  leaf.count = n0;
+  if (n0 <= kGroupMax) {
     for (int l = 1; l <= kMaxLevel; l++) {
       const BlockSpan b = block_span(code, cs, ncell, (c >> (3 * l)) << (3 * l), l);
       if (b.count > kGroupMax) break;
       L = l;
       leaf = b;
     }
-    if (leaf.r0 == r && leaf.count > 0) {  // head of a non-empty leaf
-      if (L == kMaxLevel) {
-        emit(cs[leaf.r0], leaf.count);
-      } else {
-        // greedy merge over the parent's children, in order; a child holding
-        // more than kGroupMax particles (split further) breaks the run
-        const int mine = (int)((c >> (3 * L)) & 7u);
-        const uint32_t parent = (c >> (3 * (L + 1))) << (3 * (L + 1));
-        int run_start = -1, run_r0 = 0, sum = 0;
-        for (int o = 0; o < 8; o++) {
-          const BlockSpan ch = block_span(code, cs, ncell, parent + ((uint32_t)o << (3 * L)), L);
-          if (ch.count > kGroupMax) {
-            if (run_start == mine) emit(cs[run_r0], sum);
-            run_start = -1;
-            sum = 0;
-            continue;
-          }
-          if (ch.count == 0) continue;
-          if (run_start >= 0 && sum + ch.count > kGroupMax) {
-            if (run_start == mine) emit(cs[run_r0], sum);
-            run_start = -1;
-            sum = 0;
-          }
-          if (run_start < 0) {
-            run_start = o;
-            run_r0 = ch.r0;
-          }
-          sum += ch.count;
+  }
+  if (leaf.r0 == r && leaf.count > 0) {  // head of a non-empty leaf
+    if (L == kMaxLevel) {
+      emit(cs[leaf.r0], leaf.count);
+    } else {
+      // greedy merge over the parent's children, in order. A child holding
+      // more than kGroupMax particles breaks the run; at the cell level
+      // (L = 0) an oversized cell is cut into full chunks (emitted by its own
+      // thread) and its remainder -- the END of its range, contiguous with
+      // the next cell's -- starts the next run, so a 2-particle tail shares
+      // a wave with its sibling cell instead of taking a build wave alone
+      const int mine = (int)((c >> (3 * L)) & 7u);
+      const uint32_t parent = (c >> (3 * (L + 1))) << (3 * (L + 1));
+      int run_start = -1, run_p0 = 0, sum = 0;
+      for (int o = 0; o < 8; o++) {
+        const BlockSpan ch = block_span(code, cs, ncell, parent + ((uint32_t)o << (3 * L)), L);
+        int cnt = ch.count, p0 = cs[ch.r0];
+        if (cnt > kGroupMax) {
+          if (run_start == mine) emit(run_p0, sum);
+          run_start = -1;
+          sum = 0;
+          if (L > 0) continue;  // a block of several cells: split at a lower level
+#if !SWH_GROUP_TAIL_MERGE
+          if (o == mine)  // rounds 1-5: the remainder is a group of its own
+            for (int q = 0; q < cnt; q += kGroupMax) emit(p0 + q, min(kGroupMax, cnt - q));
+          continue;
+#endif
+          const int full = cnt / kGroupMax * kGroupMax;
+          if (o == mine)
+            for (int q = 0; q < full; q += kGroupMax) emit(p0 + q, kGroupMax);
+          cnt -= full;  // the remainder joins the run that follows
+          p0 += full;
         }
-        if (run_start == mine) emit(cs[run_r0], sum);
+        if (cnt == 0) continue;
+        if (run_start >= 0 && sum + cnt > kGroupMax) {
+          if (run_start == mine) emit(run_p0, sum);
+          run_start = -1;
+          sum = 0;
+        }
+        if (run_start < 0) {
+          run_start = o;
+          run_p0 = p0;
+        }
+        sum += cnt;
       }
+      if (run_start == mine) emit(run_p0, sum);
     }
   }
   if (!WRITE) ngroup[r] = ng;

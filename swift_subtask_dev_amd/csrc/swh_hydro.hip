@@ -198,7 +198,7 @@ void list_build_kernel(GridDev g, SoA a, ListDev ld,
 #define SWH_WALK_WPE_DENS 4
 #endif
 template <int LOOP, typename T>
-__global__ __launch_bounds__(256)
+__global__ __launch_bounds__(kWalkBlock)
 #if SWH_WALK_WPE > 0
 __attribute__((amdgpu_waves_per_eu(SWH_WALK_WPE)))
 #endif
@@ -214,7 +214,7 @@ void walk_kernel(GridDev g, SoA a, ListDev ld, int i0, int n,
 // want 132 VGPRs, i.e. 3 waves; at <= 128 it runs 1.157 -> 1.10 ms per loop
 // at 128^3; the force walk already fits 128 and does not gain).
 template <typename T>
-__global__ __launch_bounds__(256)
+__global__ __launch_bounds__(kWalkBlock)
 #if SWH_WALK_WPE_DENS > 0
 __attribute__((amdgpu_waves_per_eu(SWH_WALK_WPE_DENS)))
 #endif
@@ -942,14 +942,15 @@ static void launch_typed(swh_space* s, const GridDev& gd, const SegList* subset,
                        search_slot(s), max_active_bin, a2H, hmax_slot(s), ctr, ncount);
     return;
   }
+  constexpr int wppb = kWalkBlock / kWalkLpi;
   if (LOOP == LOOP_DENSITY && sizeof(T) == 8)  // (the fp32 walk would spill)
-    hipLaunchKernelGGL((density_walk_kernel<T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
-                       s->stream, gd, soa_of(s), ld, 0, nitems, max_active_bin, a2H,
-                       hmax_slot(s), ctr, ncount);
+    hipLaunchKernelGGL((density_walk_kernel<T>), dim3((nitems + wppb - 1) / wppb),
+                       dim3(kWalkBlock), 0, s->stream, gd, soa_of(s), ld, 0, nitems,
+                       max_active_bin, a2H, hmax_slot(s), ctr, ncount);
   else
-    hipLaunchKernelGGL((walk_kernel<LOOP, T>), dim3((nitems + ppb - 1) / ppb), dim3(block), 0,
-                       s->stream, gd, soa_of(s), ld, 0, nitems, max_active_bin, a2H,
-                       hmax_slot(s), ctr, ncount);
+    hipLaunchKernelGGL((walk_kernel<LOOP, T>), dim3((nitems + wppb - 1) / wppb),
+                       dim3(kWalkBlock), 0, s->stream, gd, soa_of(s), ld, 0, nitems,
+                       max_active_bin, a2H, hmax_slot(s), ctr, ncount);
   hipLaunchKernelGGL((overflow_kernel<LOOP, T>), dim3(64), dim3(block), 0, s->stream, gd,
                      soa_of(s), ld, ld.ovf, ld.ovf_n, max_active_bin, a2H, hmax_slot(s), ctr,
                      ncount);

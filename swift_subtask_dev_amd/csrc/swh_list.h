@@ -735,13 +735,21 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
 
 // One loop over every active, listed particle: LPI lanes per i, 256/LPI
 // consecutive sorted particles per workgroup.
+// Threads per block of the list walks: the waves of one block share a CU's
+// L1, so a larger block walks a contiguous run of sorted i's whose
+// neighbours overlap.
+#ifndef SWH_WALK_BLOCK
+#define SWH_WALK_BLOCK 256
+#endif
+constexpr int kWalkBlock = SWH_WALK_BLOCK;
+
 template <int LOOP, typename T, int LPI>
 __device__ __forceinline__ void list_walk(const GridDev& g, SoA& a, const ListDev ld, int i0, int n,
                                           int max_active_bin, T a2H,
                                           const unsigned int* __restrict__ hmax_bits,
                                           unsigned long long* counter, int* __restrict__ ncount) {
   using S = LoopState<LOOP, T>;
-  constexpr int PPB = 256 / LPI;
+  constexpr int PPB = kWalkBlock / LPI;
   const int i = i0 + xcd_block_id() * PPB + (int)threadIdx.x / LPI;
   const int s = (int)threadIdx.x % LPI;
   bool act = i < n && active_part(a, i, max_active_bin);

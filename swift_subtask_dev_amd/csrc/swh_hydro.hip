@@ -37,10 +37,7 @@ __global__ __launch_bounds__(kCounterStripes) void stripe_reduce_kernel(
 // ---------------------------------------------------------------------------
 // The step's pair lists (swh_list.h).
 // ---------------------------------------------------------------------------
-#ifndef SWH_WALK_LPI
-#define SWH_WALK_LPI 4
-#endif
-constexpr int kWalkLpi = SWH_WALK_LPI;  // lanes per i of the list walks
+// (kWalkLpi, the lanes per i of the list walks: swh_list.h)
 
 // `run_if` (nullable): the list-build kernels of a kept-list step run only
 // when the device check (list_check_kernel) found the kept lists stale, so
@@ -834,7 +831,7 @@ static ListDev list_dev(swh_space* s) {
   d.base = s->nbr_base.as<int>();
   d.reach = s->nbr_reach.as<float>();
   d.K = s->list_K;
-  d.KS = (s->list_K + 15) & ~15;
+  d.KS = list_ks(s->list_K);
   d.skin1 = 1.f + s->list_skin_cur;
   d.rwrap_bits = rwrap_slot(s);
   d.ovf = s->nbr_ovf.as<int>();
@@ -857,7 +854,7 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
   unsigned long long* stripes = nullptr;
   if (count) SWH_TRY(stripes_slot(s, &stripes));
   s->list_skin_cur = skin;
-  SWH_TRY(s->nbr.reserve((size_t)std::max(1, s->ngroups) * ((K + 15) & ~15) * kListSlots *
+  SWH_TRY(s->nbr.reserve((size_t)std::max(1, s->ngroups) * list_ks(K) * kListSlots *
                          sizeof(int)));
   if (K % 4 != 0) {
     set_error("list_capacity must be a multiple of 4");

@@ -49,19 +49,31 @@ constexpr int kListLpiBuild = 4;  // lanes per i in the list build
 constexpr int kListRegion = SWH_LIST_REGION;  // staged candidates per region of the build
 constexpr int kListBlk = 8;  // candidates per lane per test block of the build
 
-// Layout of a group's lists: 16 slots x KS entries (KS = K rounded up to 16).
-// Entry k of slot sl is the m-th entry (m = k / 4) of walk lane s = k % 4 of
-// that slot; lane l = 4 sl + s keeps its entries 4w .. 4w + 3 in one 16-byte
-// word of window w (256 ints: one word per lane), so a walk lane reads four
-// indices with one load.
+// Lanes per i of the list walks (WL); the list layout follows it.
+#ifndef SWH_WALK_LPI
+#define SWH_WALK_LPI 4
+#endif
+constexpr int kWalkLpi = SWH_WALK_LPI;
+static_assert(kWalkLpi == 2 || kWalkLpi == 4 || kWalkLpi == 8, "walk lanes per i: 2, 4 or 8");
+constexpr int kWinInts = kListSlots * kWalkLpi * 4;  // one window row of a group's lists
+
+// Layout of a group's lists: 16 slots x KS entries (KS = K rounded up to
+// 4 WL). Entry k of slot sl is the m-th entry (m = k / WL) of walk lane
+// s = k % WL of that slot; the lane keeps its entries 4w .. 4w + 3 in one
+// 16-byte word of window w (a row of 16 slots x WL words), so a walk lane
+// reads four indices with one load, and at each step the WL lanes of an i
+// take WL consecutive entries.
+__host__ __device__ constexpr int list_ks(int K) {
+  return (K + 4 * kWalkLpi - 1) & ~(4 * kWalkLpi - 1);
+}
 __device__ __forceinline__ size_t list_lane(int base, int KS) {  // base = group * 16 + slot
-  return (size_t)(base >> 4) * (size_t)(kListSlots * KS) + (size_t)((base & 15) * 16);
+  return (size_t)(base >> 4) * (size_t)(kListSlots * KS) + (size_t)((base & 15) * kWalkLpi * 4);
 }
 __device__ __forceinline__ size_t list_off4(int s, int m) {
-  return (size_t)((m >> 2) * 256 + s * 4 + (m & 3));
+  return (size_t)((m >> 2) * kWinInts + s * 4 + (m & 3));
 }
 __device__ __forceinline__ size_t list_at(int base, int KS, int k) {
-  return list_lane(base, KS) + list_off4(k & 3, k >> 2);
+  return list_lane(base, KS) + list_off4(k % kWalkLpi, k / kWalkLpi);
 }
 
 // Per i-group box of the list build (group_prep_kernel): the active
@@ -95,7 +107,7 @@ struct ListDev {
   float* reach;  // per particle: R = gamma h (1 + skin) at build (0: not listed)
   const float4* posf;  // per particle: x, y, z relative to its grid cell's corner, h
   int K;
-  int KS;        // entries per slot in memory (K rounded up to 16)
+  int KS;        // entries per slot in memory (list_ks(K))
   float skin1;   // 1 + skin
   const unsigned int* rwrap_bits;  // max R at build (float bits): particles farther than
                                    // this from every face need no periodic wrap
@@ -276,13 +288,20 @@ __device__ __forceinline__ void list_flush(const ListDev& ld, LDS& L, int& nq, i
       for (int q = 0; q < 4; q++) sl[q] = t + q * LPI < nk ? list[t + q * LPI] : 0;
 #pragma unroll
       for (int q = 0; q < 4; q++) jv[q] = L.candj[sl[q]];
-      if (LPI == 4 && (wr & 15) == 0 && t + 3 * LPI < nk) {
+      if (LPI == 4 && kWalkLpi == 4 && (wr & 15) == 0 && t + 3 * LPI < nk) {
         // an i's first flush (wr = 0, the usual case) puts a lane's four
         // entries wr + t + 4q in one 16-byte word of the walk layout
         // (list_off4: entry k -> column k % 4, row k / 4, rows 4w..4w+3 of
         // window w together): one store
         *reinterpret_cast<int4*>(&ld.nbr[list_at(gbase + il, ld.KS, wr + t)]) =
             make_int4(jv[0], jv[1], jv[2], jv[3]);
+      } else if (LPI == 4 && kWalkLpi == 8 && (wr & 31) == 0 && t + 3 * LPI < nk) {
+        // eight walk lanes: entries wr + t + {0, 8} are rows m, m + 1 of walk
+        // lane t % 8 (m even), wr + t + {4, 12} those of lane t % 8 + 4
+        *reinterpret_cast<int2*>(&ld.nbr[list_at(gbase + il, ld.KS, wr + t)]) =
+            make_int2(jv[0], jv[2]);
+        *reinterpret_cast<int2*>(&ld.nbr[list_at(gbase + il, ld.KS, wr + t + 4)]) =
+            make_int2(jv[1], jv[3]);
       } else {
 #pragma unroll
         for (int q = 0; q < 4; q++)
@@ -677,7 +696,7 @@ __device__ __forceinline__ bool near_face(const GridDev& g, const double4& p, do
 template <int LPI, bool WRAP, typename T, class S>
 __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, const ListDev& ld,
                                              const double4& pi, int nl, int lb, int s, S& st) {
-  static_assert(LPI == 4, "the list layout gives each of four lanes per i its own windows");
+  static_assert(LPI == kWalkLpi, "the list layout gives each walk lane of an i its own windows");
   const int nme = nl > s ? (nl - s + LPI - 1) / LPI : 0;  // this lane's entries
   const int nw = (nme + 3) >> 2;
   if (nw == 0) return;
@@ -703,7 +722,7 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
       const int q = m & 3;
       if (q == 0) {
         cur = wv;
-        if (m + 4 < nme) wv = *reinterpret_cast<const int4*>(lanep + ((m >> 2) + 1) * 256);
+        if (m + 4 < nme) wv = *reinterpret_cast<const int4*>(lanep + ((m >> 2) + 1) * kWinInts);
       }
       const int j = q == 0 ? cur.x : q == 1 ? cur.y : q == 2 ? cur.z : cur.w;
       const double4 pj = a.pos[j];
@@ -714,7 +733,7 @@ __device__ __forceinline__ void walk_entries(const GridDev& g, const SoA& a, con
   }
   for (int w = 0; w < nw; w++) {
     const int jv[4] = {wv.x, wv.y, wv.z, wv.w};
-    if (w + 1 < nw) wv = *reinterpret_cast<const int4*>(lanep + (w + 1) * 256);
+    if (w + 1 < nw) wv = *reinterpret_cast<const int4*>(lanep + (w + 1) * kWinInts);
     const int mrem = nme - 4 * w;  // entries of this window (>= 1)
     {
       double4 pj[4];

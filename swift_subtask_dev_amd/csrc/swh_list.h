@@ -275,7 +275,9 @@ template <int LPI, class LDS>
 __device__ __forceinline__ void list_flush(const ListDev& ld, LDS& L, int& nq, int& wr, int il,
                                            int s, int gbase, TileStats& ts) {
   wave_sync();  // list entries were written by the other lanes of i
+#ifndef SWH_DIAG_CELLS
   ts.bsteps += (unsigned int)(nq > s ? (nq - s + LPI - 1) / LPI : 0);  // this lane's entries
+#endif
   const typename LDS::HitT* list = &L.hits[il * LDS::kStride];
 
   if (ld.diag != 2) {
@@ -338,7 +340,9 @@ __device__ __forceinline__ void list_consume(const GridDev& g, const ListDev& ld
   constexpr int GS = 64 / LPI;
   const int dummy = GS * LDS::kStride + il * LPI + s;
   const int nblk = (nst + kListBlk * LPI - 1) / (kListBlk * LPI);
+#ifndef SWH_DIAG_CELLS
   ts.asteps += (unsigned int)(nblk * kListBlk);
+#endif
   const float bx = (float)g.dim[0], by = (float)g.dim[1], bz = (float)g.dim[2];
   for (int b = 0; b < nblk; b++) {
     if (__any(nq > LDS::kICap - kListBlk * LPI)) list_flush<LPI>(ld, L, nq, wr, il, s, gbase, ts);
@@ -567,6 +571,10 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
           if (gx * gx + gy * gy + gz * gz > Rc * Rc * (1. + 1e-6)) cnt = 0;
         }
       }
+#ifdef SWH_DIAG_CELLS  // profiling only: asteps / bsteps count cells enumerated / staged from
+      if (lane == 0) ts.asteps += (unsigned int)min(64, ncells - cb);
+      ts.bsteps += cnt > 0 ? 1u : 0u;
+#endif
       const int inc = wave_incl_scan(cnt);
       const int total = __builtin_amdgcn_readlane(inc, 63);
       const int cpre = inc - cnt;  // this lane's cell: first position in the batch

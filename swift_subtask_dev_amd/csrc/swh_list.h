@@ -571,6 +571,9 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
           if (gx * gx + gy * gy + gz * gz > Rc * Rc * (1. + 1e-6)) cnt = 0;
         }
       }
+#ifdef SWH_DIAG_ENUM  // profiling only (diag 1): enumerate and prune the cells, stage nothing
+      if (diag == 1) cnt = 0;
+#endif
 #ifdef SWH_DIAG_CELLS  // profiling only: asteps / bsteps count cells enumerated / staged from
       if (lane == 0) ts.asteps += (unsigned int)min(64, ncells - cb);
       ts.bsteps += cnt > 0 ? 1u : 0u;

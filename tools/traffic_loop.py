@@ -32,7 +32,7 @@ def measured_commit():
     except OSError:
         return None
 
-DENSITY = ["swh::posf_kernel", "swh::group_box_kernel", "swh::group_prep_kernel", "swh::list_build_kernel",
+DENSITY = ["swh::posf_kernel", "swh::group_box_kernel", "swh::cell_reach_kernel", "swh::group_prep_kernel", "swh::list_build_kernel",
            "void swh::density_walk_kernel<double>", "void swh::overflow_kernel<0, double>"]
 MAIN_OVF_GRID = 64 * 256
 

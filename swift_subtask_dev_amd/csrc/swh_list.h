@@ -515,7 +515,11 @@ __device__ __forceinline__ BuildSlot list_build(const GridDev& g, const SoA& a, 
     }
     const int nx = P.nx;
     const int nxy = P.nxy;
+#ifdef SWH_DIAG_NOENUM  // profiling only (diag 1): no cell enumerated
+    const int ncells = diag == 1 ? 0 : P.ncells;
+#else
     const int ncells = P.ncells;
+#endif
     const double delta = P.delta;
     const float deltaf = P.deltaf;
     const float xi = (float)(pi.x - ctr[0]);

@@ -58,7 +58,7 @@ __device__ __forceinline__ unsigned int rwrap_of(float base, float dx) {
 // group, four groups per wave; the groups partition every particle in a
 // cell): each particle's cell-local fp32 position for the staging (posf) and
 // the displacement record at build time (xd0 = xdiff: a kept list measures
-// drifts from here), and each group's box over its active particles
+// drifts from here; null when nothing drifted since the re-bin, xdiff = 0), and each group's box over its active particles
 // (GroupBox), reduced across the group's 16 lanes, turned into the group's
 // BuildPlan (cell range, centre, rounding bound) that the build's waves read
 // with scalar loads. Thread 0 resets the build's device counters.
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void group_prep_kernel(
     const double4 p = a.pos[i];
     const int pc = pcell[i];
     posf[i] = pc >= 0 ? cell_local(g, p, pc) : make_float4(0.f, 0.f, 0.f, 0.f);
-    xd0[i] = xdiff[i];
+    if (xd0) xd0[i] = xdiff[i];
     if (active_part(a, i, max_active_bin)) box_add(b, p, p.w * (double)kGamma * gs1);
   }
   for (int o = 8; o > 0; o >>= 1) {
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void list_disp_kernel(const float4* __restrict
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     if (tb[i] == kTimeBinInhibited) continue;
-    const float4 a = xdiff[i], b = xd0[i];
+    const float4 a = xdiff[i], b = xd0 ? xd0[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     const float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
     d = fmaxf(d, sqrtf(dx * dx + dy * dy + dz * dz) * (1.f + 1e-5f));
   }
@@ -866,6 +866,18 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
   SWH_TRY(s->nbr_ovf.reserve((size_t)s->n * sizeof(int)));
   SWH_TRY(s->posf.reserve((size_t)s->n * sizeof(float4)));
   SWH_TRY(s->list_xd0.reserve((size_t)s->n * sizeof(float4)));
+  // The displacement record: with no drift since the re-bin (xdiff = 0) the
+  // build's record is zero and is not written (s->xd0_zero); before a build
+  // after a drift, which the device may skip, the record is made real.
+#ifndef SWH_XD0_SKIP
+#define SWH_XD0_SKIP 1
+#endif
+  const bool no_drift = SWH_XD0_SKIP && s->grid.dx == 0.;
+  if (!no_drift && s->xd0_zero) {
+    SWH_HIP(hipMemsetAsync(s->list_xd0.ptr, 0, (size_t)s->n * sizeof(float4), s->stream));
+    s->xd0_zero = false;
+  }
+  if (no_drift) s->xd0_zero = true;
   SWH_TRY(s->cell_hreach.reserve((size_t)std::max(1, s->grid.ncell) * sizeof(float)));
   s->list_K = K;
   const ListDev ld = list_dev(s);
@@ -883,7 +895,8 @@ static swh_status build_lists(swh_space* s, const swh_hydro_params* P, bool coun
                      s->stream, grid_dev(s), soa_of(s), s->pcell.as<const int>(),
                      s->xdiff.as<const float4>(), s->groups.as<const int2>(), s->ngroups,
                      P->max_active_bin, (double)ld.skin1, s->posf.as<float4>(),
-                     s->list_xd0.as<float4>(), s->gplan.as<BuildPlan>(), hmax_slot(s),
+                     no_drift ? nullptr : s->list_xd0.as<float4>(), s->gplan.as<BuildPlan>(),
+                     hmax_slot(s),
                      (float)(kGamma * ld.skin1), (float)s->grid.dx, rwrap_slot(s),
                      rwrap_base_slot(s), ovf_slot(s), nbuild_slot(s), run_if);
   hipLaunchKernelGGL(list_build_kernel, dim3(s->ngroups), dim3(64), 0, s->stream, grid_dev(s),
@@ -905,7 +918,8 @@ static swh_status check_kept_lists(swh_space* s, const swh_hydro_params* P, bool
   const int nb = (int)((s->n + 255) / 256);
   SWH_HIP(hipMemsetAsync(keep_stale_slot(s), 0, 2 * sizeof(unsigned int), s->stream));
   hipLaunchKernelGGL(list_disp_kernel, dim3(std::min(nb, kReduceBlocks)), dim3(256), 0, s->stream,
-                     s->xdiff.as<const float4>(), s->list_xd0.as<const float4>(),
+                     s->xdiff.as<const float4>(),
+                     s->xd0_zero ? nullptr : s->list_xd0.as<const float4>(),
                      s->tb.as<const int8_t>(), s->n, disp_slot(s));
   hipLaunchKernelGGL(list_check_kernel, dim3(std::min(nb, kReduceBlocks)), dim3(256), 0, s->stream, soa_of(s), list_dev(s),
                      s->n, P->max_active_bin, s->pcell.as<const int>(), disp_slot(s),

@@ -206,6 +206,7 @@ struct swh_space {
   swh::DevBuf gplan;  // BuildPlan per i-group: the list build's wave-uniform setup
   swh::DevBuf list_xd0;  // float4: the displacement record (xdiff) at the list build
   bool list_valid = false;
+  bool xd0_zero = false;  // list_xd0 is logically zero (built with no drift since the re-bin)
   bool list_check = false;  // kept lists after a drift: the device checks them first
   // particles the ghost converged with H past their list reach (queue
   // grown_q, u32[17]): the gradient / force loops search them (and, force,
